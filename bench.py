@@ -1,0 +1,290 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident GiB/s of the L4 checksum over a packet batch.
+
+BASELINE.json metric "device-resident GiB/s, L4 checksum over packet batch;
+1/2/4/8 MI355X".  One step = one launch of the gfx950 L4 checksum kernel over
+one whole batch already resident in HBM (reference: calc_l4_checksum,
+checksum.cpp:8-36, once per segment of a PacketBatch).
+
+Workloads (--workload):
+  config2 (default)  1,048,576 x 1500 B IPv4/UDP per GPU, uniform PacketBatch
+                     (BASELINE configs[1]); N GPUs = N independent shards,
+                     weak scaling, no data-path collective.
+  config5            16,777,216 x 1500 B mixed v4/v6 x TCP/UDP (descriptor
+                     batch) split across the N GPUs (configs[4]); strong scaling.
+  config4            4,194,304 bimodal 64 B / 9000 B IPv4/UDP (configs[3]), 1 GPU shape.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec HBM3E peak (MI355X_MICROARCH.md, chip table)
+SEG = 1500
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="config2", choices=["config2", "config4", "config5"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall seconds of the CPU baseline sample")
+    return ap.parse_args()
+
+
+def build_workload(wga, torch, name: str, rank: int, world: int, dev):
+    """Returns (launch_fn, n_packets, payload_bytes_per_step, alg_bytes_per_launch, cfg, host_sample_fn)."""
+    if name == "config2":
+        n = 1 << 20
+        seed = 0x5EED0002
+        buf = torch.empty(n * SEG, dtype=torch.uint8, device=dev)
+        # shard-invariant data: byte counter and packet index offset by rank
+        wga.synth_fill(buf, seed, counter_base=rank * n * SEG)
+        desc = wga.synth_desc_stride(n, SEG, SEG, 0, seed, rank * n, device=dev)
+        wga.synth_headers(buf, desc, seed, rank * n)
+        out = torch.empty(n, dtype=torch.uint16, device=dev)
+        del desc
+
+        def launch():
+            wga.calc_l4_checksum_batch(buf, SEG, False, False, 20, out=out)
+
+        cfg = {"workload": "config2: 1,048,576 x 1500 B IPv4/UDP per GPU, uniform PacketBatch (stride 1500)",
+               "packets_per_gpu": n, "segment_size": SEG, "csum_start": 20, "layout": "uniform",
+               "parallelism": f"shard{world} (independent packet shards, no data-path collective)"}
+        alg = n * SEG + 2 * n
+        payload = n * SEG
+
+        def sample(npk):
+            return buf[: npk * SEG].cpu().numpy(), out[:npk].cpu().numpy(), ("uniform", SEG, 20, 0)
+
+        return launch, n, payload, alg, cfg, sample, "weak"
+    if name == "config5":
+        total = 1 << 24
+        lo = total * rank // world
+        hi = total * (rank + 1) // world
+        n = hi - lo
+        seed = 0x5EED0005
+        buf = torch.empty(n * SEG, dtype=torch.uint8, device=dev)
+        wga.synth_fill(buf, seed, counter_base=lo * SEG)
+        desc = wga.synth_desc_stride(n, SEG, SEG, 1, seed, lo, device=dev)
+        wga.synth_headers(buf, desc, seed, lo)
+        out = torch.empty(n, dtype=torch.uint16, device=dev)
+
+        def launch():
+            wga.calc_l4_checksum_desc(buf, desc, out=out)
+
+        cfg = {"workload": "config5: 16,777,216 x 1500 B mixed IPv4/IPv6 x TCP/UDP split across GPUs (descriptor batch)",
+               "packets_total": total, "packets_per_gpu": n, "segment_size": SEG, "layout": "descriptor",
+               "parallelism": f"shard{world} (contiguous packet ranges, no data-path collective)"}
+        alg = n * SEG + 2 * n + 16 * n
+
+        def sample(npk):
+            return buf[: npk * SEG].cpu().numpy(), out[:npk].cpu().numpy(), ("desc", desc[:npk].cpu().numpy())
+
+        return launch, n, n * SEG, alg, cfg, sample, "strong"
+    # config4 bimodal
+    import numpy as np
+
+    n = 1 << 22
+    seed = 0x5EED0004
+    rng = np.random.default_rng(seed)
+    lens = np.where(rng.random(n) < 0.5, 64, 9000).astype(np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])])
+    total = int(offs[-1] + lens[-1])
+    raw = np.zeros((n, 2), dtype=np.int64)
+    raw[:, 0] = offs
+    raw[:, 1] = lens | (20 << 32)  # len | csum_start << 32 | flags << 48 (v4/UDP)
+    desc = torch.from_numpy(raw).to(dev)
+    buf = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    wga.synth_fill(buf, seed)
+    wga.synth_headers(buf, desc, seed, 0)
+    out = torch.empty(n, dtype=torch.uint16, device=dev)
+
+    def launch():
+        wga.calc_l4_checksum_desc(buf, desc, out=out)
+
+    cfg = {"workload": "config4: 4,194,304 IPv4/UDP packets, 64 B / 9000 B 50/50, packed, descriptor batch",
+           "packets_per_gpu": n, "layout": "descriptor", "parallelism": f"shard{world}"}
+    alg = total + 2 * n + 16 * n
+
+    def sample(npk):
+        end = int(offs[npk - 1] + lens[npk - 1])
+        return buf[:end].cpu().numpy(), out[:npk].cpu().numpy(), ("desc", raw[:npk])
+
+    return launch, n, total, alg, cfg, sample, "weak"
+
+
+def cpu_baseline(sample_fn, seconds: float):
+    """The oracle (C restatement of checksum.cpp + a fastcsum-class nofold) on
+    the host cores of this box, on a bounded sample of the same workload."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import numpy as np
+    import oracle  # test infrastructure: the CPU baseline leg only
+
+    npk = 1 << 16
+    host, gpu_out, kind = sample_fn(npk)
+    threads = oracle.default_threads()
+    if kind[0] == "uniform":
+        _, seg, cs, fl = kind
+        exp = oracle.l4_uniform(host, seg, cs, fl, threads)
+        t1c = oracle.time_l4_uniform(host, seg, cs, fl, 1, 1)
+        reps1 = max(1, int(seconds / 3 / max(t1c, 1e-6)))
+        t_1core = oracle.time_l4_uniform(host, seg, cs, fl, 1, reps1) / reps1
+        tall1 = oracle.time_l4_uniform(host, seg, cs, fl, threads, 1)
+        reps = max(1, int(math.ceil(seconds / max(tall1, 1e-6))))
+        t_all = oracle.time_l4_uniform(host, seg, cs, fl, threads, reps) / reps
+        nbytes = host.size
+    else:
+        d = kind[1]
+        exp = oracle.l4_desc(host, d, threads)
+        t0 = time.perf_counter()
+        oracle.l4_desc(host, d, 1)
+        t_1core = time.perf_counter() - t0
+        reps = max(1, int(seconds * threads / max(t_1core, 1e-6)))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            oracle.l4_desc(host, d, threads)
+        t_all = (time.perf_counter() - t0) / reps
+        nbytes = int(np.ascontiguousarray(d).view(oracle.PKT_DESC)["len"].astype(np.int64).sum())
+    parity = bool(np.array_equal(exp, gpu_out))
+    try:
+        cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except Exception:
+        cpu_model = "unknown"
+    return {
+        "value": nbytes / t_all / 2**30,
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "value_1core": nbytes / t_1core / 2**30,
+        "cpu_model": cpu_model,
+        "sample": f"first {npk} packets ({nbytes} B) of the same batch, oracle/csum_oracle.c "
+                  f"(calc_l4_checksum restatement), {threads} pthreads; bit-exact vs GPU: {parity}",
+        "parity_with_gpu": parity,
+    }
+
+
+def load_traffic(workload: str):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary
+    (profiles/pmc_<workload>.json, gfx950 FETCH_SIZE x2 correction applied
+    there), or None if no such profile exists."""
+    p = ROOT / "profiles" / f"pmc_{workload}.json"
+    if not p.exists():
+        return None
+    try:
+        return json.loads(p.read_text()).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import wireglider_amd as wga
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    launch, n, payload, alg, cfg, sample, scaling = build_workload(wga, torch, args.workload, rank, world, dev)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        launch()
+    barrier()
+
+    # Timed region: exactly K launches, per-launch HIP events on the launch stream.
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier()
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        launch()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    wall = t1 - t0
+    kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / args.steps
+    if world > 1:
+        t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, kern_ms_max = float(t[0]), float(t[1])
+        tot = torch.tensor([payload], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        total_payload = float(tot[0])
+    else:
+        kern_ms_max = kern_ms
+        total_payload = float(payload)
+
+    ms_per_step = wall / args.steps * 1e3
+    value = total_payload * args.steps / wall / 2**30
+    achieved = alg / (kern_ms * 1e-3) / 1e9
+    traffic = load_traffic(args.workload)
+    line = {
+        "metric": "device-resident GiB/s, L4 checksum over packet batch; 1/2/4/8 MI355X",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": scaling,
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (device-generated, seeded; BASELINE config shapes)",
+        "config": cfg,
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": "wg::l4csum_wave_kernel",
+            "alg_bytes_per_launch": alg,
+            "kernel_ms_avg": round(kern_ms, 5),
+            "kernel_ms_avg_max_over_ranks": round(kern_ms_max, 5),
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(sample, args.cpu_seconds)
+    elif rank == 0:
+        line["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,204 @@
+/*
+ * wireglider_amd.h — C ABI of the MI355X (gfx950) Internet-checksum engine.
+ *
+ * This is the drop-in boundary behind wireglider's checksum hot path
+ * (reference dinhngtu/wireglider @ 2024-11-01; citations relative to its
+ * root).  Every entry point takes plain pointers and sizes; `stream` is a
+ * hipStream_t passed as void* (NULL = the legacy default stream).  All
+ * packet/descriptor/output pointers are DEVICE pointers (hipMalloc'd, or
+ * host memory registered/mapped for the device) unless a name says _host.
+ *
+ * Ownership follows the reference: every buffer is borrowed
+ * from the caller; nothing is allocated per call; entry points are
+ * reentrant and may be called from several host threads on different
+ * streams.  Launches are asynchronous on `stream`.
+ *
+ * Error convention: the reference has no error channel (checksum.cpp:8-36
+ * returns the checksum only).  Here a negative return is a launch/argument
+ * failure and never changes checksum semantics; 0 = launched.
+ *
+ * Byte order: checksums are returned in native (little-endian) order, as
+ * the reference does, so callers memcpy them straight into headers
+ * (worker/offload.cpp:72-77,185-186,203-204).
+ */
+#ifndef WIREGLIDER_AMD_H
+#define WIREGLIDER_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WG_ABI_VERSION 1
+
+/* Return codes. */
+#define WG_OK 0
+#define WG_ERR_INVALID (-1)  /* bad geometry / null pointer / misaligned descriptor array */
+#define WG_ERR_NODEV (-2)    /* no HIP device visible */
+#define WG_ERR_LAUNCH (-3)   /* hipLaunchKernel / hipGetLastError failed */
+#define WG_ERR_RUNTIME (-4)  /* other HIP runtime failure (alloc, copy, sync) */
+
+/* Packet flags (descriptor `flags`, uniform-batch `flags`). */
+#define WG_PKT_V6 0x01u  /* IPv6: addresses at byte 8 / 24, 16 B each; else IPv4 at 12 / 16, 4 B */
+#define WG_PKT_TCP 0x02u /* pseudo-header proto 6; else 17 (UDP) */
+
+/*
+ * One packet of a variable-length batch.  16 bytes, 16-byte aligned array.
+ * The packet is dev_base[offset, offset + len).  Replaces the per-call
+ * (span, isv6, istcp, csum_start) arguments of calc_l4_checksum.
+ */
+typedef struct wg_pkt_desc {
+    uint64_t offset;
+    uint32_t len;
+    uint16_t csum_start;
+    uint8_t flags; /* WG_PKT_* */
+    uint8_t reserved;
+} wg_pkt_desc;
+
+/* ------------------------------------------------------------------------
+ * L4 checksum over a packet batch.
+ *
+ * Per packet this computes exactly
+ *     wireglider::calc_l4_checksum(pkt, isv6, istcp, csum_start)
+ * (checksum.cpp:8-36): ~fold16(pseudo-header(proto, src, dst,
+ * (uint16_t)(len - csum_start)) + sum of LE words of pkt[csum_start:]),
+ * with word pairing relative to csum_start and the odd tail byte as the low
+ * byte (include/netio/checksum.hpp:30-149).  Generate mode: the caller has
+ * zeroed the checksum field, the result is the value to store
+ * (worker/offload.cpp:64,149,202-204).  Verify mode: the field holds the
+ * received checksum and the result is 0 iff valid
+ * (include/worker/evaluator.hpp:64,93).
+ *
+ * Out-of-contract packets (len < 20/40 or len < csum_start; undefined in
+ * the reference) are computed with the missing bytes treated as absent;
+ * nothing outside a packet is ever read.
+ * ---------------------------------------------------------------------- */
+
+/*
+ * Uniform batch = the reference's PacketBatch (include/worker/offload.hpp:19-29,
+ * include/util/packets.hpp:11-47): packet i is
+ * dev_base[i*segment_size, min((i+1)*segment_size, total_len)), i.e.
+ * nr_segments() = ceil(total_len / segment_size) packets, the last one may be
+ * short.  dev_out receives nr_segments() uint16 results.
+ * Replaces: calc_l4_checksum (include/netio/checksum.hpp:151, checksum.cpp:8)
+ * called once per segment by worker/offload.cpp:202 and
+ * include/worker/evaluator.hpp:64,93.
+ */
+int wg_l4csum_uniform(const uint8_t *dev_base, uint64_t total_len, uint32_t segment_size,
+                      uint16_t csum_start, uint32_t flags, uint16_t *dev_out, void *stream);
+
+/*
+ * Variable batch: n descriptors (dev_desc 16-byte aligned), one result each.
+ * Replaces the same per-packet calc_l4_checksum calls for batches whose
+ * packets differ in length / family / protocol (decap GRO batches,
+ * worker/decap_ref.cpp:53-89 -> include/worker/evaluator.hpp:112-149).
+ */
+int wg_l4csum_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_desc, uint64_t n,
+                   uint16_t *dev_out, void *stream);
+
+/*
+ * checksum(span, 0) per descriptor (flags and csum_start ignored): the
+ * IPv4 header checksum callers, worker/offload.cpp:71,184,
+ * worker/evaluator.cpp:28, include/worker/flowkey_ref.hpp:108.
+ * Replaces: wireglider::checksum (include/netio/checksum.hpp:146-149).
+ */
+int wg_checksum_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_desc, uint64_t n,
+                     uint16_t *dev_out, void *stream);
+
+/* ------------------------------------------------------------------------
+ * GSO split (TSO/USO segmentation + per-segment checksum fixup), batched.
+ * Per super-buffer this is worker_impl::do_tun_gso_split
+ * (worker/offload.cpp:46-216) bit for bit, including its quirks:
+ *   - gso_type with VIRTIO_NET_HDR_GSO_ECN set is segmented as TCP for the
+ *     header length but fixed up / checksummed as UDP (:55 vs :151);
+ *   - a UDP checksum that computes to 0 is stored as 0 (:202-204);
+ *   - the input prefix's ip_sum and L4 checksum field are zeroed in place
+ *     (:145-149), and GSO_NONE + NEEDS_CSUM packets are checksummed in
+ *     place (:56-78).
+ * ---------------------------------------------------------------------- */
+
+/* Native-order mirror of struct virtio_net_hdr (linux/virtio_net.h). */
+typedef struct wg_vnet_hdr {
+    uint8_t flags;    /* VIRTIO_NET_HDR_F_NEEDS_CSUM = 1 */
+    uint8_t gso_type; /* NONE 0, TCPV4 1, TCPV6 4, UDP_L4 5, | ECN 0x80 */
+    uint16_t hdr_len;
+    uint16_t gso_size;
+    uint16_t csum_start;
+    uint16_t csum_offset;
+} wg_vnet_hdr;
+
+typedef struct wg_gso_desc {
+    uint64_t in_offset;  /* super-buffer (IP header onwards) = dev_in[in_offset, +in_len) */
+    uint64_t out_offset; /* its segments are written to dev_out[out_offset, +out_cap) */
+    uint32_t in_len;
+    uint32_t out_cap;
+    wg_vnet_hdr vnet;
+    uint16_t reserved[3];
+} wg_gso_desc; /* 40 bytes */
+
+typedef struct wg_gso_result {
+    uint64_t out_len;      /* PacketBatch.data.size() (== in_len on passthrough) */
+    uint32_t segment_size; /* PacketBatch.segment_size */
+    uint16_t hdr_len;      /* vnethdr.hdr_len after the call (:110,:114) */
+    uint8_t isv6;
+    uint8_t ecn;
+    int8_t status;       /* 0 ok; -1 gso_size 0 with payload; -2 out_cap < reserve_size; -3 out of contract */
+    uint8_t passthrough; /* 1: batch is the (possibly in-place checksummed) input */
+    uint8_t pad[6];
+} wg_gso_result; /* 24 bytes */
+
+/* Segment n super-buffers.  dev_desc / dev_res are device arrays of n. */
+int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
+                 wg_gso_result *dev_res, void *stream);
+
+/* ------------------------------------------------------------------------
+ * Host-memory path: the batch starts and ends in host
+ * memory.  Pinned staging + hipMemcpyAsync H2D -> kernel -> D2H on the
+ * engine's per-thread stream; synchronous.  Uses a per-thread device
+ * workspace that grows to the largest batch seen.
+ * ---------------------------------------------------------------------- */
+int wg_l4csum_uniform_host(const uint8_t *host_base, uint64_t total_len, uint32_t segment_size,
+                           uint16_t csum_start, uint32_t flags, uint16_t *host_out);
+
+/* ------------------------------------------------------------------------
+ * Synthetic batches (benchmark / test data, written on the device; not part
+ * of the reference interface).  Deterministic in `seed` and in the global
+ * packet index, so shards generated on different GPUs agree.
+ * ---------------------------------------------------------------------- */
+
+/* Fill dev[0, nbytes) with counter-based pseudo-random bytes. */
+int wg_synth_fill(uint8_t *dev, uint64_t nbytes, uint64_t seed, uint64_t counter_base,
+                  void *stream);
+
+/* Write IPv4/IPv6 + TCP/UDP headers for each descriptor (payload untouched,
+ * L4 checksum field zeroed = generate mode, IPv4 header checksum valid).
+ * index_base offsets the packet index used to derive header fields. */
+int wg_synth_headers(uint8_t *dev_base, const wg_pkt_desc *dev_desc, uint64_t n, uint64_t seed,
+                     uint64_t index_base, void *stream);
+
+/* Fill descriptors for a uniform-stride batch: packet i at i*stride, length
+ * len, family/protocol by `mode`: 0 = all v4/UDP, 1 = v4/v6 x TCP/UDP mixed
+ * 50/50 by a hash of (seed, index_base + i) (BASELINE config 5). */
+int wg_synth_desc_stride(wg_pkt_desc *dev_desc, uint64_t n, uint64_t stride, uint32_t len,
+                         int mode, uint64_t seed, uint64_t index_base, void *stream);
+
+/* Store each packet's result into its L4 checksum field (csum_start +
+ * 6 for UDP, +16 for TCP), turning a generate-mode batch into a valid one. */
+int wg_store_l4csum(uint8_t *dev_base, const wg_pkt_desc *dev_desc, uint64_t n,
+                    const uint16_t *dev_csum, void *stream);
+
+/* ------------------------------------------------------------------------
+ * Misc.
+ * ---------------------------------------------------------------------- */
+int wg_abi_version(void);
+const char *wg_strerror(int code);
+/* HIP device count (0 when no GPU); never throws. */
+int wg_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WIREGLIDER_AMD_H */

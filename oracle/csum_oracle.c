@@ -1,0 +1,388 @@
+/*
+ * csum_oracle.c — CPU restatement of wireglider's checksum hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see csum_oracle.h).  Never linked into, loaded
+ * by, or called from the wireglider_amd product library.
+ *
+ * Reference citations are dinhngtu/wireglider @ 2024-11-01, relative to the
+ * reference root.
+ */
+#define _GNU_SOURCE
+#include "csum_oracle.h"
+
+#include <pthread.h>
+#include <string.h>
+#include <time.h>
+
+/* ------------------------------------------------------------------------ */
+/* Scalar arithmetic                                                        */
+/* ------------------------------------------------------------------------ */
+
+/* tests/checksum_tests.hpp:11-34: LE 16-bit words into a 64-bit sum, odd
+ * trailing byte as the low byte (RFC 1071 erratum 3133, :20-26), fold with
+ * a carry loop, complement. */
+uint16_t orc_checksum_ref1(const uint8_t *data, size_t size) {
+    uint64_t csum = 0;
+    size_t i = size;
+    while (i > 1) {
+        uint16_t word;
+        memcpy(&word, data + (size - i), sizeof(word));
+        csum += word;
+        i -= 2;
+    }
+    if (i == 1)
+        csum += (uint16_t)data[size - 1];
+    for (;;) {
+        uint64_t carry = csum >> 16;
+        if (!carry)
+            break;
+        csum = (csum & 0xffff) + carry;
+    }
+    return (uint16_t)(~csum & 0xffff);
+}
+
+/* One's-complement 64-bit add with end-around carry: the primitive of
+ * checksum_impl::checksum_add / checksum_nofold<N> (include/netio/checksum.hpp:20-77). */
+static inline uint64_t add_eac(uint64_t a, uint64_t b) {
+    uint64_t s = a + b;
+    return s + (s < b);
+}
+
+/* include/netio/checksum.hpp:79-100.  The reference dispatches to one of
+ * fastcsum's nofold kernels; all of them satisfy the same contract, checked
+ * by tests/test-checksum.cpp:11-51: the folded result equals checksum_ref1.
+ * Here: LE 32-bit words summed into a 64-bit accumulator (no carry can be
+ * lost below 2^32 words), then the 0..3 byte tail as a 16-bit word and a low
+ * byte, then an end-around-carry add of `initial`.  The accumulator is
+ * congruent to (initial + sum of LE 16-bit words) mod 0xFFFF and is zero only
+ * when initial and every byte are zero, so it folds to the reference value. */
+uint64_t orc_nofold(const uint8_t *b, size_t n, uint64_t initial) {
+    uint64_t acc = 0;
+    size_t i = 0;
+    for (; i + 4 <= n; i += 4) {
+        uint32_t w;
+        memcpy(&w, b + i, 4);
+        acc += w;
+    }
+    if (n - i >= 2) {
+        uint16_t w;
+        memcpy(&w, b + i, 2);
+        acc += w;
+        i += 2;
+    }
+    if (n - i == 1)
+        acc += b[i]; /* low byte on little-endian (checksum.hpp:69-77) */
+    return add_eac(acc, initial);
+}
+
+/* fastcsum_fold_complement: 64 -> 32 -> 16 with end-around carry, then ~. */
+uint16_t orc_fold_complement(uint64_t sum) {
+    uint64_t s = (sum & 0xffffffffu) + (sum >> 32);
+    s = (s & 0xffffffffu) + (s >> 32);
+    s = (s & 0xffffu) + (s >> 16);
+    s = (s & 0xffffu) + (s >> 16);
+    s = (s & 0xffffu) + (s >> 16);
+    return (uint16_t)(~s & 0xffffu);
+}
+
+/* include/netio/checksum.hpp:146-149 */
+uint16_t orc_checksum(const uint8_t *b, size_t n, uint64_t initial) {
+    return orc_fold_complement(orc_nofold(b, n, initial));
+}
+
+/* include/netio/checksum.hpp:102-116: sum(src) + sum(dst) + the 4 bytes
+ * {0x00, proto, l4Len>>8, l4Len&0xff} (store_big_u16 at :112-113). */
+uint64_t orc_pseudo_header_nofold(uint8_t proto, const uint8_t *src, const uint8_t *dst,
+                                  size_t addrlen, uint16_t l4len) {
+    uint8_t tail[4] = {0, proto, (uint8_t)(l4len >> 8), (uint8_t)(l4len & 0xff)};
+    uint64_t sum = orc_nofold(src, addrlen, 0);
+    sum = orc_nofold(dst, addrlen, sum);
+    return orc_nofold(tail, 4, sum);
+}
+
+/* include/netio/checksum.hpp:120-144 */
+uint16_t orc_pseudo_header_checksum(uint8_t proto, const uint8_t *src, const uint8_t *dst,
+                                    size_t addrlen, uint16_t l4len) {
+    return orc_fold_complement(orc_pseudo_header_nofold(proto, src, dst, addrlen, l4len));
+}
+
+/* checksum.cpp:8-36.  v6 addresses at offsetof(ip6_hdr, ip6_src) = 8 and
+ * +16 (:14-18); v4 at offsetof(struct ip, ip_src) = 12 and +4 (:24-28);
+ * proto = istcp ? 6 : 17; l4Len = (uint16_t)(len - csum_start) (:23,33);
+ * body = checksum(ippkt.subspan(csum_start), pseudo) (:35). */
+uint16_t orc_calc_l4_checksum(const uint8_t *pkt, size_t len, int isv6, int istcp,
+                              uint16_t csum_start) {
+    const size_t ao = isv6 ? 8 : 12;
+    const size_t al = isv6 ? 16 : 4;
+    uint8_t src[16] = {0}, dst[16] = {0};
+    for (size_t j = 0; j < al; j++) {
+        if (ao + j < len)
+            src[j] = pkt[ao + j];
+        if (ao + al + j < len)
+            dst[j] = pkt[ao + al + j];
+    }
+    uint64_t s = orc_pseudo_header_nofold(istcp ? 6 : 17, src, dst, al,
+                                          (uint16_t)(len - csum_start));
+    if (csum_start >= len)
+        return orc_fold_complement(s);
+    return orc_checksum(pkt + csum_start, len - csum_start, s);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Batched drivers                                                          */
+/* ------------------------------------------------------------------------ */
+
+typedef struct {
+    int kind; /* 0 uniform l4, 1 desc l4, 2 desc checksum */
+    const uint8_t *base;
+    uint64_t total_len;
+    uint32_t segment_size;
+    uint16_t csum_start;
+    uint32_t flags;
+    const orc_pkt_desc *desc;
+    uint16_t *out;
+    uint64_t lo, hi;
+} job_t;
+
+static void run_job(job_t *j) {
+    for (uint64_t i = j->lo; i < j->hi; i++) {
+        if (j->kind == 0) {
+            uint64_t off = i * (uint64_t)j->segment_size;
+            uint64_t len = j->total_len - off;
+            if (len > j->segment_size)
+                len = j->segment_size;
+            j->out[i] = orc_calc_l4_checksum(j->base + off, (size_t)len, j->flags & 1,
+                                             (j->flags >> 1) & 1, j->csum_start);
+        } else if (j->kind == 1) {
+            const orc_pkt_desc *d = &j->desc[i];
+            j->out[i] = orc_calc_l4_checksum(j->base + d->offset, d->len, d->flags & 1,
+                                             (d->flags >> 1) & 1, d->csum_start);
+        } else {
+            const orc_pkt_desc *d = &j->desc[i];
+            j->out[i] = orc_checksum(j->base + d->offset, d->len, 0);
+        }
+    }
+}
+
+static void *job_thread(void *arg) {
+    run_job((job_t *)arg);
+    return NULL;
+}
+
+#define ORC_MAX_THREADS 256
+
+static void run_parallel(job_t proto, uint64_t n, int threads) {
+    if (threads < 1)
+        threads = 1;
+    if (threads > ORC_MAX_THREADS)
+        threads = ORC_MAX_THREADS;
+    if ((uint64_t)threads > n)
+        threads = n ? (int)n : 1;
+    if (threads == 1) {
+        proto.lo = 0;
+        proto.hi = n;
+        run_job(&proto);
+        return;
+    }
+    pthread_t tids[ORC_MAX_THREADS];
+    job_t jobs[ORC_MAX_THREADS];
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = proto;
+        jobs[t].lo = n * (uint64_t)t / (uint64_t)threads;
+        jobs[t].hi = n * (uint64_t)(t + 1) / (uint64_t)threads;
+        pthread_create(&tids[t], NULL, job_thread, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++)
+        pthread_join(tids[t], NULL);
+}
+
+void orc_l4_uniform(const uint8_t *base, uint64_t total_len, uint32_t segment_size,
+                    uint16_t csum_start, uint32_t flags, uint16_t *out, int threads) {
+    if (!segment_size)
+        return;
+    job_t j = {0};
+    j.kind = 0;
+    j.base = base;
+    j.total_len = total_len;
+    j.segment_size = segment_size;
+    j.csum_start = csum_start;
+    j.flags = flags;
+    j.out = out;
+    /* nr_segments(): include/worker/offload.hpp:26-28 */
+    uint64_t n = (total_len + segment_size - 1) / segment_size;
+    run_parallel(j, n, threads);
+}
+
+void orc_l4_desc(const uint8_t *base, const orc_pkt_desc *desc, uint64_t n, uint16_t *out,
+                 int threads) {
+    job_t j = {0};
+    j.kind = 1;
+    j.base = base;
+    j.desc = desc;
+    j.out = out;
+    run_parallel(j, n, threads);
+}
+
+void orc_checksum_desc(const uint8_t *base, const orc_pkt_desc *desc, uint64_t n,
+                       uint16_t *out, int threads) {
+    job_t j = {0};
+    j.kind = 2;
+    j.base = base;
+    j.desc = desc;
+    j.out = out;
+    run_parallel(j, n, threads);
+}
+
+double orc_time_l4_uniform(const uint8_t *base, uint64_t total_len, uint32_t segment_size,
+                           uint16_t csum_start, uint32_t flags, uint16_t *out, int threads,
+                           int reps) {
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (int r = 0; r < reps; r++)
+        orc_l4_uniform(base, total_len, segment_size, csum_start, flags, out, threads);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}
+
+/* ------------------------------------------------------------------------ */
+/* GSO split: worker/offload.cpp:46-216                                     */
+/* ------------------------------------------------------------------------ */
+
+static inline uint16_t ld_be16(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
+static inline uint32_t ld_be32(const uint8_t *p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+static inline void st_be16(uint8_t *p, uint16_t v) {
+    p[0] = (uint8_t)(v >> 8);
+    p[1] = (uint8_t)v;
+}
+static inline void st_be32(uint8_t *p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 24);
+    p[1] = (uint8_t)(v >> 16);
+    p[2] = (uint8_t)(v >> 8);
+    p[3] = (uint8_t)v;
+}
+
+#define VNET_F_NEEDS_CSUM 1
+#define VNET_GSO_NONE 0
+#define VNET_GSO_TCPV4 1
+#define VNET_GSO_TCPV6 4
+#define VNET_GSO_UDP_L4 5 /* include/worker/offload.hpp:11-15 */
+#define VNET_GSO_ECN 0x80
+
+int orc_gso_split(uint8_t *in, size_t in_len, orc_vnet_hdr *v, uint8_t *out, size_t out_cap,
+                  orc_gso_result *res) {
+    memset(res, 0, sizeof(*res));
+    const size_t cs = v->csum_start;
+    const size_t l4off = (size_t)v->csum_start + v->csum_offset; /* :47 */
+    /* Out of the reference's contract (undefined behaviour there). */
+    if (in_len < 1 || cs > in_len)
+        return -3;
+    const int isv6 = (in[0] >> 4) == 6; /* :48 */
+    if (in_len < (isv6 ? 40u : 20u))
+        return -3;
+    /* :49-53, IPTOS_ECN = & 0x03 */
+    const uint8_t ecn = isv6 ? (uint8_t)((ld_be32(in) >> 20) & 3) : (uint8_t)(in[1] & 3);
+    res->isv6 = (uint8_t)isv6;
+    res->ecn = ecn;
+    res->out_len = in_len;
+    res->segment_size = in_len;
+    res->passthrough = 1;
+    res->hdr_len = v->hdr_len;
+
+    switch (v->gso_type & ~VNET_GSO_ECN) { /* :55 */
+    case VNET_GSO_NONE:
+        if (v->flags & VNET_F_NEEDS_CSUM) { /* :56-78 */
+            if (l4off + 2 > in_len)
+                return -3;
+            if (!isv6) {
+                in[10] = 0; /* ip_sum */
+                in[11] = 0;
+            }
+            in[l4off] = 0;
+            in[l4off + 1] = 0;
+            int istcp = isv6 ? in[6] == 6 : in[9] == 6; /* ip6_nxt / ip_p */
+            if (!isv6) {
+                uint16_t c = orc_checksum(in, cs, 0);
+                memcpy(in + 10, &c, 2); /* native order, :72-73 */
+            }
+            uint16_t l4 = orc_calc_l4_checksum(in, in_len, isv6, istcp, (uint16_t)cs);
+            memcpy(in + l4off, &l4, 2);
+        }
+        return 0;
+    case VNET_GSO_TCPV4:
+    case VNET_GSO_TCPV6: {
+        if (in_len - cs < 20) /* :91 */
+            return 0;
+        size_t thlen = 4u * (in[cs + 12] >> 4); /* tcphdr.doff, :100 */
+        if (thlen < 20)                          /* :101 */
+            return 0;
+        v->hdr_len = (uint16_t)(cs + thlen); /* :110 */
+        break;
+    }
+    case VNET_GSO_UDP_L4:
+        v->hdr_len = (uint16_t)(cs + 8); /* :114 */
+        break;
+    default:
+        return 0; /* :116-123 */
+    }
+    res->hdr_len = v->hdr_len;
+    const size_t hdr_len = v->hdr_len;
+    if (in_len < hdr_len) /* :126-134 */
+        return 0;
+    if (l4off + 2 > hdr_len)
+        return -3;
+
+    const size_t rest_len = in_len - hdr_len;
+    const size_t gso = v->gso_size;
+    if (rest_len && !gso)
+        return -1;
+    const size_t nseg = gso ? (rest_len + gso - 1) / gso : 0;
+    if (out_cap < in_len + nseg * hdr_len) /* reserve_size assert, :139-143 */
+        return -2;
+
+    if (!isv6) { /* :145-147 */
+        in[10] = 0;
+        in[11] = 0;
+    }
+    in[l4off] = 0; /* :149 */
+    in[l4off + 1] = 0;
+
+    const int istcp = v->gso_type == VNET_GSO_TCPV4 || v->gso_type == VNET_GSO_TCPV6; /* :151 */
+    uint32_t seq0 = istcp ? ld_be32(in + cs + 4) : 0;                                   /* :152-154 */
+
+    const uint8_t *rest = in + hdr_len;
+    size_t remaining = rest_len, pb = 0;
+    for (size_t i = 0; remaining; i++) { /* :157-208 */
+        size_t datalen = remaining < gso ? remaining : gso;
+        size_t pktlen = hdr_len + datalen;
+        uint8_t *seg = out + pb;
+        pb += pktlen;
+        memcpy(seg, in, hdr_len);            /* :165 */
+        memcpy(seg + hdr_len, rest, datalen); /* :166 */
+        if (isv6) {
+            st_be16(seg + 4, (uint16_t)(pktlen - cs)); /* ip6_plen, :168-172 */
+        } else {
+            if (i)
+                st_be16(seg + 4, (uint16_t)(ld_be16(seg + 4) + i)); /* ip_id, :178-182 */
+            st_be16(seg + 2, (uint16_t)pktlen);                     /* ip_len, :183 */
+            uint16_t c = orc_checksum(seg, cs, 0);                  /* :184 */
+            memcpy(seg + 10, &c, 2);
+        }
+        if (istcp) {
+            st_be32(seg + cs + 4, (uint32_t)(seq0 + gso * i)); /* :190-192 */
+            if (datalen < remaining)
+                seg[cs + 13] &= (uint8_t)~0x09; /* fin, psh: :193-195 */
+        } else {
+            st_be16(seg + cs + 4, (uint16_t)(pktlen - cs)); /* udp->len, :197-199 */
+        }
+        uint16_t l4 = orc_calc_l4_checksum(seg, pktlen, isv6, istcp, (uint16_t)cs); /* :202 */
+        memcpy(seg + l4off, &l4, 2);
+        rest += datalen;
+        remaining -= datalen;
+    }
+    res->passthrough = 0;
+    res->out_len = pb;                      /* :210-215 */
+    res->segment_size = hdr_len + gso;
+    return 0;
+}

@@ -1,0 +1,126 @@
+/*
+ * csum_oracle.h — CPU restatement of wireglider's checksum hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the parity checker for the
+ * MI355X engine in wireglider_amd/.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it; the product path never does.
+ *
+ * Every function cites the reference (dinhngtu/wireglider @ 2024-11-01,
+ * paths relative to the reference root) that it restates.  Pinning: the
+ * byte-sum/fold arithmetic is pinned against golden vectors produced by
+ * compiling the reference's own test oracle (tests/checksum_tests.hpp:11-48)
+ * in place (see oracle/Makefile, tests/golden/).  checksum.cpp and
+ * worker/offload.cpp need boost.endian and the un-vendored fastcsum library,
+ * neither of which is in the image, so they are unbuildable here; the L4 and
+ * GSO-split restatements are pinned by the reference tests' own assertions
+ * (tests/test-checksum.cpp:53-82 verify-to-zero, tests/test-offload.cpp:21-171
+ * segment geometry) and by an independent RFC 768/793 textbook
+ * implementation in tests/.  See DESIGN.md §Oracle.
+ */
+#ifndef WG_CSUM_ORACLE_H
+#define WG_CSUM_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* tests/checksum_tests.hpp:11-34 (checksum_ref1, the snabb scalar oracle). */
+uint16_t orc_checksum_ref1(const uint8_t *data, size_t size);
+
+/* include/netio/checksum.hpp:79-100 — the dynamic-extent nofold sum
+ * (fastcsum_nofold_generic64 contract): 64-bit one's-complement accumulation
+ * of the native (LE) words of b, pairing relative to b[0], odd tail byte
+ * as the low byte, added to `initial` with end-around carry. */
+uint64_t orc_nofold(const uint8_t *b, size_t n, uint64_t initial);
+
+/* fastcsum_fold_complement contract (include/netio/checksum.hpp:127,148):
+ * fold 64 -> 16 bits with end-around carry, then one's complement. */
+uint16_t orc_fold_complement(uint64_t sum);
+
+/* include/netio/checksum.hpp:146-149 */
+uint16_t orc_checksum(const uint8_t *b, size_t n, uint64_t initial);
+
+/* include/netio/checksum.hpp:102-116 (addresses as dynamic spans; the
+ * fixed-extent N=4/16 specialisations at :30-58 give the same value). */
+uint64_t orc_pseudo_header_nofold(uint8_t proto, const uint8_t *src, const uint8_t *dst,
+                                  size_t addrlen, uint16_t l4len);
+
+/* include/netio/checksum.hpp:120-144 */
+uint16_t orc_pseudo_header_checksum(uint8_t proto, const uint8_t *src, const uint8_t *dst,
+                                    size_t addrlen, uint16_t l4len);
+
+/* checksum.cpp:8-36.  Preconditions as in the reference (unchecked there):
+ * len >= 20 (v4) / 40 (v6) and len >= csum_start.  The oracle defines the
+ * out-of-contract cases the same way the GPU engine does: bytes past `len`
+ * are never read and count as absent. */
+uint16_t orc_calc_l4_checksum(const uint8_t *pkt, size_t len, int isv6, int istcp,
+                              uint16_t csum_start);
+
+/* Batched drivers (threads > 1 splits the packet range into contiguous
+ * slices, one std::thread-equivalent pthread per slice). */
+
+/* PacketBatch layout, include/worker/offload.hpp:19-29 and
+ * include/util/packets.hpp:11-47: packet i = base[i*S, min((i+1)*S, total)). */
+void orc_l4_uniform(const uint8_t *base, uint64_t total_len, uint32_t segment_size,
+                    uint16_t csum_start, uint32_t flags, uint16_t *out, int threads);
+
+/* Descriptor batch (same layout as wg_pkt_desc in include/wireglider_amd.h). */
+typedef struct orc_pkt_desc {
+    uint64_t offset;
+    uint32_t len;
+    uint16_t csum_start;
+    uint8_t flags; /* bit0 = v6, bit1 = tcp */
+    uint8_t reserved;
+} orc_pkt_desc;
+
+void orc_l4_desc(const uint8_t *base, const orc_pkt_desc *desc, uint64_t n, uint16_t *out,
+                 int threads);
+
+/* checksum(span, 0) per packet of a descriptor batch (IPv4 header checksum
+ * use: worker/offload.cpp:71,184, worker/evaluator.cpp:28). */
+void orc_checksum_desc(const uint8_t *base, const orc_pkt_desc *desc, uint64_t n,
+                       uint16_t *out, int threads);
+
+/* worker/offload.cpp:46-216 — do_tun_gso_split.  `in` is modified in place
+ * exactly as the reference modifies it (ip_sum and the L4 checksum field of
+ * the prefix are zeroed; GSO_NONE+NEEDS_CSUM fills checksums in place).
+ * vnet fields are the native-order virtio_net_hdr members.  Returns 0 on
+ * success, negative on a case the reference does not define
+ * (-1: gso_size == 0 with payload -> the reference loops forever;
+ *  -2: output capacity below the reference's reserve_size assert). */
+typedef struct orc_gso_result {
+    uint64_t out_len;      /* PacketBatch.data.size() */
+    uint64_t segment_size; /* PacketBatch.segment_size */
+    uint16_t hdr_len;      /* vnethdr.hdr_len after the call */
+    uint8_t isv6;
+    uint8_t ecn;
+    uint8_t passthrough;   /* 1: data == inbuf (returned unsegmented) */
+    uint8_t pad[3];
+} orc_gso_result;
+
+typedef struct orc_vnet_hdr {
+    uint8_t flags;
+    uint8_t gso_type;
+    uint16_t hdr_len;
+    uint16_t gso_size;
+    uint16_t csum_start;
+    uint16_t csum_offset;
+} orc_vnet_hdr;
+
+int orc_gso_split(uint8_t *in, size_t in_len, orc_vnet_hdr *vnet, uint8_t *out, size_t out_cap,
+                  orc_gso_result *res);
+
+/* Timing helper for the cpu_baseline: runs orc_l4_uniform `reps` times and
+ * returns elapsed seconds (monotonic clock). */
+double orc_time_l4_uniform(const uint8_t *base, uint64_t total_len, uint32_t segment_size,
+                           uint16_t csum_start, uint32_t flags, uint16_t *out, int threads,
+                           int reps);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,164 @@
+"""ctypes binding of the CPU oracle (oracle/csum_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker / CPU baseline.  The product
+package wireglider_amd never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "build" / "libcsum_oracle.so"
+
+PKT_DESC = np.dtype([("offset", "<u8"), ("len", "<u4"), ("csum_start", "<u2"), ("flags", "u1"),
+                     ("reserved", "u1")])
+assert PKT_DESC.itemsize == 16
+
+VNET_HDR = np.dtype([("flags", "u1"), ("gso_type", "u1"), ("hdr_len", "<u2"), ("gso_size", "<u2"),
+                     ("csum_start", "<u2"), ("csum_offset", "<u2")])
+GSO_RESULT = np.dtype([("out_len", "<u8"), ("segment_size", "<u8"), ("hdr_len", "<u2"), ("isv6", "u1"),
+                       ("ecn", "u1"), ("passthrough", "u1"), ("pad", "u1", 3)])
+assert GSO_RESULT.itemsize == 24
+
+
+class _VNet(ctypes.Structure):
+    _fields_ = [("flags", ctypes.c_uint8), ("gso_type", ctypes.c_uint8), ("hdr_len", ctypes.c_uint16),
+                ("gso_size", ctypes.c_uint16), ("csum_start", ctypes.c_uint16), ("csum_offset", ctypes.c_uint16)]
+
+
+class _GsoRes(ctypes.Structure):
+    _fields_ = [("out_len", ctypes.c_uint64), ("segment_size", ctypes.c_uint64), ("hdr_len", ctypes.c_uint16),
+                ("isv6", ctypes.c_uint8), ("ecn", ctypes.c_uint8), ("passthrough", ctypes.c_uint8),
+                ("pad", ctypes.c_uint8 * 3)]
+
+
+def build() -> None:
+    import subprocess
+
+    subprocess.run(["make", "-C", str(HERE)], check=True, capture_output=True)
+
+
+def _load():
+    if not LIB.exists():
+        build()
+    lib = ctypes.CDLL(str(LIB))
+    vp, u64, u32, u16, i32, sz = (ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint16,
+                                  ctypes.c_int, ctypes.c_size_t)
+    lib.orc_checksum_ref1.restype = u16
+    lib.orc_checksum_ref1.argtypes = [vp, sz]
+    lib.orc_nofold.restype = u64
+    lib.orc_nofold.argtypes = [vp, sz, u64]
+    lib.orc_fold_complement.restype = u16
+    lib.orc_fold_complement.argtypes = [u64]
+    lib.orc_checksum.restype = u16
+    lib.orc_checksum.argtypes = [vp, sz, u64]
+    lib.orc_pseudo_header_nofold.restype = u64
+    lib.orc_pseudo_header_nofold.argtypes = [ctypes.c_uint8, vp, vp, sz, u16]
+    lib.orc_calc_l4_checksum.restype = u16
+    lib.orc_calc_l4_checksum.argtypes = [vp, sz, i32, i32, u16]
+    lib.orc_l4_uniform.restype = None
+    lib.orc_l4_uniform.argtypes = [vp, u64, u32, u16, u32, vp, i32]
+    lib.orc_l4_desc.restype = None
+    lib.orc_l4_desc.argtypes = [vp, vp, u64, vp, i32]
+    lib.orc_checksum_desc.restype = None
+    lib.orc_checksum_desc.argtypes = [vp, vp, u64, vp, i32]
+    lib.orc_gso_split.restype = i32
+    lib.orc_gso_split.argtypes = [vp, sz, ctypes.POINTER(_VNet), vp, sz, ctypes.POINTER(_GsoRes)]
+    lib.orc_time_l4_uniform.restype = ctypes.c_double
+    lib.orc_time_l4_uniform.argtypes = [vp, u64, u32, u16, u32, vp, i32, i32]
+    return lib
+
+
+lib = _load()
+
+
+def default_threads() -> int:
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit():
+        return max(1, int(env))
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def _u8(buf) -> np.ndarray:
+    a = np.ascontiguousarray(np.frombuffer(buf, dtype=np.uint8) if not isinstance(buf, np.ndarray) else buf)
+    assert a.dtype == np.uint8
+    return a
+
+
+def checksum_ref1(buf) -> int:
+    a = _u8(buf)
+    return int(lib.orc_checksum_ref1(a.ctypes.data, a.size))
+
+
+def checksum(buf, initial: int = 0) -> int:
+    a = _u8(buf)
+    return int(lib.orc_checksum(a.ctypes.data, a.size, initial))
+
+
+def nofold(buf, initial: int = 0) -> int:
+    a = _u8(buf)
+    return int(lib.orc_nofold(a.ctypes.data, a.size, initial))
+
+
+def fold_complement(x: int) -> int:
+    return int(lib.orc_fold_complement(x))
+
+
+def calc_l4_checksum(pkt, isv6: bool, istcp: bool, csum_start: int) -> int:
+    a = _u8(pkt)
+    return int(lib.orc_calc_l4_checksum(a.ctypes.data, a.size, int(isv6), int(istcp), csum_start))
+
+
+def l4_uniform(buf: np.ndarray, segment_size: int, csum_start: int, flags: int,
+               threads: int | None = None) -> np.ndarray:
+    a = _u8(buf)
+    n = (a.size + segment_size - 1) // segment_size
+    out = np.empty(n, dtype=np.uint16)
+    lib.orc_l4_uniform(a.ctypes.data, a.size, segment_size, csum_start, flags, out.ctypes.data,
+                       threads or default_threads())
+    return out
+
+
+def l4_desc(buf: np.ndarray, desc: np.ndarray, threads: int | None = None) -> np.ndarray:
+    a = _u8(buf)
+    d = np.ascontiguousarray(desc).view(PKT_DESC).reshape(-1)
+    out = np.empty(d.size, dtype=np.uint16)
+    lib.orc_l4_desc(a.ctypes.data, d.ctypes.data, d.size, out.ctypes.data, threads or default_threads())
+    return out
+
+
+def checksum_desc(buf: np.ndarray, desc: np.ndarray, threads: int | None = None) -> np.ndarray:
+    a = _u8(buf)
+    d = np.ascontiguousarray(desc).view(PKT_DESC).reshape(-1)
+    out = np.empty(d.size, dtype=np.uint16)
+    lib.orc_checksum_desc(a.ctypes.data, d.ctypes.data, d.size, out.ctypes.data, threads or default_threads())
+    return out
+
+
+def gso_split(inbuf: np.ndarray, vnet: dict, out_cap: int):
+    """Returns (status, in_after, out_bytes, vnet_after, result dict)."""
+    a = np.array(_u8(inbuf), copy=True)
+    v = _VNet(vnet.get("flags", 0), vnet.get("gso_type", 0), vnet.get("hdr_len", 0), vnet.get("gso_size", 0),
+              vnet.get("csum_start", 0), vnet.get("csum_offset", 0))
+    out = np.zeros(max(out_cap, 1), dtype=np.uint8)
+    r = _GsoRes()
+    st = lib.orc_gso_split(a.ctypes.data, a.size, ctypes.byref(v), out.ctypes.data, out_cap, ctypes.byref(r))
+    res = dict(out_len=r.out_len, segment_size=r.segment_size, hdr_len=r.hdr_len, isv6=r.isv6, ecn=r.ecn,
+               passthrough=r.passthrough)
+    vafter = dict(flags=v.flags, gso_type=v.gso_type, hdr_len=v.hdr_len, gso_size=v.gso_size,
+                  csum_start=v.csum_start, csum_offset=v.csum_offset)
+    return st, a, out[: r.out_len if (st == 0 and not r.passthrough) else 0], vafter, res
+
+
+def time_l4_uniform(buf: np.ndarray, segment_size: int, csum_start: int, flags: int, threads: int,
+                    reps: int) -> float:
+    a = _u8(buf)
+    n = (a.size + segment_size - 1) // segment_size
+    out = np.empty(n, dtype=np.uint16)
+    return float(lib.orc_time_l4_uniform(a.ctypes.data, a.size, segment_size, csum_start, flags,
+                                         out.ctypes.data, threads, reps))

@@ -1,0 +1,241 @@
+"""wireglider_amd — MI355X-native Internet-checksum engine (Python plumbing).
+
+The engine itself is C++/HIP (libwireglider_amd.so, C ABI in
+include/wireglider_amd.h).  This module binds that ABI with ctypes and takes
+torch tensors for device memory and streams; torch is plumbing only.
+
+Mirrors the reference's interface for the path (dinhngtu/wireglider
+@ 2024-11-01):
+  calc_l4_checksum_batch  <- checksum.cpp:8-36 over a PacketBatch
+                             (include/worker/offload.hpp:19-29)
+  calc_l4_checksum_desc   <- the same over a descriptor batch
+  checksum_desc           <- include/netio/checksum.hpp:146-149
+  gso_split               <- worker/offload.cpp:46-216 (batched)
+
+There is no CPU fallback: importing without the built library raises, and
+every compute call requires a HIP device.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = _PKG / "lib" / "libwireglider_amd.so"
+
+WG_OK = 0
+WG_PKT_V6 = 0x01
+WG_PKT_TCP = 0x02
+ABI_VERSION = 1
+
+# Every symbol declared in include/wireglider_amd.h.
+EXPORTED_SYMBOLS = (
+    "wg_l4csum_uniform",
+    "wg_l4csum_desc",
+    "wg_checksum_desc",
+    "wg_gso_split",
+    "wg_l4csum_uniform_host",
+    "wg_synth_fill",
+    "wg_synth_headers",
+    "wg_synth_desc_stride",
+    "wg_store_l4csum",
+    "wg_abi_version",
+    "wg_strerror",
+    "wg_device_count",
+)
+
+# struct layouts (include/wireglider_amd.h)
+PKT_DESC_BYTES = 16
+GSO_DESC_BYTES = 40
+GSO_RESULT_BYTES = 24
+
+
+class WireGliderError(RuntimeError):
+    pass
+
+
+def _load() -> ctypes.CDLL:
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(wireglider_amd has no CPU fallback)"
+        )
+    lib = ctypes.CDLL(str(LIB_PATH))
+    u8p = ctypes.c_void_p
+    vp = ctypes.c_void_p
+    u64 = ctypes.c_uint64
+    u32 = ctypes.c_uint32
+    u16 = ctypes.c_uint16
+    i32 = ctypes.c_int
+    sig = {
+        "wg_l4csum_uniform": (i32, [u8p, u64, u32, u16, u32, vp, vp]),
+        "wg_l4csum_desc": (i32, [u8p, vp, u64, vp, vp]),
+        "wg_checksum_desc": (i32, [u8p, vp, u64, vp, vp]),
+        "wg_gso_split": (i32, [u8p, vp, u64, u8p, vp, vp]),
+        "wg_l4csum_uniform_host": (i32, [u8p, u64, u32, u16, u32, vp]),
+        "wg_synth_fill": (i32, [u8p, u64, u64, u64, vp]),
+        "wg_synth_headers": (i32, [u8p, vp, u64, u64, u64, vp]),
+        "wg_synth_desc_stride": (i32, [vp, u64, u64, u32, i32, u64, u64, vp]),
+        "wg_store_l4csum": (i32, [u8p, vp, u64, vp, vp]),
+        "wg_abi_version": (i32, []),
+        "wg_strerror": (ctypes.c_char_p, [i32]),
+        "wg_device_count": (i32, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.wg_abi_version() != ABI_VERSION:
+        raise ImportError(f"ABI mismatch: library {lib.wg_abi_version()} != {ABI_VERSION}")
+    return lib
+
+
+lib = _load()
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != WG_OK:
+        raise WireGliderError(f"{what}: {lib.wg_strerror(rc).decode()} ({rc})")
+
+
+# ---------------------------------------------------------------------------
+# torch plumbing
+# ---------------------------------------------------------------------------
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _stream_ptr(stream) -> int | None:
+    torch = _torch()
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream
+
+
+def _require_cuda(t, name: str):
+    if not t.is_cuda:
+        raise WireGliderError(f"{name} must be a device tensor (wireglider_amd has no CPU path)")
+    if not t.is_contiguous():
+        raise WireGliderError(f"{name} must be contiguous")
+
+
+def nr_segments(total_len: int, segment_size: int) -> int:
+    """PacketBatch::nr_segments (include/worker/offload.hpp:26-28)."""
+    return (total_len + segment_size - 1) // segment_size
+
+
+def calc_l4_checksum_batch(batch, segment_size: int, isv6: bool, istcp: bool, csum_start: int,
+                           out=None, stream=None):
+    """calc_l4_checksum (checksum.cpp:8-36) for every segment of a PacketBatch.
+
+    batch: 1-D uint8 device tensor = PacketBatch.data; segment i is
+    batch[i*S : min((i+1)*S, len)].  Returns a uint16 device tensor.
+    """
+    torch = _torch()
+    _require_cuda(batch, "batch")
+    n = nr_segments(batch.numel(), segment_size)
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint16, device=batch.device)
+    flags = (WG_PKT_V6 if isv6 else 0) | (WG_PKT_TCP if istcp else 0)
+    rc = lib.wg_l4csum_uniform(batch.data_ptr(), batch.numel(), segment_size, csum_start, flags,
+                               out.data_ptr(), _stream_ptr(stream))
+    _check(rc, "wg_l4csum_uniform")
+    return out
+
+
+def calc_l4_checksum_desc(base, desc, out=None, stream=None):
+    """calc_l4_checksum per descriptor.  desc: (n, 16) uint8 or (n, 2) int64
+    device tensor in wg_pkt_desc layout."""
+    torch = _torch()
+    _require_cuda(base, "base")
+    _require_cuda(desc, "desc")
+    n = desc.numel() * desc.element_size() // PKT_DESC_BYTES
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint16, device=base.device)
+    rc = lib.wg_l4csum_desc(base.data_ptr(), desc.data_ptr(), n, out.data_ptr(), _stream_ptr(stream))
+    _check(rc, "wg_l4csum_desc")
+    return out
+
+
+def checksum_desc(base, desc, out=None, stream=None):
+    """checksum(span, 0) (include/netio/checksum.hpp:146-149) per descriptor."""
+    torch = _torch()
+    _require_cuda(base, "base")
+    _require_cuda(desc, "desc")
+    n = desc.numel() * desc.element_size() // PKT_DESC_BYTES
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint16, device=base.device)
+    rc = lib.wg_checksum_desc(base.data_ptr(), desc.data_ptr(), n, out.data_ptr(), _stream_ptr(stream))
+    _check(rc, "wg_checksum_desc")
+    return out
+
+
+def gso_split(inbuf, gso_desc, outbuf, results=None, stream=None):
+    """Batched do_tun_gso_split (worker/offload.cpp:46-216).  gso_desc:
+    device tensor of n x 40 B wg_gso_desc; results: n x 24 B wg_gso_result."""
+    torch = _torch()
+    for t, nm in ((inbuf, "inbuf"), (gso_desc, "gso_desc"), (outbuf, "outbuf")):
+        _require_cuda(t, nm)
+    n = gso_desc.numel() * gso_desc.element_size() // GSO_DESC_BYTES
+    if results is None:
+        results = torch.zeros(n * GSO_RESULT_BYTES, dtype=torch.uint8, device=inbuf.device)
+    rc = lib.wg_gso_split(inbuf.data_ptr(), gso_desc.data_ptr(), n, outbuf.data_ptr(),
+                          results.data_ptr(), _stream_ptr(stream))
+    _check(rc, "wg_gso_split")
+    return results
+
+
+def calc_l4_checksum_host(buf: bytes | bytearray | memoryview, segment_size: int, isv6: bool,
+                          istcp: bool, csum_start: int):
+    """Host-memory path: host buffer in, host uint16 array out (H2D, kernel, D2H)."""
+    import numpy as np
+
+    mv = np.frombuffer(buf, dtype=np.uint8)
+    n = nr_segments(mv.size, segment_size)
+    out = np.empty(n, dtype=np.uint16)
+    flags = (WG_PKT_V6 if isv6 else 0) | (WG_PKT_TCP if istcp else 0)
+    rc = lib.wg_l4csum_uniform_host(mv.ctypes.data, mv.size, segment_size, csum_start, flags,
+                                    out.ctypes.data)
+    _check(rc, "wg_l4csum_uniform_host")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# synthetic batches (bench / tests)
+# ---------------------------------------------------------------------------
+
+
+def synth_fill(buf, seed: int, counter_base: int = 0, stream=None) -> None:
+    _require_cuda(buf, "buf")
+    _check(lib.wg_synth_fill(buf.data_ptr(), buf.numel() * buf.element_size(), seed, counter_base,
+                             _stream_ptr(stream)), "wg_synth_fill")
+
+
+def synth_headers(base, desc, seed: int, index_base: int = 0, stream=None) -> None:
+    n = desc.numel() * desc.element_size() // PKT_DESC_BYTES
+    _check(lib.wg_synth_headers(base.data_ptr(), desc.data_ptr(), n, seed, index_base,
+                                _stream_ptr(stream)), "wg_synth_headers")
+
+
+def synth_desc_stride(n: int, stride: int, length: int, mode: int, seed: int, index_base: int = 0,
+                      device=None, stream=None):
+    torch = _torch()
+    desc = torch.empty((n, 2), dtype=torch.int64, device=device or "cuda")
+    _check(lib.wg_synth_desc_stride(desc.data_ptr(), n, stride, length, mode, seed, index_base,
+                                    _stream_ptr(stream)), "wg_synth_desc_stride")
+    return desc
+
+
+def store_l4csum(base, desc, csum, stream=None) -> None:
+    n = desc.numel() * desc.element_size() // PKT_DESC_BYTES
+    _check(lib.wg_store_l4csum(base.data_ptr(), desc.data_ptr(), n, csum.data_ptr(),
+                               _stream_ptr(stream)), "wg_store_l4csum")
+
+
+def device_count() -> int:
+    return int(lib.wg_device_count())

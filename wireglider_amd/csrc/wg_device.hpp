@@ -1,0 +1,116 @@
+// wg_device.hpp — gfx950 device primitives for the one's-complement engine.
+//
+// Arithmetic model: every byte b at absolute
+// address x contributes b << (8 * (x & 1)) to a plain integer sum; that sum
+// is congruent mod 0xFFFF to the RFC 1071 sum paired at even addresses, and
+// is zero only if every byte is zero.  A region whose word pairing starts at
+// an odd address (the reference pairs relative to the span start,
+// include/netio/checksum.hpp:30-100) is corrected by one byte swap of its
+// folded value (x * 256 mod 0xFFFF == bswap16(x)).  Folding is end-around and
+// zero-preserving, so the reference's 0x0000-vs-0xFFFF split falls out
+// exactly: the final result is 0xFFFF only when the whole sum is zero.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wg {
+
+// 64 -> 16 bit end-around fold; result in [0, 0xFFFF], 0 iff x == 0.
+__device__ __forceinline__ uint32_t fold16(uint64_t x) {
+    uint64_t t = (x & 0xffffffffull) + (x >> 32);  // <= 2^33
+    uint32_t u = (uint32_t)(t & 0xffffu) + (uint32_t)((t >> 16) & 0xffffu) + (uint32_t)(t >> 32);
+    u = (u & 0xffffu) + (u >> 16);
+    u = (u & 0xffffu) + (u >> 16);
+    return u;
+}
+
+__device__ __forceinline__ uint32_t fold16_32(uint32_t u) {
+    u = (u & 0xffffu) + (u >> 16);
+    u = (u & 0xffffu) + (u >> 16);
+    return u;
+}
+
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) {
+    return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu);
+}
+
+// Native 4 x u32 vector (trivially copyable in every address space).
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint64_t sum4(v4u v) {
+    return (uint64_t)v.x + (uint64_t)v.y + (uint64_t)v.z + (uint64_t)v.w;
+}
+
+// DPP controls (GFX9 encoding).
+enum : int {
+    kDppQuadPerm1032 = 0xB1,  // quad_perm:[1,0,3,2]
+    kDppQuadPerm2301 = 0x4E,  // quad_perm:[2,3,0,1]
+    kDppRowHalfMirror = 0x141,
+    kDppRowMirror = 0x140,
+};
+
+// Sum of v over all 64 lanes, returned wave-uniform.  EXEC must be full.
+// In-row butterfly by DPP (4 VALU), then 4 readlanes across the rows.
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppQuadPerm1032, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppQuadPerm2301, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppRowHalfMirror, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppRowMirror, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+           (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+
+// Sum over aligned groups of G lanes (G = 4, 8 or 16); every lane of a group
+// receives its group's total.  EXEC must be full.
+template <int G>
+__device__ __forceinline__ uint32_t group_sum_u32(uint32_t v) {
+    static_assert(G == 4 || G == 8 || G == 16, "group size");
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppQuadPerm1032, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppQuadPerm2301, 0xF, 0xF, false);
+    if (G >= 8)
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppRowHalfMirror, 0xF, 0xF, false);
+    if (G >= 16)
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppRowMirror, 0xF, 0xF, false);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// Wave index within the grid, provably uniform to the compiler.
+__device__ __forceinline__ uint32_t wave_in_block() {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+}
+
+// XCD-aware block remap (guide T1): blocks b and b+8 share an XCD under the
+// observed round-robin dispatch, so give each XCD a contiguous run of virtual
+// block ids.  Speed only; any placement is correct.  Needs nblocks % 8 == 0
+// for the bijection, otherwise identity.
+__device__ __forceinline__ uint32_t xcd_swizzle(uint32_t b, uint32_t nblocks) {
+    if (nblocks & 7u)
+        return b;
+    return (b & 7u) * (nblocks >> 3) + (b >> 3);
+}
+
+// Loads through the GLOBAL address space (global_load_*, not flat_*: flat
+// ops count against both vmcnt and lgkmcnt and return out of order).
+typedef __attribute__((address_space(1))) const v4u g_v4u;
+typedef __attribute__((address_space(1))) const uint8_t g_u8;
+
+// 16-byte load of an aligned chunk at absolute address `addr`.
+__device__ __forceinline__ v4u ld16(uintptr_t addr) {
+    return *reinterpret_cast<g_v4u *>(addr);
+}
+
+__device__ __forceinline__ uint32_t ld8(uintptr_t addr) {
+    return *reinterpret_cast<g_u8 *>(addr);
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+}  // namespace wg

@@ -1,0 +1,18 @@
+// wg_internal.hpp — host-side internals shared by the engine's translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wg {
+
+// Launch geometry, read once from the environment (WG_L4_BLOCKS, ...); the
+// defaults are the measured best on MI355X.
+struct Tune {
+    uint64_t l4_blocks;   // grid cap for the wave-per-packet checksum kernels
+    uint64_t gso_blocks;  // grid cap for the GSO split kernel
+};
+
+const Tune &tune();
+
+}  // namespace wg
