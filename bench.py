@@ -43,11 +43,14 @@ def parse():
     ap.add_argument("--workload", default="config2", choices=["config2", "config4", "config5"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall seconds of the CPU baseline sample")
+    ap.add_argument("--settle-seconds", type=float, default=0.3,
+                    help="untimed back-to-back launches before the warmup (clock/memory settle)")
     return ap.parse_args()
 
 
 def build_workload(wga, torch, name: str, rank: int, world: int, dev):
-    """Returns (launch_fn, n_packets, payload_bytes_per_step, alg_bytes_per_launch, cfg, host_sample_fn)."""
+    """Returns (launch_fn, n_packets, payload_bytes_per_step, alg_bytes_per_launch, cfg,
+    host_sample_fn, scaling, batch_buffer)."""
     if name == "config2":
         n = 1 << 20
         seed = 0x5EED0002
@@ -71,7 +74,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev):
         def sample(npk):
             return buf[: npk * SEG].cpu().numpy(), out[:npk].cpu().numpy(), ("uniform", SEG, 20, 0)
 
-        return launch, n, payload, alg, cfg, sample, "weak"
+        return launch, n, payload, alg, cfg, sample, "weak", buf
     if name == "config5":
         total = 1 << 24
         lo = total * rank // world
@@ -95,7 +98,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev):
         def sample(npk):
             return buf[: npk * SEG].cpu().numpy(), out[:npk].cpu().numpy(), ("desc", desc[:npk].cpu().numpy())
 
-        return launch, n, n * SEG, alg, cfg, sample, "strong"
+        return launch, n, n * SEG, alg, cfg, sample, "strong", buf
     # config4 bimodal
     import numpy as np
 
@@ -125,7 +128,42 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev):
         end = int(offs[npk - 1] + lens[npk - 1])
         return buf[:end].cpu().numpy(), out[:npk].cpu().numpy(), ("desc", raw[:npk])
 
-    return launch, n, total, alg, cfg, sample, "weak"
+    return launch, n, total, alg, cfg, sample, "weak", buf
+
+
+def settle(torch, fn, seconds: float) -> int:
+    """Run `fn` back to back until `seconds` of wall time have passed, so the
+    timed region starts at the sustained clock/memory state rather than the
+    idle ramp (MI355X: the first ~10 launches run up to 30% slower)."""
+    import time as _t
+
+    t0 = _t.perf_counter()
+    k = 0
+    while _t.perf_counter() - t0 < seconds:
+        for _ in range(20):
+            fn()
+        k += 20
+        torch.cuda.synchronize()
+    return k
+
+
+def measured_read_peak(torch, wga, buf, iters: int = 30) -> float:
+    """Read-roofline probe over the batch buffer itself: the same bytes,
+    read by the same access structure with no checksum work (GB/s)."""
+    acc = torch.zeros(1, dtype=torch.int64, device=buf.device)
+    n = buf.numel() // 16 * 16
+    view = buf[:n]
+    best = 0.0
+    for kib in (2, 4, 8):
+        settle(torch, lambda: wga.probe_read(view, acc, kib), 0.05)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            wga.probe_read(view, acc, kib)
+        e1.record()
+        torch.cuda.synchronize()
+        best = max(best, n * iters / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+    return best
 
 
 def cpu_baseline(sample_fn, seconds: float):
@@ -135,7 +173,9 @@ def cpu_baseline(sample_fn, seconds: float):
     import numpy as np
     import oracle  # test infrastructure: the CPU baseline leg only
 
-    npk = 1 << 16
+    # 2^19 packets (~786 MB for 1500 B) so the sample does not sit in the
+    # host's last-level cache (EPYC 9575F: 256 MB L3) between repetitions.
+    npk = 1 << 19
     host, gpu_out, kind = sample_fn(npk)
     threads = oracle.default_threads()
     if kind[0] == "uniform":
@@ -208,8 +248,10 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    launch, n, payload, alg, cfg, sample, scaling = build_workload(wga, torch, args.workload, rank, world, dev)
+    launch, n, payload, alg, cfg, sample, scaling, batch_buf = build_workload(wga, torch, args.workload, rank, world,
+                                                                            dev)
     torch.cuda.synchronize()
+    settled = settle(torch, launch, args.settle_seconds)
 
     def barrier():
         if world > 1:
@@ -249,6 +291,7 @@ def main():
     value = total_payload * args.steps / wall / 2**30
     achieved = alg / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args.workload)
+    read_peak = measured_read_peak(torch, wga, batch_buf) if rank == 0 else None
     line = {
         "metric": "device-resident GiB/s, L4 checksum over packet batch; 1/2/4/8 MI355X",
         "value": round(value, 3),
@@ -256,6 +299,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "settle_launches": settled,
         "ms_per_step": round(ms_per_step, 5),
         "higher_is_better": True,
         "scaling": scaling,
@@ -270,8 +314,11 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "wg::l4csum_wave_kernel",
+            "kernel": "wg::l4csum_kernel",
             "alg_bytes_per_launch": alg,
+            "traffic_source": "profiles/pmc_%s.json (rocprofv3 FETCH_SIZEx2 + WRITE_SIZE, per launch)" % args.workload,
+            "measured_read_peak": round(read_peak, 1) if read_peak else None,
+            "frac_of_measured_read_peak": round(achieved / read_peak, 4) if read_peak else None,
             "kernel_ms_avg": round(kern_ms, 5),
             "kernel_ms_avg_max_over_ranks": round(kern_ms_max, 5),
         },

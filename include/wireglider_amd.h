@@ -197,6 +197,20 @@ const char *wg_strerror(int code);
 /* HIP device count (0 when no GPU); never throws. */
 int wg_device_count(void);
 
+/* Launch-geometry knobs (also read once from the environment as WG_L4_BLOCKS,
+ * WG_L4_PPW, WG_L4_NT, WG_GSO_BLOCKS).  Keys: "l4_blocks" (grid cap),
+ * "l4_ppw" (packets per wave iteration: 1, 2, 4, 8), "l4_nt" (0/1
+ * non-temporal loads), "gso_blocks".  Results never depend on them.  Not
+ * synchronised with concurrent launches from other threads. */
+int wg_tune_set(const char *key, uint64_t value);
+
+/* Read-roofline probe (benchmark support): streams dev[0, nbytes) with
+ * non-temporal 16-B loads, one-shot waves of `kib_per_wave` (1/2/4/8)
+ * contiguous KiB each, and adds a folded sum into *dev_out.  Its bandwidth
+ * is the measured read ceiling the checksum kernels are compared against. */
+int wg_probe_read(const uint8_t *dev, uint64_t nbytes, uint64_t *dev_out, uint32_t kib_per_wave,
+                  uint32_t reserved, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

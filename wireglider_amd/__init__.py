@@ -43,6 +43,8 @@ EXPORTED_SYMBOLS = (
     "wg_abi_version",
     "wg_strerror",
     "wg_device_count",
+    "wg_tune_set",
+    "wg_probe_read",
 )
 
 # struct layouts (include/wireglider_amd.h)
@@ -81,6 +83,8 @@ def _load() -> ctypes.CDLL:
         "wg_abi_version": (i32, []),
         "wg_strerror": (ctypes.c_char_p, [i32]),
         "wg_device_count": (i32, []),
+        "wg_tune_set": (i32, [ctypes.c_char_p, u64]),
+        "wg_probe_read": (i32, [u8p, u64, vp, u32, u32, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -235,6 +239,17 @@ def store_l4csum(base, desc, csum, stream=None) -> None:
     n = desc.numel() * desc.element_size() // PKT_DESC_BYTES
     _check(lib.wg_store_l4csum(base.data_ptr(), desc.data_ptr(), n, csum.data_ptr(),
                                _stream_ptr(stream)), "wg_store_l4csum")
+
+
+def tune_set(key: str, value: int) -> None:
+    """Launch-geometry knob (results never depend on it)."""
+    _check(lib.wg_tune_set(key.encode(), int(value)), f"wg_tune_set({key})")
+
+
+def probe_read(buf, out, kib_per_wave: int = 4, stream=None) -> None:
+    """Launch the read-roofline probe over a device buffer."""
+    _check(lib.wg_probe_read(buf.data_ptr(), buf.numel() * buf.element_size(), out.data_ptr(), kib_per_wave, 0,
+                             _stream_ptr(stream)), "wg_probe_read")
 
 
 def device_count() -> int:

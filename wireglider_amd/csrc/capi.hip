@@ -4,7 +4,9 @@
 
 #include <cstdlib>
 #include <mutex>
+#include <string>
 
+#include "wg_device.hpp"
 #include "wg_internal.hpp"
 #include "wireglider_amd.h"
 
@@ -19,16 +21,23 @@ static uint64_t env_u64(const char *name, uint64_t dflt) {
     return (end && *end == 0 && x > 0) ? (uint64_t)x : dflt;
 }
 
-const Tune &tune() {
+Tune &tune_mut() {
     static Tune t = [] {
         Tune x;
-        // 256 CUs x 8 four-wave blocks = 32 waves/CU resident at <= 64 VGPRs.
-        x.l4_blocks = env_u64("WG_L4_BLOCKS", 2048);
+        // Measured on MI355X (tools/tune_l4.py, profiles/): one iteration per
+        // wave (grid = n / (4 * ppw), i.e. no grid-stride loop), 4 packets per
+        // wave, non-temporal loads: 7.26 TB/s vs 5.6 TB/s for a 2048-block
+        // grid-stride launch with default-policy loads.
+        x.l4_blocks = env_u64("WG_L4_BLOCKS", 1u << 20);
+        x.l4_ppw = (uint32_t)env_u64("WG_L4_PPW", 4);
+        x.l4_nt = (uint32_t)env_u64("WG_L4_NT", 1);
         x.gso_blocks = env_u64("WG_GSO_BLOCKS", 2048);
         return x;
     }();
     return t;
 }
+
+const Tune &tune() { return tune_mut(); }
 
 // Per-host-thread device workspace for the host-memory path.  Grows to the
 // largest batch seen; freed at thread exit.
@@ -84,9 +93,56 @@ static int host_ctx_reserve(size_t bytes, size_t outs) {
     return WG_OK;
 }
 
+// Read-roofline probe: the checksum kernels' access structure with nothing
+// else — one-shot waves (no grid-stride loop), each streaming U contiguous
+// KiB with non-temporal global_load_dwordx4 (all U issued before the first
+// use), folded into one word per wave.  Its bandwidth is the measured read
+// ceiling the checksum kernels are compared against.
+template <int U>
+__global__ __launch_bounds__(256) void probe_read_kernel(const uint8_t *dev, uint64_t nchunks, uint64_t *out) {
+    const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
+    const uint64_t c0 = wave * (uint64_t)U * 64u;
+    const uintptr_t base = reinterpret_cast<uintptr_t>(dev);
+    const uint32_t lane = lane_id();
+    if (c0 >= nchunks)
+        return;
+    const uint64_t last = nchunks - 1;
+    v4u v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        uint64_t c = c0 + (uint64_t)u * 64u + lane;
+        v[u] = ld16_nt(base + 16u * (c < last ? c : last));
+    }
+    Acc acc;
+#pragma unroll
+    for (int u = 0; u < U; u++) acc.add4(v[u]);
+    const uint32_t s = wave_sum_u32(fold16(acc.value()));
+    // Keep the loads live without a contended atomic: a data-dependent store
+    // that (for any real data) never fires.
+    if (lane == 0 && s == 0xFFFFFFFFu) *out = s;
+}
+
 }  // namespace wg
 
 using namespace wg;
+
+extern "C" int wg_probe_read(const uint8_t *dev, uint64_t nbytes, uint64_t *dev_out, uint32_t kib_per_wave,
+                             uint32_t unused, void *stream) {
+    (void)unused;
+    if (!dev || !dev_out || (reinterpret_cast<uintptr_t>(dev) & 15) || nbytes < 16) return WG_ERR_INVALID;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint64_t nch = nbytes >> 4;
+    const uint32_t U = kib_per_wave == 2 || kib_per_wave == 4 || kib_per_wave == 8 ? kib_per_wave : 1;
+    uint64_t blocks = (nch + 256ull * U - 1) / (256ull * U);
+    if (blocks >= 8) blocks = (blocks + 7) & ~7ull;
+    switch (U) {
+    case 2: hipLaunchKernelGGL(probe_read_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, st, dev, nch, dev_out); break;
+    case 4: hipLaunchKernelGGL(probe_read_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, st, dev, nch, dev_out); break;
+    case 8: hipLaunchKernelGGL(probe_read_kernel<8>, dim3((unsigned)blocks), dim3(256), 0, st, dev, nch, dev_out); break;
+    default: hipLaunchKernelGGL(probe_read_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, st, dev, nch, dev_out); break;
+    }
+    return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+}
 
 extern "C" int wg_abi_version(void) { return WG_ABI_VERSION; }
 
@@ -99,6 +155,24 @@ extern "C" const char *wg_strerror(int code) {
     case WG_ERR_RUNTIME: return "HIP runtime failure";
     default: return "unknown error";
     }
+}
+
+extern "C" int wg_tune_set(const char *key, uint64_t value) {
+    if (!key)
+        return WG_ERR_INVALID;
+    Tune &t = tune_mut();
+    const std::string k(key);
+    if (k == "l4_blocks" && value >= 1 && value <= (1u << 20))
+        t.l4_blocks = value;
+    else if (k == "l4_ppw" && (value == 1 || value == 2 || value == 4 || value == 8))
+        t.l4_ppw = (uint32_t)value;
+    else if (k == "l4_nt" && value <= 1)
+        t.l4_nt = (uint32_t)value;
+    else if (k == "gso_blocks" && value >= 1 && value <= (1u << 20))
+        t.gso_blocks = value;
+    else
+        return WG_ERR_INVALID;
+    return WG_OK;
 }
 
 extern "C" int wg_device_count(void) {

@@ -2,13 +2,19 @@
 //
 // Replaces, at batch granularity, wireglider::calc_l4_checksum
 // (reference checksum.cpp:8-36) and wireglider::checksum
-// (include/netio/checksum.hpp:146-149).  One wavefront per packet: the
-// 16-byte-aligned interior of the summed region streams through
-// global_load_dwordx4 (64 lanes x 16 B = 1 KiB per instruction, coalesced),
-// the <=15-byte unaligned head and tail plus the pseudo-header addresses come
-// in through ONE byte-gather instruction (one lane per byte), and the
-// wave's partial sums meet in a DPP butterfly.  No LDS: every byte is used
-// exactly once, so staging it would only add LDS traffic.
+// (include/netio/checksum.hpp:146-149).
+//
+// Structure: one wavefront per packet, P packets per wave iteration.  For
+// each of its P packets a lane first ISSUES its loads — the 16-byte-aligned
+// interior of the summed region through global_load_dwordx4 (64 lanes x 16 B
+// = 1 KiB per instruction, coalesced; the first 2 KiB of every packet in this
+// phase) and one global_load_ubyte that gathers the <=15-byte unaligned head
+// and tail plus the pseudo-header address bytes (one lane per byte) — and
+// only then FINISHES the packets one by one (rest of a long packet, fold,
+// DPP butterfly, pseudo-header constants).  So P x ~1.5 KiB per wave are in
+// flight before the first wait, which is what an HBM-bound stream needs.
+// No LDS: every byte is used exactly once; staging it would only add LDS
+// traffic.
 #include <hip/hip_runtime.h>
 
 #include "wg_device.hpp"
@@ -16,81 +22,6 @@
 #include "wireglider_amd.h"
 
 namespace wg {
-
-// This lane's share of one packet's one's-complement sum, in TRUE pairing
-// (relative to the packet's csum_start / address start).  kL4 adds the
-// pseudo-header source/destination address bytes; the constant
-// proto/length words are added by the caller once per packet.
-template <bool kL4>
-__device__ __forceinline__ uint32_t packet_partial(const uint8_t *pkt, uint32_t len, uint32_t cs,
-                                                   bool v6, uint32_t lane) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(pkt);
-    const uintptr_t r1 = a + len;
-    const uintptr_t r0 = cs < len ? a + cs : r1;  // summed region [r0, r1)
-    const uintptr_t c0 = (r0 + 15) & ~(uintptr_t)15;
-    const uintptr_t c1 = r1 & ~(uintptr_t)15;
-
-    // Interior: whole aligned 16-B chunks, 4 in flight per lane per round.
-    uint64_t acc = 0;
-    if (c1 > c0) {
-        const uint32_t nint = (uint32_t)((c1 - c0) >> 4);
-        const uintptr_t q = c0;
-        uint32_t k = lane;
-        for (; k + 192 < nint; k += 256) {
-            v4u v0 = ld16(q + 16ull * k);
-            v4u v1 = ld16(q + 16ull * (k + 64));
-            v4u v2 = ld16(q + 16ull * (k + 128));
-            v4u v3 = ld16(q + 16ull * (k + 192));
-            acc += sum4(v0) + sum4(v1) + sum4(v2) + sum4(v3);
-        }
-        if (k + 64 < nint) {
-            v4u v0 = ld16(q + 16ull * k);
-            v4u v1 = ld16(q + 16ull * (k + 64));
-            acc += sum4(v0) + sum4(v1);
-            k += 128;
-        }
-        if (k < nint)
-            acc += sum4(ld16(q + 16ull * k));
-    }
-
-    // One byte per lane: lanes 0-31 pseudo-header addresses (true pairing
-    // relative to the address start, which is even in the packet), lanes
-    // 32-47 the unaligned head [r0, min(c0, r1)), lanes 48-63 the tail
-    // [max(c1, c0), r1) (absolute-address pairing, like the interior).
-    uintptr_t bp = 0;
-    bool true_pair = false;
-    if (lane < 32) {
-        if (kL4) {
-            const uint32_t ao = v6 ? 8u : 12u, al = v6 ? 32u : 8u;
-            if (lane < al && ao + lane < len) {
-                bp = a + ao + lane;
-                true_pair = true;
-            }
-        }
-    } else if (lane < 48) {
-        const uintptr_t he = c0 < r1 ? c0 : r1;
-        const uintptr_t x = r0 + (lane - 32);
-        if (x < he)
-            bp = x;
-    } else {
-        const uintptr_t ts = c1 > c0 ? c1 : c0;
-        const uintptr_t x = ts + (lane - 48);
-        if (x < r1)
-            bp = x;
-    }
-    uint32_t bv = 0;
-    if (bp) {
-        const uint32_t par = true_pair ? (lane & 1u) : (uint32_t)(bp & 1u);
-        bv = ld8(bp) << (8u * par);
-    }
-    if (!true_pair)
-        acc += bv;
-
-    uint32_t f = fold16(acc);
-    if (r0 & 1u)  // region pairs from an odd address: swap its folded sum
-        f = bswap16(f);
-    return f + (true_pair ? bv : 0u);
-}
 
 struct L4Params {
     const uint8_t *base;
@@ -105,61 +36,192 @@ struct L4Params {
 
 enum Kind : int { kUniformL4 = 0, kDescL4 = 1, kDescPlain = 2 };
 
+struct Geom {
+    uintptr_t a;  // packet start
+    uint32_t len, cs, fl;
+};
+
 template <int kKind>
-__global__ __launch_bounds__(256) void l4csum_wave_kernel(L4Params p) {
+__device__ __forceinline__ Geom load_geom(const L4Params &p, uint64_t i) {
+    Geom g;
+    if (i >= p.n) {  // padding slot of the last iteration: empty packet
+        g.a = reinterpret_cast<uintptr_t>(p.base);
+        g.len = 0;
+        g.cs = 0;
+        g.fl = 0;
+        return g;
+    }
+    if constexpr (kKind == kUniformL4) {
+        // PacketBatch segment i (include/util/packets.hpp:23-36)
+        const uint64_t off = i * (uint64_t)p.seg;
+        const uint64_t rem = p.total_len - off;
+        g.a = reinterpret_cast<uintptr_t>(p.base) + off;
+        g.len = rem < p.seg ? (uint32_t)rem : p.seg;
+        g.cs = p.cs;
+        g.fl = p.flags;
+    } else {
+        const wg_pkt_desc d = p.desc[i];
+        g.a = reinterpret_cast<uintptr_t>(p.base) + d.offset;
+        g.len = d.len;
+        g.cs = kKind == kDescPlain ? 0u : d.csum_start;
+        g.fl = d.flags;
+    }
+    return g;
+}
+
+// Always-valid, always-zero 16 B: the load target of lanes (and packets)
+// with nothing to read, so the issue phase needs no branches — a branch
+// around a load makes the compiler wait for it inside the branch.
+__device__ v4u g_zero16;
+
+// Per-packet state between the issue and finish phases.
+struct Front {
+    v4u v0, v1;      // interior chunks lane, lane + 64 (masked to zero)
+    uint32_t bv;     // gathered byte, already shifted to its pairing
+    bool bt;         // bv is in TRUE pairing (pseudo-header address byte)
+    uintptr_t r0;    // start of the summed region
+    uintptr_t c0;    // first aligned interior chunk
+    uint32_t nint;   // interior chunk count
+};
+
+// Issue phase.  Summed region [r0, r1) = [a + cs, a + len) (empty when
+// cs >= len).  Interior = whole aligned chunks [c0, c1); the unaligned head
+// [r0, min(c0, r1)) and tail [max(c1, c0), r1) are <= 15 bytes each.
+// Branch-free: out-of-range lanes re-read a valid chunk and are masked.
+template <bool kL4, bool kNT>
+__device__ __forceinline__ void issue(const Geom &g, uint32_t lane, Front &f) {
+    const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
+    const uintptr_t r1 = g.a + g.len;
+    const uintptr_t r0 = g.cs < g.len ? g.a + g.cs : r1;
+    const uintptr_t c0 = (r0 + 15) & ~(uintptr_t)15;
+    const uintptr_t c1 = r1 & ~(uintptr_t)15;
+    const uint32_t nint = c1 > c0 ? (uint32_t)((c1 - c0) >> 4) : 0u;
+    f.r0 = r0;
+    f.c0 = c0;
+    f.nint = nint;
+    // wave-uniform base and clamp, per-lane 32-bit offset
+    const uintptr_t base = nint ? c0 : zero;
+    const uint32_t last = nint ? nint - 1 : 0u;
+    const uint32_t k0 = lane < last ? lane : last;
+    const uint32_t k1 = lane + 64 < last ? lane + 64 : last;
+    const v4u t0 = ld16x<kNT>(base + 16u * k0);
+    const v4u t1 = ld16x<kNT>(base + 16u * k1);
+    const v4u z = v4u{0, 0, 0, 0};
+    f.v0 = lane < nint ? t0 : z;
+    f.v1 = lane + 64 < nint ? t1 : z;
+
+    // One byte per lane: lanes 0-31 pseudo-header addresses (pairing
+    // relative to the address start, an even packet offset: 12 for v4, 8 for
+    // v6 — checksum.cpp:14-28), lanes 32-47 the head, lanes 48-63 the tail
+    // (absolute-address pairing, like the interior).
+    const bool v6 = g.fl & WG_PKT_V6;
+    const uint32_t ao = v6 ? 8u : 12u, al = v6 ? 32u : 8u;
+    const bool bt = kL4 && lane < al && ao + lane < g.len;
+    const uintptr_t he = c0 < r1 ? c0 : r1;
+    const uintptr_t ts = c1 > c0 ? c1 : c0;
+    const uintptr_t xh = r0 + (lane - 32);
+    const uintptr_t xt = ts + (lane - 48);
+    const bool bh = lane >= 32 && lane < 48 && xh < he;
+    const bool btl = lane >= 48 && xt < r1;
+    const uintptr_t bp = bt ? g.a + ao + lane : (bh ? xh : (btl ? xt : zero));
+    const uint32_t par = bt ? (lane & 1u) : (uint32_t)(bp & 1u);
+    f.bv = ld8(bp) << (8u * par);
+    f.bt = bt;
+}
+
+// Finish phase: this lane's share of the packet's sum in TRUE pairing.
+template <bool kNT>
+__device__ __forceinline__ uint32_t finish(uint32_t lane, const Front &f) {
+    Acc acc;
+    acc.add4(f.v0);
+    acc.add4(f.v1);
+    if (f.nint > 128) {  // long packet (> ~2 KiB): stream the rest, 4 loads in flight
+        const uintptr_t q = f.c0;
+        uint32_t k = lane + 128;
+        for (; k + 192 < f.nint; k += 256) {
+            v4u a0 = ld16x<kNT>(q + 16ull * k);
+            v4u a1 = ld16x<kNT>(q + 16ull * (k + 64));
+            v4u a2 = ld16x<kNT>(q + 16ull * (k + 128));
+            v4u a3 = ld16x<kNT>(q + 16ull * (k + 192));
+            acc.add4(a0);
+            acc.add4(a1);
+            acc.add4(a2);
+            acc.add4(a3);
+        }
+        for (; k < f.nint; k += 64)
+            acc.add4(ld16x<kNT>(q + 16ull * k));
+    }
+    if (!f.bt)
+        acc.add(f.bv);
+    uint32_t s = fold16(acc.value());
+    if (f.r0 & 1u)  // region pairs from an odd address: swap its folded sum
+        s = bswap16(s);
+    return s + (f.bt ? f.bv : 0u);
+}
+
+template <int kKind, int P, bool kNT>
+__global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
+    constexpr bool kL4 = kKind != kDescPlain;
     const uint32_t lane = lane_id();
     const uint64_t wave0 = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
-    const uint64_t nw = (uint64_t)gridDim.x * 4u;
-    for (uint64_t i = wave0; i < p.n; i += nw) {
-        const uint8_t *pkt;
-        uint32_t len, cs, fl;
-        if (kKind == kUniformL4) {
-            const uint64_t off = i * (uint64_t)p.seg;
-            const uint64_t rem = p.total_len - off;
-            len = rem < p.seg ? (uint32_t)rem : p.seg;
-            pkt = p.base + off;
-            cs = p.cs;
-            fl = p.flags;
-        } else {
-            const wg_pkt_desc d = p.desc[i];
-            pkt = p.base + d.offset;
-            len = d.len;
-            cs = kKind == kDescPlain ? 0u : d.csum_start;
-            fl = d.flags;
+    const uint64_t step = (uint64_t)gridDim.x * 4u * P;
+    for (uint64_t i0 = wave0 * P; i0 < p.n; i0 += step) {
+        Geom g[P];
+        Front f[P];
+#pragma unroll
+        for (int j = 0; j < P; j++) {
+            g[j] = load_geom<kKind>(p, i0 + j);
+            issue<kL4, kNT>(g[j], lane, f[j]);
         }
-        const uint32_t part = packet_partial<kKind != kDescPlain>(pkt, len, cs, fl & WG_PKT_V6, lane);
-        uint32_t s = wave_sum_u32(part);
-        if (lane == 0) {
-            if (kKind != kDescPlain) {
+        uint32_t res = 0;
+#pragma unroll
+        for (int j = 0; j < P; j++) {
+            uint32_t s = wave_sum_u32(finish<kNT>(lane, f[j]));
+            if (kL4) {
                 // {0x00, proto, l4len>>8, l4len&0xff} as LE words
-                // (include/netio/checksum.hpp:111-114, checksum.cpp:23,33).
-                const uint32_t proto = (fl & WG_PKT_TCP) ? 6u : 17u;
-                s += (proto << 8) + bswap16((len - cs) & 0xffffu);
+                // (include/netio/checksum.hpp:111-114); l4len is uint16_t
+                // (checksum.cpp:23,33).
+                const uint32_t proto = (g[j].fl & WG_PKT_TCP) ? 6u : 17u;
+                s += (proto << 8) + bswap16((g[j].len - g[j].cs) & 0xffffu);
             }
-            p.out[i] = (uint16_t)(~fold16_32(s) & 0xffffu);
+            const uint32_t r = ~fold16_32(s) & 0xffffu;
+            if (lane == (uint32_t)j)
+                res = r;
         }
+        if (lane < (uint32_t)P && i0 + lane < p.n)
+            p.out[i0 + lane] = (uint16_t)res;
+    }
+}
+
+template <int kKind, int P, bool kNT>
+static void launch_variant(const L4Params &p, uint64_t blocks, hipStream_t st) {
+    hipLaunchKernelGGL((l4csum_kernel<kKind, P, kNT>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+}
+
+template <int kKind>
+static void launch_kind(const L4Params &p, uint64_t blocks, uint32_t P, bool nt, hipStream_t st) {
+    switch (P) {
+    case 1: nt ? launch_variant<kKind, 1, true>(p, blocks, st) : launch_variant<kKind, 1, false>(p, blocks, st); break;
+    case 2: nt ? launch_variant<kKind, 2, true>(p, blocks, st) : launch_variant<kKind, 2, false>(p, blocks, st); break;
+    case 8: nt ? launch_variant<kKind, 8, true>(p, blocks, st) : launch_variant<kKind, 8, false>(p, blocks, st); break;
+    default: nt ? launch_variant<kKind, 4, true>(p, blocks, st) : launch_variant<kKind, 4, false>(p, blocks, st); break;
     }
 }
 
 static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
     if (p.n == 0)
         return WG_OK;
-    const uint64_t want = (p.n + 3) / 4;
-    uint64_t cap = tune().l4_blocks;
-    uint64_t blocks = want < cap ? want : cap;
+    const Tune &t = tune();
+    const uint32_t P = t.l4_ppw;
+    const uint64_t want = (p.n + 4ull * P - 1) / (4ull * P);
+    uint64_t blocks = want < t.l4_blocks ? want : t.l4_blocks;
     if (blocks >= 8)
         blocks &= ~7ull;  // keep the XCD swizzle bijective
-    dim3 grid((unsigned)blocks), block(256);
+    const bool nt = t.l4_nt != 0;
     switch (kind) {
-    case kUniformL4:
-        hipLaunchKernelGGL(l4csum_wave_kernel<kUniformL4>, grid, block, 0, st, p);
-        break;
-    case kDescL4:
-        hipLaunchKernelGGL(l4csum_wave_kernel<kDescL4>, grid, block, 0, st, p);
-        break;
-    default:
-        hipLaunchKernelGGL(l4csum_wave_kernel<kDescPlain>, grid, block, 0, st, p);
-        break;
+    case kUniformL4: launch_kind<kUniformL4>(p, blocks, P, nt, st); break;
+    case kDescL4: launch_kind<kDescL4>(p, blocks, P, nt, st); break;
+    default: launch_kind<kDescPlain>(p, blocks, P, nt, st); break;
     }
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }
@@ -169,8 +231,7 @@ static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
 using namespace wg;
 
 extern "C" int wg_l4csum_uniform(const uint8_t *dev_base, uint64_t total_len, uint32_t segment_size,
-                                 uint16_t csum_start, uint32_t flags, uint16_t *dev_out,
-                                 void *stream) {
+                                 uint16_t csum_start, uint32_t flags, uint16_t *dev_out, void *stream) {
     if (!segment_size || (total_len && (!dev_base || !dev_out)))
         return WG_ERR_INVALID;
     L4Params p{};

@@ -42,6 +42,24 @@ __device__ __forceinline__ uint64_t sum4(v4u v) {
     return (uint64_t)v.x + (uint64_t)v.y + (uint64_t)v.z + (uint64_t)v.w;
 }
 
+// 64-bit accumulator as two u32 with explicit carry: 2 VALU per dword
+// (v_add_co_u32 + v_addc_co_u32), no zero-extension moves.
+struct Acc {
+    uint32_t lo = 0, hi = 0;
+    __device__ __forceinline__ void add(uint32_t x) {
+        uint32_t c;
+        lo = __builtin_addc(lo, x, 0u, &c);
+        hi += c;
+    }
+    __device__ __forceinline__ void add4(v4u v) {
+        add(v.x);
+        add(v.y);
+        add(v.z);
+        add(v.w);
+    }
+    __device__ __forceinline__ uint64_t value() const { return ((uint64_t)hi << 32) | lo; }
+};
+
 // DPP controls (GFX9 encoding).
 enum : int {
     kDppQuadPerm1032 = 0xB1,  // quad_perm:[1,0,3,2]
@@ -100,6 +118,19 @@ typedef __attribute__((address_space(1))) const uint8_t g_u8;
 // 16-byte load of an aligned chunk at absolute address `addr`.
 __device__ __forceinline__ v4u ld16(uintptr_t addr) {
     return *reinterpret_cast<g_v4u *>(addr);
+}
+
+// Non-temporal variant (global_load_dwordx4 ... nt): for once-read streams.
+__device__ __forceinline__ v4u ld16_nt(uintptr_t addr) {
+    return __builtin_nontemporal_load(reinterpret_cast<g_v4u *>(addr));
+}
+
+template <bool kNT>
+__device__ __forceinline__ v4u ld16x(uintptr_t addr) {
+    if constexpr (kNT)
+        return ld16_nt(addr);
+    else
+        return ld16(addr);
 }
 
 __device__ __forceinline__ uint32_t ld8(uintptr_t addr) {

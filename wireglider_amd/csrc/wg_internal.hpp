@@ -10,9 +10,12 @@ namespace wg {
 // defaults are the measured best on MI355X.
 struct Tune {
     uint64_t l4_blocks;   // grid cap for the wave-per-packet checksum kernels
+    uint32_t l4_ppw;      // packets per wave iteration (1, 2, 4, 8)
+    uint32_t l4_nt;       // 1: non-temporal packet loads
     uint64_t gso_blocks;  // grid cap for the GSO split kernel
 };
 
 const Tune &tune();
+Tune &tune_mut();
 
 }  // namespace wg
