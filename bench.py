@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="config2", choices=["config2", "config4", "config5"])
+    ap.add_argument("--workload", default="config2", choices=["config2", "config3", "config4", "config5"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall seconds of the CPU baseline sample")
     ap.add_argument("--settle-seconds", type=float, default=0.3,
@@ -99,6 +99,43 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev):
             return buf[: npk * SEG].cpu().numpy(), out[:npk].cpu().numpy(), ("desc", desc[:npk].cpu().numpy())
 
         return launch, n, n * SEG, alg, cfg, sample, "strong", buf
+    if name == "config3":
+        import numpy as np
+
+        n, in_stride, out_stride = 1 << 18, 65536, 73216  # outbuf stride of worker/encap.cpp:26
+        in_len, gso = 65535, 1460
+        seed = 0x5EED0003
+        buf = torch.empty(n * in_stride, dtype=torch.uint8, device=dev)
+        wga.synth_fill(buf, seed)
+        pd = np.zeros(n, dtype=wga.PKT_DESC_DTYPE)
+        pd["offset"] = np.arange(n, dtype=np.uint64) * in_stride
+        pd["len"], pd["csum_start"], pd["flags"] = in_len, 20, 2  # IPv4 + TCP (doff 5, ACK|PSH)
+        wga.synth_headers(buf, torch.from_numpy(pd.view(np.uint8).copy()).to(dev), seed, rank * n)
+        desc = np.zeros(n, dtype=wga.GSO_DESC_DTYPE)
+        desc["in_offset"] = pd["offset"]
+        desc["out_offset"] = np.arange(n, dtype=np.uint64) * out_stride
+        desc["in_len"], desc["out_cap"] = in_len, out_stride
+        desc["vnet"]["flags"], desc["vnet"]["gso_type"], desc["vnet"]["gso_size"] = 1, 1, gso
+        desc["vnet"]["csum_start"], desc["vnet"]["csum_offset"] = 20, 16
+        d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
+        out = torch.empty(n * out_stride, dtype=torch.uint8, device=dev)
+        res = torch.empty(n * wga.GSO_RESULT_BYTES, dtype=torch.uint8, device=dev)
+        nseg = (in_len - 40 + gso - 1) // gso
+        out_len = in_len - 40 + nseg * 40
+
+        def launch():
+            wga.gso_split(buf, d_desc, out, results=res)
+
+        cfg = {"workload": "config3: 262,144 x 64 KiB GSO super-buffers (IPv4/TCP, 65535 B) -> 45 x 1460 B "
+                           "segments each, fused copy + header fix-up + IPv4/TCP checksums",
+               "super_buffers_per_gpu": n, "gso_size": gso, "segments_per_buffer": nseg,
+               "parallelism": f"shard{world}"}
+        alg = n * in_len + n * out_len + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES)
+
+        def sample(npk):
+            return None, None, ("gso",)
+
+        return launch, n, n * in_len, alg, cfg, sample, "weak", buf
     # config4 bimodal
     import numpy as np
 
@@ -177,6 +214,8 @@ def cpu_baseline(sample_fn, seconds: float):
     # host's last-level cache (EPYC 9575F: 256 MB L3) between repetitions.
     npk = 1 << 19
     host, gpu_out, kind = sample_fn(npk)
+    if kind[0] == "gso":
+        return None
     threads = oracle.default_threads()
     if kind[0] == "uniform":
         _, seg, cs, fl = kind
@@ -314,7 +353,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "wg::l4csum_kernel",
+            "kernel": "wg::gso_split_kernel" if args.workload == "config3" else "wg::l4csum_kernel",
             "alg_bytes_per_launch": alg,
             "traffic_source": "profiles/pmc_%s.json (rocprofv3 FETCH_SIZEx2 + WRITE_SIZE, per launch)" % args.workload,
             "measured_read_peak": round(read_peak, 1) if read_peak else None,

@@ -200,8 +200,11 @@ int wg_device_count(void);
 /* Launch-geometry knobs (also read once from the environment as WG_L4_BLOCKS,
  * WG_L4_PPW, WG_L4_NT, WG_GSO_BLOCKS).  Keys: "l4_blocks" (grid cap),
  * "l4_ppw" (packets per wave iteration: 1, 2, 4, 8), "l4_nt" (0/1
- * non-temporal loads), "gso_blocks".  Results never depend on them.  Not
- * synchronised with concurrent launches from other threads. */
+ * non-temporal loads), "gso_blocks", "gso_waves" (waves per block: 4, 8, 16),
+ * "gso_split" (blocks per super-buffer, 1-64), "gso_spw" (segments in flight per wave: 1, 2), "gso_ablate"
+ * (profiling only: 1 = non-temporal payload stores; 2..7 select timing-only
+ * GSO variants whose output is WRONG; 0 restores the default kernel).  Results never depend on the geometry
+ * knobs.  Not synchronised with concurrent launches from other threads. */
 int wg_tune_set(const char *key, uint64_t value);
 
 /* Read-roofline probe (benchmark support): streams dev[0, nbytes) with
@@ -210,6 +213,11 @@ int wg_tune_set(const char *key, uint64_t value);
  * is the measured read ceiling the checksum kernels are compared against. */
 int wg_probe_read(const uint8_t *dev, uint64_t nbytes, uint64_t *dev_out, uint32_t kib_per_wave,
                   uint32_t reserved, void *stream);
+
+/* Copy-roofline probe: dst[0, nbytes) = src[0, nbytes) by one-shot waves of
+ * `kib_per_wave` (1/2/4) KiB, non-temporal loads and stores; the measured
+ * read+write ceiling for the GSO split kernel. */
+int wg_probe_copy(const uint8_t *src, uint8_t *dst, uint64_t nbytes, uint32_t kib_per_wave, void *stream);
 
 #ifdef __cplusplus
 }

@@ -275,11 +275,15 @@ int orc_gso_split(uint8_t *in, size_t in_len, orc_vnet_hdr *v, uint8_t *out, siz
     memset(res, 0, sizeof(*res));
     const size_t cs = v->csum_start;
     const size_t l4off = (size_t)v->csum_start + v->csum_offset; /* :47 */
-    /* Out of the reference's contract (undefined behaviour there). */
-    if (in_len < 1 || cs > in_len)
+    /* Out of contract (-3) = inputs the reference reads out of bounds on, or
+     * whose header geometry makes its fixups overlap the IP header: a packet
+     * shorter than its fixed IP header, csum_start inside the fixed IP
+     * header, or a checksum field outside the L4 header. */
+    if (in_len < 1)
         return -3;
     const int isv6 = (in[0] >> 4) == 6; /* :48 */
-    if (in_len < (isv6 ? 40u : 20u))
+    const size_t iph_min = isv6 ? 40u : 20u;
+    if (in_len < iph_min)
         return -3;
     /* :49-53, IPTOS_ECN = & 0x03 */
     const uint8_t ecn = isv6 ? (uint8_t)((ld_be32(in) >> 20) & 3) : (uint8_t)(in[1] & 3);
@@ -293,7 +297,7 @@ int orc_gso_split(uint8_t *in, size_t in_len, orc_vnet_hdr *v, uint8_t *out, siz
     switch (v->gso_type & ~VNET_GSO_ECN) { /* :55 */
     case VNET_GSO_NONE:
         if (v->flags & VNET_F_NEEDS_CSUM) { /* :56-78 */
-            if (l4off + 2 > in_len)
+            if (cs < iph_min || cs > in_len || l4off + 2 > in_len)
                 return -3;
             if (!isv6) {
                 in[10] = 0; /* ip_sum */
@@ -312,6 +316,8 @@ int orc_gso_split(uint8_t *in, size_t in_len, orc_vnet_hdr *v, uint8_t *out, siz
         return 0;
     case VNET_GSO_TCPV4:
     case VNET_GSO_TCPV6: {
+        if (cs > in_len)
+            return -3; /* :91 would wrap and read past the buffer */
         if (in_len - cs < 20) /* :91 */
             return 0;
         size_t thlen = 4u * (in[cs + 12] >> 4); /* tcphdr.doff, :100 */
@@ -330,13 +336,13 @@ int orc_gso_split(uint8_t *in, size_t in_len, orc_vnet_hdr *v, uint8_t *out, siz
     const size_t hdr_len = v->hdr_len;
     if (in_len < hdr_len) /* :126-134 */
         return 0;
-    if (l4off + 2 > hdr_len)
+    if (cs < iph_min || l4off < cs || l4off + 2 > hdr_len)
         return -3;
 
     const size_t rest_len = in_len - hdr_len;
     const size_t gso = v->gso_size;
     if (rest_len && !gso)
-        return -1;
+        return -1; /* the reference loops forever (:157-158) */
     const size_t nseg = gso ? (rest_len + gso - 1) / gso : 0;
     if (out_cap < in_len + nseg * hdr_len) /* reserve_size assert, :139-143 */
         return -2;

@@ -1,0 +1,223 @@
+"""Parity of the gfx950 GSO split kernel (wg_gso_split) against the oracle's
+do_tun_gso_split restatement (worker/offload.cpp:46-216): for every
+super-buffer the status, the PacketBatch geometry, the whole output byte
+range and the input buffer after the call (the reference modifies it in
+place) must be identical.  Cases: the reference tests' packets
+(tests/test-offload.cpp), random v4/v6 x TCP/UDP_L4 x ECN super-buffers with
+random gso_size, payload length, TCP options, FIN/PSH, unaligned input and
+output offsets, GSO_NONE in-place checksums, passthrough types and every
+error status; then config 3 at full size through size-independent properties.
+"""
+import numpy as np
+import pytest
+
+import oracle
+import pktbuild
+
+pytestmark = pytest.mark.gpu
+
+NEEDS_CSUM = 1
+
+
+def _wga():
+    import wireglider_amd
+
+    return wireglider_amd
+
+
+def run_batch(gpu, cases, out_cap_fn=lambda c: None, seed=0):
+    """cases: list of (pkt bytes, vnet dict, out_cap or None).  Lays the
+    super-buffers out at random (unaligned) offsets, runs the GPU once, and
+    compares each against the oracle."""
+    import torch
+
+    wga = _wga()
+    rng = np.random.default_rng(seed)
+    n = len(cases)
+    desc = np.zeros(n, dtype=wga.GSO_DESC_DTYPE)
+    in_off, out_off = 0, 0
+    caps = []
+    for k, (pkt, vnet, cap) in enumerate(cases):
+        in_off += int(rng.integers(0, 17))
+        out_off += int(rng.integers(0, 17))
+        if cap is None:
+            cap = len(pkt) + (len(pkt) // max(1, vnet.get("gso_size", 1)) + 2) * 200
+        desc[k]["in_offset"], desc[k]["out_offset"] = in_off, out_off
+        desc[k]["in_len"], desc[k]["out_cap"] = len(pkt), cap
+        for f in ("flags", "gso_type", "hdr_len", "gso_size", "csum_start", "csum_offset"):
+            desc[k]["vnet"][f] = vnet.get(f, 0)
+        caps.append(cap)
+        in_off += len(pkt)
+        out_off += cap
+    inbuf = np.zeros(in_off + 64, np.uint8)
+    for k, (pkt, _, _) in enumerate(cases):
+        o = int(desc[k]["in_offset"])
+        inbuf[o:o + len(pkt)] = np.frombuffer(pkt, np.uint8)
+    sentinel = 0xA5
+    d_in = torch.from_numpy(inbuf.copy()).to(gpu)
+    d_out = torch.full((out_off + 64,), sentinel, dtype=torch.uint8, device=gpu)
+    d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(gpu)
+    d_res = wga.gso_split(d_in, d_desc, d_out)
+    torch.cuda.synchronize()
+    g_in, g_out = d_in.cpu().numpy(), d_out.cpu().numpy()
+    g_res = d_res.cpu().numpy().view(wga.GSO_RESULT_DTYPE)
+    for k, (pkt, vnet, _) in enumerate(cases):
+        st, o_in, o_out, vafter, res = oracle.gso_split(np.frombuffer(pkt, np.uint8), vnet, caps[k])
+        r = g_res[k]
+        ctx = f"case {k}: vnet={vnet} len={len(pkt)}"
+        assert int(r["status"]) == st, ctx
+        io = int(desc[k]["in_offset"])
+        oo = int(desc[k]["out_offset"])
+        if st != 0:
+            continue
+        assert int(r["passthrough"]) == res["passthrough"], ctx
+        assert int(r["out_len"]) == res["out_len"], ctx
+        assert int(r["segment_size"]) == res["segment_size"], ctx
+        assert int(r["hdr_len"]) == vafter["hdr_len"], ctx
+        assert int(r["isv6"]) == res["isv6"] and int(r["ecn"]) == res["ecn"], ctx
+        np.testing.assert_array_equal(g_in[io:io + len(pkt)], o_in, err_msg="input after: " + ctx)
+        if not res["passthrough"]:
+            np.testing.assert_array_equal(g_out[oo:oo + len(o_out)], o_out, err_msg="output: " + ctx)
+            # nothing written past the batch
+            assert np.all(g_out[oo + len(o_out):oo + caps[k]] == sentinel), ctx
+        else:
+            assert np.all(g_out[oo:oo + caps[k]] == sentinel), ctx
+
+
+def test_reference_offload_cases(gpu):
+    cases = []
+    a4 = ("192.0.2.1", "192.0.2.2")
+    a6 = ("2001:db8::1", "2001:db8::2")
+    for hdr in (40, 0):
+        p = pktbuild.make_tcp(False, a4[0], 1, a4[1], 1, 0x18, 200, 9999)
+        cases.append((p, dict(flags=1, gso_type=1, hdr_len=hdr or len(p), gso_size=100, csum_start=20,
+                              csum_offset=16), None))
+        p = pktbuild.make_tcp(False, a4[0], 1, a4[1], 1, 0x19, 100, 9999)
+        cases.append((p, dict(flags=1, gso_type=0, hdr_len=hdr or len(p), gso_size=100, csum_start=20,
+                              csum_offset=16), None))
+    for hdr in (60, 0):
+        p = pktbuild.make_tcp(True, a6[0], 1, a6[1], 1, 0x18, 200, 9999)
+        cases.append((p, dict(flags=1, gso_type=4, hdr_len=hdr or len(p), gso_size=100, csum_start=40,
+                              csum_offset=16), None))
+        p = pktbuild.make_tcp(True, a6[0], 1, a6[1], 1, 0x19, 100, 9999)
+        cases.append((p, dict(flags=1, gso_type=0, hdr_len=hdr or len(p), gso_size=100, csum_start=40,
+                              csum_offset=16), None))
+    for isv6, cs, hdr in ((False, 20, 28), (True, 40, 48)):
+        a = a6 if isv6 else a4
+        p = pktbuild.make_udp(isv6, a[0], 1, a[1], 1, 200)
+        for h in (hdr, len(p)):
+            cases.append((p, dict(flags=1, gso_type=5, hdr_len=h, gso_size=100, csum_start=cs, csum_offset=6), None))
+    # ECN quirk, 4 x 1460
+    p = pktbuild.build(False, True, bytes(4 * 1460), pktbuild.ipv4_addr("10.0.0.1"), pktbuild.ipv4_addr("10.0.0.2"),
+                       seq=100, fill_l4=False)
+    cases.append((p, dict(flags=1, gso_type=0x81, gso_size=1460, csum_start=20, csum_offset=16), None))
+    run_batch(gpu, cases)
+
+
+def random_case(rng):
+    isv6 = bool(rng.integers(0, 2))
+    kind = int(rng.integers(0, 10))
+    istcp = kind < 5
+    plen = int(rng.choice([0, 1, 2, 15, 16, 17, int(rng.integers(0, 3000)), int(rng.integers(0, 65000))]))
+    cs = 40 if isv6 else 20
+    opts = b""
+    if not isv6 and rng.integers(0, 4) == 0:
+        opts = bytes([1]) * (4 * int(rng.integers(1, 11)))  # IPv4 options -> csum_start 24..60
+        cs += len(opts)
+    al = 16 if isv6 else 4
+    thl = 20
+    pkt = bytearray(pktbuild.build(isv6, istcp, rng.integers(0, 256, plen, dtype=np.uint8).tobytes(),
+                                   rng.integers(0, 256, al, dtype=np.uint8).tobytes(),
+                                   rng.integers(0, 256, al, dtype=np.uint8).tobytes(),
+                                   seq=int(rng.integers(0, 2**32)), tcp_flags=int(rng.choice([0x10, 0x18, 0x19, 0x11])),
+                                   ident=int(rng.integers(0, 65536)), fill_l4=bool(rng.integers(0, 2)),
+                                   ip_options=opts))
+    if istcp and rng.integers(0, 3) == 0 and len(pkt) >= cs + 60:
+        thl = 4 * int(rng.integers(5, 16))  # TCP options: doff 5..15 (payload bytes become options)
+        pkt[cs + 12] = (thl // 4) << 4
+    gso = int(rng.choice([1, 7, 100, 536, 1448, 1460, int(rng.integers(1, 9000))]))
+    if kind < 5:
+        gt = 4 if isv6 else 1
+        if rng.integers(0, 4) == 0:
+            gt |= 0x80  # ECN quirk
+    elif kind < 8:
+        gt = 5
+    elif kind == 8:
+        gt = 0  # GSO_NONE (in place if NEEDS_CSUM)
+    else:
+        gt = int(rng.choice([3, 2, 6, 0x85]))  # passthrough types
+    vnet = dict(flags=int(rng.choice([0, 1, 1, 1])), gso_type=gt, hdr_len=int(rng.integers(0, 200)), gso_size=gso,
+                csum_start=cs, csum_offset=16 if (istcp and gt != 5) else 6)
+    if rng.integers(0, 12) == 0:
+        vnet["csum_offset"] = int(rng.integers(0, 30))  # odd / overlapping field positions
+    if rng.integers(0, 15) == 0:
+        vnet["gso_size"] = 0
+    cap = None
+    if rng.integers(0, 15) == 0:
+        cap = int(rng.integers(0, len(pkt) + 100))
+    return bytes(pkt), vnet, cap
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_super_buffers(gpu, seed):
+    rng = np.random.default_rng(seed)
+    cases = [random_case(rng) for _ in range(400)]
+    run_batch(gpu, cases, seed=seed)
+
+
+def test_config3_full_size_properties(gpu):
+    """BASELINE config 3: 262,144 x (IPv4 20 + TCP 20 + 65495 B) -> 45 x 1460 B
+    segments each.  Properties at full size: every segment's IPv4 header and
+    L4 checksum verify (wg_checksum_desc / wg_l4csum_uniform == 0), payload
+    bytes equal the input payload, and a sample of super-buffers equals the
+    oracle byte for byte."""
+    import torch
+
+    wga = _wga()
+    n, in_stride, out_stride = 262144, 65536, 73216
+    in_len, hl, gso = 65535, 40, 1460
+    nseg = (in_len - hl + gso - 1) // gso
+    out_len = in_len - hl + nseg * hl
+    seed = 0x5EED0003
+    d_in = torch.empty(n * in_stride, dtype=torch.uint8, device=gpu)
+    wga.synth_fill(d_in, seed)
+    pd = np.zeros(n, dtype=wga.PKT_DESC_DTYPE)
+    pd["offset"] = np.arange(n, dtype=np.uint64) * in_stride
+    pd["len"], pd["csum_start"], pd["flags"] = in_len, 20, 2
+    d_pd = torch.from_numpy(pd.view(np.uint8).copy()).to(gpu)
+    wga.synth_headers(d_in, d_pd, seed, 0)
+    desc = np.zeros(n, dtype=wga.GSO_DESC_DTYPE)
+    desc["in_offset"] = pd["offset"]
+    desc["out_offset"] = np.arange(n, dtype=np.uint64) * out_stride
+    desc["in_len"], desc["out_cap"] = in_len, out_stride
+    desc["vnet"]["flags"], desc["vnet"]["gso_type"], desc["vnet"]["gso_size"] = 1, 1, gso
+    desc["vnet"]["csum_start"], desc["vnet"]["csum_offset"] = 20, 16
+    d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(gpu)
+    sample = [0, 1, 77777, n - 1]
+    host_in = {b: d_in[b * in_stride:b * in_stride + in_len].cpu().numpy() for b in sample}
+    d_out = torch.empty(n * out_stride, dtype=torch.uint8, device=gpu)
+    res = wga.gso_split(d_in, d_desc, d_out)
+    torch.cuda.synchronize()
+    r = res.cpu().numpy().view(wga.GSO_RESULT_DTYPE)
+    assert np.all(r["status"] == 0) and np.all(r["out_len"] == out_len) and np.all(r["segment_size"] == hl + gso)
+    # verify every segment: view the outputs as one descriptor batch of segments
+    sd = np.zeros(n * nseg, dtype=wga.PKT_DESC_DTYPE)
+    base = (np.arange(n, dtype=np.uint64) * out_stride)[:, None] + np.arange(nseg, dtype=np.uint64)[None, :] * (hl + gso)
+    sd["offset"] = base.reshape(-1)
+    lens = np.full((n, nseg), hl + gso, np.uint32)
+    lens[:, -1] = out_len - (nseg - 1) * (hl + gso)
+    sd["len"], sd["csum_start"], sd["flags"] = lens.reshape(-1), 20, 2
+    d_sd = torch.from_numpy(sd.view(np.uint8).copy()).to(gpu)
+    l4 = wga.calc_l4_checksum_desc(d_out, d_sd)
+    ih = sd.copy()
+    ih["len"] = 20
+    ipc = wga.checksum_desc(d_out, torch.from_numpy(ih.view(np.uint8).copy()).to(gpu))
+    torch.cuda.synchronize()
+    assert int(l4.to(torch.int32).abs().sum()) == 0
+    assert int(ipc.to(torch.int32).abs().sum()) == 0
+    for b in sample:
+        st, o_in, o_out, _, _ = oracle.gso_split(host_in[b], dict(flags=1, gso_type=1, gso_size=gso, csum_start=20,
+                                                                  csum_offset=16), out_stride)
+        assert st == 0
+        np.testing.assert_array_equal(d_out[b * out_stride:b * out_stride + out_len].cpu().numpy(), o_out)
+        np.testing.assert_array_equal(d_in[b * in_stride:b * in_stride + in_len].cpu().numpy(), o_in)

@@ -45,12 +45,31 @@ EXPORTED_SYMBOLS = (
     "wg_device_count",
     "wg_tune_set",
     "wg_probe_read",
+    "wg_probe_copy",
 )
 
 # struct layouts (include/wireglider_amd.h)
 PKT_DESC_BYTES = 16
 GSO_DESC_BYTES = 40
 GSO_RESULT_BYTES = 24
+
+
+def _np_dtypes():
+    import numpy as np
+
+    pkt = np.dtype([("offset", "<u8"), ("len", "<u4"), ("csum_start", "<u2"), ("flags", "u1"),
+                    ("reserved", "u1")])
+    vnet = np.dtype([("flags", "u1"), ("gso_type", "u1"), ("hdr_len", "<u2"), ("gso_size", "<u2"),
+                     ("csum_start", "<u2"), ("csum_offset", "<u2")])
+    gso = np.dtype([("in_offset", "<u8"), ("out_offset", "<u8"), ("in_len", "<u4"), ("out_cap", "<u4"),
+                    ("vnet", vnet), ("reserved", "<u2", 3)])
+    res = np.dtype([("out_len", "<u8"), ("segment_size", "<u4"), ("hdr_len", "<u2"), ("isv6", "u1"),
+                    ("ecn", "u1"), ("status", "i1"), ("passthrough", "u1"), ("pad", "u1", 6)])
+    assert pkt.itemsize == PKT_DESC_BYTES and gso.itemsize == GSO_DESC_BYTES and res.itemsize == GSO_RESULT_BYTES
+    return pkt, gso, res
+
+
+PKT_DESC_DTYPE, GSO_DESC_DTYPE, GSO_RESULT_DTYPE = _np_dtypes()
 
 
 class WireGliderError(RuntimeError):
@@ -85,6 +104,7 @@ def _load() -> ctypes.CDLL:
         "wg_device_count": (i32, []),
         "wg_tune_set": (i32, [ctypes.c_char_p, u64]),
         "wg_probe_read": (i32, [u8p, u64, vp, u32, u32, vp]),
+        "wg_probe_copy": (i32, [u8p, u8p, u64, u32, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -250,6 +270,12 @@ def probe_read(buf, out, kib_per_wave: int = 4, stream=None) -> None:
     """Launch the read-roofline probe over a device buffer."""
     _check(lib.wg_probe_read(buf.data_ptr(), buf.numel() * buf.element_size(), out.data_ptr(), kib_per_wave, 0,
                              _stream_ptr(stream)), "wg_probe_read")
+
+
+def probe_copy(src, dst, kib_per_wave: int = 2, stream=None) -> None:
+    """Launch the copy-roofline probe (dst = src) over device buffers."""
+    n = min(src.numel() * src.element_size(), dst.numel() * dst.element_size())
+    _check(lib.wg_probe_copy(src.data_ptr(), dst.data_ptr(), n, kib_per_wave, _stream_ptr(stream)), "wg_probe_copy")
 
 
 def device_count() -> int:

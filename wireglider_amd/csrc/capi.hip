@@ -31,7 +31,13 @@ Tune &tune_mut() {
         x.l4_blocks = env_u64("WG_L4_BLOCKS", 1u << 20);
         x.l4_ppw = (uint32_t)env_u64("WG_L4_PPW", 4);
         x.l4_nt = (uint32_t)env_u64("WG_L4_NT", 1);
-        x.gso_blocks = env_u64("WG_GSO_BLOCKS", 2048);
+        x.gso_blocks = env_u64("WG_GSO_BLOCKS", 1u << 20);
+        // GSO: one 4-wave block per super-buffer, 2 segments in flight per
+        // wave (tools/tune_gso.py, profiles/r01_tune_gso.json).
+        x.gso_waves = (uint32_t)env_u64("WG_GSO_WAVES", 4);
+        x.gso_split = (uint32_t)env_u64("WG_GSO_SPLIT", 1);
+        x.gso_spw = (uint32_t)env_u64("WG_GSO_SPW", 2);
+        x.gso_ablate = 0;
         return x;
     }();
     return t;
@@ -122,9 +128,49 @@ __global__ __launch_bounds__(256) void probe_read_kernel(const uint8_t *dev, uin
     if (lane == 0 && s == 0xFFFFFFFFu) *out = s;
 }
 
+// Copy-roofline probe: one-shot waves, each copying U contiguous KiB
+// (non-temporal loads, all issued first, then non-temporal stores).
+template <int U>
+__global__ __launch_bounds__(256) void probe_copy_kernel(const uint8_t *src, uint8_t *dst, uint64_t nchunks) {
+    const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
+    const uint64_t c0 = wave * (uint64_t)U * 64u;
+    const uint32_t lane = lane_id();
+    if (c0 >= nchunks)
+        return;
+    const uintptr_t s = reinterpret_cast<uintptr_t>(src), d = reinterpret_cast<uintptr_t>(dst);
+    v4u v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint64_t c = c0 + (uint64_t)u * 64u + lane;
+        v[u] = ld16_nt(s + 16u * (c < nchunks ? c : nchunks - 1));
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint64_t c = c0 + (uint64_t)u * 64u + lane;
+        if (c < nchunks)
+            __builtin_nontemporal_store(v[u], reinterpret_cast<__attribute__((address_space(1))) v4u *>(d + 16u * c));
+    }
+}
+
 }  // namespace wg
 
 using namespace wg;
+
+extern "C" int wg_probe_copy(const uint8_t *src, uint8_t *dst, uint64_t nbytes, uint32_t kib_per_wave, void *stream) {
+    if (!src || !dst || ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) || nbytes < 16)
+        return WG_ERR_INVALID;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint64_t nch = nbytes >> 4;
+    const uint32_t U = kib_per_wave == 2 || kib_per_wave == 4 ? kib_per_wave : 1;
+    uint64_t blocks = (nch + 256ull * U - 1) / (256ull * U);
+    if (blocks >= 8) blocks = (blocks + 7) & ~7ull;
+    switch (U) {
+    case 2: hipLaunchKernelGGL(probe_copy_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, nch); break;
+    case 4: hipLaunchKernelGGL(probe_copy_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, nch); break;
+    default: hipLaunchKernelGGL(probe_copy_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, nch); break;
+    }
+    return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+}
 
 extern "C" int wg_probe_read(const uint8_t *dev, uint64_t nbytes, uint64_t *dev_out, uint32_t kib_per_wave,
                              uint32_t unused, void *stream) {
@@ -170,6 +216,14 @@ extern "C" int wg_tune_set(const char *key, uint64_t value) {
         t.l4_nt = (uint32_t)value;
     else if (k == "gso_blocks" && value >= 1 && value <= (1u << 20))
         t.gso_blocks = value;
+    else if (k == "gso_waves" && (value == 4 || value == 8 || value == 16))
+        t.gso_waves = (uint32_t)value;
+    else if (k == "gso_split" && value >= 1 && value <= 64)
+        t.gso_split = (uint32_t)value;
+    else if (k == "gso_spw" && (value == 1 || value == 2))
+        t.gso_spw = (uint32_t)value;
+    else if (k == "gso_ablate" && value <= 7 && value != 5)
+        t.gso_ablate = (uint32_t)value;
     else
         return WG_ERR_INVALID;
     return WG_OK;

@@ -19,6 +19,7 @@
 
 #include "wg_device.hpp"
 #include "wg_internal.hpp"
+#include "wg_l4wave.hpp"
 #include "wireglider_amd.h"
 
 namespace wg {
@@ -35,11 +36,6 @@ struct L4Params {
 };
 
 enum Kind : int { kUniformL4 = 0, kDescL4 = 1, kDescPlain = 2 };
-
-struct Geom {
-    uintptr_t a;  // packet start
-    uint32_t len, cs, fl;
-};
 
 template <int kKind>
 __device__ __forceinline__ Geom load_geom(const L4Params &p, uint64_t i) {
@@ -67,96 +63,6 @@ __device__ __forceinline__ Geom load_geom(const L4Params &p, uint64_t i) {
         g.fl = d.flags;
     }
     return g;
-}
-
-// Always-valid, always-zero 16 B: the load target of lanes (and packets)
-// with nothing to read, so the issue phase needs no branches — a branch
-// around a load makes the compiler wait for it inside the branch.
-__device__ v4u g_zero16;
-
-// Per-packet state between the issue and finish phases.
-struct Front {
-    v4u v0, v1;      // interior chunks lane, lane + 64 (masked to zero)
-    uint32_t bv;     // gathered byte, already shifted to its pairing
-    bool bt;         // bv is in TRUE pairing (pseudo-header address byte)
-    uintptr_t r0;    // start of the summed region
-    uintptr_t c0;    // first aligned interior chunk
-    uint32_t nint;   // interior chunk count
-};
-
-// Issue phase.  Summed region [r0, r1) = [a + cs, a + len) (empty when
-// cs >= len).  Interior = whole aligned chunks [c0, c1); the unaligned head
-// [r0, min(c0, r1)) and tail [max(c1, c0), r1) are <= 15 bytes each.
-// Branch-free: out-of-range lanes re-read a valid chunk and are masked.
-template <bool kL4, bool kNT>
-__device__ __forceinline__ void issue(const Geom &g, uint32_t lane, Front &f) {
-    const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
-    const uintptr_t r1 = g.a + g.len;
-    const uintptr_t r0 = g.cs < g.len ? g.a + g.cs : r1;
-    const uintptr_t c0 = (r0 + 15) & ~(uintptr_t)15;
-    const uintptr_t c1 = r1 & ~(uintptr_t)15;
-    const uint32_t nint = c1 > c0 ? (uint32_t)((c1 - c0) >> 4) : 0u;
-    f.r0 = r0;
-    f.c0 = c0;
-    f.nint = nint;
-    // wave-uniform base and clamp, per-lane 32-bit offset
-    const uintptr_t base = nint ? c0 : zero;
-    const uint32_t last = nint ? nint - 1 : 0u;
-    const uint32_t k0 = lane < last ? lane : last;
-    const uint32_t k1 = lane + 64 < last ? lane + 64 : last;
-    const v4u t0 = ld16x<kNT>(base + 16u * k0);
-    const v4u t1 = ld16x<kNT>(base + 16u * k1);
-    const v4u z = v4u{0, 0, 0, 0};
-    f.v0 = lane < nint ? t0 : z;
-    f.v1 = lane + 64 < nint ? t1 : z;
-
-    // One byte per lane: lanes 0-31 pseudo-header addresses (pairing
-    // relative to the address start, an even packet offset: 12 for v4, 8 for
-    // v6 — checksum.cpp:14-28), lanes 32-47 the head, lanes 48-63 the tail
-    // (absolute-address pairing, like the interior).
-    const bool v6 = g.fl & WG_PKT_V6;
-    const uint32_t ao = v6 ? 8u : 12u, al = v6 ? 32u : 8u;
-    const bool bt = kL4 && lane < al && ao + lane < g.len;
-    const uintptr_t he = c0 < r1 ? c0 : r1;
-    const uintptr_t ts = c1 > c0 ? c1 : c0;
-    const uintptr_t xh = r0 + (lane - 32);
-    const uintptr_t xt = ts + (lane - 48);
-    const bool bh = lane >= 32 && lane < 48 && xh < he;
-    const bool btl = lane >= 48 && xt < r1;
-    const uintptr_t bp = bt ? g.a + ao + lane : (bh ? xh : (btl ? xt : zero));
-    const uint32_t par = bt ? (lane & 1u) : (uint32_t)(bp & 1u);
-    f.bv = ld8(bp) << (8u * par);
-    f.bt = bt;
-}
-
-// Finish phase: this lane's share of the packet's sum in TRUE pairing.
-template <bool kNT>
-__device__ __forceinline__ uint32_t finish(uint32_t lane, const Front &f) {
-    Acc acc;
-    acc.add4(f.v0);
-    acc.add4(f.v1);
-    if (f.nint > 128) {  // long packet (> ~2 KiB): stream the rest, 4 loads in flight
-        const uintptr_t q = f.c0;
-        uint32_t k = lane + 128;
-        for (; k + 192 < f.nint; k += 256) {
-            v4u a0 = ld16x<kNT>(q + 16ull * k);
-            v4u a1 = ld16x<kNT>(q + 16ull * (k + 64));
-            v4u a2 = ld16x<kNT>(q + 16ull * (k + 128));
-            v4u a3 = ld16x<kNT>(q + 16ull * (k + 192));
-            acc.add4(a0);
-            acc.add4(a1);
-            acc.add4(a2);
-            acc.add4(a3);
-        }
-        for (; k < f.nint; k += 64)
-            acc.add4(ld16x<kNT>(q + 16ull * k));
-    }
-    if (!f.bt)
-        acc.add(f.bv);
-    uint32_t s = fold16(acc.value());
-    if (f.r0 & 1u)  // region pairs from an odd address: swap its folded sum
-        s = bswap16(s);
-    return s + (f.bt ? f.bv : 0u);
 }
 
 template <int kKind, int P, bool kNT>
