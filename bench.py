@@ -2,21 +2,26 @@
 """Benchmark: device-resident GiB/s of the L4 checksum over a packet batch.
 
 BASELINE.json metric "device-resident GiB/s, L4 checksum over packet batch;
-1/2/4/8 MI355X".  One step = one launch of the gfx950 L4 checksum kernel over
-one whole batch already resident in HBM (reference: calc_l4_checksum,
-checksum.cpp:8-36, once per segment of a PacketBatch).
+1/2/4/8 MI355X".  One step = one launch of the gfx950 kernel over one whole
+batch already resident in HBM (reference: calc_l4_checksum, checksum.cpp:8-36,
+once per segment of a PacketBatch, include/worker/offload.hpp:19-29).
 
-Workloads (--workload):
+Workloads (--workload; BASELINE.json configs):
   config2 (default)  1,048,576 x 1500 B IPv4/UDP per GPU, uniform PacketBatch
-                     (BASELINE configs[1]); N GPUs = N independent shards,
-                     weak scaling, no data-path collective.
-  config5            16,777,216 x 1500 B mixed v4/v6 x TCP/UDP (descriptor
-                     batch) split across the N GPUs (configs[4]); strong scaling.
-  config4            4,194,304 bimodal 64 B / 9000 B IPv4/UDP (configs[3]), 1 GPU shape.
+                     (configs[1]); N GPUs = N independent shards, weak
+                     scaling, no data-path collective.
+  config3            262,144 x 64 KiB GSO super-buffers -> 45 x 1460 B TCP
+                     segments per GPU (configs[2]), fused split + checksums.
+  config4            4,194,304 bimodal 64 B / 9000 B IPv4/UDP (configs[3]).
+  config5            16,777,216 x 1500 B mixed v4/v6 x TCP/UDP split across
+                     the N GPUs (configs[4]); strong scaling.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2]
-  torchrun --nproc-per-node N bench.py --gpus N ...
-Rank 0 prints ONE JSON line.
+  torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+Rank 0 prints ONE JSON line.  Outside the timed region: a GPU verify pass
+(store the checksums, re-run in verify mode, every result must be 0),
+an RCCL all-gather of the results (timed separately) and an order-independent
+result hash; rank 0 at N=1 also times the CPU oracle on a sample.
 """
 from __future__ import annotations
 
@@ -26,7 +31,9 @@ import math
 import os
 import sys
 import time
+from dataclasses import dataclass, field
 from pathlib import Path
+from typing import Callable, Optional
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
@@ -48,9 +55,26 @@ def parse():
     return ap.parse_args()
 
 
-def build_workload(wga, torch, name: str, rank: int, world: int, dev):
-    """Returns (launch_fn, n_packets, payload_bytes_per_step, alg_bytes_per_launch, cfg,
-    host_sample_fn, scaling, batch_buffer)."""
+@dataclass
+class Workload:
+    launch: Callable[[], None]
+    n_units: int                 # packets (or super-buffers) on this rank
+    payload_bytes: int           # bytes counted by the metric (this rank)
+    alg_bytes: int               # algorithmic HBM bytes per launch (roofline numerator)
+    cfg: dict
+    scaling: str
+    buf: object                  # the batch buffer (read-roofline probe target)
+    kernel: str
+    first_index: int = 0         # global index of this rank's first packet
+    out: Optional[object] = None      # uint16 results (L4 workloads)
+    desc: Optional[object] = None     # descriptor tensor (verify pass)
+    sample: Optional[Callable] = None  # host sample for the CPU baseline
+    counts: list = field(default_factory=list)  # packets per rank
+
+
+def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workload:
+    import numpy as np
+
     if name == "config2":
         n = 1 << 20
         seed = 0x5EED0002
@@ -60,25 +84,23 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev):
         desc = wga.synth_desc_stride(n, SEG, SEG, 0, seed, rank * n, device=dev)
         wga.synth_headers(buf, desc, seed, rank * n)
         out = torch.empty(n, dtype=torch.uint16, device=dev)
-        del desc
 
         def launch():
             wga.calc_l4_checksum_batch(buf, SEG, False, False, 20, out=out)
 
-        cfg = {"workload": "config2: 1,048,576 x 1500 B IPv4/UDP per GPU, uniform PacketBatch (stride 1500)",
-               "packets_per_gpu": n, "segment_size": SEG, "csum_start": 20, "layout": "uniform",
-               "parallelism": f"shard{world} (independent packet shards, no data-path collective)"}
-        alg = n * SEG + 2 * n
-        payload = n * SEG
-
         def sample(npk):
             return buf[: npk * SEG].cpu().numpy(), out[:npk].cpu().numpy(), ("uniform", SEG, 20, 0)
 
-        return launch, n, payload, alg, cfg, sample, "weak", buf
+        cfg = {"workload": "config2: 1,048,576 x 1500 B IPv4/UDP per GPU, uniform PacketBatch (stride 1500)",
+               "packets_per_gpu": n, "segment_size": SEG, "csum_start": 20, "layout": "uniform",
+               "parallelism": f"shard{world} (independent packet shards, no data-path collective)"}
+        return Workload(launch, n, n * SEG, n * SEG + 2 * n, cfg, "weak", buf, "wg::l4csum_kernel<0,4,nt>",
+                        rank * n, out, desc, sample, [n] * world)
     if name == "config5":
+        from wireglider_amd import dist as wdist
+
         total = 1 << 24
-        lo = total * rank // world
-        hi = total * (rank + 1) // world
+        lo, hi = wdist.shard_bounds(total, world, rank)
         n = hi - lo
         seed = 0x5EED0005
         buf = torch.empty(n * SEG, dtype=torch.uint8, device=dev)
@@ -90,57 +112,52 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev):
         def launch():
             wga.calc_l4_checksum_desc(buf, desc, out=out)
 
-        cfg = {"workload": "config5: 16,777,216 x 1500 B mixed IPv4/IPv6 x TCP/UDP split across GPUs (descriptor batch)",
-               "packets_total": total, "packets_per_gpu": n, "segment_size": SEG, "layout": "descriptor",
-               "parallelism": f"shard{world} (contiguous packet ranges, no data-path collective)"}
-        alg = n * SEG + 2 * n + 16 * n
-
         def sample(npk):
             return buf[: npk * SEG].cpu().numpy(), out[:npk].cpu().numpy(), ("desc", desc[:npk].cpu().numpy())
 
-        return launch, n, n * SEG, alg, cfg, sample, "strong", buf
+        cfg = {"workload": "config5: 16,777,216 x 1500 B mixed IPv4/IPv6 x TCP/UDP split across GPUs "
+                           "(descriptor batch)",
+               "packets_total": total, "packets_per_gpu": n, "segment_size": SEG, "layout": "descriptor",
+               "parallelism": f"shard{world} (contiguous packet ranges, no data-path collective)"}
+        counts = [wdist.shard_bounds(total, world, r)[1] - wdist.shard_bounds(total, world, r)[0]
+                  for r in range(world)]
+        return Workload(launch, n, n * SEG, n * SEG + 2 * n + 16 * n, cfg, "strong", buf,
+                        "wg::l4csum_kernel<1,4,nt>", lo, out, desc, sample, counts)
     if name == "config3":
-        import numpy as np
-
         n, in_stride, out_stride = 1 << 18, 65536, 73216  # outbuf stride of worker/encap.cpp:26
         in_len, gso = 65535, 1460
         seed = 0x5EED0003
         buf = torch.empty(n * in_stride, dtype=torch.uint8, device=dev)
-        wga.synth_fill(buf, seed)
+        wga.synth_fill(buf, seed, counter_base=rank * n * in_stride)
         pd = np.zeros(n, dtype=wga.PKT_DESC_DTYPE)
         pd["offset"] = np.arange(n, dtype=np.uint64) * in_stride
         pd["len"], pd["csum_start"], pd["flags"] = in_len, 20, 2  # IPv4 + TCP (doff 5, ACK|PSH)
         wga.synth_headers(buf, torch.from_numpy(pd.view(np.uint8).copy()).to(dev), seed, rank * n)
-        desc = np.zeros(n, dtype=wga.GSO_DESC_DTYPE)
-        desc["in_offset"] = pd["offset"]
-        desc["out_offset"] = np.arange(n, dtype=np.uint64) * out_stride
-        desc["in_len"], desc["out_cap"] = in_len, out_stride
-        desc["vnet"]["flags"], desc["vnet"]["gso_type"], desc["vnet"]["gso_size"] = 1, 1, gso
-        desc["vnet"]["csum_start"], desc["vnet"]["csum_offset"] = 20, 16
-        d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
-        out = torch.empty(n * out_stride, dtype=torch.uint8, device=dev)
+        gd = np.zeros(n, dtype=wga.GSO_DESC_DTYPE)
+        gd["in_offset"] = pd["offset"]
+        gd["out_offset"] = np.arange(n, dtype=np.uint64) * out_stride
+        gd["in_len"], gd["out_cap"] = in_len, out_stride
+        gd["vnet"]["flags"], gd["vnet"]["gso_type"], gd["vnet"]["gso_size"] = 1, 1, gso
+        gd["vnet"]["csum_start"], gd["vnet"]["csum_offset"] = 20, 16
+        d_desc = torch.from_numpy(gd.view(np.uint8).copy()).to(dev)
+        outb = torch.empty(n * out_stride, dtype=torch.uint8, device=dev)
         res = torch.empty(n * wga.GSO_RESULT_BYTES, dtype=torch.uint8, device=dev)
         nseg = (in_len - 40 + gso - 1) // gso
         out_len = in_len - 40 + nseg * 40
 
         def launch():
-            wga.gso_split(buf, d_desc, out, results=res)
+            wga.gso_split(buf, d_desc, outb, results=res)
 
         cfg = {"workload": "config3: 262,144 x 64 KiB GSO super-buffers (IPv4/TCP, 65535 B) -> 45 x 1460 B "
                            "segments each, fused copy + header fix-up + IPv4/TCP checksums",
                "super_buffers_per_gpu": n, "gso_size": gso, "segments_per_buffer": nseg,
                "parallelism": f"shard{world}"}
         alg = n * in_len + n * out_len + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES)
-
-        def sample(npk):
-            return None, None, ("gso",)
-
-        return launch, n, n * in_len, alg, cfg, sample, "weak", buf
+        return Workload(launch, n, n * in_len, alg, cfg, "weak", buf, "wg::gso_split_kernel<4,2,0>",
+                        rank * n, counts=[n] * world)
     # config4 bimodal
-    import numpy as np
-
     n = 1 << 22
-    seed = 0x5EED0004
+    seed = 0x5EED0004 + rank
     rng = np.random.default_rng(seed)
     lens = np.where(rng.random(n) < 0.5, 64, 9000).astype(np.int64)
     offs = np.concatenate([[0], np.cumsum(lens[:-1])])
@@ -157,26 +174,23 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev):
     def launch():
         wga.calc_l4_checksum_desc(buf, desc, out=out)
 
-    cfg = {"workload": "config4: 4,194,304 IPv4/UDP packets, 64 B / 9000 B 50/50, packed, descriptor batch",
-           "packets_per_gpu": n, "layout": "descriptor", "parallelism": f"shard{world}"}
-    alg = total + 2 * n + 16 * n
-
     def sample(npk):
         end = int(offs[npk - 1] + lens[npk - 1])
         return buf[:end].cpu().numpy(), out[:npk].cpu().numpy(), ("desc", raw[:npk])
 
-    return launch, n, total, alg, cfg, sample, "weak", buf
+    cfg = {"workload": "config4: 4,194,304 IPv4/UDP packets, 64 B / 9000 B 50/50, packed, descriptor batch",
+           "packets_per_gpu": n, "layout": "descriptor", "parallelism": f"shard{world}"}
+    return Workload(launch, n, total, total + 2 * n + 16 * n, cfg, "weak", buf, "wg::l4csum_kernel<1,4,nt>",
+                    rank * n, out, desc, sample, [n] * world)
 
 
 def settle(torch, fn, seconds: float) -> int:
     """Run `fn` back to back until `seconds` of wall time have passed, so the
     timed region starts at the sustained clock/memory state rather than the
     idle ramp (MI355X: the first ~10 launches run up to 30% slower)."""
-    import time as _t
-
-    t0 = _t.perf_counter()
+    t0 = time.perf_counter()
     k = 0
-    while _t.perf_counter() - t0 < seconds:
+    while time.perf_counter() - t0 < seconds:
         for _ in range(20):
             fn()
         k += 20
@@ -188,7 +202,7 @@ def measured_read_peak(torch, wga, buf, iters: int = 30) -> float:
     """Read-roofline probe over the batch buffer itself: the same bytes,
     read by the same access structure with no checksum work (GB/s)."""
     acc = torch.zeros(1, dtype=torch.int64, device=buf.device)
-    n = buf.numel() // 16 * 16
+    n = min(buf.numel(), 4 << 30) // 16 * 16
     view = buf[:n]
     best = 0.0
     for kib in (2, 4, 8):
@@ -214,8 +228,6 @@ def cpu_baseline(sample_fn, seconds: float):
     # host's last-level cache (EPYC 9575F: 256 MB L3) between repetitions.
     npk = 1 << 19
     host, gpu_out, kind = sample_fn(npk)
-    if kind[0] == "gso":
-        return None
     threads = oracle.default_threads()
     if kind[0] == "uniform":
         _, seg, cs, fl = kind
@@ -252,7 +264,8 @@ def cpu_baseline(sample_fn, seconds: float):
         "value_1core": nbytes / t_1core / 2**30,
         "cpu_model": cpu_model,
         "sample": f"first {npk} packets ({nbytes} B) of the same batch, oracle/csum_oracle.c "
-                  f"(calc_l4_checksum restatement), {threads} pthreads; bit-exact vs GPU: {parity}",
+                  f"(calc_l4_checksum restatement), {threads} pthreads, ~{seconds:.1f} s wall; "
+                  f"bit-exact vs GPU: {parity}",
         "parity_with_gpu": parity,
     }
 
@@ -270,27 +283,61 @@ def load_traffic(workload: str):
         return None
 
 
+def post_checks(torch, wga, wl: Workload, world: int, dev):
+    """Outside the timed region: verify pass, result hash, RCCL gather."""
+    from wireglider_amd import dist as wdist
+
+    info = {}
+    if wl.out is None:
+        return info
+    torch.cuda.synchronize()
+    h = wdist.allreduce_hash(wdist.result_hash(wl.out, wl.first_index))
+    info["result_hash"] = h
+    t0 = time.perf_counter()
+    full = wdist.gather_results(wl.out, wl.counts)
+    torch.cuda.synchronize()
+    info["gather_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+    info["gathered_results"] = int(full.numel())
+    # generate -> store -> verify (offload.cpp:202-204, evaluator.hpp:64,93)
+    wga.store_l4csum(wl.buf, wl.desc, wl.out)
+    ver = wga.calc_l4_checksum_desc(wl.buf, wl.desc)
+    bad = torch.count_nonzero(ver.to(torch.int32)).to(torch.int64).reshape(1)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.all_reduce(bad, op=dist.ReduceOp.SUM)
+    info["verify_nonzero"] = int(bad.item())
+    return info
+
+
 def main():
     args = parse()
     import torch
     import torch.distributed as dist
 
     import wireglider_amd as wga
+    from wireglider_amd import dist as wdist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+    # one process per GPU; WG_DIST_BACKEND=gloo (with ranks sharing a GPU)
+    # only rehearses the multi-rank logic on a one-GPU box
+    backend = os.environ.get("WG_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
-    launch, n, payload, alg, cfg, sample, scaling, batch_buf = build_workload(wga, torch, args.workload, rank, world,
-                                                                            dev)
+    wl = build_workload(wga, torch, args.workload, rank, world, dev)
     torch.cuda.synchronize()
-    settled = settle(torch, launch, args.settle_seconds)
+    settled = settle(torch, wl.launch, args.settle_seconds)
 
     def barrier():
         if world > 1:
@@ -298,7 +345,7 @@ def main():
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        launch()
+        wl.launch()
     barrier()
 
     # Timed region: exactly K launches, per-launch HIP events on the launch stream.
@@ -308,29 +355,27 @@ def main():
     t0 = time.perf_counter()
     for e0, e1 in evs:
         e0.record(stream)
-        launch()
+        wl.launch()
         e1.record(stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
-    wall = t1 - t0
     kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / args.steps
+    wall = wdist.max_over_ranks(t1 - t0, dev)
+    kern_ms_max = wdist.max_over_ranks(kern_ms, dev)
     if world > 1:
-        t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall, kern_ms_max = float(t[0]), float(t[1])
-        tot = torch.tensor([payload], dtype=torch.float64, device=dev)
+        tot = torch.tensor([wl.payload_bytes], dtype=torch.float64, device=dev)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         total_payload = float(tot[0])
     else:
-        kern_ms_max = kern_ms
-        total_payload = float(payload)
+        total_payload = float(wl.payload_bytes)
 
     ms_per_step = wall / args.steps * 1e3
     value = total_payload * args.steps / wall / 2**30
-    achieved = alg / (kern_ms * 1e-3) / 1e9
+    achieved = wl.alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args.workload)
-    read_peak = measured_read_peak(torch, wga, batch_buf) if rank == 0 else None
+    read_peak = measured_read_peak(torch, wga, wl.buf) if rank == 0 else None
+    post = post_checks(torch, wga, wl, world, dev)
     line = {
         "metric": "device-resident GiB/s, L4 checksum over packet batch; 1/2/4/8 MI355X",
         "value": round(value, 3),
@@ -341,11 +386,11 @@ def main():
         "settle_launches": settled,
         "ms_per_step": round(ms_per_step, 5),
         "higher_is_better": True,
-        "scaling": scaling,
+        "scaling": wl.scaling,
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (device-generated, seeded; BASELINE config shapes)",
-        "config": cfg,
+        "config": wl.cfg,
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved, 2),
@@ -353,17 +398,18 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "wg::gso_split_kernel" if args.workload == "config3" else "wg::l4csum_kernel",
-            "alg_bytes_per_launch": alg,
-            "traffic_source": "profiles/pmc_%s.json (rocprofv3 FETCH_SIZEx2 + WRITE_SIZE, per launch)" % args.workload,
+            "kernel": wl.kernel,
+            "alg_bytes_per_launch": wl.alg_bytes,
+            "traffic_source": f"profiles/pmc_{args.workload}.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)",
             "measured_read_peak": round(read_peak, 1) if read_peak else None,
             "frac_of_measured_read_peak": round(achieved / read_peak, 4) if read_peak else None,
             "kernel_ms_avg": round(kern_ms, 5),
             "kernel_ms_avg_max_over_ranks": round(kern_ms_max, 5),
         },
+        "post_checks": post,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(sample, args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and wl.sample is not None:
+        line["cpu_baseline"] = cpu_baseline(wl.sample, args.cpu_seconds)
     elif rank == 0:
         line["cpu_baseline"] = None
     if rank == 0:

@@ -1,0 +1,114 @@
+"""World-size-2 (and 3) gloo tests of the sharded path on CPU.
+
+The sharding, result gather and hash reduction are the same code the GPU
+bench runs over RCCL; here each rank's per-shard compute is the CPU oracle
+(test infrastructure), so the test checks that the sharded job reproduces
+the single-process answer bit for bit.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from wireglider_amd import dist as wdist
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def make_batch(n, seed=5):
+    """Deterministic variable-length batch: (bytes, desc structured array)."""
+    import oracle
+
+    rng = np.random.default_rng(seed)
+    lens = np.where(rng.random(n) < 0.5, 64, rng.integers(40, 3000, n)).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)])
+    buf = rng.integers(0, 256, int(offs[-1] + lens[-1]), dtype=np.uint8)
+    d = np.zeros(n, dtype=oracle.PKT_DESC)
+    d["offset"], d["len"] = offs, lens
+    d["flags"] = rng.integers(0, 4, n)
+    d["csum_start"] = np.where(d["flags"] & 1, 40, 20)
+    return buf, d
+
+
+def _worker(rank, world, port, n, q):
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "oracle"), str(root / "tests")]
+    import oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        buf, d = make_batch(n)
+        bounds = wdist.shard_bounds_by_bytes(d["len"], world)
+        lo, hi = bounds[rank]
+        local = torch.from_numpy(oracle.l4_desc(buf, d[lo:hi], threads=1).astype(np.int32)).to(torch.uint16)
+        full = wdist.gather_results(local, [b - a for a, b in bounds])
+        h = wdist.allreduce_hash(wdist.result_hash(local, lo))
+        t = wdist.max_over_ranks(float(rank + 1))
+        if rank == 0:
+            q.put((full.numpy().astype(np.uint16).tobytes(), h, t, bounds))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_equals_single_process(world):
+    import oracle
+
+    n = 3000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    full_bytes, h, t, bounds = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    buf, d = make_batch(n)
+    ref = oracle.l4_desc(buf, d)
+    got = np.frombuffer(full_bytes, dtype=np.uint16)
+    np.testing.assert_array_equal(got, ref)
+    assert h == wdist.result_hash(torch.from_numpy(ref.astype(np.int32)), 0).item() % wdist.HASH_MOD
+    assert t == float(world)
+    # byte balance: each shard within one max-size packet of the mean
+    per = [int(d["len"][a:b].astype(np.int64).sum()) for a, b in bounds]
+    assert max(per) - min(per) <= 2 * int(d["len"].max())
+
+
+def test_shard_bounds_properties():
+    assert wdist.shard_bounds(10, 3, 0) == (0, 3)
+    assert wdist.shard_bounds(10, 3, 2) == (6, 10)
+    rng = np.random.default_rng(0)
+    for world in (1, 2, 4, 8):
+        lens = np.where(rng.random(10001) < 0.5, 64, 9000)
+        b = wdist.shard_bounds_by_bytes(lens, world)
+        assert b[0][0] == 0 and b[-1][1] == lens.size
+        assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+        per = [int(lens[x:y].sum()) for x, y in b]
+        assert max(per) - min(per) <= 2 * 9000
+    # degenerate: more ranks than packets
+    b = wdist.shard_bounds_by_bytes([100, 100], 4)
+    assert sum(y - x for x, y in b) == 2
+
+
+def test_hash_is_split_invariant():
+    v = torch.randint(0, 65536, (1000,), dtype=torch.int32).to(torch.uint16)
+    whole = wdist.result_hash(v, 0).item()
+    parts = (wdist.result_hash(v[:300], 0) + wdist.result_hash(v[300:], 300)).item() % wdist.HASH_MOD
+    assert whole == parts

@@ -24,7 +24,8 @@ def main():
     import wireglider_amd as wga
 
     dev = torch.device("cuda:0")
-    launch, n, payload, alg, cfg, sample, _, _ = bench.build_workload(wga, torch, args.workload, 0, 1, dev)
+    wl = bench.build_workload(wga, torch, args.workload, 0, 1, dev)
+    launch, payload, alg = wl.launch, wl.payload_bytes, wl.alg_bytes
     buf = torch.empty(payload // 16 * 16, dtype=torch.uint8, device=dev)
     buf.fill_(3)
     acc = torch.zeros(1, dtype=torch.int64, device=dev)

@@ -18,7 +18,8 @@ def main():
     import wireglider_amd as wga
 
     dev = torch.device("cuda:0")
-    launch, n, payload, alg, cfg, sample, _, _ = bench.build_workload(wga, torch, "config3", 0, 1, dev)
+    wl = bench.build_workload(wga, torch, "config3", 0, 1, dev)
+    launch, payload, alg = wl.launch, wl.payload_bytes, wl.alg_bytes
     torch.cuda.synchronize()
     variants = list(itertools.product([4, 8], [1, 2], [1, 2, 4, 8, 12]))
     res = {v: [] for v in variants}

@@ -31,7 +31,8 @@ def main():
     import wireglider_amd as wga
 
     dev = torch.device("cuda:0")
-    launch, n, payload, alg, cfg, sample, _, _ = bench.build_workload(wga, torch, args.workload, 0, 1, dev)
+    wl = bench.build_workload(wga, torch, args.workload, 0, 1, dev)
+    launch, payload, alg = wl.launch, wl.payload_bytes, wl.alg_bytes
     torch.cuda.synchronize()
 
     def timeit(fn, iters):
