@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--nt", default="0,1")
     ap.add_argument("--blocks", default="1024,2048,4096,16384")
     ap.add_argument("--probe", action="store_true")
+    ap.add_argument("--descv", default="0")
     args = ap.parse_args()
     import torch
 
@@ -45,12 +46,13 @@ def main():
         return [e0.elapsed_time(e1) for e0, e1 in ev]
 
     variants = list(itertools.product([int(x) for x in args.ppw.split(",")], [int(x) for x in args.nt.split(",")],
-                                      [int(x) for x in args.blocks.split(",")]))
+                                      [int(x) for x in args.blocks.split(",")], [int(x) for x in args.descv.split(",")]))
     res = {v: [] for v in variants}
     ref_out = None
     for r in range(args.rounds):
         for v in variants:
-            ppw, nt, blocks = v
+            ppw, nt, blocks, dv = v
+            wga.tune_set("l4_descv", dv)
             wga.tune_set("l4_ppw", ppw)
             wga.tune_set("l4_nt", nt)
             wga.tune_set("l4_blocks", blocks)
@@ -59,7 +61,7 @@ def main():
     rows = []
     for v, ts in res.items():
         med = statistics.median(ts)
-        rows.append({"ppw": v[0], "nt": v[1], "blocks": v[2], "ms_med": round(med, 4), "ms_min": round(min(ts), 4),
+        rows.append({"ppw": v[0], "nt": v[1], "blocks": v[2], "descv": v[3], "ms_med": round(med, 4), "ms_min": round(min(ts), 4),
                      "GBps_med": round(alg / (med * 1e-3) / 1e9, 1)})
     rows.sort(key=lambda x: x["ms_med"])
     out = {"workload": args.workload, "alg_bytes": alg, "variants": rows}

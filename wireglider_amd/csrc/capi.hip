@@ -31,6 +31,7 @@ Tune &tune_mut() {
         x.l4_blocks = env_u64("WG_L4_BLOCKS", 1u << 20);
         x.l4_ppw = (uint32_t)env_u64("WG_L4_PPW", 4);
         x.l4_nt = (uint32_t)env_u64("WG_L4_NT", 1);
+        x.l4_descv = (uint32_t)env_u64("WG_L4_DESCV", 0);
         x.gso_blocks = env_u64("WG_GSO_BLOCKS", 1u << 20);
         // GSO: one 4-wave block per super-buffer, 2 segments in flight per
         // wave (tools/tune_gso.py, profiles/r01_tune_gso.json).
@@ -214,6 +215,8 @@ extern "C" int wg_tune_set(const char *key, uint64_t value) {
         t.l4_ppw = (uint32_t)value;
     else if (k == "l4_nt" && value <= 1)
         t.l4_nt = (uint32_t)value;
+    else if (k == "l4_descv" && value <= 1)
+        t.l4_descv = (uint32_t)value;
     else if (k == "gso_blocks" && value >= 1 && value <= (1u << 20))
         t.gso_blocks = value;
     else if (k == "gso_waves" && (value == 4 || value == 8 || value == 16))

@@ -65,7 +65,32 @@ __device__ __forceinline__ Geom load_geom(const L4Params &p, uint64_t i) {
     return g;
 }
 
-template <int kKind, int P, bool kNT>
+// Descriptors of packets i0 .. i0+P-1 with ONE coalesced vector load (lane j
+// holds descriptor j) instead of P scalar loads, then v_readlane to make them
+// wave-uniform.
+template <int kKind, int P>
+__device__ __forceinline__ void load_geoms_vec(const L4Params &p, uint64_t i0, uint32_t lane, Geom *g) {
+    const uint64_t di = i0 + (lane & (uint32_t)(P - 1));
+    const uint64_t dc = di < p.n ? di : p.n - 1;
+    const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * dc);
+#pragma unroll
+    for (int j = 0; j < P; j++) {
+        if (i0 + j >= p.n) {  // padding slot: empty packet
+            g[j].a = reinterpret_cast<uintptr_t>(p.base);
+            g[j].len = g[j].cs = g[j].fl = 0;
+            continue;
+        }
+        const uint64_t off = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dv.x, j) |
+                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dv.y, j) << 32);
+        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)dv.w, j);
+        g[j].a = reinterpret_cast<uintptr_t>(p.base) + off;
+        g[j].len = (uint32_t)__builtin_amdgcn_readlane((int)dv.z, j);
+        g[j].cs = kKind == kDescPlain ? 0u : (w & 0xffffu);
+        g[j].fl = (w >> 16) & 0xffu;
+    }
+}
+
+template <int kKind, int P, bool kNT, bool kVD>
 __global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
     constexpr bool kL4 = kKind != kDescPlain;
     const uint32_t lane = lane_id();
@@ -74,9 +99,12 @@ __global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
     for (uint64_t i0 = wave0 * P; i0 < p.n; i0 += step) {
         Geom g[P];
         Front f[P];
+        if constexpr (kVD && kKind != kUniformL4)
+            load_geoms_vec<kKind, P>(p, i0, lane, g);
 #pragma unroll
         for (int j = 0; j < P; j++) {
-            g[j] = load_geom<kKind>(p, i0 + j);
+            if constexpr (!(kVD && kKind != kUniformL4))
+                g[j] = load_geom<kKind>(p, i0 + j);
             issue<kL4, kNT>(g[j], lane, f[j]);
         }
         uint32_t res = 0;
@@ -101,7 +129,10 @@ __global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
 
 template <int kKind, int P, bool kNT>
 static void launch_variant(const L4Params &p, uint64_t blocks, hipStream_t st) {
-    hipLaunchKernelGGL((l4csum_kernel<kKind, P, kNT>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+    if (kKind != kUniformL4 && tune().l4_descv)
+        hipLaunchKernelGGL((l4csum_kernel<kKind, P, kNT, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+    else
+        hipLaunchKernelGGL((l4csum_kernel<kKind, P, kNT, false>), dim3((unsigned)blocks), dim3(256), 0, st, p);
 }
 
 template <int kKind>

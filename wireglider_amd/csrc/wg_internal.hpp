@@ -12,6 +12,7 @@ struct Tune {
     uint64_t l4_blocks;   // grid cap for the wave-per-packet checksum kernels
     uint32_t l4_ppw;      // packets per wave iteration (1, 2, 4, 8)
     uint32_t l4_nt;       // 1: non-temporal packet loads
+    uint32_t l4_descv;    // 1: descriptors by one vector load per wave (else scalar loads)
     uint64_t gso_blocks;  // grid cap for the GSO split kernel (one block per super-buffer)
     uint32_t gso_waves;   // waves per block (4, 8, 16)
     uint32_t gso_split;   // blocks per super-buffer (grid y)
