@@ -153,7 +153,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                "super_buffers_per_gpu": n, "gso_size": gso, "segments_per_buffer": nseg,
                "parallelism": f"shard{world}"}
         alg = n * in_len + n * out_len + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES)
-        return Workload(launch, n, n * in_len, alg, cfg, "weak", buf, "wg::gso_split_kernel<4,2,0>",
+        return Workload(launch, n, n * in_len, alg, cfg, "weak", buf, "wg::gso_split_kernel<4,1,0> (pipelined)",
                         rank * n, counts=[n] * world)
     # config4 bimodal
     n = 1 << 22

@@ -202,7 +202,8 @@ int wg_device_count(void);
  * "l4_ppw" (packets per wave iteration: 1, 2, 4, 8), "l4_nt" (0/1
  * non-temporal loads), "l4_descv" (0/1: descriptors by one vector load per
  * wave instead of scalar loads), "gso_blocks", "gso_waves" (waves per block: 4, 8, 16),
- * "gso_split" (blocks per super-buffer, 1-64), "gso_spw" (segments in flight per wave: 1, 2), "gso_ablate"
+ * "gso_split" (blocks per super-buffer, 1-64), "gso_spw" (1: ping-pong pipeline of segments per wave,
+ * 2: two segments issued then finished), "gso_ablate"
  * (profiling only: 1 = non-temporal payload stores; 2..7 select timing-only
  * GSO variants whose output is WRONG; 0 restores the default kernel).  Results never depend on the geometry
  * knobs.  Not synchronised with concurrent launches from other threads. */

@@ -33,11 +33,12 @@ Tune &tune_mut() {
         x.l4_nt = (uint32_t)env_u64("WG_L4_NT", 1);
         x.l4_descv = (uint32_t)env_u64("WG_L4_DESCV", 0);
         x.gso_blocks = env_u64("WG_GSO_BLOCKS", 1u << 20);
-        // GSO: one 4-wave block per super-buffer, 2 segments in flight per
-        // wave (tools/tune_gso.py, profiles/r01_tune_gso.json).
+        // GSO: one 4-wave block per super-buffer, each wave a ping-pong
+        // pipeline (next segment's loads in flight while this one finishes)
+        // (tools/tune_gso.py, profiles/r01_tune_gso*.json).
         x.gso_waves = (uint32_t)env_u64("WG_GSO_WAVES", 4);
         x.gso_split = (uint32_t)env_u64("WG_GSO_SPLIT", 1);
-        x.gso_spw = (uint32_t)env_u64("WG_GSO_SPW", 2);
+        x.gso_spw = (uint32_t)env_u64("WG_GSO_SPW", 1);
         x.gso_ablate = 0;
         return x;
     }();

@@ -187,22 +187,51 @@ __device__ __forceinline__ void st8(uintptr_t addr, uint32_t b) {
 }
 
 // One output segment by one wave, in two phases so a wave can have several
-// segments' loads in flight: seg_issue() computes the geometry and issues
-// every load of the segment (branch-free: clamped addresses, masked use);
-// seg_finish() re-aligns, stores, sums and writes the header.
+// segments' loads in flight: seg_issue() issues every load of the segment
+// (branch-free: clamped addresses, masked use); seg_finish() re-aligns,
+// stores, sums and writes the header.  Only the loaded data and the segment
+// index cross the phase boundary; the (scalar) geometry is recomputed, which
+// keeps the scalar register file from spilling.
+struct SegGeom {
+    uintptr_t seg, oa, ob, d, c0, c1, sa, smin, smax, a0;
+    uint32_t datalen, pktlen, nint, q, r;
+    bool last;
+};
+
+__device__ __forceinline__ SegGeom seg_geom(const Ctx &c, uintptr_t out_base, uint32_t i) {
+    SegGeom g;
+    g.seg = out_base + (uintptr_t)i * (c.hdr_len + c.gso);
+    const uint32_t off = i * c.gso;
+    g.datalen = c.rest - off < c.gso ? c.rest - off : c.gso;
+    g.pktlen = c.hdr_len + g.datalen;
+    g.last = i + 1 == c.nseg;
+    g.oa = g.seg + c.hdr_len;  // payload, destination
+    g.ob = g.seg + g.pktlen;
+    g.sa = c.in + c.hdr_len + off;  // payload, source
+    g.d = g.sa - g.oa;              // source = destination + d (mod 2^64)
+    const uint32_t delta = (uint32_t)(g.d & 15u);
+    g.q = delta >> 2;
+    g.r = delta & 3u;
+    g.c0 = (g.oa + 15) & ~(uintptr_t)15;  // destination-aligned interior chunks
+    g.c1 = g.ob & ~(uintptr_t)15;
+    g.nint = g.c1 > g.c0 ? (uint32_t)((g.c1 - g.c0) >> 4) : 0u;
+    g.smin = g.sa & ~(uintptr_t)15;
+    g.smax = (g.sa + g.datalen - 1) & ~(uintptr_t)15;
+    g.a0 = (g.c0 + g.d) & ~(uintptr_t)15;
+    return g;
+}
+
 struct SegFront {
-    uintptr_t seg, c0, d, xb, sa, smin, smax, a0;
-    uint32_t pktlen, nint, q, r, pb, i;
-    bool last, bh, btl;
+    uint32_t i, pb;
     v4u lo0, lo1;  // source chunks a0 + 16 * lane and a0 + 16 * (lane + 64)
 };
 
-// Source chunk m of the segment (a0 = aligned source of output chunk 0),
-// clamped into the chunks that hold payload bytes: the clamp never changes a
-// byte an in-range output chunk needs, and keeps every load in bounds.
-__device__ __forceinline__ v4u src_chunk(const SegFront &f, uint64_t m) {
-    uintptr_t A = f.a0 + 16ull * m;
-    A = A < f.smin ? f.smin : (A > f.smax ? f.smax : A);
+// Source chunk m of the segment, clamped into the chunks that hold payload
+// bytes: the clamp never changes a byte an in-range output chunk needs, and
+// keeps every load in bounds.
+__device__ __forceinline__ v4u src_chunk(const SegGeom &g, uint64_t m) {
+    uintptr_t A = g.a0 + 16ull * m;
+    A = A < g.smin ? g.smin : (A > g.smax ? g.smax : A);
     return ld16(A);
 }
 
@@ -229,71 +258,61 @@ __device__ __forceinline__ v4u lane0(v4u v) {
     return r;
 }
 
-template <int Abl>
-__device__ __forceinline__ void seg_issue(const Ctx &c, uintptr_t out_base, uint32_t i, uint32_t lane, SegFront &f) {
-    f.i = i;
-    f.seg = out_base + (uintptr_t)i * (c.hdr_len + c.gso);
-    const uint32_t off = i * c.gso;
-    const uint32_t datalen = c.rest - off < c.gso ? c.rest - off : c.gso;
-    f.pktlen = c.hdr_len + datalen;
-    f.last = i + 1 == c.nseg;
-
-    // payload geometry (destination-aligned chunks)
-    const uintptr_t oa = f.seg + c.hdr_len, ob = f.seg + f.pktlen;
-    f.sa = c.in + c.hdr_len + off;
-    f.d = f.sa - oa;  // source = destination + d (mod 2^64)
-    const uint32_t delta = (uint32_t)(f.d & 15u);
-    f.q = delta >> 2;
-    f.r = delta & 3u;
-    f.c0 = (oa + 15) & ~(uintptr_t)15;
-    const uintptr_t c1 = ob & ~(uintptr_t)15;
-    f.nint = c1 > f.c0 ? (uint32_t)((c1 - f.c0) >> 4) : 0u;
-    f.smin = f.sa & ~(uintptr_t)15;
-    f.smax = (f.sa + datalen - 1) & ~(uintptr_t)15;
-    f.a0 = (f.c0 + f.d) & ~(uintptr_t)15;
-    f.lo0 = src_chunk(f, lane);
-    f.lo1 = src_chunk(f, lane + 64);
-
-    // head bytes [oa, min(c0, ob)) on lanes 0-15, tail [max(c1, c0), ob) on 16-31
-    const uintptr_t he = f.c0 < ob ? f.c0 : ob;
-    const uintptr_t ts = c1 > f.c0 ? c1 : f.c0;
-    const uintptr_t xh = oa + lane, xt = ts + (lane - 16);
-    f.bh = lane < 16 && xh < he;
-    f.btl = lane >= 16 && lane < 32 && xt < ob;
-    f.xb = f.bh ? xh : xt;
-    f.pb = ld8((f.bh || f.btl) ? f.xb + f.d : f.sa);
+// Payload head [oa, min(c0, ob)) on lanes 0-15, tail [max(c1, c0), ob) on
+// lanes 16-31: this lane's byte address, or 0.
+__device__ __forceinline__ uintptr_t edge_byte(const SegGeom &g, uint32_t lane) {
+    const uintptr_t he = g.c0 < g.ob ? g.c0 : g.ob;
+    const uintptr_t ts = g.c1 > g.c0 ? g.c1 : g.c0;
+    const uintptr_t xh = g.oa + lane, xt = ts + (lane - 16);
+    if (lane < 16 && xh < he)
+        return xh;
+    if (lane >= 16 && lane < 32 && xt < g.ob)
+        return xt;
+    return 0;
 }
 
 template <int Abl>
-__device__ __forceinline__ void seg_finish(const Ctx &c, const SegFront &f, uint32_t lane) {
-    const uint32_t i = f.i, pktlen = f.pktlen;
+__device__ __forceinline__ void seg_issue(const Ctx &c, uintptr_t out_base, uint32_t i, uint32_t lane, SegFront &f) {
+    const SegGeom g = seg_geom(c, out_base, i);
+    f.i = i;
+    f.lo0 = src_chunk(g, lane);
+    f.lo1 = src_chunk(g, lane + 64);
+    const uintptr_t xb = edge_byte(g, lane);
+    f.pb = ld8(xb ? xb + g.d : g.sa);
+}
+
+template <int Abl>
+__device__ __forceinline__ void seg_finish(const Ctx &c, uintptr_t out_base, const SegFront &f, uint32_t lane) {
+    const SegGeom g = seg_geom(c, out_base, f.i);
+    const uint32_t i = f.i, pktlen = g.pktlen;
     Acc acc;
     // payload: re-align, store, sum
-    if (f.nint) {
-        const v4u nx1 = f.nint > 127 ? lane0(src_chunk(f, 128)) : f.lo1;
+    if (g.nint) {
+        const v4u nx1 = g.nint > 127 ? lane0(src_chunk(g, 128)) : f.lo1;
         const v4u hi0 = next_chunk(f.lo0, lane0(f.lo1), lane);
         const v4u hi1 = next_chunk(f.lo1, nx1, lane);
-        if (lane < f.nint) {
-            const v4u v = funnel(f.lo0, (Abl & kAblOneLoad) ? f.lo0 : hi0, f.q, f.r);
-            st16x<Abl>(f.c0 + 16ull * lane, v);
+        if (lane < g.nint) {
+            const v4u v = funnel(f.lo0, (Abl & kAblOneLoad) ? f.lo0 : hi0, g.q, g.r);
+            st16x<Abl>(g.c0 + 16ull * lane, v);
             acc.add4(v);
         }
-        if (lane + 64 < f.nint) {
-            const v4u v = funnel(f.lo1, (Abl & kAblOneLoad) ? f.lo1 : hi1, f.q, f.r);
-            st16x<Abl>(f.c0 + 16ull * (lane + 64), v);
+        if (lane + 64 < g.nint) {
+            const v4u v = funnel(f.lo1, (Abl & kAblOneLoad) ? f.lo1 : hi1, g.q, g.r);
+            st16x<Abl>(g.c0 + 16ull * (lane + 64), v);
             acc.add4(v);
         }
-        for (uint32_t k = lane + 128; k < f.nint; k += 64) {  // long segments (gso > ~2 KiB)
-            const v4u lo = src_chunk(f, k);
-            const v4u v = funnel(lo, src_chunk(f, k + 1), f.q, f.r);
-            st16x<Abl>(f.c0 + 16ull * k, v);
+        for (uint32_t k = lane + 128; k < g.nint; k += 64) {  // long segments (gso > ~2 KiB)
+            const v4u lo = src_chunk(g, k);
+            const v4u v = funnel(lo, src_chunk(g, k + 1), g.q, g.r);
+            st16x<Abl>(g.c0 + 16ull * k, v);
             acc.add4(v);
         }
     }
-    if (f.bh || f.btl) {
+    const uintptr_t xb = edge_byte(g, lane);
+    if (xb) {
         if (!(Abl & kAblNoByteStores))
-            st8(f.xb, f.pb);
-        acc.add(f.pb << (8u * (uint32_t)(f.xb & 1u)));
+            st8(xb, f.pb);
+        acc.add(f.pb << (8u * (uint32_t)(xb & 1u)));
     }
 
     // checksums: the invariant header sums plus this segment's fields
@@ -304,12 +323,12 @@ __device__ __forceinline__ void seg_finish(const Ctx &c, const SegFront &f, uint
     uint32_t l4h = c.l4h_base;
     if (c.tcp) {
         const uint32_t seq = c.seq0 + c.gso * i;
-        l4h += bswap16(seq >> 16) + bswap16(seq & 0xffffu) + ((f.last ? c.flags13 : (c.flags13 & ~0x09u)) << 8);
+        l4h += bswap16(seq >> 16) + bswap16(seq & 0xffffu) + ((g.last ? c.flags13 : (c.flags13 & ~0x09u)) << 8);
     } else {
         l4h += bswap16((pktlen - c.cs) & 0xffffu);
     }
     uint32_t lp = fold16(acc.value());
-    if ((f.seg + c.cs) & 1u)  // payload summed in absolute pairing; the L4 region pairs from seg + cs
+    if ((g.seg + c.cs) & 1u)  // payload summed in absolute pairing; the L4 region pairs from seg + cs
         lp = bswap16(lp);
     uint32_t T = wave_sum_u32(lp) + l4h + c.ps_sum;
     T += ((c.tcp ? 6u : 17u) << 8) + bswap16((pktlen - c.cs) & 0xffffu);
@@ -324,16 +343,16 @@ __device__ __forceinline__ void seg_finish(const Ctx &c, const SegFront &f, uint
         if (j == c.l4off + 1) return l4cs >> 8;
         return s4;
     };
-    auto s4 = [&](uint32_t j, uint32_t b) { return stage_l4(c, j, stage_ip(c, j, b, i, pktlen), i, pktlen, f.last); };
+    auto s4 = [&](uint32_t j, uint32_t b) { return stage_l4(c, j, stage_ip(c, j, b, i, pktlen), i, pktlen, g.last); };
     if (Abl & kAblNoByteStores) {
-        if (lane == 0 && l4cs == 0x12345u) st8(f.seg, 0);  // keep the sums live
+        if (lane == 0 && l4cs == 0x12345u) st8(g.seg, 0);  // keep the sums live
         return;
     }
-    if (j0 < c.hdr_len) st8(f.seg + j0, final_byte(j0, s4(j0, c.hb0)));
-    if (j1 < c.hdr_len) st8(f.seg + j1, final_byte(j1, s4(j1, c.hb1)));
+    if (j0 < c.hdr_len) st8(g.seg + j0, final_byte(j0, s4(j0, c.hb0)));
+    if (j1 < c.hdr_len) st8(g.seg + j1, final_byte(j1, s4(j1, c.hb1)));
     for (uint32_t j = lane + 128; j < c.hdr_len; j += 64) {
         const uint32_t b2 = stage_ip(c, j, ld8(c.in + j), i, pktlen);
-        st8(f.seg + j, final_byte(j, stage_l4(c, j, b2, i, pktlen, f.last)));
+        st8(g.seg + j, final_byte(j, stage_l4(c, j, b2, i, pktlen, g.last)));
     }
 }
 
@@ -496,15 +515,37 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
             }
             hdr_bases(c, lane);
             const uintptr_t out_base = reinterpret_cast<uintptr_t>(p.out) + dsc.out_offset;
-            for (uint32_t i0 = gw * S; i0 < c.nseg; i0 += gstride) {
-                SegFront f[S];
+            if constexpr (S == 1) {
+                // ping-pong software pipeline: the next segment's loads are in
+                // flight while this one is re-aligned, stored and summed
+                const uint32_t last = c.nseg - 1;
+                uint32_t i = gw;
+                SegFront A, B;
+                seg_issue<Abl>(c, out_base, i, lane, A);
+                for (;;) {
+                    const uint32_t i1 = i + gstride;
+                    seg_issue<Abl>(c, out_base, i1 < last ? i1 : last, lane, B);
+                    seg_finish<Abl>(c, out_base, A, lane);
+                    if (i1 > last)
+                        break;
+                    const uint32_t i2 = i1 + gstride;
+                    seg_issue<Abl>(c, out_base, i2 < last ? i2 : last, lane, A);
+                    seg_finish<Abl>(c, out_base, B, lane);
+                    if (i2 > last)
+                        break;
+                    i = i2;
+                }
+            } else {
+                for (uint32_t i0 = gw * S; i0 < c.nseg; i0 += gstride) {
+                    SegFront f[S];
 #pragma unroll
-                for (int k = 0; k < S; k++)
-                    seg_issue<Abl>(c, out_base, i0 + k < c.nseg ? i0 + k : c.nseg - 1, lane, f[k]);
+                    for (int k = 0; k < S; k++)
+                        seg_issue<Abl>(c, out_base, i0 + k < c.nseg ? i0 + k : c.nseg - 1, lane, f[k]);
 #pragma unroll
-                for (int k = 0; k < S; k++)
-                    if (i0 + k < c.nseg)
-                        seg_finish<Abl>(c, f[k], lane);
+                    for (int k = 0; k < S; k++)
+                        if (i0 + k < c.nseg)
+                            seg_finish<Abl>(c, out_base, f[k], lane);
+                }
             }
         } else if (cl.inplace && gw == 0) {
             c.tcp = (cl.isv6 ? pbyte(c, 6) : pbyte(c, 9)) == 6;  // :67-70
