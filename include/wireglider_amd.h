@@ -108,6 +108,27 @@ int wg_checksum_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_desc, uint6
                      uint16_t *dev_out, void *stream);
 
 /* ------------------------------------------------------------------------
+ * Decap verify gates, batched: per packet the checksum
+ * decisions of evaluate_packet (include/worker/evaluator.hpp:112-149):
+ * size bounds (20/40 <= len <= 65535), fill_fk_ip4 (worker/evaluator.cpp:14-40:
+ * ihl == 5, len == ip_len, (ip_off & ~IP_DF) == 0, IPv4 header checksum == 0)
+ * or fill_fk_ip6 (:42-58: len - 40 == ip6_plen), then for TCP len - ihs > 20
+ * and for UDP len - ihs > 8 (include/worker/evaluator.hpp:61,91) and
+ * calc_l4_checksum(pkt, isv6, istcp, ihs) == 0 (:64,93).  The family is the
+ * version nibble; descriptor csum_start/flags are ignored.  GRO policy after
+ * these gates (TCP doff/flag rules, ECN, has_uso) stays with the caller.
+ * dev_verdict[i] = WG_VERDICT_* bits; dev_l4 (nullable) = the L4 checksum
+ * result when one was computed, else 0.
+ * ---------------------------------------------------------------------- */
+#define WG_VERDICT_IP_OK 0x01u /* size bounds + IP header gates pass */
+#define WG_VERDICT_L4_OK 0x02u /* TCP/UDP length floor and L4 checksum == 0 */
+#define WG_VERDICT_TCP 0x04u
+#define WG_VERDICT_UDP 0x08u
+#define WG_VERDICT_V6 0x10u
+int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_desc, uint64_t n, uint8_t *dev_verdict,
+                   uint16_t *dev_l4, void *stream);
+
+/* ------------------------------------------------------------------------
  * GSO split (TSO/USO segmentation + per-segment checksum fixup), batched.
  * Per super-buffer this is worker_impl::do_tun_gso_split
  * (worker/offload.cpp:46-216) bit for bit, including its quirks:

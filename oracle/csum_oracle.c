@@ -128,12 +128,68 @@ uint16_t orc_calc_l4_checksum(const uint8_t *pkt, size_t len, int isv6, int istc
     return orc_checksum(pkt + csum_start, len - csum_start, s);
 }
 
+/* Decap verify gates: evaluator.hpp:112-149 -> evaluator.cpp:14-58 ->
+ * evaluator.hpp:59-65 (TCP) / :89-94 (UDP).  Only the checksum-related
+ * decisions; GRO policy after them (TCP flag and doff rules, ECN, has_uso)
+ * stays with the caller.  l4_out (optional) gets calc_l4_checksum when an L4
+ * checksum was computed, else 0. */
+uint8_t orc_verify(const uint8_t *pkt, size_t len, uint16_t *l4_out) {
+    uint8_t v = 0;
+    if (l4_out)
+        *l4_out = 0;
+    if (len < 1)
+        return 0;
+    const int isv6 = (pkt[0] >> 4) == 6;
+    if (isv6)
+        v |= ORC_V_V6;
+    const size_t ihs = isv6 ? 40 : 20;
+    if (len < ihs || len > 65535) /* evaluator.hpp:118-121 */
+        return v;
+    uint8_t proto;
+    if (!isv6) {
+        if ((pkt[0] & 0x0f) * 4u != 20) /* ip_hl, evaluator.cpp:19 */
+            return v;
+        if (len != (size_t)((pkt[2] << 8) | pkt[3])) /* ip_len, :21 */
+            return v;
+        if (((pkt[6] << 8) | pkt[7]) & ~0x4000) /* ip_off & ~IP_DF, :24 */
+            return v;
+        if (orc_checksum(pkt, 20, 0)) /* :27 */
+            return v;
+        proto = pkt[9];
+    } else {
+        if (len - 40 != (size_t)((pkt[4] << 8) | pkt[5])) /* ip6_plen, :47 */
+            return v;
+        proto = pkt[6];
+    }
+    v |= ORC_V_IP_OK;
+    if (proto == 6) {
+        v |= ORC_V_TCP;
+        if (len - ihs <= 20) /* evaluator.hpp:61 */
+            return v;
+        uint16_t c = orc_calc_l4_checksum(pkt, len, isv6, 1, (uint16_t)ihs);
+        if (l4_out)
+            *l4_out = c;
+        if (!c)
+            v |= ORC_V_L4_OK;
+    } else if (proto == 17) {
+        v |= ORC_V_UDP;
+        if (len - ihs <= 8) /* evaluator.hpp:91 */
+            return v;
+        uint16_t c = orc_calc_l4_checksum(pkt, len, isv6, 0, (uint16_t)ihs);
+        if (l4_out)
+            *l4_out = c;
+        if (!c)
+            v |= ORC_V_L4_OK;
+    }
+    return v;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Batched drivers                                                          */
 /* ------------------------------------------------------------------------ */
 
 typedef struct {
-    int kind; /* 0 uniform l4, 1 desc l4, 2 desc checksum */
+    int kind; /* 0 uniform l4, 1 desc l4, 2 desc checksum, 3 desc verify */
     const uint8_t *base;
     uint64_t total_len;
     uint32_t segment_size;
@@ -141,6 +197,7 @@ typedef struct {
     uint32_t flags;
     const orc_pkt_desc *desc;
     uint16_t *out;
+    uint8_t *verdict;
     uint64_t lo, hi;
 } job_t;
 
@@ -157,9 +214,12 @@ static void run_job(job_t *j) {
             const orc_pkt_desc *d = &j->desc[i];
             j->out[i] = orc_calc_l4_checksum(j->base + d->offset, d->len, d->flags & 1,
                                              (d->flags >> 1) & 1, d->csum_start);
-        } else {
+        } else if (j->kind == 2) {
             const orc_pkt_desc *d = &j->desc[i];
             j->out[i] = orc_checksum(j->base + d->offset, d->len, 0);
+        } else {
+            const orc_pkt_desc *d = &j->desc[i];
+            j->verdict[i] = orc_verify(j->base + d->offset, d->len, j->out ? &j->out[i] : NULL);
         }
     }
 }
@@ -230,6 +290,17 @@ void orc_checksum_desc(const uint8_t *base, const orc_pkt_desc *desc, uint64_t n
     j.base = base;
     j.desc = desc;
     j.out = out;
+    run_parallel(j, n, threads);
+}
+
+void orc_verify_desc(const uint8_t *base, const orc_pkt_desc *desc, uint64_t n, uint8_t *verdict, uint16_t *l4,
+                     int threads) {
+    job_t j = {0};
+    j.kind = 3;
+    j.base = base;
+    j.desc = desc;
+    j.out = l4;
+    j.verdict = verdict;
     run_parallel(j, n, threads);
 }
 

@@ -113,6 +113,21 @@ typedef struct orc_vnet_hdr {
 int orc_gso_split(uint8_t *in, size_t in_len, orc_vnet_hdr *vnet, uint8_t *out, size_t out_cap,
                   orc_gso_result *res);
 
+/* Decap verify gates: the checksum-related decisions of
+ * evaluate_packet (include/worker/evaluator.hpp:112-149) with fill_fk_ip4 /
+ * fill_fk_ip6 (worker/evaluator.cpp:14-58) and the checksum gates of
+ * fill_fk_tcp / fill_fk_udp (include/worker/evaluator.hpp:59-65,89-94).
+ * The IP family is the version nibble (the decap caller's choice).
+ * Verdict bits: */
+#define ORC_V_IP_OK 0x01  /* size bounds + fill_fk_ip4/ip6 pass (v4 header checksum == 0) */
+#define ORC_V_L4_OK 0x02  /* TCP/UDP length floor and calc_l4_checksum == 0 */
+#define ORC_V_TCP 0x04
+#define ORC_V_UDP 0x08
+#define ORC_V_V6 0x10
+uint8_t orc_verify(const uint8_t *pkt, size_t len, uint16_t *l4_out);
+void orc_verify_desc(const uint8_t *base, const orc_pkt_desc *desc, uint64_t n, uint8_t *verdict, uint16_t *l4,
+                     int threads);
+
 /* Timing helper for the cpu_baseline: runs orc_l4_uniform `reps` times and
  * returns elapsed seconds (monotonic clock). */
 double orc_time_l4_uniform(const uint8_t *base, uint64_t total_len, uint32_t segment_size,

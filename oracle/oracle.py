@@ -69,6 +69,10 @@ def _load():
     lib.orc_checksum_desc.argtypes = [vp, vp, u64, vp, i32]
     lib.orc_gso_split.restype = i32
     lib.orc_gso_split.argtypes = [vp, sz, ctypes.POINTER(_VNet), vp, sz, ctypes.POINTER(_GsoRes)]
+    lib.orc_verify.restype = ctypes.c_uint8
+    lib.orc_verify.argtypes = [vp, sz, vp]
+    lib.orc_verify_desc.restype = None
+    lib.orc_verify_desc.argtypes = [vp, vp, u64, vp, vp, i32]
     lib.orc_time_l4_uniform.restype = ctypes.c_double
     lib.orc_time_l4_uniform.argtypes = [vp, u64, u32, u16, u32, vp, i32, i32]
     return lib
@@ -138,6 +142,26 @@ def checksum_desc(buf: np.ndarray, desc: np.ndarray, threads: int | None = None)
     out = np.empty(d.size, dtype=np.uint16)
     lib.orc_checksum_desc(a.ctypes.data, d.ctypes.data, d.size, out.ctypes.data, threads or default_threads())
     return out
+
+
+V_IP_OK, V_L4_OK, V_TCP, V_UDP, V_V6 = 0x01, 0x02, 0x04, 0x08, 0x10
+
+
+def verify(pkt) -> tuple[int, int]:
+    a = _u8(pkt)
+    c = ctypes.c_uint16(0)
+    v = int(lib.orc_verify(a.ctypes.data, a.size, ctypes.byref(c)))
+    return v, int(c.value)
+
+
+def verify_desc(buf: np.ndarray, desc: np.ndarray, threads: int | None = None):
+    a = _u8(buf)
+    d = np.ascontiguousarray(desc).view(PKT_DESC).reshape(-1)
+    verdict = np.empty(d.size, dtype=np.uint8)
+    l4 = np.empty(d.size, dtype=np.uint16)
+    lib.orc_verify_desc(a.ctypes.data, d.ctypes.data, d.size, verdict.ctypes.data, l4.ctypes.data,
+                        threads or default_threads())
+    return verdict, l4
 
 
 def gso_split(inbuf: np.ndarray, vnet: dict, out_cap: int):

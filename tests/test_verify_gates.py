@@ -1,0 +1,160 @@
+"""Decap verify gates: oracle restatement pinned by the
+reference's own decap tests, and GPU parity of wg_verify_desc.
+
+Reference semantics: include/worker/evaluator.hpp:112-149 (evaluate_packet),
+worker/evaluator.cpp:14-58 (fill_fk_ip4 / fill_fk_ip6), evaluator.hpp:59-65
+and 89-94 (TCP / UDP checksum gates).  Reference tests restated:
+tests/test-flowkey-own.cpp:170-200 "coalesceItemInvalidCSum" (a flipped L4
+checksum -> GRO_NOADD) and :456-501 "DecapBatch invalid packets".
+"""
+import struct
+
+import numpy as np
+import pytest
+
+import oracle
+import pktbuild
+
+V = oracle
+OK = V.V_IP_OK | V.V_L4_OK
+
+
+def tcp4(n=100, seq=1):
+    return bytearray(pktbuild.make_tcp(False, "192.0.2.1", 1, "192.0.2.2", 1, 0x10, n, seq))
+
+
+def udp4(n=100):
+    return bytearray(pktbuild.make_udp(False, "192.0.2.1", 1, "192.0.2.2", 1, n))
+
+
+def tcp6(n=100):
+    return bytearray(pktbuild.make_tcp(True, "2001:db8::1", 1, "2001:db8::2", 1, 0x10, n, 1))
+
+
+def udp6(n=100):
+    return bytearray(pktbuild.make_udp(True, "2001:db8::1", 1, "2001:db8::2", 1, n))
+
+
+def flip_l4(p, isv6, istcp):
+    off = (40 if isv6 else 20) + (16 if istcp else 6)
+    p[off] ^= 0xFF
+    p[off + 1] ^= 0xFF
+    return p
+
+
+def test_valid_packets_pass():
+    assert V.verify(tcp4())[0] == OK | V.V_TCP
+    assert V.verify(udp4())[0] == OK | V.V_UDP
+    assert V.verify(tcp6())[0] == OK | V.V_TCP | V.V_V6
+    assert V.verify(udp6())[0] == OK | V.V_UDP | V.V_V6
+
+
+def test_coalesce_item_invalid_csum():
+    # tests/test-flowkey-own.cpp:170-200: flipped L4 checksum -> not coalesced
+    for mk, v6, tcp in ((tcp4, False, True), (udp4, False, False), (tcp6, True, True), (udp6, True, False)):
+        v, c = V.verify(flip_l4(mk(), v6, tcp))
+        assert v & V.V_IP_OK and not v & V.V_L4_OK and c != 0
+
+
+def test_invalid_packets():
+    # tests/test-flowkey-own.cpp:456-501
+    assert not V.verify(tcp4()[:40])[0] & V.V_IP_OK         # tcp4 too short (ip_len mismatch)
+    assert not V.verify(udp4()[:28])[0] & V.V_IP_OK         # udp4 too short
+    assert not V.verify(tcp6()[:60])[0] & V.V_IP_OK         # tcp6 too short (plen mismatch)
+    assert not V.verify(udp6()[:48])[0] & V.V_IP_OK         # udp6 too short
+    assert V.verify(bytes(1))[0] == 0                        # invalid IP version / size
+    p = tcp4()
+    p[0] |= 0xF                                              # invalid IP header len
+    assert not V.verify(p)[0] & V.V_IP_OK
+    p = tcp4()
+    p[9] = 47                                                # ip4 invalid protocol (GRE)
+    p[10:12] = b"\0\0"
+    c = oracle.checksum(np.frombuffer(bytes(p[:20]), np.uint8), 0)
+    p[10:12] = struct.pack("<H", c)
+    assert V.verify(p)[0] == V.V_IP_OK
+    p = tcp6()
+    p[6] = 47                                                # ip6 invalid protocol
+    assert V.verify(p)[0] == V.V_IP_OK | V.V_V6
+
+
+def test_ip_header_gates():
+    p = tcp4()
+    p[6] |= 0x20  # MF set -> fragment (evaluator.cpp:24)
+    assert not V.verify(p)[0] & V.V_IP_OK
+    p = tcp4()
+    p[6] = 0x40  # DF alone is fine, but it changes the header checksum
+    assert not V.verify(p)[0] & V.V_IP_OK
+    p = tcp4()
+    p[8] ^= 1  # TTL change -> header checksum fails (evaluator.cpp:27)
+    assert not V.verify(p)[0] & V.V_IP_OK
+    # L4 length floors: TCP needs > 20 bytes after the IP header, UDP > 8
+    p = tcp4(0)
+    v, c = V.verify(p)
+    assert v == V.V_IP_OK | V.V_TCP and c == 0
+    p = udp4(0)
+    assert V.verify(p)[0] == V.V_IP_OK | V.V_UDP
+
+
+def random_verify_batch(rng, n):
+    pkts = []
+    for _ in range(n):
+        v6, tcp = bool(rng.integers(0, 2)), bool(rng.integers(0, 2))
+        plen = int(rng.choice([0, 1, 7, 8, 9, 20, 21, int(rng.integers(0, 3000))]))
+        al = 16 if v6 else 4
+        p = bytearray(pktbuild.build(v6, tcp, rng.integers(0, 256, plen, dtype=np.uint8).tobytes(),
+                                     rng.integers(0, 256, al, dtype=np.uint8).tobytes(),
+                                     rng.integers(0, 256, al, dtype=np.uint8).tobytes()))
+        k = int(rng.integers(0, 10))
+        if k == 0:
+            flip_l4(p, v6, tcp) if len(p) >= (40 if v6 else 20) + (18 if tcp else 8) else None
+        elif k == 1:
+            p[int(rng.integers(0, len(p)))] ^= 1 << int(rng.integers(0, 8))
+        elif k == 2:
+            p = p[: int(rng.integers(0, len(p) + 1))]
+        elif k == 3 and not v6:
+            p[6] |= 0x20
+        elif k == 4:
+            p[6 if v6 else 9] = int(rng.choice([1, 47, 58, 132]))
+        pkts.append(bytes(p))
+    return pkts
+
+
+def pack(pkts, rng):
+    offs, o = [], int(rng.integers(0, 16))
+    for p in pkts:
+        offs.append(o)
+        o += len(p) + int(rng.integers(0, 5))
+    buf = np.zeros(o + 16, np.uint8)
+    for off, p in zip(offs, pkts):
+        buf[off:off + len(p)] = np.frombuffer(p, np.uint8)
+    d = np.zeros(len(pkts), dtype=oracle.PKT_DESC)
+    d["offset"], d["len"] = offs, [len(p) for p in pkts]
+    return buf, d
+
+
+def test_oracle_verify_desc_matches_scalar():
+    rng = np.random.default_rng(3)
+    pkts = random_verify_batch(rng, 500)
+    buf, d = pack(pkts, rng)
+    verdict, l4 = oracle.verify_desc(buf, d, threads=3)
+    for i, p in enumerate(pkts):
+        assert (verdict[i], l4[i]) == V.verify(p)
+
+
+@pytest.mark.gpu
+def test_gpu_verify_parity(gpu):
+    import torch
+
+    import wireglider_amd as wga
+
+    rng = np.random.default_rng(11)
+    pkts = random_verify_batch(rng, 20000)
+    buf, d = pack(pkts, rng)
+    dbuf = torch.from_numpy(buf).to(gpu)
+    dd = torch.from_numpy(d.view(np.int64).reshape(-1, 2).copy()).to(gpu)
+    verdict, l4 = wga.verify_desc(dbuf, dd)
+    torch.cuda.synchronize()
+    ev, el4 = oracle.verify_desc(buf, d)
+    np.testing.assert_array_equal(verdict.cpu().numpy(), ev)
+    np.testing.assert_array_equal(l4.cpu().numpy(), el4)
+    assert (ev & OK == OK).mean() > 0.3 and (ev & OK != OK).mean() > 0.2  # both outcomes exercised

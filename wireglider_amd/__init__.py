@@ -34,6 +34,7 @@ EXPORTED_SYMBOLS = (
     "wg_l4csum_uniform",
     "wg_l4csum_desc",
     "wg_checksum_desc",
+    "wg_verify_desc",
     "wg_gso_split",
     "wg_l4csum_uniform_host",
     "wg_synth_fill",
@@ -93,6 +94,7 @@ def _load() -> ctypes.CDLL:
         "wg_l4csum_uniform": (i32, [u8p, u64, u32, u16, u32, vp, vp]),
         "wg_l4csum_desc": (i32, [u8p, vp, u64, vp, vp]),
         "wg_checksum_desc": (i32, [u8p, vp, u64, vp, vp]),
+        "wg_verify_desc": (i32, [u8p, vp, u64, vp, vp, vp]),
         "wg_gso_split": (i32, [u8p, vp, u64, u8p, vp, vp]),
         "wg_l4csum_uniform_host": (i32, [u8p, u64, u32, u16, u32, vp]),
         "wg_synth_fill": (i32, [u8p, u64, u64, u64, vp]),
@@ -197,6 +199,25 @@ def checksum_desc(base, desc, out=None, stream=None):
     rc = lib.wg_checksum_desc(base.data_ptr(), desc.data_ptr(), n, out.data_ptr(), _stream_ptr(stream))
     _check(rc, "wg_checksum_desc")
     return out
+
+
+VERDICT_IP_OK, VERDICT_L4_OK, VERDICT_TCP, VERDICT_UDP, VERDICT_V6 = 0x01, 0x02, 0x04, 0x08, 0x10
+
+
+def verify_desc(base, desc, with_l4: bool = True, stream=None):
+    """Decap verify gates (evaluate_packet's checksum decisions,
+    include/worker/evaluator.hpp:112-149) per descriptor.  Returns
+    (verdict uint8 tensor, L4 result uint16 tensor or None)."""
+    torch = _torch()
+    _require_cuda(base, "base")
+    _require_cuda(desc, "desc")
+    n = desc.numel() * desc.element_size() // PKT_DESC_BYTES
+    verdict = torch.empty(n, dtype=torch.uint8, device=base.device)
+    l4 = torch.empty(n, dtype=torch.uint16, device=base.device) if with_l4 else None
+    rc = lib.wg_verify_desc(base.data_ptr(), desc.data_ptr(), n, verdict.data_ptr(),
+                            l4.data_ptr() if l4 is not None else None, _stream_ptr(stream))
+    _check(rc, "wg_verify_desc")
+    return verdict, l4
 
 
 def gso_split(inbuf, gso_desc, outbuf, results=None, stream=None):

@@ -163,9 +163,140 @@ static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }
 
+// ---------------------------------------------------------------------------
+// Decap verify gates: the checksum decisions of
+// evaluate_packet (include/worker/evaluator.hpp:112-149): size bounds,
+// fill_fk_ip4 (worker/evaluator.cpp:14-40: ihl == 5, len == ip_len, no
+// fragmentation, header checksum == 0) or fill_fk_ip6 (:42-58: plen), then
+// the TCP / UDP length floors and calc_l4_checksum == 0
+// (include/worker/evaluator.hpp:59-65, 89-94).  Per wave P packets: one byte
+// load per packet brings header bytes 0-39 (decoded with v_readlane), then
+// the L4 issue/finish machinery with csum_start = 20 / 40.
+// ---------------------------------------------------------------------------
+struct VerifyParams {
+    const uint8_t *base;
+    const wg_pkt_desc *desc;
+    uint8_t *verdict;
+    uint16_t *l4;
+    uint64_t n;
+};
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t j) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
+    const uint32_t lane = lane_id();
+    const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
+    const uint64_t i0 = wave * P;
+    if (i0 >= p.n)
+        return;
+    const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
+    uintptr_t a[P];
+    uint32_t len[P], hv[P];
+#pragma unroll
+    for (int j = 0; j < P; j++) {
+        const uint64_t i = i0 + j < p.n ? i0 + j : p.n - 1;
+        const wg_pkt_desc d = p.desc[i];
+        a[j] = reinterpret_cast<uintptr_t>(p.base) + d.offset;
+        len[j] = i0 + j < p.n ? d.len : 0u;
+        const uint32_t hl = len[j] < 40u ? len[j] : 40u;
+        hv[j] = ld8(lane < hl ? a[j] + lane : (hl ? a[j] : zero));
+    }
+    // decode (wave-uniform) and issue the L4 loads of every packet
+    Geom g[P];
+    Front f[P];
+    uint32_t verdict[P];
+    bool do_l4[P];
+#pragma unroll
+    for (int j = 0; j < P; j++) {
+        const uint32_t L = len[j];
+        uint32_t v = 0;
+        bool ip_ok = false, tcp = false, l4 = false;
+        uint32_t ihs = 20;
+        // IPv4 header sum over bytes 0-19 (pairing from byte 0)
+        const uint32_t hs = wave_sum_u32(lane < 20 && lane < L ? hv[j] << (8u * (lane & 1u)) : 0u);
+        if (L >= 1) {
+            const uint32_t b0 = rl(hv[j], 0);
+            const bool v6 = (b0 >> 4) == 6;
+            if (v6)
+                v |= WG_VERDICT_V6;
+            ihs = v6 ? 40u : 20u;
+            if (L >= ihs && L <= 65535u) {  // evaluator.hpp:118-121
+                uint32_t proto;
+                if (!v6) {
+                    ip_ok = (b0 & 0xfu) == 5u &&                                   // ip_hl, evaluator.cpp:19
+                            L == ((rl(hv[j], 2) << 8) | rl(hv[j], 3)) &&            // ip_len, :21
+                            (((rl(hv[j], 6) << 8) | rl(hv[j], 7)) & ~0x4000u) == 0 &&  // ip_off & ~IP_DF, :24
+                            fold16_32(hs) == 0xffffu;                             // checksum == 0, :27
+                    proto = rl(hv[j], 9);
+                } else {
+                    ip_ok = L - 40u == ((rl(hv[j], 4) << 8) | rl(hv[j], 5));  // ip6_plen, :47
+                    proto = rl(hv[j], 6);
+                }
+                if (ip_ok) {
+                    v |= WG_VERDICT_IP_OK;
+                    if (proto == 6u) {
+                        v |= WG_VERDICT_TCP;
+                        tcp = true;
+                        l4 = L - ihs > 20u;  // evaluator.hpp:61
+                    } else if (proto == 17u) {
+                        v |= WG_VERDICT_UDP;
+                        l4 = L - ihs > 8u;  // evaluator.hpp:91
+                    }
+                }
+            }
+        }
+        verdict[j] = v;
+        do_l4[j] = l4;
+        g[j].a = l4 ? a[j] : reinterpret_cast<uintptr_t>(p.base);
+        g[j].len = l4 ? L : 0u;
+        g[j].cs = ihs;
+        g[j].fl = ((v & WG_VERDICT_V6) ? WG_PKT_V6 : 0u) | (tcp ? WG_PKT_TCP : 0u);
+        issue<true, true>(g[j], lane, f[j]);
+    }
+    uint32_t rv = 0, rc = 0;
+#pragma unroll
+    for (int j = 0; j < P; j++) {
+        uint32_t s = wave_sum_u32(finish<true>(lane, f[j]));
+        uint32_t c = 0;
+        if (do_l4[j]) {
+            const uint32_t proto = (g[j].fl & WG_PKT_TCP) ? 6u : 17u;
+            s += (proto << 8) + bswap16((g[j].len - g[j].cs) & 0xffffu);
+            c = ~fold16_32(s) & 0xffffu;
+            if (c == 0)
+                verdict[j] |= WG_VERDICT_L4_OK;
+        }
+        if (lane == (uint32_t)j) {
+            rv = verdict[j];
+            rc = c;
+        }
+    }
+    if (lane < (uint32_t)P && i0 + lane < p.n) {
+        p.verdict[i0 + lane] = (uint8_t)rv;
+        if (p.l4)
+            p.l4[i0 + lane] = (uint16_t)rc;
+    }
+}
+
 }  // namespace wg
 
 using namespace wg;
+
+extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_desc, uint64_t n,
+                              uint8_t *dev_verdict, uint16_t *dev_l4, void *stream) {
+    if (!n)
+        return WG_OK;
+    if (!dev_base || !dev_desc || !dev_verdict || (reinterpret_cast<uintptr_t>(dev_desc) & 15))
+        return WG_ERR_INVALID;
+    VerifyParams p{dev_base, dev_desc, dev_verdict, dev_l4, n};
+    uint64_t blocks = (n + 15) / 16;
+    if (blocks >= 8)
+        blocks = (blocks + 7) & ~7ull;
+    hipLaunchKernelGGL(verify_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), p);
+    return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+}
 
 extern "C" int wg_l4csum_uniform(const uint8_t *dev_base, uint64_t total_len, uint32_t segment_size,
                                  uint16_t csum_start, uint32_t flags, uint16_t *dev_out, void *stream) {
