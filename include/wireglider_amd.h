@@ -175,6 +175,28 @@ int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8
                  wg_gso_result *dev_res, void *stream);
 
 /* ------------------------------------------------------------------------
+ * GRO finalize, batched, in place on each coalesced flow's
+ * header buffer: PacketRefBatch::finalize (include/worker/flowkey_ref.hpp:82-117)
+ * — UDP len / IPv6 plen / IPv4 total length, IPv4 header checksum, and the
+ * NEEDS_CSUM seed pseudo_header_checksum(proto, src, dst, l4len) (the
+ * complemented fold, as the reference stores it) over the header's
+ * ADDRESSES.  The reference's call sums the std::span objects instead
+ * (pointer-dependent) and is not reproduced.
+ * status (out): 0, or -3 when the header geometry is out of contract.
+ * ---------------------------------------------------------------------- */
+typedef struct wg_gro_desc {
+    uint64_t hdr_offset;    /* header buffer = dev_hdrs[hdr_offset, + hdr_len) */
+    uint64_t payload_bytes; /* size_bytes() of the coalesced batch */
+    uint16_t hdr_len;
+    uint16_t csum_start;
+    uint16_t csum_offset;
+    uint8_t flags; /* WG_PKT_V6 | WG_PKT_TCP */
+    int8_t status; /* out */
+} wg_gro_desc;      /* 24 bytes */
+
+int wg_gro_finalize(uint8_t *dev_hdrs, wg_gro_desc *dev_desc, uint64_t n, void *stream);
+
+/* ------------------------------------------------------------------------
  * Host-memory path: the batch starts and ends in host
  * memory.  Pinned staging + hipMemcpyAsync H2D -> kernel -> D2H on the
  * engine's per-thread stream; synchronous.  Uses a per-thread device

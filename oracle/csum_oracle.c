@@ -463,3 +463,34 @@ int orc_gso_split(uint8_t *in, size_t in_len, orc_vnet_hdr *v, uint8_t *out, siz
     res->segment_size = hdr_len + gso;
     return 0;
 }
+
+/* ------------------------------------------------------------------------ */
+/* GRO finalize: include/worker/flowkey_ref.hpp:82-117                      */
+/* ------------------------------------------------------------------------ */
+
+int orc_gro_finalize(uint8_t *hdr, size_t hdr_len, uint16_t csum_start, uint16_t csum_offset, int isv6,
+                     int istcp, uint64_t payload_bytes) {
+    const size_t cs = csum_start, l4off = (size_t)csum_start + csum_offset;
+    const size_t iph = isv6 ? 40 : 20;
+    if (cs < iph || cs > hdr_len || l4off < cs || l4off + 2 > hdr_len || (!istcp && cs + 8 > hdr_len))
+        return -3;
+    const uint64_t l4len = hdr_len - cs + payload_bytes; /* :84 */
+    if (!istcp)
+        st_be16(hdr + cs + 4, (uint16_t)l4len); /* udp->len, :85-86 */
+    size_t proto_off, src_off, dst_off, alen;
+    if (isv6) {
+        proto_off = 6; src_off = 8; dst_off = 24; alen = 16; /* :89-93 */
+        st_be16(hdr + 4, (uint16_t)l4len);                  /* ip6_plen, :95 */
+    } else {
+        proto_off = 9; src_off = 12; dst_off = 16; alen = 4; /* :97-100 */
+        st_be16(hdr + 2, (uint16_t)(hdr_len + payload_bytes)); /* ip_len, :103 */
+        hdr[10] = 0;                                           /* :104 */
+        hdr[11] = 0;
+        uint16_t c = orc_checksum(hdr, cs, 0); /* :106, native order */
+        memcpy(hdr + 10, &c, 2);
+    }
+    uint16_t seed = orc_pseudo_header_checksum(hdr[proto_off], hdr + src_off, hdr + dst_off, alen,
+                                               (uint16_t)l4len); /* :108-112 (intended) */
+    memcpy(hdr + l4off, &seed, 2); /* native order, :114 */
+    return 0;
+}

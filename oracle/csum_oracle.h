@@ -128,6 +128,17 @@ uint8_t orc_verify(const uint8_t *pkt, size_t len, uint16_t *l4_out);
 void orc_verify_desc(const uint8_t *base, const orc_pkt_desc *desc, uint64_t n, uint8_t *verdict, uint16_t *l4,
                      int threads);
 
+/* GRO finalize: PacketRefBatch::finalize
+ * (include/worker/flowkey_ref.hpp:82-117) / OwnedPacketBatch::finalize
+ * (include/worker/flowkey_own.hpp:83-115) on one coalesced flow's header
+ * buffer, in place.  The NEEDS_CSUM seed is pseudo_header_checksum over the
+ * header's source/destination ADDRESSES (complemented fold, as the reference
+ * stores it); the reference's call binds the TAddress overload and sums the
+ * std::span objects instead, which is pointer-dependent and
+ * not reproduced.  Returns 0, or -3 if the geometry is out of contract. */
+int orc_gro_finalize(uint8_t *hdr, size_t hdr_len, uint16_t csum_start, uint16_t csum_offset, int isv6,
+                     int istcp, uint64_t payload_bytes);
+
 /* Timing helper for the cpu_baseline: runs orc_l4_uniform `reps` times and
  * returns elapsed seconds (monotonic clock). */
 double orc_time_l4_uniform(const uint8_t *base, uint64_t total_len, uint32_t segment_size,

@@ -73,6 +73,8 @@ def _load():
     lib.orc_verify.argtypes = [vp, sz, vp]
     lib.orc_verify_desc.restype = None
     lib.orc_verify_desc.argtypes = [vp, vp, u64, vp, vp, i32]
+    lib.orc_gro_finalize.restype = i32
+    lib.orc_gro_finalize.argtypes = [vp, sz, u16, u16, i32, i32, u64]
     lib.orc_time_l4_uniform.restype = ctypes.c_double
     lib.orc_time_l4_uniform.argtypes = [vp, u64, u32, u16, u32, vp, i32, i32]
     return lib
@@ -162,6 +164,14 @@ def verify_desc(buf: np.ndarray, desc: np.ndarray, threads: int | None = None):
     lib.orc_verify_desc(a.ctypes.data, d.ctypes.data, d.size, verdict.ctypes.data, l4.ctypes.data,
                         threads or default_threads())
     return verdict, l4
+
+
+def gro_finalize(hdr, csum_start: int, csum_offset: int, isv6: bool, istcp: bool, payload_bytes: int):
+    """Returns (status, header after)."""
+    a = np.array(_u8(hdr), copy=True)
+    st = int(lib.orc_gro_finalize(a.ctypes.data, a.size, csum_start, csum_offset, int(isv6), int(istcp),
+                                  payload_bytes))
+    return st, a
 
 
 def gso_split(inbuf: np.ndarray, vnet: dict, out_cap: int):

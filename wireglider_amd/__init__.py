@@ -36,6 +36,7 @@ EXPORTED_SYMBOLS = (
     "wg_checksum_desc",
     "wg_verify_desc",
     "wg_gso_split",
+    "wg_gro_finalize",
     "wg_l4csum_uniform_host",
     "wg_synth_fill",
     "wg_synth_headers",
@@ -53,6 +54,7 @@ EXPORTED_SYMBOLS = (
 PKT_DESC_BYTES = 16
 GSO_DESC_BYTES = 40
 GSO_RESULT_BYTES = 24
+GRO_DESC_BYTES = 24
 
 
 def _np_dtypes():
@@ -66,11 +68,14 @@ def _np_dtypes():
                     ("vnet", vnet), ("reserved", "<u2", 3)])
     res = np.dtype([("out_len", "<u8"), ("segment_size", "<u4"), ("hdr_len", "<u2"), ("isv6", "u1"),
                     ("ecn", "u1"), ("status", "i1"), ("passthrough", "u1"), ("pad", "u1", 6)])
+    gro = np.dtype([("hdr_offset", "<u8"), ("payload_bytes", "<u8"), ("hdr_len", "<u2"), ("csum_start", "<u2"),
+                    ("csum_offset", "<u2"), ("flags", "u1"), ("status", "i1")])
     assert pkt.itemsize == PKT_DESC_BYTES and gso.itemsize == GSO_DESC_BYTES and res.itemsize == GSO_RESULT_BYTES
-    return pkt, gso, res
+    assert gro.itemsize == GRO_DESC_BYTES
+    return pkt, gso, res, gro
 
 
-PKT_DESC_DTYPE, GSO_DESC_DTYPE, GSO_RESULT_DTYPE = _np_dtypes()
+PKT_DESC_DTYPE, GSO_DESC_DTYPE, GSO_RESULT_DTYPE, GRO_DESC_DTYPE = _np_dtypes()
 
 
 class WireGliderError(RuntimeError):
@@ -96,6 +101,7 @@ def _load() -> ctypes.CDLL:
         "wg_checksum_desc": (i32, [u8p, vp, u64, vp, vp]),
         "wg_verify_desc": (i32, [u8p, vp, u64, vp, vp, vp]),
         "wg_gso_split": (i32, [u8p, vp, u64, u8p, vp, vp]),
+        "wg_gro_finalize": (i32, [u8p, vp, u64, vp]),
         "wg_l4csum_uniform_host": (i32, [u8p, u64, u32, u16, u32, vp]),
         "wg_synth_fill": (i32, [u8p, u64, u64, u64, vp]),
         "wg_synth_headers": (i32, [u8p, vp, u64, u64, u64, vp]),
@@ -233,6 +239,16 @@ def gso_split(inbuf, gso_desc, outbuf, results=None, stream=None):
                           results.data_ptr(), _stream_ptr(stream))
     _check(rc, "wg_gso_split")
     return results
+
+
+def gro_finalize(hdrs, gro_desc, stream=None):
+    """Batched GRO finalize (include/worker/flowkey_ref.hpp:82-117) in place on
+    header buffers; gro_desc: device tensor of n x 24 B wg_gro_desc (status
+    written back)."""
+    for t, nm in ((hdrs, "hdrs"), (gro_desc, "gro_desc")):
+        _require_cuda(t, nm)
+    n = gro_desc.numel() * gro_desc.element_size() // GRO_DESC_BYTES
+    _check(lib.wg_gro_finalize(hdrs.data_ptr(), gro_desc.data_ptr(), n, _stream_ptr(stream)), "wg_gro_finalize")
 
 
 def calc_l4_checksum_host(buf: bytes | bytearray | memoryview, segment_size: int, isv6: bool,
