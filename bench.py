@@ -15,6 +15,12 @@ Workloads (--workload; BASELINE.json configs):
   config4            4,194,304 bimodal 64 B / 9000 B IPv4/UDP (configs[3]).
   config5            16,777,216 x 1500 B mixed v4/v6 x TCP/UDP split across
                      the N GPUs (configs[4]); strong scaling.
+  verify             SURVEY §8 f1: decap verify gates (wg_verify_desc) over
+                     1,048,576 x 1500 B mixed v4/v6 x TCP/UDP per GPU with
+                     checksums stored; metric GiB/s of packets verified.
+  gro                SURVEY §8 f2: GRO finalize (wg_gro_finalize) of
+                     4,194,304 coalesced flows per GPU, headers in 64 B slots,
+                     mixed v4/v6 x TCP/UDP; metric Mflows/s.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2]
   torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -47,7 +53,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="config2", choices=["config2", "config3", "config4", "config5"])
+    ap.add_argument("--workload", default="config2", choices=["config2", "config3", "config4", "config5", "verify", "gro"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall seconds of the CPU baseline sample")
     ap.add_argument("--settle-seconds", type=float, default=0.3,
@@ -70,6 +76,10 @@ class Workload:
     desc: Optional[object] = None     # descriptor tensor (verify pass)
     sample: Optional[Callable] = None  # host sample for the CPU baseline
     counts: list = field(default_factory=list)  # packets per rank
+    metric: Optional[str] = None      # overrides the default metric (f-row workloads)
+    unit: str = "GiB/s"
+    value_scale: float = 2.0**-30     # metric value = payload units/s x value_scale
+    post: Optional[Callable] = None   # workload-specific post-check
 
 
 def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workload:
@@ -155,6 +165,97 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
         alg = n * in_len + n * out_len + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES)
         return Workload(launch, n, n * in_len, alg, cfg, "weak", buf, "wg::gso_split_kernel<4,1,0> (pipelined)",
                         rank * n, counts=[n] * world)
+    if name == "verify":
+        n = 1 << 20
+        seed = 0x5EED00F1
+        buf = torch.empty(n * SEG, dtype=torch.uint8, device=dev)
+        wga.synth_fill(buf, seed, counter_base=rank * n * SEG)
+        desc = wga.synth_desc_stride(n, SEG, SEG, 1, seed, rank * n, device=dev)  # mixed v4/v6 x TCP/UDP
+        wga.synth_headers(buf, desc, seed, rank * n)
+        wga.store_l4csum(buf, desc, wga.calc_l4_checksum_desc(buf, desc))  # received packets are valid
+        torch.cuda.synchronize()
+        verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+        l4 = torch.empty(n, dtype=torch.uint16, device=dev)
+
+        def launch():
+            wga.verify_desc(buf, desc, verdict=verdict, l4=l4)
+
+        def post():
+            # every packet must pass both gates; L4 results all zero
+            flags = desc.view(torch.uint8).reshape(n, 16)[:, 14]
+            okbits = 0x03
+            bad = int(((verdict & okbits) != okbits).sum().item()) + int(torch.count_nonzero(l4.to(torch.int32)).item())
+            v6 = int(((verdict & 0x10) != 0).sum().item())
+            return {"verify_failures": bad, "v6_packets": v6, "v6_expected": int((flags & 1).sum().item())}
+
+        def sample(npk):
+            d = desc[:npk].cpu().numpy()
+            v, l = wga.verify_desc(buf, desc[:npk])
+            torch.cuda.synchronize()
+            end = npk * SEG
+            return buf[:end].cpu().numpy(), (v.cpu().numpy(), l.cpu().numpy()), ("verify", d)
+
+        cfg = {"workload": "verify (SURVEY §8 f1): 1,048,576 x 1500 B mixed IPv4/IPv6 x TCP/UDP per GPU, "
+                           "checksums stored, evaluate_packet checksum gates (wg_verify_desc)",
+               "packets_per_gpu": n, "segment_size": SEG, "layout": "descriptor", "parallelism": f"shard{world}"}
+        return Workload(launch, n, n * SEG, n * SEG + 16 * n + n + 2 * n, cfg, "weak", buf,
+                        "wg::verify_kernel<4>", rank * n, sample=sample, counts=[n] * world,
+                        metric="device-resident GiB/s, decap verify gates over packet batch (SURVEY f1)",
+                        post=post)
+    if name == "gro":
+        n, slot = 1 << 22, 64
+        rng = np.random.default_rng(0x5EED00F2 + rank)
+        fam = rng.integers(0, 4, n)  # bit0 v6, bit1 tcp
+        isv6, istcp = (fam & 1).astype(bool), (fam & 2).astype(bool)
+        cs = np.where(isv6, 40, 20)
+        hdr_len = cs + np.where(istcp, 20, 8)
+        hdr = np.zeros((n, slot), dtype=np.uint8)
+        # random addresses (v6: bytes 8-39; v4: 12-19), lengths/checksums stale (0)
+        hdr[:, 8:40] = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        hdr[isv6, 0] = 0x60
+        hdr[isv6, 6] = np.where(istcp[isv6], 6, 17)
+        hdr[isv6, 7] = 64
+        hdr[~isv6, 0:12] = np.array([0x45, 0, 0, 0, 0, 1, 0x40, 0, 64, 0, 0, 0], np.uint8)
+        hdr[~isv6, 9] = np.where(istcp[~isv6], 6, 17)
+        hdr[~isv6, 20:40] = 0
+        gd = np.zeros(n, dtype=wga.GRO_DESC_DTYPE)
+        gd["hdr_offset"] = np.arange(n, dtype=np.uint64) * slot
+        gd["payload_bytes"] = rng.integers(1, 65000, n)
+        gd["hdr_len"], gd["csum_start"] = hdr_len, cs
+        gd["csum_offset"] = np.where(istcp, 16, 6)
+        gd["flags"] = (isv6.astype(np.uint8)) | (istcp.astype(np.uint8) << 1)
+        d_hdr = torch.from_numpy(hdr.reshape(-1)).to(dev)
+        d_desc = torch.from_numpy(gd.view(np.uint8).copy()).to(dev)
+        hdr_bytes = int(hdr_len.sum())
+        written = int(np.where(isv6, 4, 6).sum() + 2 * (~istcp).sum())  # length fields, ip_sum, seed
+
+        def launch():
+            wga.gro_finalize(d_hdr, d_desc)
+
+        def post():
+            st = d_desc.cpu().numpy().view(wga.GRO_DESC_DTYPE)["status"]
+            # self-check on the GPU: every finalized IPv4 header verifies to 0
+            v4 = np.nonzero(~isv6)[0]
+            pd = np.zeros(v4.size, dtype=wga.PKT_DESC_DTYPE)
+            pd["offset"], pd["len"] = v4.astype(np.uint64) * slot, 20
+            ipc = wga.checksum_desc(d_hdr, torch.from_numpy(pd.view(np.uint8).copy()).to(dev))
+            return {"status_nonzero": int(np.count_nonzero(st)),
+                    "ipv4_header_nonzero": int(torch.count_nonzero(ipc.to(torch.int32)).item())}
+
+        def sample(npk):
+            # the pre-finalize headers (host copy kept) and the GPU's finalized ones
+            gd_s = gd[:npk].copy()
+            got = d_hdr[: npk * slot].cpu().numpy()
+            st = d_desc[: npk * 24].cpu().numpy().view(wga.GRO_DESC_DTYPE)["status"]
+            return hdr.reshape(-1)[: npk * slot].copy(), (got, st), ("gro", gd_s)
+
+        cfg = {"workload": "gro (SURVEY §8 f2): 4,194,304 coalesced flows per GPU, headers in 64 B slots, "
+                           "mixed IPv4/IPv6 x TCP/UDP, in-place finalize (wg_gro_finalize)",
+               "flows_per_gpu": n, "slot_bytes": slot, "parallelism": f"shard{world}"}
+        return Workload(launch, n, n, n * 24 + hdr_bytes + written + n, cfg, "weak", d_hdr,
+                        "wg::gro_finalize_kernel", rank * n, sample=sample, counts=[n] * world,
+                        metric="device-resident Mflows/s, GRO finalize (SURVEY f2)", unit="Mflows/s",
+                        value_scale=1e-6, post=post)
     # config4 bimodal
     n = 1 << 22
     seed = 0x5EED0004 + rank
@@ -239,6 +340,34 @@ def cpu_baseline(sample_fn, seconds: float):
         reps = max(1, int(math.ceil(seconds / max(tall1, 1e-6))))
         t_all = oracle.time_l4_uniform(host, seg, cs, fl, threads, reps) / reps
         nbytes = host.size
+    elif kind[0] == "verify":
+        d = kind[1]
+        exp_v, exp_l4 = oracle.verify_desc(host, d, threads)
+        t0 = time.perf_counter()
+        oracle.verify_desc(host, d, 1)
+        t_1core = time.perf_counter() - t0
+        reps = max(1, int(seconds * threads / max(t_1core, 1e-6)))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            oracle.verify_desc(host, d, threads)
+        t_all = (time.perf_counter() - t0) / reps
+        nbytes = int(np.ascontiguousarray(d).view(oracle.PKT_DESC)["len"].astype(np.int64).sum())
+        exp = np.concatenate([exp_v.astype(np.int64), exp_l4.astype(np.int64)])
+        gpu_out = np.concatenate([gpu_out[0].astype(np.int64), gpu_out[1].astype(np.int64)])
+    elif kind[0] == "gro":
+        d = kind[1]
+        hdr_after, st = oracle.gro_finalize_desc(host, d, threads)
+        exp = np.concatenate([hdr_after.astype(np.int64), st.astype(np.int64)])
+        t0 = time.perf_counter()
+        oracle.gro_finalize_desc(host, d, 1)
+        t_1core = time.perf_counter() - t0
+        reps = max(1, int(seconds * threads / max(t_1core, 1e-6)))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            oracle.gro_finalize_desc(host, d, threads)
+        t_all = (time.perf_counter() - t0) / reps
+        nbytes = d.size  # flows
+        gpu_out = np.concatenate([gpu_out[0].astype(np.int64), gpu_out[1].astype(np.int64)])
     else:
         d = kind[1]
         exp = oracle.l4_desc(host, d, threads)
@@ -256,15 +385,18 @@ def cpu_baseline(sample_fn, seconds: float):
         cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except Exception:
         cpu_model = "unknown"
+    scale, unit = (1e-6, "Mflows/s") if kind[0] == "gro" else (2.0**-30, "GiB/s")
+    what = {"verify": "decap verify gates restatement (orc_verify)", "gro": "GRO finalize restatement"}.get(
+        kind[0], "calc_l4_checksum restatement")
     return {
-        "value": nbytes / t_all / 2**30,
-        "unit": "GiB/s",
+        "value": nbytes / t_all * scale,
+        "unit": unit,
         "cores": threads,
         "kind": "port",
-        "value_1core": nbytes / t_1core / 2**30,
+        "value_1core": nbytes / t_1core * scale,
         "cpu_model": cpu_model,
-        "sample": f"first {npk} packets ({nbytes} B) of the same batch, oracle/csum_oracle.c "
-                  f"(calc_l4_checksum restatement), {threads} pthreads, ~{seconds:.1f} s wall; "
+        "sample": f"first {npk} units of the same batch, oracle/csum_oracle.c "
+                  f"({what}), {threads} pthreads, ~{seconds:.1f} s wall; "
                   f"bit-exact vs GPU: {parity}",
         "parity_with_gpu": parity,
     }
@@ -288,6 +420,9 @@ def post_checks(torch, wga, wl: Workload, world: int, dev):
     from wireglider_amd import dist as wdist
 
     info = {}
+    if wl.post is not None:
+        torch.cuda.synchronize()
+        info.update(wl.post())
     if wl.out is None:
         return info
     torch.cuda.synchronize()
@@ -371,15 +506,15 @@ def main():
         total_payload = float(wl.payload_bytes)
 
     ms_per_step = wall / args.steps * 1e3
-    value = total_payload * args.steps / wall / 2**30
+    value = total_payload * args.steps / wall * wl.value_scale
     achieved = wl.alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args.workload)
     read_peak = measured_read_peak(torch, wga, wl.buf) if rank == 0 else None
     post = post_checks(torch, wga, wl, world, dev)
     line = {
-        "metric": "device-resident GiB/s, L4 checksum over packet batch; 1/2/4/8 MI355X",
+        "metric": wl.metric or "device-resident GiB/s, L4 checksum over packet batch; 1/2/4/8 MI355X",
         "value": round(value, 3),
-        "unit": "GiB/s",
+        "unit": wl.unit,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,

@@ -198,6 +198,8 @@ typedef struct {
     const orc_pkt_desc *desc;
     uint16_t *out;
     uint8_t *verdict;
+    uint8_t *wbase;
+    orc_gro_desc *gdesc;
     uint64_t lo, hi;
 } job_t;
 
@@ -217,9 +219,14 @@ static void run_job(job_t *j) {
         } else if (j->kind == 2) {
             const orc_pkt_desc *d = &j->desc[i];
             j->out[i] = orc_checksum(j->base + d->offset, d->len, 0);
-        } else {
+        } else if (j->kind == 3) {
             const orc_pkt_desc *d = &j->desc[i];
             j->verdict[i] = orc_verify(j->base + d->offset, d->len, j->out ? &j->out[i] : NULL);
+        } else {
+            orc_gro_desc *d = &j->gdesc[i];
+            d->status = (int8_t)orc_gro_finalize(j->wbase + d->hdr_offset, d->hdr_len, d->csum_start,
+                                                 d->csum_offset, d->flags & 1, (d->flags >> 1) & 1,
+                                                 d->payload_bytes);
         }
     }
 }
@@ -301,6 +308,14 @@ void orc_verify_desc(const uint8_t *base, const orc_pkt_desc *desc, uint64_t n, 
     j.desc = desc;
     j.out = l4;
     j.verdict = verdict;
+    run_parallel(j, n, threads);
+}
+
+void orc_gro_finalize_desc(uint8_t *base, orc_gro_desc *desc, uint64_t n, int threads) {
+    job_t j = {0};
+    j.kind = 4;
+    j.wbase = base;
+    j.gdesc = desc;
     run_parallel(j, n, threads);
 }
 

@@ -139,6 +139,20 @@ void orc_verify_desc(const uint8_t *base, const orc_pkt_desc *desc, uint64_t n, 
 int orc_gro_finalize(uint8_t *hdr, size_t hdr_len, uint16_t csum_start, uint16_t csum_offset, int isv6,
                      int istcp, uint64_t payload_bytes);
 
+/* Batched form over the wg_gro_desc layout (include/wireglider_amd.h);
+ * status written back into each descriptor. */
+typedef struct orc_gro_desc {
+    uint64_t hdr_offset;
+    uint64_t payload_bytes;
+    uint16_t hdr_len;
+    uint16_t csum_start;
+    uint16_t csum_offset;
+    uint8_t flags; /* bit0 = v6, bit1 = tcp */
+    int8_t status;
+} orc_gro_desc;
+
+void orc_gro_finalize_desc(uint8_t *base, orc_gro_desc *desc, uint64_t n, int threads);
+
 /* Timing helper for the cpu_baseline: runs orc_l4_uniform `reps` times and
  * returns elapsed seconds (monotonic clock). */
 double orc_time_l4_uniform(const uint8_t *base, uint64_t total_len, uint32_t segment_size,

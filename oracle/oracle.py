@@ -75,6 +75,8 @@ def _load():
     lib.orc_verify_desc.argtypes = [vp, vp, u64, vp, vp, i32]
     lib.orc_gro_finalize.restype = i32
     lib.orc_gro_finalize.argtypes = [vp, sz, u16, u16, i32, i32, u64]
+    lib.orc_gro_finalize_desc.restype = None
+    lib.orc_gro_finalize_desc.argtypes = [vp, vp, u64, i32]
     lib.orc_time_l4_uniform.restype = ctypes.c_double
     lib.orc_time_l4_uniform.argtypes = [vp, u64, u32, u16, u32, vp, i32, i32]
     return lib
@@ -172,6 +174,23 @@ def gro_finalize(hdr, csum_start: int, csum_offset: int, isv6: bool, istcp: bool
     st = int(lib.orc_gro_finalize(a.ctypes.data, a.size, csum_start, csum_offset, int(isv6), int(istcp),
                                   payload_bytes))
     return st, a
+
+
+GRO_DESC = np.dtype([("hdr_offset", "<u8"), ("payload_bytes", "<u8"), ("hdr_len", "<u2"), ("csum_start", "<u2"),
+                     ("csum_offset", "<u2"), ("flags", "u1"), ("status", "i1")])
+assert GRO_DESC.itemsize == 24
+
+
+def gro_finalize_desc(hdrs: np.ndarray, desc: np.ndarray, threads: int | None = None):
+    """Batched GRO finalize; returns (headers after, status array).  Inputs
+    are not modified."""
+    a = np.array(_u8(hdrs), copy=True)
+    d = np.array(np.ascontiguousarray(desc).view(GRO_DESC).reshape(-1), copy=True)
+    end = (d["hdr_offset"].astype(np.int64) + d["hdr_len"]).max() if d.size else 0
+    if end > a.size:
+        raise ValueError("gro_finalize_desc: descriptor past the header buffer")
+    lib.orc_gro_finalize_desc(a.ctypes.data, d.ctypes.data, d.size, threads or default_threads())
+    return a, d["status"].copy()
 
 
 def gso_split(inbuf: np.ndarray, vnet: dict, out_cap: int):

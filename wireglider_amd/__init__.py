@@ -210,16 +210,21 @@ def checksum_desc(base, desc, out=None, stream=None):
 VERDICT_IP_OK, VERDICT_L4_OK, VERDICT_TCP, VERDICT_UDP, VERDICT_V6 = 0x01, 0x02, 0x04, 0x08, 0x10
 
 
-def verify_desc(base, desc, with_l4: bool = True, stream=None):
+def verify_desc(base, desc, with_l4: bool = True, stream=None, verdict=None, l4=None):
     """Decap verify gates (evaluate_packet's checksum decisions,
     include/worker/evaluator.hpp:112-149) per descriptor.  Returns
-    (verdict uint8 tensor, L4 result uint16 tensor or None)."""
+    (verdict uint8 tensor, L4 result uint16 tensor or None); preallocated
+    outputs may be passed in."""
     torch = _torch()
     _require_cuda(base, "base")
     _require_cuda(desc, "desc")
     n = desc.numel() * desc.element_size() // PKT_DESC_BYTES
-    verdict = torch.empty(n, dtype=torch.uint8, device=base.device)
-    l4 = torch.empty(n, dtype=torch.uint16, device=base.device) if with_l4 else None
+    if verdict is None:
+        verdict = torch.empty(n, dtype=torch.uint8, device=base.device)
+    if l4 is None and with_l4:
+        l4 = torch.empty(n, dtype=torch.uint16, device=base.device)
+    if verdict.numel() < n or (l4 is not None and l4.numel() < n):
+        raise ValueError("verify_desc: output tensors shorter than the descriptor batch")
     rc = lib.wg_verify_desc(base.data_ptr(), desc.data_ptr(), n, verdict.data_ptr(),
                             l4.data_ptr() if l4 is not None else None, _stream_ptr(stream))
     _check(rc, "wg_verify_desc")

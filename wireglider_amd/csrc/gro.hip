@@ -10,7 +10,7 @@
 // overload and sums the std::span objects (pointer + size) instead —
 // pointer-dependent, not reproduced.
 //
-// Header-only work (<= a few hundred bytes per flow): one thread per flow.
+// Header-only work (tens of bytes per flow): one thread per flow.
 #include <hip/hip_runtime.h>
 
 #include "wg_device.hpp"
@@ -24,48 +24,136 @@ __device__ __forceinline__ void st_be16(uint8_t *p, uint32_t v) {
     p[1] = (uint8_t)v;
 }
 
+// Fast path: the bytes finalize reads (v4: [0, csum_start); v6: [0, 40)) lie
+// within 64 bytes of the header start.  They are fetched as (at most) five
+// aligned 16-byte chunks — an aligned chunk holding a valid byte never
+// crosses a page, and chunks past the last needed byte are clamped onto it —
+// then funnel-shifted (v_alignbyte) into 16 header-relative dwords R[0..15],
+// so every field sits at a static byte position.  The IPv4 length and
+// checksum bytes are excluded from the header sum and the new length added,
+// so nothing is read after it is written.
+constexpr uint32_t kFastNeed = 64;
+
+__device__ __forceinline__ uint32_t keep_below(uint32_t w, int m, uint32_t lim) {
+    // bytes of header-relative dword m at positions < lim
+    const int k = (int)lim - 4 * m;
+    return k >= 4 ? w : (k <= 0 ? 0u : (w & ((1u << (8 * k)) - 1u)));
+}
+
+__device__ __forceinline__ uint32_t sum16x2(uint32_t w) { return (w & 0xffffu) + (w >> 16); }
+
+__device__ __forceinline__ void st16_ne(uint8_t *p, uint32_t v) {  // native-order 16-bit store
+    if (!((uintptr_t)p & 1u)) {
+        *reinterpret_cast<uint16_t *>(p) = (uint16_t)v;
+    } else {
+        p[0] = (uint8_t)v;
+        p[1] = (uint8_t)(v >> 8);
+    }
+}
+
+__device__ __forceinline__ void gro_fast(uint8_t *h, const wg_gro_desc &d, bool v6, uint64_t l4len, uint32_t need) {
+    const uint64_t addr = (uint64_t)(uintptr_t)h;
+    const uint32_t s = (uint32_t)(addr & 15u);
+    const uintptr_t a0 = (uintptr_t)(addr - s);
+    const uintptr_t alast = (uintptr_t)((addr + need - 1) & ~15ull);
+    uint32_t W[20];
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+        const uintptr_t a = a0 + 16u * c;
+        const v4u v = ld16(a > alast ? alast : a);
+        W[4 * c] = v[0];
+        W[4 * c + 1] = v[1];
+        W[4 * c + 2] = v[2];
+        W[4 * c + 3] = v[3];
+    }
+    const uint32_t q = s >> 2, sh = s & 3u;
+    uint32_t R[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++) {
+        const uint32_t lo = q == 0 ? W[m] : q == 1 ? W[m + 1] : q == 2 ? W[m + 2] : W[m + 3];
+        const uint32_t hi = q == 0 ? W[m + 1] : q == 1 ? W[m + 2] : q == 2 ? W[m + 3] : W[m + 4];
+        R[m] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    }
+    const uint32_t cs = d.csum_start;
+    const uint32_t l16 = (uint32_t)l4len & 0xffffu;
+    uint32_t sad, proto;
+    if (!v6) {
+        const uint32_t T = (uint32_t)((uint64_t)d.hdr_len + d.payload_bytes) & 0xffffu;
+        uint32_t sip = (R[0] & 0xffffu) + sum16x2(R[1]) + (R[2] & 0xffffu);  // skip ip_len (2-3), ip_sum (10-11)
+#pragma unroll
+        for (int m = 3; m < 16; m++)
+            sip += sum16x2(keep_below(R[m], m, cs));
+        const uint32_t c = ~fold16_32(sip + bswap16(T)) & 0xffffu;  // :103-106
+        st16_ne(h + 2, bswap16(T));
+        st16_ne(h + 10, c);  // native order
+        sad = sum16x2(R[3]) + sum16x2(R[4]);
+        proto = (R[2] >> 8) & 0xffu;
+    } else {
+        st16_ne(h + 4, bswap16(l16));  // :95
+        sad = 0;
+#pragma unroll
+        for (int m = 2; m < 10; m++)
+            sad += sum16x2(R[m]);
+        proto = (R[1] >> 16) & 0xffu;
+    }
+    const uint32_t seed = ~fold16_32(sad + (proto << 8) + bswap16(l16)) & 0xffffu;  // :108-112
+    st16_ne(h + cs + d.csum_offset, seed);                                          // native order, :114
+}
+
+// General path (header fields beyond 64 bytes): byte loop in reference order.
+__device__ __noinline__ void gro_slow(uint8_t *h, uint32_t H, uint32_t cs, uint32_t l4off, uint64_t payload_bytes,
+                                     bool v6, uint64_t l4len) {
+    uint32_t proto, ao, al;
+    if (v6) {
+        proto = h[6];
+        ao = 8;
+        al = 32;
+        st_be16(h + 4, (uint32_t)l4len);
+    } else {
+        proto = h[9];
+        ao = 12;
+        al = 8;
+        st_be16(h + 2, (uint32_t)((uint64_t)H + payload_bytes));
+        uint32_t s = 0;
+        for (uint32_t j = 0; j < cs; j++)
+            s += (j == 10 || j == 11) ? 0u : (uint32_t)h[j] << (8u * (j & 1));
+        const uint32_t c = ~fold16_32(s) & 0xffffu;
+        stb(h + 10, c & 0xffu);
+        stb(h + 11, c >> 8);
+    }
+    uint32_t ps = 0;
+    for (uint32_t j = 0; j < al; j++)
+        ps += (uint32_t)h[ao + j] << (8u * (j & 1u));
+    ps += (proto << 8) + bswap16((uint32_t)l4len & 0xffffu);
+    const uint32_t seed = ~fold16_32(ps) & 0xffffu;
+    stb(h + l4off, seed & 0xffu);
+    stb(h + l4off + 1, seed >> 8);
+}
+
 __global__ __launch_bounds__(256) void gro_finalize_kernel(uint8_t *hdrs, wg_gro_desc *desc, uint64_t n) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        wg_gro_desc d = desc[i];
-        uint8_t *h = hdrs + d.hdr_offset;
-        const uint32_t H = d.hdr_len, cs = d.csum_start, l4off = (uint32_t)d.csum_start + d.csum_offset;
-        const bool v6 = d.flags & WG_PKT_V6, tcp = d.flags & WG_PKT_TCP;
-        const uint32_t iph = v6 ? 40u : 20u;
-        if (cs < iph || cs > H || l4off < cs || l4off + 2 > H || (!tcp && cs + 8 > H)) {
-            desc[i].status = -3;
-            continue;
-        }
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const wg_gro_desc d = desc[i];
+    uint8_t *h = hdrs + d.hdr_offset;
+    const uint32_t H = d.hdr_len, cs = d.csum_start, l4off = (uint32_t)d.csum_start + d.csum_offset;
+    const bool v6 = d.flags & WG_PKT_V6, tcp = d.flags & WG_PKT_TCP;
+    const uint32_t iph = v6 ? 40u : 20u;
+    int8_t st = 0;
+    if (cs < iph || cs > H || l4off < cs || l4off + 2 > H || (!tcp && cs + 8 > H)) {
+        st = -3;
+    } else {
         const uint64_t l4len = (uint64_t)(H - cs) + d.payload_bytes;  // :84
         if (!tcp)
             st_be16(h + cs + 4, (uint32_t)l4len);  // udp->len (uint16), :85-86
-        uint32_t proto, ao, al;
-        if (v6) {
-            proto = h[6];
-            ao = 8;
-            al = 32;
-            st_be16(h + 4, (uint32_t)l4len);  // ip6_plen, :95
-        } else {
-            proto = h[9];
-            ao = 12;
-            al = 8;
-            st_be16(h + 2, (uint32_t)((uint64_t)H + d.payload_bytes));  // ip_len, :103
-            uint32_t s = 0;  // checksum(hdrbuf[0:cs]) with ip_sum = 0, :104-106
-            for (uint32_t j = 0; j < cs; j++)
-                s += (j == 10 || j == 11) ? 0u : (uint32_t)h[j] << (8u * (j & 1u));
-            const uint32_t c = ~fold16_32(s) & 0xffffu;
-            stb(h + 10, c & 0xffu);  // native order
-            stb(h + 11, c >> 8);
-        }
-        uint32_t ps = 0;  // pseudo-header: addresses + {0, proto} + l4len (uint16), :108-112
-        for (uint32_t j = 0; j < al; j++)
-            ps += (uint32_t)h[ao + j] << (8u * (j & 1u));
-        ps += (proto << 8) + bswap16((uint32_t)l4len & 0xffffu);
-        const uint32_t seed = ~fold16_32(ps) & 0xffffu;
-        stb(h + l4off, seed & 0xffu);  // native order, :114
-        stb(h + l4off + 1, seed >> 8);
-        desc[i].status = 0;
+        const uint32_t need = v6 ? 40u : cs;
+        if (need <= kFastNeed)
+            gro_fast(h, d, v6, l4len, need);
+        else
+            gro_slow(h, H, cs, l4off, d.payload_bytes, v6, l4len);
     }
+    if (d.status != st)  // leave descriptor lines clean when the caller pre-zeroed status
+        reinterpret_cast<int8_t *>(desc)[i * sizeof(wg_gro_desc) + offsetof(wg_gro_desc, status)] = st;
 }
 
 }  // namespace wg
@@ -77,9 +165,9 @@ extern "C" int wg_gro_finalize(uint8_t *dev_hdrs, wg_gro_desc *dev_desc, uint64_
         return WG_OK;
     if (!dev_hdrs || !dev_desc || (reinterpret_cast<uintptr_t>(dev_desc) & 7))
         return WG_ERR_INVALID;
-    uint64_t blocks = (n + 255) / 256;
-    if (blocks > 8192)
-        blocks = 8192;
+    const uint64_t blocks = (n + 255) / 256;
+    if (blocks > 0x7fffffffull)
+        return WG_ERR_INVALID;
     hipLaunchKernelGGL(gro_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
                        dev_hdrs, dev_desc, n);
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
