@@ -15,7 +15,7 @@ HDR = ROOT / "include" / "wireglider_amd.h"
 
 def declared_symbols():
     txt = HDR.read_text()
-    return sorted(set(re.findall(r"^(?:int|const char \*)\s*(wg_\w+)\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|uint64_t|const char \*)\s*(wg_\w+)\(", txt, flags=re.M)))
 
 
 def test_header_declares_expected():

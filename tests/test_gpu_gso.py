@@ -25,6 +25,15 @@ def _wga():
     return wireglider_amd
 
 
+@pytest.fixture(params=[0, 32], ids=["swizzled", "launch-order"])
+def variant(request):
+    """Both correct block -> super-buffer mappings of the GSO kernel."""
+    wga = _wga()
+    wga.tune_set("gso_ablate", request.param)
+    yield request.param
+    wga.tune_set("gso_ablate", 0)
+
+
 def run_batch(gpu, cases, out_cap_fn=lambda c: None, seed=0):
     """cases: list of (pkt bytes, vnet dict, out_cap or None).  Lays the
     super-buffers out at random (unaligned) offsets, runs the GPU once, and
@@ -84,7 +93,7 @@ def run_batch(gpu, cases, out_cap_fn=lambda c: None, seed=0):
             assert np.all(g_out[oo:oo + caps[k]] == sentinel), ctx
 
 
-def test_reference_offload_cases(gpu):
+def test_reference_offload_cases(gpu, variant):
     cases = []
     a4 = ("192.0.2.1", "192.0.2.2")
     a6 = ("2001:db8::1", "2001:db8::2")
@@ -159,10 +168,40 @@ def random_case(rng):
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_random_super_buffers(gpu, seed):
+def test_random_super_buffers(gpu, variant, seed):
     rng = np.random.default_rng(seed)
     cases = [random_case(rng) for _ in range(400)]
     run_batch(gpu, cases, seed=seed)
+
+
+def _far_csum_start(rng, cs, plen, istcp=True):
+    """IPv4 super-buffer whose csum_start lies `cs - 20` bytes past the IP
+    header (the reference takes csum_start from the vnet header as is)."""
+    base = pktbuild.build(False, istcp, rng.integers(0, 256, plen, dtype=np.uint8).tobytes(),
+                          pktbuild.ipv4_addr("10.1.2.3"), pktbuild.ipv4_addr("10.3.2.1"), seq=77, fill_l4=False)
+    return base[:20] + rng.integers(0, 256, cs - 20, dtype=np.uint8).tobytes() + base[20:]
+
+
+def test_geometry_edges(gpu):
+    """Segment shapes at the kernel's edges: segments shorter than a 16-B
+    chunk, thousands of segments per super-buffer, headers past the 128
+    prefix bytes held in registers (csum_start 508 / 600), and last segments
+    of 1..17 bytes."""
+    rng = np.random.default_rng(99)
+    cases = []
+    for gso, plen in ((1, 7000), (3, 20000), (5, 33), (15, 16 * 97 + 1), (16, 4097), (17, 300)):
+        p = pktbuild.build(False, True, rng.integers(0, 256, plen, dtype=np.uint8).tobytes(),
+                           pktbuild.ipv4_addr("10.0.0.1"), pktbuild.ipv4_addr("10.0.0.2"), seq=5, fill_l4=False)
+        cases.append((p, dict(flags=1, gso_type=1, gso_size=gso, csum_start=20, csum_offset=16), None))
+    for tail in range(1, 18):
+        p = pktbuild.build(True, False, rng.integers(0, 256, 1448 * 3 + tail, dtype=np.uint8).tobytes(),
+                           pktbuild.ipv6_addr("2001:db8::5"), pktbuild.ipv6_addr("2001:db8::6"), fill_l4=False)
+        cases.append((p, dict(flags=1, gso_type=5, gso_size=1448, csum_start=40, csum_offset=6), None))
+    for cs in (508, 600):
+        p = _far_csum_start(rng, cs, 5000)
+        cases.append((p, dict(flags=1, gso_type=1, gso_size=1000, csum_start=cs, csum_offset=16), None))
+    run_batch(gpu, cases, seed=7)
+    run_batch(gpu, cases, seed=8)
 
 
 def test_config3_full_size_properties(gpu):

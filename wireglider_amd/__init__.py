@@ -101,6 +101,7 @@ def _load() -> ctypes.CDLL:
         "wg_checksum_desc": (i32, [u8p, vp, u64, vp, vp]),
         "wg_verify_desc": (i32, [u8p, vp, u64, vp, vp, vp]),
         "wg_gso_split": (i32, [u8p, vp, u64, u8p, vp, vp]),
+
         "wg_gro_finalize": (i32, [u8p, vp, u64, vp]),
         "wg_l4csum_uniform_host": (i32, [u8p, u64, u32, u16, u32, vp]),
         "wg_synth_fill": (i32, [u8p, u64, u64, u64, vp]),

@@ -226,7 +226,7 @@ extern "C" int wg_tune_set(const char *key, uint64_t value) {
         t.gso_split = (uint32_t)value;
     else if (k == "gso_spw" && (value == 1 || value == 2))
         t.gso_spw = (uint32_t)value;
-    else if (k == "gso_ablate" && value <= 7 && value != 5)
+    else if (k == "gso_ablate" && ((value <= 7 && value != 5) || value == 32))
         t.gso_ablate = (uint32_t)value;
     else
         return WG_ERR_INVALID;

@@ -18,131 +18,11 @@
 
 #include "wg_device.hpp"
 #include "wg_internal.hpp"
+#include "wg_gso.hpp"
 #include "wg_l4wave.hpp"
 #include "wireglider_amd.h"
 
 namespace wg {
-
-enum : uint32_t {
-    kNeedsCsum = 1,
-    kGsoNone = 0,
-    kGsoTcp4 = 1,
-    kGsoTcp6 = 4,
-    kGsoUdpL4 = 5,  // include/worker/offload.hpp:11-15
-    kGsoEcn = 0x80,
-};
-
-struct GsoParams {
-    uint8_t *in;
-    const wg_gso_desc *desc;
-    uint64_t n;
-    uint8_t *out;
-    wg_gso_result *res;
-};
-
-// Wave-uniform byte load (every lane reads the same address).
-__device__ __forceinline__ uint32_t ubyte_u(uintptr_t a) {
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)ld8(a));
-}
-
-struct Ctx {
-    uintptr_t in;
-    uint32_t in_len, cs, l4off, hdr_len, gso, nseg;
-    uint32_t rest;  // payload bytes after the prefix
-    uint32_t id0, seq0;
-    bool v6, tcp;
-    // Per-super-buffer header sums over the bytes that do NOT change from
-    // segment to segment (computed once by each wave, hdr_bases()):
-    uint32_t ip_base;   // IPv4 header [0, cs) minus len/id, ip_sum = 0 (pairing from byte 0)
-    uint32_t l4h_base;  // L4 header [cs, hdr_len) minus seq/flags (TCP) or len (UDP) (pairing from cs)
-    uint32_t ps_sum;    // pseudo-header addresses
-    uint32_t flags13;   // TCP flags byte of the prefix
-    uint32_t hb0, hb1;  // this lane's prefix bytes lane, lane + 64 (one load for the whole wave)
-};
-
-// Prefix byte j, wave-uniform: from the registers of the one prefix load
-// when j < 128, else a direct load.
-__device__ __forceinline__ uint32_t pbyte(const Ctx &c, uint32_t j) {
-    if (j < 64)
-        return (uint32_t)__builtin_amdgcn_readlane((int)c.hb0, (int)j);
-    if (j < 128)
-        return (uint32_t)__builtin_amdgcn_readlane((int)c.hb1, (int)(j - 64));
-    return ubyte_u(c.in + j);
-}
-
-// Is prefix byte j one of the per-segment L4 header fields?
-__device__ __forceinline__ bool l4_varying(const Ctx &c, uint32_t j) {
-    return c.tcp ? ((j >= c.cs + 4 && j < c.cs + 8) || j == c.cs + 13) : (j == c.cs + 4 || j == c.cs + 5);
-}
-
-// One pass over the prefix per wave: exact integer sums of the invariant
-// header bytes (the reference's values after the :145-149 zeroing).
-__device__ void hdr_bases(Ctx &c, uint32_t lane) {
-    const uint32_t ao = c.v6 ? 8u : 12u, al = c.v6 ? 32u : 8u;
-    uint32_t ip = 0, l4 = 0, ps = 0;
-    for (uint32_t j = lane; j < c.hdr_len; j += 64) {
-        uint32_t b = j < 64 ? c.hb0 : (j < 128 ? c.hb1 : ld8(c.in + j));
-        if ((!c.v6 && (j == 10 || j == 11)) || j == c.l4off || j == c.l4off + 1)
-            b = 0;
-        if (j < c.cs) {
-            if (!(!c.v6 && j >= 2 && j <= 5))
-                ip += b << (8u * (j & 1u));
-        } else if (!l4_varying(c, j)) {
-            l4 += b << (8u * ((j - c.cs) & 1u));
-        }
-        if (j >= ao && j < ao + al)
-            ps += b << (8u * ((j - ao) & 1u));
-    }
-    c.ip_base = wave_sum_u32(ip);
-    c.l4h_base = wave_sum_u32(l4);
-    c.ps_sum = wave_sum_u32(ps);
-    const uint32_t j13 = c.cs + 13;
-    c.flags13 = (c.tcp && j13 < c.hdr_len && j13 != c.l4off && j13 != c.l4off + 1) ? pbyte(c, j13) : 0u;
-}
-
-// Prefix byte j of segment i after the IP fix-ups (offload.cpp:145-149
-// zeroing of ip_sum / L4 field, then :168-183).
-__device__ __forceinline__ uint32_t stage_ip(const Ctx &c, uint32_t j, uint32_t b, uint32_t i, uint32_t pktlen) {
-    if (!c.v6 && (j == 10 || j == 11))
-        b = 0;
-    if (j == c.l4off || j == c.l4off + 1)
-        b = 0;
-    if (c.v6) {
-        const uint32_t plen = pktlen - c.cs;  // ip6_plen (uint16 on store)
-        if (j == 4) b = (plen >> 8) & 0xffu;
-        if (j == 5) b = plen & 0xffu;
-    } else {
-        if (j == 2) b = (pktlen >> 8) & 0xffu;  // ip_len
-        if (j == 3) b = pktlen & 0xffu;
-        if (i) {
-            const uint32_t id = c.id0 + i;  // ip_id += i (uint16)
-            if (j == 4) b = (id >> 8) & 0xffu;
-            if (j == 5) b = id & 0xffu;
-        }
-    }
-    return b;
-}
-
-// ... then the L4 header fix-ups (:189-200).  `istcp` is the UNMASKED
-// gso_type test of :151, so TCP|ECN super-buffers get the UDP fix-up.
-__device__ __forceinline__ uint32_t stage_l4(const Ctx &c, uint32_t j, uint32_t b, uint32_t i, uint32_t pktlen,
-                                             bool last) {
-    if (j < c.cs)
-        return b;
-    if (c.tcp) {
-        if (j >= c.cs + 4 && j < c.cs + 8) {
-            const uint32_t seq = c.seq0 + c.gso * i;
-            b = (seq >> (8u * (c.cs + 7u - j))) & 0xffu;
-        } else if (j == c.cs + 13 && !last) {
-            b &= ~0x09u;  // FIN, PSH only on the last segment
-        }
-    } else {
-        const uint32_t ulen = pktlen - c.cs;
-        if (j == c.cs + 4) b = (ulen >> 8) & 0xffu;
-        if (j == c.cs + 5) b = ulen & 0xffu;
-    }
-    return b;
-}
 
 // Bytes delta..delta+15 of the 32-byte window lo|hi; q = delta >> 2 is
 // wave-uniform (scalar branch), r = delta & 3 goes to v_alignbyte.
@@ -172,7 +52,10 @@ __device__ __forceinline__ void st16_nt(uintptr_t addr, v4u v) {
 // Timing-only (WRONG output, to price one part of the kernel, guide §5.4
 // rule 17): 2 = no byte stores (header / payload head & tail), 4 = no
 // re-alignment window (one source chunk per output chunk).
-enum : int { kAblNtStore = 1, kAblNoByteStores = 2, kAblOneLoad = 4 };
+// 32 = blocks -> super-buffers in launch order instead of XCD-swizzled (a
+// correct variant; the swizzle keeps consecutive super-buffers on one XCD,
+// +2.7 % on config 3).
+enum : int { kAblNtStore = 1, kAblNoByteStores = 2, kAblOneLoad = 4, kAblNoSwizzle = 32 };
 
 template <int A>
 __device__ __forceinline__ void st16x(uintptr_t addr, v4u v) {
@@ -182,9 +65,6 @@ __device__ __forceinline__ void st16x(uintptr_t addr, v4u v) {
         *reinterpret_cast<__attribute__((address_space(1))) v4u *>(addr) = v;
 }
 
-__device__ __forceinline__ void st8(uintptr_t addr, uint32_t b) {
-    *reinterpret_cast<__attribute__((address_space(1))) uint8_t *>(addr) = (uint8_t)b;
-}
 
 // One output segment by one wave, in two phases so a wave can have several
 // segments' loads in flight: seg_issue() issues every load of the segment
@@ -238,14 +118,15 @@ __device__ __forceinline__ v4u src_chunk(const SegGeom &g, uint64_t m) {
 // Output chunk k needs source chunks k and k + 1 (re-alignment window):
 // chunk k + 1 of lane l is chunk k of lane l + 1, fetched by a lane shuffle;
 // lane 63 takes it from `next` (lane 0's chunk of the following row).
-__device__ __forceinline__ v4u next_chunk(v4u lo, v4u next, uint32_t lane) {
+__device__ __forceinline__ v4u next_chunk(v4u lo, v4u next) {
+    // DPP wave_shl:1 — lane l reads lane l + 1; lane 63 has no source and
+    // keeps `old` = next (bound_ctrl off).  (A ds_bpermute shuffle measured
+    // the same, tools/ab_gso.py.)
     v4u h;
-    h.x = (uint32_t)__shfl_down((int)lo.x, 1);
-    h.y = (uint32_t)__shfl_down((int)lo.y, 1);
-    h.z = (uint32_t)__shfl_down((int)lo.z, 1);
-    h.w = (uint32_t)__shfl_down((int)lo.w, 1);
-    if (lane == 63)
-        h = next;
+    h.x = (uint32_t)__builtin_amdgcn_update_dpp((int)next.x, (int)lo.x, 0x130, 0xf, 0xf, false);
+    h.y = (uint32_t)__builtin_amdgcn_update_dpp((int)next.y, (int)lo.y, 0x130, 0xf, 0xf, false);
+    h.z = (uint32_t)__builtin_amdgcn_update_dpp((int)next.z, (int)lo.z, 0x130, 0xf, 0xf, false);
+    h.w = (uint32_t)__builtin_amdgcn_update_dpp((int)next.w, (int)lo.w, 0x130, 0xf, 0xf, false);
     return h;
 }
 
@@ -289,8 +170,8 @@ __device__ __forceinline__ void seg_finish(const Ctx &c, uintptr_t out_base, con
     // payload: re-align, store, sum
     if (g.nint) {
         const v4u nx1 = g.nint > 127 ? lane0(src_chunk(g, 128)) : f.lo1;
-        const v4u hi0 = next_chunk(f.lo0, lane0(f.lo1), lane);
-        const v4u hi1 = next_chunk(f.lo1, nx1, lane);
+        const v4u hi0 = next_chunk(f.lo0, lane0(f.lo1));
+        const v4u hi1 = next_chunk(f.lo1, nx1);
         if (lane < g.nint) {
             const v4u v = funnel(f.lo0, (Abl & kAblOneLoad) ? f.lo0 : hi0, g.q, g.r);
             st16x<Abl>(g.c0 + 16ull * lane, v);
@@ -333,158 +214,18 @@ __device__ __forceinline__ void seg_finish(const Ctx &c, uintptr_t out_base, con
     uint32_t T = wave_sum_u32(lp) + l4h + c.ps_sum;
     T += ((c.tcp ? 6u : 17u) << 8) + bswap16((pktlen - c.cs) & 0xffffu);
     const uint32_t l4cs = ~fold16_32(T) & 0xffffu;
-    const uint32_t j0 = lane, j1 = lane + 64;
-
-    // write the header prefix (checksums in native order, :185-186, :203-204)
-    auto final_byte = [&](uint32_t j, uint32_t s4) {
-        if (!c.v6 && j == 10) return ipcs & 0xffu;
-        if (!c.v6 && j == 11) return ipcs >> 8;
-        if (j == c.l4off) return l4cs & 0xffu;
-        if (j == c.l4off + 1) return l4cs >> 8;
-        return s4;
-    };
-    auto s4 = [&](uint32_t j, uint32_t b) { return stage_l4(c, j, stage_ip(c, j, b, i, pktlen), i, pktlen, g.last); };
+    // write the header prefix: each byte is the prefix byte or one byte of a
+    // per-segment value, by its precomputed field code (checksums in native
+    // order, :185-186, :203-204)
     if (Abl & kAblNoByteStores) {
         if (lane == 0 && l4cs == 0x12345u) st8(g.seg, 0);  // keep the sums live
         return;
     }
-    if (j0 < c.hdr_len) st8(g.seg + j0, final_byte(j0, s4(j0, c.hb0)));
-    if (j1 < c.hdr_len) st8(g.seg + j1, final_byte(j1, s4(j1, c.hb1)));
-    for (uint32_t j = lane + 128; j < c.hdr_len; j += 64) {
-        const uint32_t b2 = stage_ip(c, j, ld8(c.in + j), i, pktlen);
-        st8(g.seg + j, final_byte(j, stage_l4(c, j, b2, i, pktlen, g.last)));
-    }
-}
-
-// GSO_NONE + NEEDS_CSUM (offload.cpp:56-78): both checksums in place, one wave.
-__device__ void do_inplace(const Ctx &c, uint32_t lane) {
-    // IPv4 header checksum over [0, cs) with ip_sum zeroed.
-    uint32_t ipcs = 0;
-    if (!c.v6) {
-        uint32_t part = 0;
-        for (uint32_t j = lane; j < c.cs; j += 64) {
-            uint32_t b = ld8(c.in + j);
-            if (j == 10 || j == 11) b = 0;
-            part += b << (8u * (j & 1u));
-        }
-        ipcs = ~fold16_32(wave_sum_u32(part)) & 0xffffu;
-    }
-    // L4 over the bytes as they are, then replace the checksum field's
-    // contribution by zero: adding 0xFFFF - x is subtracting x mod 0xFFFF,
-    // and the total is never zero (the pseudo-header carries the protocol),
-    // so the fold only depends on the sum mod 0xFFFF.
-    Geom g;
-    g.a = c.in;
-    g.len = c.in_len;
-    g.cs = c.cs;
-    g.fl = (c.v6 ? WG_PKT_V6 : 0u) | (c.tcp ? WG_PKT_TCP : 0u);
-    Front f;
-    issue<true, false>(g, lane, f);
-    const uint32_t f0 = ld8(c.in + c.l4off), f1 = ld8(c.in + c.l4off + 1);
-    uint32_t T = wave_sum_u32(finish<false>(lane, f));
-    const uint32_t fw = ((c.l4off - c.cs) & 1u) ? ((f0 << 8) | f1) : (f0 | (f1 << 8));
-    T += 0xffffu - fw;
-    T += ((c.tcp ? 6u : 17u) << 8) + bswap16((c.in_len - c.cs) & 0xffffu);
-    const uint32_t l4cs = ~fold16_32(T) & 0xffffu;
-    if (lane == 0) {
-        if (!c.v6) {
-            st8(c.in + 10, ipcs & 0xffu);
-            st8(c.in + 11, ipcs >> 8);
-        }
-        st8(c.in + c.l4off, l4cs & 0xffu);
-        st8(c.in + c.l4off + 1, l4cs >> 8);
-    }
-}
-
-// Classification of one super-buffer (mirrors :48-134 and the oracle).
-// kUniform: called by a whole wave (wave-uniform byte loads).
-struct Cls {
-    int status;
-    bool pass, inplace;
-    uint32_t isv6, ecn;
-};
-
-template <bool kUniform>
-__device__ __forceinline__ uint32_t ldb(const Ctx &c, uint32_t j) {
-    if constexpr (kUniform)
-        return pbyte(c, j);
-    else
-        return ld8(c.in + j);
-}
-
-template <bool kUniform>
-__device__ __forceinline__ Cls classify(const wg_gso_desc &dsc, uintptr_t in_base, Ctx &c) {
-    c.in = in_base + dsc.in_offset;
-    c.in_len = dsc.in_len;
-    c.cs = dsc.vnet.csum_start;
-    c.l4off = (uint32_t)dsc.vnet.csum_start + dsc.vnet.csum_offset;  // :47
-    c.hdr_len = dsc.vnet.hdr_len;
-    c.gso = dsc.vnet.gso_size;
-    c.rest = 0;
-    c.nseg = 0;
-    c.v6 = false;
-    const uint32_t gtype = dsc.vnet.gso_type;
-    Cls r{0, true, false, 0u, 0u};
-    if (c.in_len < 1) {
-        r.status = -3;
-        return r;
-    }
-    if constexpr (kUniform) {
-        // the whole wave loads prefix bytes 0-127 at once; every byte the
-        // classification and the header work need is then a readlane
-        const uint32_t lane = lane_id();
-        c.hb0 = ld8(c.in + (lane < c.in_len ? lane : 0u));
-        c.hb1 = ld8(c.in + (lane + 64 < c.in_len ? lane + 64 : 0u));
-    }
-    r.isv6 = (ldb<kUniform>(c, 0) >> 4) == 6;  // :48
-    const uint32_t iph_min = r.isv6 ? 40u : 20u;
-    if (c.in_len < iph_min) {
-        r.status = -3;
-        return r;
-    }
-    r.ecn = r.isv6 ? ((ldb<kUniform>(c, 1) >> 4) & 3u) : (ldb<kUniform>(c, 1) & 3u);  // :49-53
-    c.v6 = r.isv6;
-    const uint32_t g = gtype & ~kGsoEcn;  // :55
-    bool seg = false;
-    if (g == kGsoNone) {
-        if (dsc.vnet.flags & kNeedsCsum) {
-            if (c.cs < iph_min || c.cs > c.in_len || c.l4off + 2 > c.in_len)
-                r.status = -3;
-            else
-                r.inplace = true;
-        }
-    } else if (g == kGsoTcp4 || g == kGsoTcp6) {
-        if (c.cs > c.in_len) {
-            r.status = -3;
-        } else if (c.in_len - c.cs >= 20) {                                        // :91
-            const uint32_t thlen = 4u * (ldb<kUniform>(c, c.cs + 12) >> 4);  // doff, :100
-            if (thlen >= 20) {                                                    // :101
-                c.hdr_len = c.cs + thlen;                                         // :110
-                seg = true;
-            }
-        }
-    } else if (g == kGsoUdpL4) {
-        c.hdr_len = c.cs + 8;  // :114
-        seg = true;
-    }
-    if (seg && c.in_len >= c.hdr_len) {  // :126-134
-        if (c.cs < iph_min || c.l4off < c.cs || c.l4off + 2 > c.hdr_len) {
-            r.status = -3;
-        } else {
-            c.rest = c.in_len - c.hdr_len;
-            if (c.rest && !c.gso) {
-                r.status = -1;  // the reference loops forever
-            } else {
-                c.nseg = c.gso ? (c.rest + c.gso - 1) / c.gso : 0;
-                if ((uint64_t)dsc.out_cap < (uint64_t)c.in_len + (uint64_t)c.nseg * c.hdr_len)
-                    r.status = -2;  // reserve_size assert, :139-143
-                else
-                    r.pass = false;
-            }
-        }
-    }
-    c.tcp = gtype == kGsoTcp4 || gtype == kGsoTcp6;  // :151, unmasked
-    return r;
+    const HdrVals hv{pktlen, c.id0 + i, ipcs, l4cs, c.seq0 + c.gso * i, pktlen - c.cs, g.last ? 0xffu : 0xf6u};
+    if (lane < c.hdr_len) st8(g.seg + lane, hdr_byte(hv, c.hc0, c.hb0));
+    if (lane + 64 < c.hdr_len) st8(g.seg + lane + 64, hdr_byte(hv, c.hc1, c.hb1));
+    for (uint32_t j = lane + 128; j < c.hdr_len; j += 64)
+        st8(g.seg + j, hdr_byte(hv, hdr_code(c, j), ld8(c.in + j)));
 }
 
 // Main kernel: blockIdx.x walks super-buffers, blockIdx.y splits a
@@ -495,7 +236,8 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
     const uint32_t lane = lane_id();
     const uint32_t gw = blockIdx.y * W + wave_in_block();  // wave index within the super-buffer
     const uint32_t gstride = gridDim.y * W * S;
-    for (uint64_t b = blockIdx.x; b < p.n; b += gridDim.x) {
+    const uint64_t b0 = (Abl & kAblNoSwizzle) ? blockIdx.x : xcd_swizzle(blockIdx.x, gridDim.x);
+    for (uint64_t b = b0; b < p.n; b += gridDim.x) {
         const wg_gso_desc dsc = p.desc[b];
         Ctx c;
         const Cls cl = classify<true>(dsc, reinterpret_cast<uintptr_t>(p.in), c);
@@ -593,6 +335,11 @@ __global__ __launch_bounds__(256) void gso_finalize_kernel(GsoParams p) {
 
 using namespace wg;
 
+static void launch_gso_finalize(const GsoParams &p, hipStream_t st) {
+    const uint64_t fb = (p.n + 255) / 256;
+    hipLaunchKernelGGL(gso_finalize_kernel, dim3((unsigned)(fb < 65536 ? fb : 65536)), dim3(256), 0, st, p);
+}
+
 extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
                             wg_gso_result *dev_res, void *stream) {
     if (!n)
@@ -602,20 +349,22 @@ extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64
         return WG_ERR_INVALID;
     GsoParams p{dev_in, dev_desc, n, dev_out, dev_res};
     const Tune &t = tune();
-    const uint64_t blocks = n < t.gso_blocks ? n : t.gso_blocks;
     hipStream_t st = static_cast<hipStream_t>(stream);
+    uint64_t blocks = n < t.gso_blocks ? n : t.gso_blocks;
+    if (blocks >= 8)
+        blocks &= ~7ull;  // the XCD swizzle wants a multiple of 8 (the grid-stride loop covers the rest)
     const dim3 g((unsigned)blocks, t.gso_split);
-    if (t.gso_ablate) {  // timing-only variants (wrong output), 4 waves x 1 segment
+    if (t.gso_ablate) {  // A/B variants, 4 waves x 1 segment (1, 32 correct; 2, 4 timing-only)
         switch (t.gso_ablate) {
         case 1: hipLaunchKernelGGL((gso_split_kernel<4, 1, 1>), g, dim3(256), 0, st, p); break;
         case 2: hipLaunchKernelGGL((gso_split_kernel<4, 1, 2>), g, dim3(256), 0, st, p); break;
         case 3: hipLaunchKernelGGL((gso_split_kernel<4, 1, 3>), g, dim3(256), 0, st, p); break;
         case 4: hipLaunchKernelGGL((gso_split_kernel<4, 1, 4>), g, dim3(256), 0, st, p); break;
         case 6: hipLaunchKernelGGL((gso_split_kernel<4, 1, 6>), g, dim3(256), 0, st, p); break;
+        case 32: hipLaunchKernelGGL((gso_split_kernel<4, 1, 32>), g, dim3(256), 0, st, p); break;
         default: hipLaunchKernelGGL((gso_split_kernel<4, 1, 7>), g, dim3(256), 0, st, p); break;
         }
-        uint64_t fb = (n + 255) / 256;
-        hipLaunchKernelGGL(gso_finalize_kernel, dim3((unsigned)(fb < 65536 ? fb : 65536)), dim3(256), 0, st, p);
+        launch_gso_finalize(p, st);
         return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
     }
     const uint32_t key = t.gso_waves * 10 + t.gso_spw;
@@ -629,9 +378,6 @@ extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64
     }
     if (hipGetLastError() != hipSuccess)
         return WG_ERR_LAUNCH;
-    {
-        uint64_t fb = (n + 255) / 256;
-        hipLaunchKernelGGL(gso_finalize_kernel, dim3((unsigned)(fb < 65536 ? fb : 65536)), dim3(256), 0, st, p);
-    }
+    launch_gso_finalize(p, st);
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }

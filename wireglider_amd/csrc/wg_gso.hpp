@@ -1,0 +1,285 @@
+// wg_gso.hpp — per-super-buffer state shared by the GSO split kernels
+// (gso.hip):
+// classification of do_tun_gso_split (reference worker/offload.cpp:46-134),
+// the invariant header sums, the per-segment header field codes, and the
+// GSO_NONE + NEEDS_CSUM in-place path.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "wg_device.hpp"
+#include "wg_l4wave.hpp"
+#include "wireglider_amd.h"
+
+namespace wg {
+
+enum : uint32_t {
+    kNeedsCsum = 1,
+    kGsoNone = 0,
+    kGsoTcp4 = 1,
+    kGsoTcp6 = 4,
+    kGsoUdpL4 = 5,  // include/worker/offload.hpp:11-15
+    kGsoEcn = 0x80,
+};
+
+struct GsoParams {
+    uint8_t *in;
+    const wg_gso_desc *desc;
+    uint64_t n;
+    uint8_t *out;
+    wg_gso_result *res;
+};
+
+// Wave-uniform byte load (every lane reads the same address).
+__device__ __forceinline__ uint32_t ubyte_u(uintptr_t a) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)ld8(a));
+}
+
+struct Ctx {
+    uintptr_t in;
+    uint32_t in_len, cs, l4off, hdr_len, gso, nseg;
+    uint32_t rest;  // payload bytes after the prefix
+    uint32_t id0, seq0;
+    bool v6, tcp;
+    // Per-super-buffer header sums over the bytes that do NOT change from
+    // segment to segment (computed once by each wave, hdr_bases()):
+    uint32_t ip_base;   // IPv4 header [0, cs) minus len/id, ip_sum = 0 (pairing from byte 0)
+    uint32_t l4h_base;  // L4 header [cs, hdr_len) minus seq/flags (TCP) or len (UDP) (pairing from cs)
+    uint32_t ps_sum;    // pseudo-header addresses
+    uint32_t flags13;   // TCP flags byte of the prefix
+    uint32_t hb0, hb1;  // this lane's prefix bytes lane, lane + 64 (one load for the whole wave)
+    uint32_t hc0, hc1;  // per-segment field code of prefix bytes lane, lane + 64 (hdr_code)
+};
+
+// Prefix byte j, wave-uniform: from the registers of the one prefix load
+// when j < 128, else a direct load.
+__device__ __forceinline__ uint32_t pbyte(const Ctx &c, uint32_t j) {
+    if (j < 64)
+        return (uint32_t)__builtin_amdgcn_readlane((int)c.hb0, (int)j);
+    if (j < 128)
+        return (uint32_t)__builtin_amdgcn_readlane((int)c.hb1, (int)(j - 64));
+    return ubyte_u(c.in + j);
+}
+
+// Is prefix byte j one of the per-segment L4 header fields?
+__device__ __forceinline__ bool l4_varying(const Ctx &c, uint32_t j) {
+    return c.tcp ? ((j >= c.cs + 4 && j < c.cs + 8) || j == c.cs + 13) : (j == c.cs + 4 || j == c.cs + 5);
+}
+
+// Field code of prefix byte j in every output segment: a one-hot selector of
+// the per-segment value that replaces it (bits 0-7; none = the prefix byte
+// as is, kSelFlags = TCP flags with FIN/PSH cleared except on the last
+// segment) and which byte of that value (shift, bits 8-12).  Priority as in
+// the reference's write order: checksums (written last, :185-186, :203-204)
+// over the length/id/seq fix-ups.  One-hot so the per-segment select is a
+// chain of independent bit tests (a dense selector becomes a scratch table).
+enum : uint32_t { kSelTmpl = 0, kSelPkt = 1, kSelId = 2, kSelIpcs = 4, kSelL4cs = 8, kSelSeq = 16, kSelUlen = 32,
+                  kSelFlags = 64 };
+
+__device__ __forceinline__ uint32_t hdr_code(const Ctx &c, uint32_t j) {
+    if (!c.v6 && (j == 10 || j == 11))
+        return kSelIpcs | ((j == 11 ? 8u : 0u) << 8);  // native order
+    if (j == c.l4off || j == c.l4off + 1)
+        return kSelL4cs | ((j == c.l4off + 1 ? 8u : 0u) << 8);
+    if (c.v6) {
+        if (j == 4 || j == 5)  // ip6_plen = pktlen - cs (big endian)
+            return kSelUlen | ((j == 4 ? 8u : 0u) << 8);
+    } else {
+        if (j == 2 || j == 3)  // ip_len
+            return kSelPkt | ((j == 2 ? 8u : 0u) << 8);
+        if (j == 4 || j == 5)  // ip_id
+            return kSelId | ((j == 4 ? 8u : 0u) << 8);
+    }
+    if (j >= c.cs) {
+        if (c.tcp) {
+            if (j >= c.cs + 4 && j < c.cs + 8)
+                return kSelSeq | ((8u * (c.cs + 7u - j)) << 8);
+            if (j == c.cs + 13)
+                return kSelFlags;
+        } else if (j == c.cs + 4 || j == c.cs + 5) {
+            return kSelUlen | ((j == c.cs + 4 ? 8u : 0u) << 8);
+        }
+    }
+    return kSelTmpl;
+}
+
+// One pass over the prefix per wave: exact integer sums of the invariant
+// header bytes (the reference's values after the :145-149 zeroing).
+__device__ void hdr_bases(Ctx &c, uint32_t lane) {
+    const uint32_t ao = c.v6 ? 8u : 12u, al = c.v6 ? 32u : 8u;
+    uint32_t ip = 0, l4 = 0, ps = 0;
+    for (uint32_t j = lane; j < c.hdr_len; j += 64) {
+        uint32_t b = j < 64 ? c.hb0 : (j < 128 ? c.hb1 : ld8(c.in + j));
+        if ((!c.v6 && (j == 10 || j == 11)) || j == c.l4off || j == c.l4off + 1)
+            b = 0;
+        if (j < c.cs) {
+            if (!(!c.v6 && j >= 2 && j <= 5))
+                ip += b << (8u * (j & 1u));
+        } else if (!l4_varying(c, j)) {
+            l4 += b << (8u * ((j - c.cs) & 1u));
+        }
+        if (j >= ao && j < ao + al)
+            ps += b << (8u * ((j - ao) & 1u));
+    }
+    c.hc0 = hdr_code(c, lane);
+    c.hc1 = hdr_code(c, lane + 64);
+    c.ip_base = wave_sum_u32(ip);
+    c.l4h_base = wave_sum_u32(l4);
+    c.ps_sum = wave_sum_u32(ps);
+    const uint32_t j13 = c.cs + 13;
+    c.flags13 = (c.tcp && j13 < c.hdr_len && j13 != c.l4off && j13 != c.l4off + 1) ? pbyte(c, j13) : 0u;
+}
+
+__device__ __forceinline__ void st8(uintptr_t addr, uint32_t b) {
+    *reinterpret_cast<__attribute__((address_space(1))) uint8_t *>(addr) = (uint8_t)b;
+}
+
+struct HdrVals {
+    uint32_t pkt, id, ipcs, l4cs, seq, ulen, fm;
+};
+
+__device__ __forceinline__ uint32_t hdr_byte(const HdrVals &h, uint32_t code, uint32_t tb) {
+    uint32_t v = (code & kSelPkt) ? h.pkt : 0u;
+    v |= (code & kSelId) ? h.id : 0u;
+    v |= (code & kSelIpcs) ? h.ipcs : 0u;
+    v |= (code & kSelL4cs) ? h.l4cs : 0u;
+    v |= (code & kSelSeq) ? h.seq : 0u;
+    v |= (code & kSelUlen) ? h.ulen : 0u;
+    v = (v >> (code >> 8)) & 0xffu;
+    if (code & kSelFlags)
+        v = tb & h.fm;
+    return (code & 0xffu) ? v : tb;
+}
+
+// GSO_NONE + NEEDS_CSUM (offload.cpp:56-78): both checksums in place, one wave.
+__device__ void do_inplace(const Ctx &c, uint32_t lane) {
+    // IPv4 header checksum over [0, cs) with ip_sum zeroed.
+    uint32_t ipcs = 0;
+    if (!c.v6) {
+        uint32_t part = 0;
+        for (uint32_t j = lane; j < c.cs; j += 64) {
+            uint32_t b = ld8(c.in + j);
+            if (j == 10 || j == 11) b = 0;
+            part += b << (8u * (j & 1u));
+        }
+        ipcs = ~fold16_32(wave_sum_u32(part)) & 0xffffu;
+    }
+    // L4 over the bytes as they are, then replace the checksum field's
+    // contribution by zero: adding 0xFFFF - x is subtracting x mod 0xFFFF,
+    // and the total is never zero (the pseudo-header carries the protocol),
+    // so the fold only depends on the sum mod 0xFFFF.
+    Geom g;
+    g.a = c.in;
+    g.len = c.in_len;
+    g.cs = c.cs;
+    g.fl = (c.v6 ? WG_PKT_V6 : 0u) | (c.tcp ? WG_PKT_TCP : 0u);
+    Front f;
+    issue<true, false>(g, lane, f);
+    const uint32_t f0 = ld8(c.in + c.l4off), f1 = ld8(c.in + c.l4off + 1);
+    uint32_t T = wave_sum_u32(finish<false>(lane, f));
+    const uint32_t fw = ((c.l4off - c.cs) & 1u) ? ((f0 << 8) | f1) : (f0 | (f1 << 8));
+    T += 0xffffu - fw;
+    T += ((c.tcp ? 6u : 17u) << 8) + bswap16((c.in_len - c.cs) & 0xffffu);
+    const uint32_t l4cs = ~fold16_32(T) & 0xffffu;
+    if (lane == 0) {
+        if (!c.v6) {
+            st8(c.in + 10, ipcs & 0xffu);
+            st8(c.in + 11, ipcs >> 8);
+        }
+        st8(c.in + c.l4off, l4cs & 0xffu);
+        st8(c.in + c.l4off + 1, l4cs >> 8);
+    }
+}
+
+// Classification of one super-buffer (mirrors :48-134 and the oracle).
+// kUniform: called by a whole wave (wave-uniform byte loads).
+struct Cls {
+    int status;
+    bool pass, inplace;
+    uint32_t isv6, ecn;
+};
+
+template <bool kUniform>
+__device__ __forceinline__ uint32_t ldb(const Ctx &c, uint32_t j) {
+    if constexpr (kUniform)
+        return pbyte(c, j);
+    else
+        return ld8(c.in + j);
+}
+
+template <bool kUniform>
+__device__ __forceinline__ Cls classify(const wg_gso_desc &dsc, uintptr_t in_base, Ctx &c) {
+    c.in = in_base + dsc.in_offset;
+    c.in_len = dsc.in_len;
+    c.cs = dsc.vnet.csum_start;
+    c.l4off = (uint32_t)dsc.vnet.csum_start + dsc.vnet.csum_offset;  // :47
+    c.hdr_len = dsc.vnet.hdr_len;
+    c.gso = dsc.vnet.gso_size;
+    c.rest = 0;
+    c.nseg = 0;
+    c.v6 = false;
+    const uint32_t gtype = dsc.vnet.gso_type;
+    Cls r{0, true, false, 0u, 0u};
+    if (c.in_len < 1) {
+        r.status = -3;
+        return r;
+    }
+    if constexpr (kUniform) {
+        // the whole wave loads prefix bytes 0-127 at once; every byte the
+        // classification and the header work need is then a readlane
+        const uint32_t lane = lane_id();
+        c.hb0 = ld8(c.in + (lane < c.in_len ? lane : 0u));
+        c.hb1 = ld8(c.in + (lane + 64 < c.in_len ? lane + 64 : 0u));
+    }
+    r.isv6 = (ldb<kUniform>(c, 0) >> 4) == 6;  // :48
+    const uint32_t iph_min = r.isv6 ? 40u : 20u;
+    if (c.in_len < iph_min) {
+        r.status = -3;
+        return r;
+    }
+    r.ecn = r.isv6 ? ((ldb<kUniform>(c, 1) >> 4) & 3u) : (ldb<kUniform>(c, 1) & 3u);  // :49-53
+    c.v6 = r.isv6;
+    const uint32_t g = gtype & ~kGsoEcn;  // :55
+    bool seg = false;
+    if (g == kGsoNone) {
+        if (dsc.vnet.flags & kNeedsCsum) {
+            if (c.cs < iph_min || c.cs > c.in_len || c.l4off + 2 > c.in_len)
+                r.status = -3;
+            else
+                r.inplace = true;
+        }
+    } else if (g == kGsoTcp4 || g == kGsoTcp6) {
+        if (c.cs > c.in_len) {
+            r.status = -3;
+        } else if (c.in_len - c.cs >= 20) {                                        // :91
+            const uint32_t thlen = 4u * (ldb<kUniform>(c, c.cs + 12) >> 4);  // doff, :100
+            if (thlen >= 20) {                                                    // :101
+                c.hdr_len = c.cs + thlen;                                         // :110
+                seg = true;
+            }
+        }
+    } else if (g == kGsoUdpL4) {
+        c.hdr_len = c.cs + 8;  // :114
+        seg = true;
+    }
+    if (seg && c.in_len >= c.hdr_len) {  // :126-134
+        if (c.cs < iph_min || c.l4off < c.cs || c.l4off + 2 > c.hdr_len) {
+            r.status = -3;
+        } else {
+            c.rest = c.in_len - c.hdr_len;
+            if (c.rest && !c.gso) {
+                r.status = -1;  // the reference loops forever
+            } else {
+                c.nseg = c.gso ? (c.rest + c.gso - 1) / c.gso : 0;
+                if ((uint64_t)dsc.out_cap < (uint64_t)c.in_len + (uint64_t)c.nseg * c.hdr_len)
+                    r.status = -2;  // reserve_size assert, :139-143
+                else
+                    r.pass = false;
+            }
+        }
+    }
+    c.tcp = gtype == kGsoTcp4 || gtype == kGsoTcp6;  // :151, unmasked
+    return r;
+}
+
+}  // namespace wg
