@@ -1,3 +1,13 @@
+// NOT BUILT — kept as the record of a measured negative result (DESIGN.md
+// §6.2).  A plan pre-pass + one-wave-per-output-segment "chunk stream" GSO
+// engine (unaligned 16-B source loads, whole-chunk non-temporal stores,
+// header chunks assembled from an LDS template).  Bit-exact against the
+// oracle on tests/test_gpu_gso.py, but on config 3 it measured 26.8 ms
+// (one-shot waves), 11.9 ms (persistent, residency-sized grid) and 13.9 ms
+// (persistent + two-slot pipeline) against 6.4 ms for gso.hip: each wave's
+// plan -> load dependency chain and ~500 VALU per segment (vs ~230) left it
+// latency/issue bound.  It compiled against the tree at commit 4eca7b8
+// (wireglider_amd/csrc/, with GsoPlan in this file).
 // gso_rows.hip — the default GSO split engine: do_tun_gso_split (reference
 // worker/offload.cpp:46-216) for a batch of super-buffers, laid out for the
 // MI355X memory system rather than per segment.
