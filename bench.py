@@ -510,6 +510,12 @@ def main():
     achieved = wl.alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args.workload)
     read_peak = measured_read_peak(torch, wga, wl.buf) if rank == 0 else None
+    # The CPU baseline samples the batch as the timed launches saw it, so it
+    # runs before post_checks (whose verify pass stores the checksums into the
+    # packets).
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and wl.sample is not None:
+        cpu = cpu_baseline(wl.sample, args.cpu_seconds)
     post = post_checks(torch, wga, wl, world, dev)
     line = {
         "metric": wl.metric or "device-resident GiB/s, L4 checksum over packet batch; 1/2/4/8 MI355X",
@@ -543,11 +549,8 @@ def main():
         },
         "post_checks": post,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and wl.sample is not None:
-        line["cpu_baseline"] = cpu_baseline(wl.sample, args.cpu_seconds)
-    elif rank == 0:
-        line["cpu_baseline"] = None
     if rank == 0:
+        line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
