@@ -249,8 +249,13 @@ int wg_device_count(void);
  * 2: two segments issued then finished), "gso_ablate"
  * (profiling only: 1 = non-temporal payload stores; 2..7 select timing-only
  * GSO variants whose output is WRONG; 0 restores the default kernel).  Results never depend on the geometry
- * knobs.  Not synchronised with concurrent launches from other threads. */
+ * knobs.  Not synchronised with concurrent launches from other threads.
+ * Also: "gso_groups" (1-64: blocks per super-buffer, consecutive in a flat
+ * grid, so the waves of one super-buffer are short-lived and neighbours in
+ * dispatch order). */
 int wg_tune_set(const char *key, uint64_t value);
+/* Current value of a wg_tune_set key. */
+int wg_tune_get(const char *key, uint64_t *value);
 
 /* Read-roofline probe (benchmark support): streams dev[0, nbytes) with
  * non-temporal 16-B loads, one-shot waves of `kib_per_wave` (1/2/4/8)

@@ -25,13 +25,20 @@ def _wga():
     return wireglider_amd
 
 
-@pytest.fixture(params=[0, 32], ids=["swizzled", "launch-order"])
+@pytest.fixture(params=[{"gso_ablate": 0, "gso_groups": 1}, {"gso_ablate": 32, "gso_groups": 1},
+                        {"gso_groups": 3}, {"gso_groups": 12}, {"gso_groups": 5, "gso_waves": 8}],
+                ids=["swizzled", "launch-order", "groups3", "groups12", "groups5x8"])
 def variant(request):
-    """Both correct block -> super-buffer mappings of the GSO kernel."""
+    """Every correct block -> (super-buffer, segment slot) mapping of the GSO
+    kernel: one looping block per super-buffer (XCD-swizzled or in launch
+    order) and several blocks per super-buffer (flat grid groups)."""
     wga = _wga()
-    wga.tune_set("gso_ablate", request.param)
+    saved = {k: wga.tune_get(k) for k in ("gso_ablate", "gso_groups", "gso_waves")}
+    for k, v in request.param.items():
+        wga.tune_set(k, v)
     yield request.param
-    wga.tune_set("gso_ablate", 0)
+    for k, v in saved.items():
+        wga.tune_set(k, v)
 
 
 def run_batch(gpu, cases, out_cap_fn=lambda c: None, seed=0):
@@ -182,7 +189,7 @@ def _far_csum_start(rng, cs, plen, istcp=True):
     return base[:20] + rng.integers(0, 256, cs - 20, dtype=np.uint8).tobytes() + base[20:]
 
 
-def test_geometry_edges(gpu):
+def test_geometry_edges(gpu, variant):
     """Segment shapes at the kernel's edges: segments shorter than a 16-B
     chunk, thousands of segments per super-buffer, headers past the 128
     prefix bytes held in registers (csum_start 508 / 600), and last segments

@@ -46,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "wg_strerror",
     "wg_device_count",
     "wg_tune_set",
+    "wg_tune_get",
     "wg_probe_read",
     "wg_probe_copy",
 )
@@ -112,6 +113,7 @@ def _load() -> ctypes.CDLL:
         "wg_strerror": (ctypes.c_char_p, [i32]),
         "wg_device_count": (i32, []),
         "wg_tune_set": (i32, [ctypes.c_char_p, u64]),
+        "wg_tune_get": (i32, [ctypes.c_char_p, ctypes.POINTER(u64)]),
         "wg_probe_read": (i32, [u8p, u64, vp, u32, u32, vp]),
         "wg_probe_copy": (i32, [u8p, u8p, u64, u32, vp]),
     }
@@ -307,6 +309,12 @@ def store_l4csum(base, desc, csum, stream=None) -> None:
 def tune_set(key: str, value: int) -> None:
     """Launch-geometry knob (results never depend on it)."""
     _check(lib.wg_tune_set(key.encode(), int(value)), f"wg_tune_set({key})")
+
+
+def tune_get(key: str) -> int:
+    v = ctypes.c_uint64(0)
+    _check(lib.wg_tune_get(key.encode(), ctypes.byref(v)), f"wg_tune_get({key})")
+    return int(v.value)
 
 
 def probe_read(buf, out, kib_per_wave: int = 4, stream=None) -> None:

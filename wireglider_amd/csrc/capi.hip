@@ -32,13 +32,16 @@ Tune &tune_mut() {
         x.l4_ppw = (uint32_t)env_u64("WG_L4_PPW", 4);
         x.l4_nt = (uint32_t)env_u64("WG_L4_NT", 1);
         x.l4_descv = (uint32_t)env_u64("WG_L4_DESCV", 0);
-        x.gso_blocks = env_u64("WG_GSO_BLOCKS", 1u << 20);
+        x.gso_blocks = env_u64("WG_GSO_BLOCKS", 1u << 23);
         // GSO: one 4-wave block per super-buffer, each wave a ping-pong
-        // pipeline (next segment's loads in flight while this one finishes)
-        // (tools/tune_gso.py, profiles/r01_tune_gso*.json).
+        // pipeline (next segment's loads in flight while this one finishes);
+        // the verify kernel at 8 waves/SIMD (64 VGPRs, no spill)
+        // (tools/ab.py, profiles/r01_ab_*.json).
         x.gso_waves = (uint32_t)env_u64("WG_GSO_WAVES", 4);
         x.gso_split = (uint32_t)env_u64("WG_GSO_SPLIT", 1);
         x.gso_spw = (uint32_t)env_u64("WG_GSO_SPW", 1);
+        x.gso_groups = (uint32_t)env_u64("WG_GSO_GROUPS", 1);
+        x.verify_occ = (uint32_t)env_u64("WG_VERIFY_OCC", 8);
         x.gso_ablate = 0;
         return x;
     }();
@@ -218,18 +221,42 @@ extern "C" int wg_tune_set(const char *key, uint64_t value) {
         t.l4_nt = (uint32_t)value;
     else if (k == "l4_descv" && value <= 1)
         t.l4_descv = (uint32_t)value;
-    else if (k == "gso_blocks" && value >= 1 && value <= (1u << 20))
+    else if (k == "gso_blocks" && value >= 1 && value <= (1u << 23))
         t.gso_blocks = value;
-    else if (k == "gso_waves" && (value == 4 || value == 8 || value == 16))
+    else if (k == "verify_occ" && (value == 0 || value == 8))
+        t.verify_occ = (uint32_t)value;
+    else if (k == "gso_groups" && value >= 1 && value <= 64)
+        t.gso_groups = (uint32_t)value;
+    else if (k == "gso_waves" && (value == 4 || value == 8))
         t.gso_waves = (uint32_t)value;
     else if (k == "gso_split" && value >= 1 && value <= 64)
         t.gso_split = (uint32_t)value;
-    else if (k == "gso_spw" && (value == 1 || value == 2))
+    else if (k == "gso_spw" && value <= 2)
         t.gso_spw = (uint32_t)value;
-    else if (k == "gso_ablate" && ((value <= 7 && value != 5) || value == 32))
+    else if (k == "gso_ablate" && (value <= 2 || value == 32))
         t.gso_ablate = (uint32_t)value;
     else
         return WG_ERR_INVALID;
+    return WG_OK;
+}
+
+extern "C" int wg_tune_get(const char *key, uint64_t *value) {
+    if (!key || !value)
+        return WG_ERR_INVALID;
+    const Tune &t = tune();
+    const std::string k(key);
+    if (k == "l4_blocks") *value = t.l4_blocks;
+    else if (k == "l4_ppw") *value = t.l4_ppw;
+    else if (k == "l4_nt") *value = t.l4_nt;
+    else if (k == "l4_descv") *value = t.l4_descv;
+    else if (k == "gso_blocks") *value = t.gso_blocks;
+    else if (k == "gso_waves") *value = t.gso_waves;
+    else if (k == "gso_split") *value = t.gso_split;
+    else if (k == "gso_spw") *value = t.gso_spw;
+    else if (k == "gso_groups") *value = t.gso_groups;
+    else if (k == "verify_occ") *value = t.verify_occ;
+    else if (k == "gso_ablate") *value = t.gso_ablate;
+    else return WG_ERR_INVALID;
     return WG_OK;
 }
 

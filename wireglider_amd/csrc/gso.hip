@@ -4,16 +4,21 @@
 //
 // One 256-thread workgroup per super-buffer; its four waves take the
 // segments round-robin.  Per segment a wave, in ONE pass over the payload:
-//   - streams the payload's output-aligned 16-B chunks: two aligned source
-//     loads per chunk, re-aligned in registers with v_alignbyte (the shift
-//     source - destination is uniform per segment), stored non-temporally,
-//     and summed from the same registers;
+//   - streams the payload's destination-aligned 16-B chunks: ONE 16-B load
+//     per chunk from its (unaligned) source address, stored at the aligned
+//     destination and summed from the same registers;
 //   - moves the <= 15-byte unaligned head/tail of the payload one byte per lane;
 //   - rebuilds the header prefix one byte per lane with the reference's
 //     fix-ups applied in the reference's order (IPv4 id/len or IPv6 plen ->
 //     IPv4 header checksum -> TCP seq/FIN/PSH or UDP len -> L4 checksum).
 // The reference touches every payload byte twice (std::copy at :165-166, then
 // the checksum at :202); this kernel reads it once and writes it once.
+//
+// Register economy is the design constraint: the kernel is HBM-bound and its
+// bytes in flight scale with resident waves, so everything per lane is a
+// 32-bit offset from a wave-uniform base, the per-segment header values are
+// looked up (v_writelane table + ds_bpermute) instead of selected, and the
+// GSO_NONE in-place checksum is a kernel of its own.
 #include <hip/hip_runtime.h>
 
 #include "wg_device.hpp"
@@ -22,25 +27,11 @@
 #include "wg_l4wave.hpp"
 #include "wireglider_amd.h"
 
-namespace wg {
+// v_writelane_b32 (no clang builtin in this toolchain: bind the LLVM
+// intrinsic by name).
+extern "C" __device__ int wg_writelane_i32(int value, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 
-// Bytes delta..delta+15 of the 32-byte window lo|hi; q = delta >> 2 is
-// wave-uniform (scalar branch), r = delta & 3 goes to v_alignbyte.
-__device__ __forceinline__ v4u funnel(v4u lo, v4u hi, uint32_t q, uint32_t r) {
-    uint32_t w0, w1, w2, w3, w4;
-    switch (q) {
-    case 0: w0 = lo.x; w1 = lo.y; w2 = lo.z; w3 = lo.w; w4 = hi.x; break;
-    case 1: w0 = lo.y; w1 = lo.z; w2 = lo.w; w3 = hi.x; w4 = hi.y; break;
-    case 2: w0 = lo.z; w1 = lo.w; w2 = hi.x; w3 = hi.y; w4 = hi.z; break;
-    default: w0 = lo.w; w1 = hi.x; w2 = hi.y; w3 = hi.z; w4 = hi.w; break;
-    }
-    v4u v;
-    v.x = __builtin_amdgcn_alignbyte(w1, w0, r);
-    v.y = __builtin_amdgcn_alignbyte(w2, w1, r);
-    v.z = __builtin_amdgcn_alignbyte(w3, w2, r);
-    v.w = __builtin_amdgcn_alignbyte(w4, w3, r);
-    return v;
-}
+namespace wg {
 
 __device__ __forceinline__ void st16_nt(uintptr_t addr, v4u v) {
     __builtin_nontemporal_store(v, reinterpret_cast<__attribute__((address_space(1))) v4u *>(addr));
@@ -49,13 +40,11 @@ __device__ __forceinline__ void st16_nt(uintptr_t addr, v4u v) {
 // Variant bits (wg_tune_set("gso_ablate")): 1 = non-temporal payload
 // stores (a correct variant; default-policy stores measured faster because
 // the segment-edge byte stores then merge with the chunk stores in L2).
-// Timing-only (WRONG output, to price one part of the kernel, guide §5.4
-// rule 17): 2 = no byte stores (header / payload head & tail), 4 = no
-// re-alignment window (one source chunk per output chunk).
 // 32 = blocks -> super-buffers in launch order instead of XCD-swizzled (a
-// correct variant; the swizzle keeps consecutive super-buffers on one XCD,
-// +2.7 % on config 3).
-enum : int { kAblNtStore = 1, kAblNoByteStores = 2, kAblOneLoad = 4, kAblNoSwizzle = 32 };
+// correct variant; the swizzle keeps consecutive super-buffers on one XCD).
+// Timing-only (WRONG output, to price one part of the kernel, guide §5.4
+// rule 17): 2 = no byte stores (header / payload head & tail).
+enum : int { kAblNtStore = 1, kAblNoByteStores = 2, kAblNoSwizzle = 32 };
 
 template <int A>
 __device__ __forceinline__ void st16x(uintptr_t addr, v4u v) {
@@ -65,16 +54,43 @@ __device__ __forceinline__ void st16x(uintptr_t addr, v4u v) {
         *reinterpret_cast<__attribute__((address_space(1))) v4u *>(addr) = v;
 }
 
+// Per-super-buffer plan, written by gso_plan_kernel into the caller's
+// wg_gso_result slot (24 B; gso_finalize_kernel overwrites it with the
+// result): the classification and the invariant header sums, so the split
+// kernel's waves start their payload loads one (scalar) load after launch
+// instead of after the descriptor -> prefix -> classification chain.
+struct GsoPlan {
+    uint16_t hdr_len, cs;
+    uint16_t l4off;
+    uint8_t kind;  // bit 0 v6, bit 1 tcp (the unmasked :151 test), bit 7 split
+    uint8_t flags13;
+    uint16_t gso, nseg;
+    uint16_t id0, ip_base;  // sums folded to 16 bits (zero-preserving, congruent)
+    uint16_t l4h_base, ps_sum;
+    uint32_t seq0;
+};
+static_assert(sizeof(GsoPlan) == sizeof(wg_gso_result), "plan lives in the result slot");
+enum : uint32_t { kPlanV6 = 1, kPlanTcp = 2, kPlanSplit = 0x80 };
 
-// One output segment by one wave, in two phases so a wave can have several
+// Wave-uniform record loads through the constant address space: s_load.
+template <typename T>
+__device__ __forceinline__ T sload(const T *p) {
+#if __HIP_DEVICE_COMPILE__
+    return *reinterpret_cast<__attribute__((address_space(4))) const T *>(reinterpret_cast<uintptr_t>(p));
+#else
+    return *p;
+#endif
+}
+
+// One output segment by one wave, in two phases so a wave may have several
 // segments' loads in flight: seg_issue() issues every load of the segment
-// (branch-free: clamped addresses, masked use); seg_finish() re-aligns,
-// stores, sums and writes the header.  Only the loaded data and the segment
-// index cross the phase boundary; the (scalar) geometry is recomputed, which
-// keeps the scalar register file from spilling.
+// (branch-free: clamped offsets, masked use); seg_finish() stores, sums and
+// writes the header.  Only the loaded data and the segment index cross the
+// phase boundary; the (scalar) geometry is recomputed.
 struct SegGeom {
-    uintptr_t seg, oa, ob, d, c0, c1, sa, smin, smax, a0;
-    uint32_t datalen, pktlen, nint, q, r;
+    uintptr_t seg, oa, c0, sa;
+    uintptr_t base;  // source of output chunk 0 (unaligned), or the zero chunk when there is none
+    uint32_t datalen, pktlen, nint, he, ts;
     bool last;
 };
 
@@ -85,81 +101,48 @@ __device__ __forceinline__ SegGeom seg_geom(const Ctx &c, uintptr_t out_base, ui
     g.datalen = c.rest - off < c.gso ? c.rest - off : c.gso;
     g.pktlen = c.hdr_len + g.datalen;
     g.last = i + 1 == c.nseg;
-    g.oa = g.seg + c.hdr_len;  // payload, destination
-    g.ob = g.seg + g.pktlen;
+    g.oa = g.seg + c.hdr_len;       // payload, destination
     g.sa = c.in + c.hdr_len + off;  // payload, source
-    g.d = g.sa - g.oa;              // source = destination + d (mod 2^64)
-    const uint32_t delta = (uint32_t)(g.d & 15u);
-    g.q = delta >> 2;
-    g.r = delta & 3u;
-    g.c0 = (g.oa + 15) & ~(uintptr_t)15;  // destination-aligned interior chunks
-    g.c1 = g.ob & ~(uintptr_t)15;
-    g.nint = g.c1 > g.c0 ? (uint32_t)((g.c1 - g.c0) >> 4) : 0u;
-    g.smin = g.sa & ~(uintptr_t)15;
-    g.smax = (g.sa + g.datalen - 1) & ~(uintptr_t)15;
-    g.a0 = (g.c0 + g.d) & ~(uintptr_t)15;
+    const uintptr_t ob = g.oa + g.datalen;
+    g.c0 = (g.oa + 15) & ~(uintptr_t)15;  // destination-aligned interior chunks [c0, c1)
+    const uintptr_t c1 = ob & ~(uintptr_t)15;
+    g.nint = c1 > g.c0 ? (uint32_t)((c1 - g.c0) >> 4) : 0u;
+    // head [oa, he) and tail [ts, datalen) as offsets from oa, <= 15 bytes each
+    g.he = (uint32_t)((g.c0 < ob ? g.c0 : ob) - g.oa);
+    g.ts = (uint32_t)((c1 > g.c0 ? c1 : g.c0) - g.oa);
+    // Interior chunk k = ONE 16-B load at its unaligned source address
+    // c0 + 16k + (sa - oa): inside the payload, so always in bounds; an empty
+    // interior points every lane at the static zero chunk.
+    g.base = g.nint ? g.c0 + (g.sa - g.oa) : reinterpret_cast<uintptr_t>(&g_zero16);
     return g;
+}
+
+// Payload head on lanes 0-15, tail on lanes 16-31: this lane's byte offset
+// from oa (the source byte is at the same offset from sa), or kNoEdge.
+constexpr uint32_t kNoEdge = 0xffffffffu;
+__device__ __forceinline__ uint32_t edge_off(const SegGeom &g, uint32_t lane) {
+    const uint32_t xt = g.ts + lane - 16u;
+    if (lane < 16 && lane < g.he)
+        return lane;
+    if (lane >= 16 && lane < 32 && xt < g.datalen)
+        return xt;
+    return kNoEdge;
 }
 
 struct SegFront {
     uint32_t i, pb;
-    v4u lo0, lo1;  // source chunks a0 + 16 * lane and a0 + 16 * (lane + 64)
+    v4u lo0, lo1;  // interior chunks lane, lane + 64
 };
-
-// Source chunk m of the segment, clamped into the chunks that hold payload
-// bytes: the clamp never changes a byte an in-range output chunk needs, and
-// keeps every load in bounds.
-__device__ __forceinline__ v4u src_chunk(const SegGeom &g, uint64_t m) {
-    uintptr_t A = g.a0 + 16ull * m;
-    A = A < g.smin ? g.smin : (A > g.smax ? g.smax : A);
-    return ld16(A);
-}
-
-// Output chunk k needs source chunks k and k + 1 (re-alignment window):
-// chunk k + 1 of lane l is chunk k of lane l + 1, fetched by a lane shuffle;
-// lane 63 takes it from `next` (lane 0's chunk of the following row).
-__device__ __forceinline__ v4u next_chunk(v4u lo, v4u next) {
-    // DPP wave_shl:1 — lane l reads lane l + 1; lane 63 has no source and
-    // keeps `old` = next (bound_ctrl off).  (A ds_bpermute shuffle measured
-    // the same, tools/ab_gso.py.)
-    v4u h;
-    h.x = (uint32_t)__builtin_amdgcn_update_dpp((int)next.x, (int)lo.x, 0x130, 0xf, 0xf, false);
-    h.y = (uint32_t)__builtin_amdgcn_update_dpp((int)next.y, (int)lo.y, 0x130, 0xf, 0xf, false);
-    h.z = (uint32_t)__builtin_amdgcn_update_dpp((int)next.z, (int)lo.z, 0x130, 0xf, 0xf, false);
-    h.w = (uint32_t)__builtin_amdgcn_update_dpp((int)next.w, (int)lo.w, 0x130, 0xf, 0xf, false);
-    return h;
-}
-
-__device__ __forceinline__ v4u lane0(v4u v) {
-    v4u r;
-    r.x = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.x);
-    r.y = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.y);
-    r.z = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.z);
-    r.w = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.w);
-    return r;
-}
-
-// Payload head [oa, min(c0, ob)) on lanes 0-15, tail [max(c1, c0), ob) on
-// lanes 16-31: this lane's byte address, or 0.
-__device__ __forceinline__ uintptr_t edge_byte(const SegGeom &g, uint32_t lane) {
-    const uintptr_t he = g.c0 < g.ob ? g.c0 : g.ob;
-    const uintptr_t ts = g.c1 > g.c0 ? g.c1 : g.c0;
-    const uintptr_t xh = g.oa + lane, xt = ts + (lane - 16);
-    if (lane < 16 && xh < he)
-        return xh;
-    if (lane >= 16 && lane < 32 && xt < g.ob)
-        return xt;
-    return 0;
-}
 
 template <int Abl>
 __device__ __forceinline__ void seg_issue(const Ctx &c, uintptr_t out_base, uint32_t i, uint32_t lane, SegFront &f) {
     const SegGeom g = seg_geom(c, out_base, i);
     f.i = i;
-    f.lo0 = src_chunk(g, lane);
-    f.lo1 = src_chunk(g, lane + 64);
-    const uintptr_t xb = edge_byte(g, lane);
-    f.pb = ld8(xb ? xb + g.d : g.sa);
+    const uint32_t last = g.nint ? g.nint - 1 : 0u;
+    f.lo0 = ld16(g.base + 16u * (lane < last ? lane : last));
+    f.lo1 = ld16(g.base + 16u * (lane + 64 < last ? lane + 64 : last));
+    const uint32_t eo = edge_off(g, lane);
+    f.pb = ld8(g.sa + (eo != kNoEdge ? eo : 0u));
 }
 
 template <int Abl>
@@ -167,33 +150,27 @@ __device__ __forceinline__ void seg_finish(const Ctx &c, uintptr_t out_base, con
     const SegGeom g = seg_geom(c, out_base, f.i);
     const uint32_t i = f.i, pktlen = g.pktlen;
     Acc acc;
-    // payload: re-align, store, sum
-    if (g.nint) {
-        const v4u nx1 = g.nint > 127 ? lane0(src_chunk(g, 128)) : f.lo1;
-        const v4u hi0 = next_chunk(f.lo0, lane0(f.lo1));
-        const v4u hi1 = next_chunk(f.lo1, nx1);
-        if (lane < g.nint) {
-            const v4u v = funnel(f.lo0, (Abl & kAblOneLoad) ? f.lo0 : hi0, g.q, g.r);
-            st16x<Abl>(g.c0 + 16ull * lane, v);
-            acc.add4(v);
-        }
-        if (lane + 64 < g.nint) {
-            const v4u v = funnel(f.lo1, (Abl & kAblOneLoad) ? f.lo1 : hi1, g.q, g.r);
-            st16x<Abl>(g.c0 + 16ull * (lane + 64), v);
-            acc.add4(v);
-        }
-        for (uint32_t k = lane + 128; k < g.nint; k += 64) {  // long segments (gso > ~2 KiB)
-            const v4u lo = src_chunk(g, k);
-            const v4u v = funnel(lo, src_chunk(g, k + 1), g.q, g.r);
-            st16x<Abl>(g.c0 + 16ull * k, v);
+    // payload: store and sum (destination-aligned chunks: absolute pairing)
+    if (lane < g.nint) {
+        st16x<Abl>(g.c0 + 16u * lane, f.lo0);
+        acc.add4(f.lo0);
+    }
+    if (lane + 64 < g.nint) {
+        st16x<Abl>(g.c0 + 16u * (lane + 64), f.lo1);
+        acc.add4(f.lo1);
+    }
+    if (g.nint > 128) {  // long segments (gso > ~2 KiB)
+        for (uint32_t k = lane + 128; k < g.nint; k += 64) {
+            const v4u v = ld16(g.base + 16u * k);
+            st16x<Abl>(g.c0 + 16u * k, v);
             acc.add4(v);
         }
     }
-    const uintptr_t xb = edge_byte(g, lane);
-    if (xb) {
+    const uint32_t eo = edge_off(g, lane);
+    if (eo != kNoEdge) {
         if (!(Abl & kAblNoByteStores))
-            st8(xb, f.pb);
-        acc.add(f.pb << (8u * (uint32_t)(xb & 1u)));
+            st8(g.oa + eo, f.pb);
+        acc.add(f.pb << (8u * (((uint32_t)g.oa + eo) & 1u)));
     }
 
     // checksums: the invariant header sums plus this segment's fields
@@ -201,49 +178,166 @@ __device__ __forceinline__ void seg_finish(const Ctx &c, uintptr_t out_base, con
     uint32_t ipcs = 0;
     if (!c.v6)
         ipcs = ~fold16_32(c.ip_base + bswap16(pktlen & 0xffffu) + bswap16((c.id0 + i) & 0xffffu)) & 0xffffu;
+    const uint32_t seq = c.seq0 + c.gso * i;
+    const uint32_t flags = g.last ? c.flags13 : (c.flags13 & ~0x09u);  // FIN/PSH only on the last segment
     uint32_t l4h = c.l4h_base;
-    if (c.tcp) {
-        const uint32_t seq = c.seq0 + c.gso * i;
-        l4h += bswap16(seq >> 16) + bswap16(seq & 0xffffu) + ((g.last ? c.flags13 : (c.flags13 & ~0x09u)) << 8);
-    } else {
+    if (c.tcp)
+        l4h += bswap16(seq >> 16) + bswap16(seq & 0xffffu) + (flags << 8);
+    else
         l4h += bswap16((pktlen - c.cs) & 0xffffu);
-    }
     uint32_t lp = fold16(acc.value());
     if ((g.seg + c.cs) & 1u)  // payload summed in absolute pairing; the L4 region pairs from seg + cs
         lp = bswap16(lp);
     uint32_t T = wave_sum_u32(lp) + l4h + c.ps_sum;
     T += ((c.tcp ? 6u : 17u) << 8) + bswap16((pktlen - c.cs) & 0xffffu);
     const uint32_t l4cs = ~fold16_32(T) & 0xffffu;
-    // write the header prefix: each byte is the prefix byte or one byte of a
-    // per-segment value, by its precomputed field code (checksums in native
-    // order, :185-186, :203-204)
     if (Abl & kAblNoByteStores) {
         if (lane == 0 && l4cs == 0x12345u) st8(g.seg, 0);  // keep the sums live
         return;
     }
-    const HdrVals hv{pktlen, c.id0 + i, ipcs, l4cs, c.seq0 + c.gso * i, pktlen - c.cs, g.last ? 0xffu : 0xf6u};
-    if (lane < c.hdr_len) st8(g.seg + lane, hdr_byte(hv, c.hc0, c.hb0));
-    if (lane + 64 < c.hdr_len) st8(g.seg + lane + 64, hdr_byte(hv, c.hc1, c.hb1));
-    for (uint32_t j = lane + 128; j < c.hdr_len; j += 64)
-        st8(g.seg + j, hdr_byte(hv, hdr_code(c, j), ld8(c.in + j)));
+    // write the header prefix: each byte is the prefix byte or one byte of a
+    // per-segment value, by its field code (checksums in native order,
+    // :185-186, :203-204).  The values go into lanes 1-7 of one VGPR and
+    // every lane fetches its field with ONE ds_bpermute (full EXEC).
+    uint32_t tbl = 0;
+    tbl = (uint32_t)wg_writelane_i32((int)pktlen, kFldPkt, (int)tbl);
+    tbl = (uint32_t)wg_writelane_i32((int)(c.id0 + i), kFldId, (int)tbl);
+    tbl = (uint32_t)wg_writelane_i32((int)ipcs, kFldIpcs, (int)tbl);
+    tbl = (uint32_t)wg_writelane_i32((int)l4cs, kFldL4cs, (int)tbl);
+    tbl = (uint32_t)wg_writelane_i32((int)seq, kFldSeq, (int)tbl);
+    tbl = (uint32_t)wg_writelane_i32((int)(pktlen - c.cs), kFldUlen, (int)tbl);
+    tbl = (uint32_t)wg_writelane_i32((int)flags, kFldFlags, (int)tbl);
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((c.hc0 & 7u) << 2), (int)tbl);
+    const uint32_t b0 = (c.hc0 & 7u) ? (r0 >> (c.hc0 >> 8)) & 0xffu : c.hb0;
+    if (lane < c.hdr_len)
+        st8(g.seg + lane, b0);
+    if (c.hdr_len > 64) {
+        const uint32_t r1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((c.hc1 & 7u) << 2), (int)tbl);
+        const uint32_t b1 = (c.hc1 & 7u) ? (r1 >> (c.hc1 >> 8)) & 0xffu : c.hb1;
+        if (lane + 64 < c.hdr_len)
+            st8(g.seg + lane + 64, b1);
+        if (c.hdr_len > 128) {
+            HdrVals hv;
+            hv.v[0] = 0;
+            hv.v[kFldPkt] = pktlen;
+            hv.v[kFldId] = c.id0 + i;
+            hv.v[kFldIpcs] = ipcs;
+            hv.v[kFldL4cs] = l4cs;
+            hv.v[kFldSeq] = seq;
+            hv.v[kFldUlen] = pktlen - c.cs;
+            hv.v[kFldFlags] = flags;
+            for (uint32_t j = lane + 128; j < c.hdr_len; j += 64)
+                st8(g.seg + j, hdr_byte_slow(hv, hdr_code(c, j), ld8(c.in + j)));
+        }
+    }
 }
 
-// Main kernel: blockIdx.x walks super-buffers, blockIdx.y splits a
-// super-buffer's segments over gridDim.y blocks of W waves (so waves are
-// short-lived; the copy roofline on MI355X wants many small one-shot waves).
-template <int W, int S, int Abl>  // W waves per block, S segments in flight per wave
+// Main kernel.  The flat grid walks (super-buffer, group) units: unit u is
+// group u % G of super-buffer u / G, so the G blocks of one super-buffer are
+// consecutive in dispatch order (and, after the XCD swizzle, on one XCD).
+// Group g's waves take segment slots g*W .. g*W+W-1 of the super-buffer
+// (stride G*W); blockIdx.y (grid y) further splits the slots.  G = 1 (one
+// looping block per super-buffer) measured best; more groups mean shorter
+// waves but every wave pays the classification again.
+// S = segments per wave step: 0 one at a time (occupancy hides latency),
+// 1 ping-pong pipeline (the next segment's loads in flight while this one
+// finishes), 2 two issued then both finished.
+template <int W, int S, int Abl>
 __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
+    constexpr uint32_t kStep = S ? S : 1;
     const uint32_t lane = lane_id();
-    const uint32_t gw = blockIdx.y * W + wave_in_block();  // wave index within the super-buffer
-    const uint32_t gstride = gridDim.y * W * S;
-    const uint64_t b0 = (Abl & kAblNoSwizzle) ? blockIdx.x : xcd_swizzle(blockIdx.x, gridDim.x);
-    for (uint64_t b = b0; b < p.n; b += gridDim.x) {
+    const uint32_t G = p.groups;
+    const uint32_t gstride = gridDim.y * G * W * kStep;
+    const uint64_t units = p.n * G;
+    const uint64_t u0 = (Abl & kAblNoSwizzle) ? blockIdx.x : xcd_swizzle(blockIdx.x, gridDim.x);
+    for (uint64_t u = u0; u < units; u += gridDim.x) {
+        const uint64_t b = G == 1 ? u : u / G;
+        const uint32_t gw = (blockIdx.y * G + (uint32_t)(u - b * G)) * W + wave_in_block();  // segment slot
+        const GsoPlan pl = sload(reinterpret_cast<const GsoPlan *>(p.res) + b);
+        if (!(pl.kind & kPlanSplit) || gw * kStep >= pl.nseg)
+            continue;  // passthrough / error (gso_plan_kernel did any in-place work) or no segment for this slot
+        const uint64_t in_off = sload(&p.desc[b].in_offset), out_off = sload(&p.desc[b].out_offset);
+        const uint32_t in_len = sload(&p.desc[b].in_len);
+        Ctx c;
+        c.in = reinterpret_cast<uintptr_t>(p.in) + in_off;
+        c.in_len = in_len;
+        c.hdr_len = pl.hdr_len;
+        c.cs = pl.cs;
+        c.l4off = pl.l4off;
+        c.gso = pl.gso;
+        c.nseg = pl.nseg;
+        c.rest = in_len - pl.hdr_len;
+        c.v6 = pl.kind & kPlanV6;
+        c.tcp = pl.kind & kPlanTcp;
+        c.id0 = pl.id0;
+        c.seq0 = pl.seq0;
+        c.ip_base = pl.ip_base;
+        c.l4h_base = pl.l4h_base;
+        c.ps_sum = pl.ps_sum;
+        c.flags13 = pl.flags13;
+        // this lane's template bytes (used when the first header is written)
+        // and field codes
+        c.hb0 = ld8(c.in + (lane < c.hdr_len ? lane : 0u));
+        c.hb1 = ld8(c.in + (lane + 64 < c.hdr_len ? lane + 64 : 0u));
+        c.hc0 = hdr_code(c, lane);
+        c.hc1 = hdr_code(c, lane + 64);
+        const uintptr_t out_base = reinterpret_cast<uintptr_t>(p.out) + out_off;
+        if constexpr (S == 0) {
+            for (uint32_t i = gw; i < c.nseg; i += gstride) {
+                SegFront A;
+                seg_issue<Abl>(c, out_base, i, lane, A);
+                seg_finish<Abl>(c, out_base, A, lane);
+            }
+        } else if constexpr (S == 1) {
+            const uint32_t last = c.nseg - 1;
+            uint32_t i = gw;
+            SegFront A, B;
+            seg_issue<Abl>(c, out_base, i, lane, A);
+            if (i + gstride > last) {  // the slot's only segment: no second slot to fill
+                seg_finish<Abl>(c, out_base, A, lane);
+                continue;
+            }
+            for (;;) {
+                const uint32_t i1 = i + gstride;
+                seg_issue<Abl>(c, out_base, i1 < last ? i1 : last, lane, B);
+                seg_finish<Abl>(c, out_base, A, lane);
+                if (i1 > last)
+                    break;
+                const uint32_t i2 = i1 + gstride;
+                seg_issue<Abl>(c, out_base, i2 < last ? i2 : last, lane, A);
+                seg_finish<Abl>(c, out_base, B, lane);
+                if (i2 > last)
+                    break;
+                i = i2;
+            }
+        } else {
+            for (uint32_t i0 = gw * S; i0 < c.nseg; i0 += gstride) {
+                SegFront f[S];
+#pragma unroll
+                for (int k = 0; k < S; k++)
+                    seg_issue<Abl>(c, out_base, i0 + k < c.nseg ? i0 + k : c.nseg - 1, lane, f[k]);
+#pragma unroll
+                for (int k = 0; k < S; k++)
+                    if (i0 + k < c.nseg)
+                        seg_finish<Abl>(c, out_base, f[k], lane);
+            }
+        }
+    }
+}
+
+// Plan pass, one wave per super-buffer: classification (:48-134), the
+// per-super-buffer fields (IPv4 id, TCP seq read after the :145-149 zeroing)
+// and the invariant header sums into the GsoPlan; GSO_NONE + NEEDS_CSUM
+// super-buffers get both checksums in place here (:56-78).
+__global__ __launch_bounds__(256) void gso_plan_kernel(GsoParams p) {
+    const uint32_t lane = lane_id();
+    const uint64_t stride = (uint64_t)gridDim.x * 4u;
+    for (uint64_t b = (uint64_t)blockIdx.x * 4u + wave_in_block(); b < p.n; b += stride) {
         const wg_gso_desc dsc = p.desc[b];
         Ctx c;
         const Cls cl = classify<true>(dsc, reinterpret_cast<uintptr_t>(p.in), c);
+        GsoPlan pl{};
         if (!cl.pass) {
-            if (gw * S >= c.nseg)
-                continue;
             c.id0 = (pbyte(c, 4) << 8) | pbyte(c, 5);
             // seq0 is read after the prefix's L4 checksum field was zeroed
             // (:149 before :152-154), which matters when the two overlap.
@@ -256,43 +350,24 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
                 }
             }
             hdr_bases(c, lane);
-            const uintptr_t out_base = reinterpret_cast<uintptr_t>(p.out) + dsc.out_offset;
-            if constexpr (S == 1) {
-                // ping-pong software pipeline: the next segment's loads are in
-                // flight while this one is re-aligned, stored and summed
-                const uint32_t last = c.nseg - 1;
-                uint32_t i = gw;
-                SegFront A, B;
-                seg_issue<Abl>(c, out_base, i, lane, A);
-                for (;;) {
-                    const uint32_t i1 = i + gstride;
-                    seg_issue<Abl>(c, out_base, i1 < last ? i1 : last, lane, B);
-                    seg_finish<Abl>(c, out_base, A, lane);
-                    if (i1 > last)
-                        break;
-                    const uint32_t i2 = i1 + gstride;
-                    seg_issue<Abl>(c, out_base, i2 < last ? i2 : last, lane, A);
-                    seg_finish<Abl>(c, out_base, B, lane);
-                    if (i2 > last)
-                        break;
-                    i = i2;
-                }
-            } else {
-                for (uint32_t i0 = gw * S; i0 < c.nseg; i0 += gstride) {
-                    SegFront f[S];
-#pragma unroll
-                    for (int k = 0; k < S; k++)
-                        seg_issue<Abl>(c, out_base, i0 + k < c.nseg ? i0 + k : c.nseg - 1, lane, f[k]);
-#pragma unroll
-                    for (int k = 0; k < S; k++)
-                        if (i0 + k < c.nseg)
-                            seg_finish<Abl>(c, out_base, f[k], lane);
-                }
-            }
-        } else if (cl.inplace && gw == 0) {
+            pl.hdr_len = (uint16_t)c.hdr_len;
+            pl.cs = (uint16_t)c.cs;
+            pl.l4off = (uint16_t)c.l4off;
+            pl.kind = (uint8_t)(kPlanSplit | (c.v6 ? kPlanV6 : 0u) | (c.tcp ? kPlanTcp : 0u));
+            pl.flags13 = (uint8_t)c.flags13;
+            pl.gso = (uint16_t)c.gso;
+            pl.nseg = (uint16_t)c.nseg;
+            pl.id0 = (uint16_t)c.id0;
+            pl.ip_base = (uint16_t)fold16_32(c.ip_base);
+            pl.l4h_base = (uint16_t)fold16_32(c.l4h_base);
+            pl.ps_sum = (uint16_t)fold16_32(c.ps_sum);
+            pl.seq0 = c.seq0;
+        } else if (cl.inplace) {
             c.tcp = (cl.isv6 ? pbyte(c, 6) : pbyte(c, 9)) == 6;  // :67-70
             do_inplace(c, lane);
         }
+        if (lane == 0)
+            reinterpret_cast<GsoPlan *>(p.res)[b] = pl;
     }
 }
 
@@ -335,9 +410,12 @@ __global__ __launch_bounds__(256) void gso_finalize_kernel(GsoParams p) {
 
 using namespace wg;
 
-static void launch_gso_finalize(const GsoParams &p, hipStream_t st) {
-    const uint64_t fb = (p.n + 255) / 256;
-    hipLaunchKernelGGL(gso_finalize_kernel, dim3((unsigned)(fb < 65536 ? fb : 65536)), dim3(256), 0, st, p);
+template <int S, int Abl>
+static void launch_split(const GsoParams &p, dim3 g, uint32_t waves, hipStream_t st) {
+    switch (waves) {
+    case 8: hipLaunchKernelGGL((gso_split_kernel<8, S, Abl>), g, dim3(512), 0, st, p); break;
+    default: hipLaunchKernelGGL((gso_split_kernel<4, S, Abl>), g, dim3(256), 0, st, p); break;
+    }
 }
 
 extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
@@ -347,37 +425,33 @@ extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64
     if (!dev_in || !dev_desc || !dev_out || !dev_res || (reinterpret_cast<uintptr_t>(dev_desc) & 7) ||
         (reinterpret_cast<uintptr_t>(dev_res) & 7))
         return WG_ERR_INVALID;
-    GsoParams p{dev_in, dev_desc, n, dev_out, dev_res};
     const Tune &t = tune();
+    GsoParams p{dev_in, dev_desc, n, dev_out, dev_res, t.gso_groups};
     hipStream_t st = static_cast<hipStream_t>(stream);
-    uint64_t blocks = n < t.gso_blocks ? n : t.gso_blocks;
+    // 1. plans (into dev_res) + in-place checksums of GSO_NONE + NEEDS_CSUM
+    const uint64_t ib = (n + 3) / 4;
+    hipLaunchKernelGGL(gso_plan_kernel, dim3((unsigned)(ib < 65536 ? ib : 65536)), dim3(256), 0, st, p);
+    // 2. the split
+    const uint64_t units = n * t.gso_groups;
+    uint64_t blocks = units < t.gso_blocks ? units : t.gso_blocks;
     if (blocks >= 8)
         blocks &= ~7ull;  // the XCD swizzle wants a multiple of 8 (the grid-stride loop covers the rest)
     const dim3 g((unsigned)blocks, t.gso_split);
-    if (t.gso_ablate) {  // A/B variants, 4 waves x 1 segment (1, 32 correct; 2, 4 timing-only)
-        switch (t.gso_ablate) {
-        case 1: hipLaunchKernelGGL((gso_split_kernel<4, 1, 1>), g, dim3(256), 0, st, p); break;
-        case 2: hipLaunchKernelGGL((gso_split_kernel<4, 1, 2>), g, dim3(256), 0, st, p); break;
-        case 3: hipLaunchKernelGGL((gso_split_kernel<4, 1, 3>), g, dim3(256), 0, st, p); break;
-        case 4: hipLaunchKernelGGL((gso_split_kernel<4, 1, 4>), g, dim3(256), 0, st, p); break;
-        case 6: hipLaunchKernelGGL((gso_split_kernel<4, 1, 6>), g, dim3(256), 0, st, p); break;
-        case 32: hipLaunchKernelGGL((gso_split_kernel<4, 1, 32>), g, dim3(256), 0, st, p); break;
-        default: hipLaunchKernelGGL((gso_split_kernel<4, 1, 7>), g, dim3(256), 0, st, p); break;
+    switch (t.gso_ablate) {  // A/B variants (1, 32 correct; 2 timing-only)
+    case 1: launch_split<0, 1>(p, g, 4, st); break;
+    case 2: launch_split<0, 2>(p, g, 4, st); break;
+    case 32: launch_split<0, 32>(p, g, 4, st); break;
+    default:
+        switch (t.gso_spw) {
+        case 1: launch_split<1, 0>(p, g, t.gso_waves, st); break;
+        case 2: launch_split<2, 0>(p, g, t.gso_waves, st); break;
+        default: launch_split<0, 0>(p, g, t.gso_waves, st); break;
         }
-        launch_gso_finalize(p, st);
-        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
-    }
-    const uint32_t key = t.gso_waves * 10 + t.gso_spw;
-    switch (key) {
-    case 41: hipLaunchKernelGGL((gso_split_kernel<4, 1, 0>), g, dim3(256), 0, st, p); break;
-    case 42: hipLaunchKernelGGL((gso_split_kernel<4, 2, 0>), g, dim3(256), 0, st, p); break;
-    case 81: hipLaunchKernelGGL((gso_split_kernel<8, 1, 0>), g, dim3(512), 0, st, p); break;
-    case 82: hipLaunchKernelGGL((gso_split_kernel<8, 2, 0>), g, dim3(512), 0, st, p); break;
-    case 161: hipLaunchKernelGGL((gso_split_kernel<16, 1, 0>), g, dim3(1024), 0, st, p); break;
-    default: hipLaunchKernelGGL((gso_split_kernel<16, 2, 0>), g, dim3(1024), 0, st, p); break;
     }
     if (hipGetLastError() != hipSuccess)
         return WG_ERR_LAUNCH;
-    launch_gso_finalize(p, st);
+    // 3. PacketBatch records + the input prefix zeroing
+    const uint64_t fb = (n + 255) / 256;
+    hipLaunchKernelGGL(gso_finalize_kernel, dim3((unsigned)(fb < 65536 ? fb : 65536)), dim3(256), 0, st, p);
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }

@@ -169,9 +169,12 @@ static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
 // fill_fk_ip4 (worker/evaluator.cpp:14-40: ihl == 5, len == ip_len, no
 // fragmentation, header checksum == 0) or fill_fk_ip6 (:42-58: plen), then
 // the TCP / UDP length floors and calc_l4_checksum == 0
-// (include/worker/evaluator.hpp:59-65, 89-94).  Per wave P packets: one byte
-// load per packet brings header bytes 0-39 (decoded with v_readlane), then
-// the L4 issue/finish machinery with csum_start = 20 / 40.
+// (include/worker/evaluator.hpp:59-65, 89-94).  Per wave P packets, all loads
+// issued straight after the descriptors: one byte load per packet brings
+// header bytes 0-39 (decoded with v_readlane), the L4 issue machinery streams
+// bytes [40, len), which belong to the L4 region whatever the family; the
+// header bytes [ihs, 40) and the pseudo-header addresses are added from the
+// byte load once the header is decoded.
 // ---------------------------------------------------------------------------
 struct VerifyParams {
     const uint8_t *base;
@@ -185,46 +188,57 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t j) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
 }
 
-template <int P>
-__global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
+template <int P, int O = 0>  // O: waves/SIMD target (0 = compiler's choice)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_kernel(
+    VerifyParams p) {
     const uint32_t lane = lane_id();
     const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
     const uint64_t i0 = wave * P;
     if (i0 >= p.n)
         return;
     const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
-    uintptr_t a[P];
     uint32_t len[P], hv[P];
+    Geom g[P];
+    Front f[P];
+    // ISSUE, before any header is decoded: header bytes 0-39 one per lane,
+    // and bytes [40, len) — inside the L4 region for IPv4 (ihs 20) and IPv6
+    // (ihs 40) alike — through the L4 wave's issue phase.  Decoding first
+    // would put a second memory round trip in front of the payload loads.
+    // (Bytes of packets that then fail a gate are read but not used; every
+    // read lies inside the descriptor's packet.)
 #pragma unroll
     for (int j = 0; j < P; j++) {
         const uint64_t i = i0 + j < p.n ? i0 + j : p.n - 1;
         const wg_pkt_desc d = p.desc[i];
-        a[j] = reinterpret_cast<uintptr_t>(p.base) + d.offset;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + d.offset;
         len[j] = i0 + j < p.n ? d.len : 0u;
         const uint32_t hl = len[j] < 40u ? len[j] : 40u;
-        hv[j] = ld8(lane < hl ? a[j] + lane : (hl ? a[j] : zero));
+        hv[j] = ld8(lane < hl ? a + lane : (hl ? a : zero));
+        g[j].a = a;
+        g[j].len = len[j] <= 65535u ? len[j] : 0u;  // longer packets fail the size gate (evaluator.hpp:118-121)
+        g[j].cs = 40;
+        g[j].fl = 0;
+        issue<false, true>(g[j], lane, f[j]);
     }
-    // decode (wave-uniform) and issue the L4 loads of every packet
-    Geom g[P];
-    Front f[P];
-    uint32_t verdict[P];
-    bool do_l4[P];
+    // decode (wave-uniform) and finish every packet
+    uint32_t rv = 0, rc = 0;
 #pragma unroll
     for (int j = 0; j < P; j++) {
         const uint32_t L = len[j];
         uint32_t v = 0;
-        bool ip_ok = false, tcp = false, l4 = false;
-        uint32_t ihs = 20;
-        // IPv4 header sum over bytes 0-19 (pairing from byte 0)
-        const uint32_t hs = wave_sum_u32(lane < 20 && lane < L ? hv[j] << (8u * (lane & 1u)) : 0u);
+        bool ip_ok = false, tcp = false, l4 = false, v6 = false;
+        uint32_t ihs = 20, proto = 0;
+        // header byte `lane` in packet pairing (from byte 0)
+        const uint32_t hb = lane < L && lane < 40u ? hv[j] << (8u * (lane & 1u)) : 0u;
+        // IPv4 header sum over bytes 0-19
+        const uint32_t hs = wave_sum_u32(lane < 20u ? hb : 0u);
         if (L >= 1) {
             const uint32_t b0 = rl(hv[j], 0);
-            const bool v6 = (b0 >> 4) == 6;
+            v6 = (b0 >> 4) == 6;
             if (v6)
                 v |= WG_VERDICT_V6;
             ihs = v6 ? 40u : 20u;
             if (L >= ihs && L <= 65535u) {  // evaluator.hpp:118-121
-                uint32_t proto;
                 if (!v6) {
                     ip_ok = (b0 & 0xfu) == 5u &&                                   // ip_hl, evaluator.cpp:19
                             L == ((rl(hv[j], 2) << 8) | rl(hv[j], 3)) &&            // ip_len, :21
@@ -248,28 +262,22 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
                 }
             }
         }
-        verdict[j] = v;
-        do_l4[j] = l4;
-        g[j].a = l4 ? a[j] : reinterpret_cast<uintptr_t>(p.base);
-        g[j].len = l4 ? L : 0u;
-        g[j].cs = ihs;
-        g[j].fl = ((v & WG_VERDICT_V6) ? WG_PKT_V6 : 0u) | (tcp ? WG_PKT_TCP : 0u);
-        issue<true, true>(g[j], lane, f[j]);
-    }
-    uint32_t rv = 0, rc = 0;
-#pragma unroll
-    for (int j = 0; j < P; j++) {
-        uint32_t s = wave_sum_u32(finish<true>(lane, f[j]));
+        // calc_l4_checksum(pkt, isv6, istcp, ihs) (checksum.cpp:8-36): bytes
+        // [40, L) (issued above) + header bytes [ihs, 40) + the pseudo-header
+        // addresses (v4 12-19, v6 8-39), all in packet pairing — ihs and the
+        // address offsets are even, so that is the reference's pairing.
+        const bool inl4 = lane >= ihs;  // hb is zero from lane 40 on
+        const bool inps = v6 ? lane >= 8u : (lane >= 12u && lane < 20u);
+        uint32_t s = wave_sum_u32(finish<true>(lane, f[j]) + (inl4 ? hb : 0u) + (inps ? hb : 0u));
         uint32_t c = 0;
-        if (do_l4[j]) {
-            const uint32_t proto = (g[j].fl & WG_PKT_TCP) ? 6u : 17u;
-            s += (proto << 8) + bswap16((g[j].len - g[j].cs) & 0xffffu);
+        if (l4) {
+            s += ((tcp ? 6u : 17u) << 8) + bswap16((L - ihs) & 0xffffu);
             c = ~fold16_32(s) & 0xffffu;
             if (c == 0)
-                verdict[j] |= WG_VERDICT_L4_OK;
+                v |= WG_VERDICT_L4_OK;
         }
         if (lane == (uint32_t)j) {
-            rv = verdict[j];
+            rv = v;
             rc = c;
         }
     }
@@ -294,7 +302,10 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
     uint64_t blocks = (n + 15) / 16;
     if (blocks >= 8)
         blocks = (blocks + 7) & ~7ull;
-    hipLaunchKernelGGL(verify_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), p);
+    if (tune().verify_occ == 8)
+        hipLaunchKernelGGL((verify_kernel<4, 8>), dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), p);
+    else
+        hipLaunchKernelGGL((verify_kernel<4>), dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }
 

@@ -28,6 +28,7 @@ struct GsoParams {
     uint64_t n;
     uint8_t *out;
     wg_gso_result *res;
+    uint32_t groups;  // blocks per super-buffer (flat grid: block u -> super-buffer u / groups)
 };
 
 // Wave-uniform byte load (every lane reads the same address).
@@ -66,41 +67,41 @@ __device__ __forceinline__ bool l4_varying(const Ctx &c, uint32_t j) {
     return c.tcp ? ((j >= c.cs + 4 && j < c.cs + 8) || j == c.cs + 13) : (j == c.cs + 4 || j == c.cs + 5);
 }
 
-// Field code of prefix byte j in every output segment: a one-hot selector of
-// the per-segment value that replaces it (bits 0-7; none = the prefix byte
-// as is, kSelFlags = TCP flags with FIN/PSH cleared except on the last
-// segment) and which byte of that value (shift, bits 8-12).  Priority as in
-// the reference's write order: checksums (written last, :185-186, :203-204)
-// over the length/id/seq fix-ups.  One-hot so the per-segment select is a
-// chain of independent bit tests (a dense selector becomes a scratch table).
-enum : uint32_t { kSelTmpl = 0, kSelPkt = 1, kSelId = 2, kSelIpcs = 4, kSelL4cs = 8, kSelSeq = 16, kSelUlen = 32,
-                  kSelFlags = 64 };
+// Field code of prefix byte j in every output segment: which per-segment
+// value replaces it (bits 0-2, a field index; 0 = the prefix byte as is) and
+// which byte of that value (shift, bits 8-12).  Priority as in the
+// reference's write order: checksums (written last, :185-186, :203-204) over
+// the length/id/seq fix-ups.  The per-segment values sit in lanes 1-7 of one
+// VGPR (v_writelane) and each header lane fetches its field with one
+// ds_bpermute (seg_finish, gso.hip).
+enum : uint32_t { kFldTmpl = 0, kFldPkt = 1, kFldId = 2, kFldIpcs = 3, kFldL4cs = 4, kFldSeq = 5, kFldUlen = 6,
+                  kFldFlags = 7 };
 
 __device__ __forceinline__ uint32_t hdr_code(const Ctx &c, uint32_t j) {
     if (!c.v6 && (j == 10 || j == 11))
-        return kSelIpcs | ((j == 11 ? 8u : 0u) << 8);  // native order
+        return kFldIpcs | ((j == 11 ? 8u : 0u) << 8);  // native order
     if (j == c.l4off || j == c.l4off + 1)
-        return kSelL4cs | ((j == c.l4off + 1 ? 8u : 0u) << 8);
+        return kFldL4cs | ((j == c.l4off + 1 ? 8u : 0u) << 8);
     if (c.v6) {
         if (j == 4 || j == 5)  // ip6_plen = pktlen - cs (big endian)
-            return kSelUlen | ((j == 4 ? 8u : 0u) << 8);
+            return kFldUlen | ((j == 4 ? 8u : 0u) << 8);
     } else {
         if (j == 2 || j == 3)  // ip_len
-            return kSelPkt | ((j == 2 ? 8u : 0u) << 8);
+            return kFldPkt | ((j == 2 ? 8u : 0u) << 8);
         if (j == 4 || j == 5)  // ip_id
-            return kSelId | ((j == 4 ? 8u : 0u) << 8);
+            return kFldId | ((j == 4 ? 8u : 0u) << 8);
     }
     if (j >= c.cs) {
         if (c.tcp) {
             if (j >= c.cs + 4 && j < c.cs + 8)
-                return kSelSeq | ((8u * (c.cs + 7u - j)) << 8);
-            if (j == c.cs + 13)
-                return kSelFlags;
+                return kFldSeq | ((8u * (c.cs + 7u - j)) << 8);
+            if (j == c.cs + 13)  // TCP flags: the prefix's, FIN/PSH cleared except on the last segment
+                return kFldFlags;
         } else if (j == c.cs + 4 || j == c.cs + 5) {
-            return kSelUlen | ((j == c.cs + 4 ? 8u : 0u) << 8);
+            return kFldUlen | ((j == c.cs + 4 ? 8u : 0u) << 8);
         }
     }
-    return kSelTmpl;
+    return kFldTmpl;
 }
 
 // One pass over the prefix per wave: exact integer sums of the invariant
@@ -134,21 +135,20 @@ __device__ __forceinline__ void st8(uintptr_t addr, uint32_t b) {
     *reinterpret_cast<__attribute__((address_space(1))) uint8_t *>(addr) = (uint8_t)b;
 }
 
+// The per-segment field values, indexed by kFld* (entry 0 unused).
 struct HdrVals {
-    uint32_t pkt, id, ipcs, l4cs, seq, ulen, fm;
+    uint32_t v[8];
 };
 
-__device__ __forceinline__ uint32_t hdr_byte(const HdrVals &h, uint32_t code, uint32_t tb) {
-    uint32_t v = (code & kSelPkt) ? h.pkt : 0u;
-    v |= (code & kSelId) ? h.id : 0u;
-    v |= (code & kSelIpcs) ? h.ipcs : 0u;
-    v |= (code & kSelL4cs) ? h.l4cs : 0u;
-    v |= (code & kSelSeq) ? h.seq : 0u;
-    v |= (code & kSelUlen) ? h.ulen : 0u;
-    v = (v >> (code >> 8)) & 0xffu;
-    if (code & kSelFlags)
-        v = tb & h.fm;
-    return (code & 0xffu) ? v : tb;
+// Header byte by field code, for header bytes past the first 128 (rare: the
+// general path; the first 128 use the ds_bpermute lookup).
+__device__ __forceinline__ uint32_t hdr_byte_slow(const HdrVals &h, uint32_t code, uint32_t tb) {
+    const uint32_t f = code & 7u;
+    uint32_t v = tb;
+#pragma unroll
+    for (uint32_t k = 1; k < 8; k++)
+        v = f == k ? (h.v[k] >> (code >> 8)) & 0xffu : v;
+    return v;
 }
 
 // GSO_NONE + NEEDS_CSUM (offload.cpp:56-78): both checksums in place, one wave.

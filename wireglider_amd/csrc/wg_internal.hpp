@@ -14,9 +14,11 @@ struct Tune {
     uint32_t l4_nt;       // 1: non-temporal packet loads
     uint32_t l4_descv;    // 1: descriptors by one vector load per wave (else scalar loads)
     uint64_t gso_blocks;  // grid cap for the GSO split kernel (one block per super-buffer)
-    uint32_t gso_waves;   // waves per block (4, 8, 16)
+    uint32_t gso_waves;   // waves per block (4, 8)
     uint32_t gso_split;   // blocks per super-buffer (grid y)
-    uint32_t gso_spw;     // segments in flight per wave (1, 2)
+    uint32_t gso_groups;  // blocks per super-buffer, consecutive in the flat grid (one-shot waves)
+    uint32_t gso_spw;     // segments per wave step: 0 one at a time, 1 ping-pong pipeline, 2 pairs
+    uint32_t verify_occ;  // waves/SIMD target of the verify kernel (0 = compiler's choice; 8)
     uint32_t gso_ablate;  // timing-only ablation bits (0 in production; non-zero = wrong output)
 };
 
