@@ -200,6 +200,8 @@ typedef struct {
     uint8_t *verdict;
     uint8_t *wbase;
     orc_gro_desc *gdesc;
+    const orc_gso_desc *sdesc;
+    int8_t *status;
     uint64_t lo, hi;
 } job_t;
 
@@ -222,6 +224,12 @@ static void run_job(job_t *j) {
         } else if (j->kind == 3) {
             const orc_pkt_desc *d = &j->desc[i];
             j->verdict[i] = orc_verify(j->base + d->offset, d->len, j->out ? &j->out[i] : NULL);
+        } else if (j->kind == 5) {
+            const orc_gso_desc *d = &j->sdesc[i];
+            orc_vnet_hdr v = d->vnet;
+            orc_gso_result r;
+            j->status[i] = (int8_t)orc_gso_split(j->wbase + d->in_offset, d->in_len, &v,
+                                                 (uint8_t *)j->base + d->out_offset, d->out_cap, &r);
         } else {
             orc_gro_desc *d = &j->gdesc[i];
             d->status = (int8_t)orc_gro_finalize(j->wbase + d->hdr_offset, d->hdr_len, d->csum_start,
@@ -316,6 +324,17 @@ void orc_gro_finalize_desc(uint8_t *base, orc_gro_desc *desc, uint64_t n, int th
     j.kind = 4;
     j.wbase = base;
     j.gdesc = desc;
+    run_parallel(j, n, threads);
+}
+
+void orc_gso_split_desc(uint8_t *in_base, const orc_gso_desc *desc, uint64_t n, uint8_t *out_base, int8_t *status,
+                        int threads) {
+    job_t j = {0};
+    j.kind = 5;
+    j.wbase = in_base;
+    j.base = out_base;
+    j.sdesc = desc;
+    j.status = status;
     run_parallel(j, n, threads);
 }
 

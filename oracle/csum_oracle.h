@@ -113,6 +113,19 @@ typedef struct orc_vnet_hdr {
 int orc_gso_split(uint8_t *in, size_t in_len, orc_vnet_hdr *vnet, uint8_t *out, size_t out_cap,
                   orc_gso_result *res);
 
+/* A batch of super-buffers in the engine's 40-byte descriptor layout
+ * (wg_gso_desc): do_tun_gso_split per descriptor on `threads` pthreads
+ * (disjoint super-buffer ranges), status per descriptor.  The CPU baseline
+ * of BASELINE config 3. */
+typedef struct orc_gso_desc {
+    uint64_t in_offset, out_offset;
+    uint32_t in_len, out_cap;
+    orc_vnet_hdr vnet;
+    uint16_t reserved[3];
+} orc_gso_desc;
+void orc_gso_split_desc(uint8_t *in_base, const orc_gso_desc *desc, uint64_t n, uint8_t *out_base, int8_t *status,
+                        int threads);
+
 /* Decap verify gates: the checksum-related decisions of
  * evaluate_packet (include/worker/evaluator.hpp:112-149) with fill_fk_ip4 /
  * fill_fk_ip6 (worker/evaluator.cpp:14-58) and the checksum gates of

@@ -77,6 +77,8 @@ def _load():
     lib.orc_gro_finalize.argtypes = [vp, sz, u16, u16, i32, i32, u64]
     lib.orc_gro_finalize_desc.restype = None
     lib.orc_gro_finalize_desc.argtypes = [vp, vp, u64, i32]
+    lib.orc_gso_split_desc.restype = None
+    lib.orc_gso_split_desc.argtypes = [vp, vp, u64, vp, vp, i32]
     lib.orc_time_l4_uniform.restype = ctypes.c_double
     lib.orc_time_l4_uniform.argtypes = [vp, u64, u32, u16, u32, vp, i32, i32]
     return lib
@@ -206,6 +208,26 @@ def gso_split(inbuf: np.ndarray, vnet: dict, out_cap: int):
     vafter = dict(flags=v.flags, gso_type=v.gso_type, hdr_len=v.hdr_len, gso_size=v.gso_size,
                   csum_start=v.csum_start, csum_offset=v.csum_offset)
     return st, a, out[: r.out_len if (st == 0 and not r.passthrough) else 0], vafter, res
+
+
+GSO_DESC = np.dtype([("in_offset", "<u8"), ("out_offset", "<u8"), ("in_len", "<u4"), ("out_cap", "<u4"),
+                     ("vnet", VNET_HDR), ("reserved", "<u2", 3)])
+assert GSO_DESC.itemsize == 40
+
+
+def gso_split_desc(inbuf: np.ndarray, desc: np.ndarray, outbuf: np.ndarray, threads: int | None = None):
+    """do_tun_gso_split for a batch of 40-byte descriptors, in place on inbuf
+    (the reference zeroes prefix fields) and into outbuf; returns statuses."""
+    a, o = _u8(inbuf), _u8(outbuf)
+    d = np.ascontiguousarray(desc).view(GSO_DESC).reshape(-1)
+    end_in = int((d["in_offset"] + d["in_len"]).max()) if d.size else 0
+    end_out = int((d["out_offset"] + d["out_cap"]).max()) if d.size else 0
+    if end_in > a.size or end_out > o.size:
+        raise ValueError("gso_split_desc: descriptor past a buffer")
+    st = np.zeros(d.size, dtype=np.int8)
+    lib.orc_gso_split_desc(a.ctypes.data, d.ctypes.data, d.size, o.ctypes.data, st.ctypes.data,
+                           threads or default_threads())
+    return st
 
 
 def time_l4_uniform(buf: np.ndarray, segment_size: int, csum_start: int, flags: int, threads: int,

@@ -201,3 +201,43 @@ def test_error_and_passthrough_cases():
     st, inb, out, _, res = split(pkt[:40], flags=NEEDS_CSUM, gso_type=GSO_TCPV4, gso_size=100, csum_start=20,
                                  csum_offset=16)
     assert st == 0 and res["passthrough"] == 0 and res["out_len"] == 0 and inb[36] == 0 and inb[37] == 0
+
+
+def test_batch_driver_matches_per_buffer():
+    """orc_gso_split_desc (the threaded CPU baseline of config 3) gives the
+    per-super-buffer oracle's bytes, statuses and in-place input changes."""
+    rng = np.random.default_rng(31)
+    pkts, vnets = [], []
+    for k in range(40):
+        isv6, istcp = bool(k & 1), bool(k & 2)
+        p = pktbuild.build(isv6, istcp, rng.integers(0, 256, int(rng.integers(0, 9000)), dtype=np.uint8).tobytes(),
+                           rng.integers(0, 256, 16 if isv6 else 4, dtype=np.uint8).tobytes(),
+                           rng.integers(0, 256, 16 if isv6 else 4, dtype=np.uint8).tobytes(), fill_l4=False)
+        gt = (4 if isv6 else 1) if istcp else 5
+        vnets.append(dict(flags=1, gso_type=gt if k % 7 else 0, hdr_len=0, gso_size=int(rng.choice([100, 1448, 1460])),
+                          csum_start=40 if isv6 else 20, csum_offset=16 if istcp else 6))
+        pkts.append(p)
+    d = np.zeros(len(pkts), dtype=oracle.GSO_DESC)
+    io = oo = 0
+    for k, (p, v) in enumerate(zip(pkts, vnets)):
+        cap = len(p) + (len(p) // v["gso_size"] + 2) * 80
+        d[k]["in_offset"], d[k]["out_offset"], d[k]["in_len"], d[k]["out_cap"] = io + 3, oo + 5, len(p), cap
+        for f, x in v.items():
+            d[k]["vnet"][f] = x
+        io += len(p) + 3
+        oo += cap + 5
+    inbuf = np.zeros(io + 8, np.uint8)
+    for k, p in enumerate(pkts):
+        inbuf[int(d[k]["in_offset"]):int(d[k]["in_offset"]) + len(p)] = np.frombuffer(p, np.uint8)
+    outbuf = np.zeros(oo + 8, np.uint8)
+    before = inbuf.copy()
+    st = oracle.gso_split_desc(inbuf, d, outbuf, threads=4)
+    for k, (p, v) in enumerate(zip(pkts, vnets)):
+        s1, in_after, out1, _, res = oracle.gso_split(np.frombuffer(p, np.uint8), v, int(d[k]["out_cap"]))
+        assert int(st[k]) == s1
+        o = int(d[k]["in_offset"])
+        assert np.array_equal(inbuf[o:o + len(p)], in_after)
+        if s1 == 0 and not res["passthrough"]:
+            oo = int(d[k]["out_offset"])
+            assert np.array_equal(outbuf[oo:oo + len(out1)], out1)
+    assert not np.array_equal(before, inbuf)  # the reference zeroes prefix fields in place

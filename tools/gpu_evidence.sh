@@ -1,0 +1,20 @@
+#!/bin/bash
+# One GPU-box session: the whole -m gpu suite, bench lines for configs 3/4/5 and
+# the verify gates, rocprofv3 kernel stats and PMC HBM traffic for config 3 and
+# verify.  Each GPU step has its own time limit; the first failure ends it.
+# usage: tools/gpu_evidence.sh [outdir-name]
+set -u
+cd "${GRAFT_REPO_ROOT}"
+O=$(pwd)/gpurun_out/${1:-evidence}; mkdir -p $O
+export TMPDIR=/tmp
+ROOT=$(pwd)
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > $O/pytest.log 2>&1; rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
+for W in config3 verify config5 config4; do
+  timeout -k 10 300 python3 bench.py --workload $W --steps 30 > $O/bench_$W.json 2> $O/bench_$W.err || { tail $O/bench_$W.err; exit 1; }
+  cat $O/bench_$W.json
+done
+for W in config3 verify; do
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/stats_$W" -o run --output-format csv -- python3 "$ROOT/bench.py" --workload $W --steps 30 --no-cpu-baseline > "$O/stats_$W.log" 2>&1) || { echo "stats $W failed"; tail "$O/stats_$W.log"; exit 1; }
+  bash tools/pmc_profile.sh "$O/pmc_$W" --workload $W --steps 10 --settle-seconds 0.1 > "$O/pmc_$W.log" 2>&1 || { tail "$O/pmc_$W.log"; exit 1; }
+done
+echo done
