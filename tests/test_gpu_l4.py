@@ -86,11 +86,14 @@ def test_reference_golden_vectors(gpu):
 SEGS = [1, 7, 20, 21, 28, 40, 48, 59, 64, 100, 127, 128, 1460, 1500, 1501, 4096, 9000, 9001]
 
 
+@pytest.mark.parametrize("occ", [0, 7])
 @pytest.mark.parametrize("seg", SEGS)
-def test_uniform_geometry_sweep(gpu, seg):
+def test_uniform_geometry_sweep(gpu, seg, occ):
     import torch
 
     wga = _wga()
+    saved = wga.tune_get("l4_occ")
+    wga.tune_set("l4_occ", occ)
     rng = np.random.default_rng(seg)
     for trial in range(6):
         nseg = int(rng.integers(1, 40))
@@ -106,12 +109,24 @@ def test_uniform_geometry_sweep(gpu, seg):
         exp = oracle.l4_uniform(buf, seg, cs, flags)
         np.testing.assert_array_equal(out.cpu().numpy(), exp,
                                       err_msg=f"seg={seg} total={total} pad={pad} cs={cs} flags={flags}")
+    wga.tune_set("l4_occ", saved)
 
 
-def test_desc_random(gpu):
+DESC_VARIANTS = [{"l4_occ": 0}, {"l4_occ": 7}, {"l4_occ": 8}, {"l4_descv": 1}, {"l4_descv": 2, "l4_iters": 2},
+                 {"l4_descv": 2, "l4_iters": 3, "l4_occ": 0}, {"l4_descv": 2, "l4_iters": 8, "l4_ppw": 2}]
+
+
+@pytest.mark.parametrize("knobs", DESC_VARIANTS, ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()))
+def test_desc_random(gpu, knobs):
+    """Random descriptor batches under each launch variant of the kernel
+    (occupancy target, descriptor mode, iterations per wave: speed knobs that
+    must not change any result)."""
     import torch
 
     wga = _wga()
+    saved = {k: wga.tune_get(k) for k in ("l4_occ", "l4_descv", "l4_iters", "l4_ppw")}
+    for k, v in knobs.items():
+        wga.tune_set(k, v)
     rng = np.random.default_rng(1234)
     n = 20000
     lens = rng.integers(0, 9100, n)
@@ -131,6 +146,8 @@ def test_desc_random(gpu):
     out = wga.calc_l4_checksum_desc(view, dd)
     plain = wga.checksum_desc(view, dd)
     torch.cuda.synchronize()
+    for k, v in saved.items():
+        wga.tune_set(k, v)
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.l4_desc(buf, d))
     np.testing.assert_array_equal(plain.cpu().numpy(), oracle.checksum_desc(buf, d))
 

@@ -31,7 +31,12 @@ Tune &tune_mut() {
         x.l4_blocks = env_u64("WG_L4_BLOCKS", 1u << 20);
         x.l4_ppw = (uint32_t)env_u64("WG_L4_PPW", 4);
         x.l4_nt = (uint32_t)env_u64("WG_L4_NT", 1);
-        x.l4_descv = (uint32_t)env_u64("WG_L4_DESCV", 0);
+        // Descriptor batches: each wave takes 4 iterations and prefetches the
+        // next iteration's descriptors by one vector load during the current
+        // one's finish (+3-5 % on config 5, profiles/r01_ab_session2.json).
+        x.l4_descv = (uint32_t)env_u64("WG_L4_DESCV", 2);
+        x.l4_occ = (uint32_t)env_u64("WG_L4_OCC", 0);
+        x.l4_iters = (uint32_t)env_u64("WG_L4_ITERS", 4);
         x.gso_blocks = env_u64("WG_GSO_BLOCKS", 1u << 23);
         // GSO: one 4-wave block per super-buffer, each wave a ping-pong
         // pipeline (next segment's loads in flight while this one finishes);
@@ -219,8 +224,12 @@ extern "C" int wg_tune_set(const char *key, uint64_t value) {
         t.l4_ppw = (uint32_t)value;
     else if (k == "l4_nt" && value <= 1)
         t.l4_nt = (uint32_t)value;
-    else if (k == "l4_descv" && value <= 1)
+    else if (k == "l4_iters" && value >= 1 && value <= 64)
+        t.l4_iters = (uint32_t)value;
+    else if (k == "l4_descv" && value <= 2)
         t.l4_descv = (uint32_t)value;
+    else if (k == "l4_occ" && (value == 0 || value == 7 || value == 8))
+        t.l4_occ = (uint32_t)value;
     else if (k == "gso_blocks" && value >= 1 && value <= (1u << 23))
         t.gso_blocks = value;
     else if (k == "verify_occ" && (value == 0 || value == 8))
@@ -249,6 +258,8 @@ extern "C" int wg_tune_get(const char *key, uint64_t *value) {
     else if (k == "l4_ppw") *value = t.l4_ppw;
     else if (k == "l4_nt") *value = t.l4_nt;
     else if (k == "l4_descv") *value = t.l4_descv;
+    else if (k == "l4_occ") *value = t.l4_occ;
+    else if (k == "l4_iters") *value = t.l4_iters;
     else if (k == "gso_blocks") *value = t.gso_blocks;
     else if (k == "gso_waves") *value = t.gso_waves;
     else if (k == "gso_split") *value = t.gso_split;

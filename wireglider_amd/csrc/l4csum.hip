@@ -65,47 +65,70 @@ __device__ __forceinline__ Geom load_geom(const L4Params &p, uint64_t i) {
     return g;
 }
 
-// Descriptors of packets i0 .. i0+P-1 with ONE coalesced vector load (lane j
-// holds descriptor j) instead of P scalar loads, then v_readlane to make them
-// wave-uniform.
-template <int kKind, int P>
-__device__ __forceinline__ void load_geoms_vec(const L4Params &p, uint64_t i0, uint32_t lane, Geom *g) {
+// Descriptors of packets i0 .. i0+P-1 by ONE coalesced vector load (lane j
+// holds descriptor j), made wave-uniform with v_readlane.
+template <int P>
+__device__ __forceinline__ v4u load_desc_vec(const L4Params &p, uint64_t i0, uint32_t lane) {
     const uint64_t di = i0 + (lane & (uint32_t)(P - 1));
     const uint64_t dc = di < p.n ? di : p.n - 1;
-    const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * dc);
+    return ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * dc);
+}
+
+template <int kKind, int P>
+__device__ __forceinline__ void geoms_from_vec(const L4Params &p, uint64_t i0, const v4u &dv, Geom *g) {
 #pragma unroll
     for (int j = 0; j < P; j++) {
-        if (i0 + j >= p.n) {  // padding slot: empty packet
-            g[j].a = reinterpret_cast<uintptr_t>(p.base);
-            g[j].len = g[j].cs = g[j].fl = 0;
-            continue;
-        }
+        const bool live = i0 + j < p.n;  // else a padding slot: empty packet
         const uint64_t off = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dv.x, j) |
                              ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dv.y, j) << 32);
         const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)dv.w, j);
-        g[j].a = reinterpret_cast<uintptr_t>(p.base) + off;
-        g[j].len = (uint32_t)__builtin_amdgcn_readlane((int)dv.z, j);
-        g[j].cs = kKind == kDescPlain ? 0u : (w & 0xffffu);
-        g[j].fl = (w >> 16) & 0xffu;
+        g[j].a = reinterpret_cast<uintptr_t>(p.base) + (live ? off : 0u);
+        g[j].len = live ? (uint32_t)__builtin_amdgcn_readlane((int)dv.z, j) : 0u;
+        g[j].cs = kKind == kDescPlain || !live ? 0u : (w & 0xffffu);
+        g[j].fl = live ? (w >> 16) & 0xffu : 0u;
     }
 }
 
-template <int kKind, int P, bool kNT, bool kVD>
-__global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
+// Descriptor modes (kDM): 0 = scalar loads per iteration; 1 = one vector load
+// per iteration (measured slower: the readlanes wait on it); 2 = scalar loads
+// for a wave's first iteration, and each iteration's vector load of the NEXT
+// iteration's descriptors issued right after its own packet loads, so from
+// the second iteration on a wave starts its packet loads with no descriptor
+// round trip in front of them (the launcher gives each wave l4_iters
+// iterations).
+template <int kKind, int P, bool kNT, int kDM, int O = 0>  // O: waves/SIMD target (0 = compiler's choice)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void l4csum_kernel(
+    L4Params p) {
     constexpr bool kL4 = kKind != kDescPlain;
+    constexpr int DM = kKind == kUniformL4 ? 0 : kDM;
     const uint32_t lane = lane_id();
     const uint64_t wave0 = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
     const uint64_t step = (uint64_t)gridDim.x * 4u * P;
+    v4u nextd = v4u{0, 0, 0, 0};
+    bool have_next = false;
     for (uint64_t i0 = wave0 * P; i0 < p.n; i0 += step) {
         Geom g[P];
         Front f[P];
-        if constexpr (kVD && kKind != kUniformL4)
-            load_geoms_vec<kKind, P>(p, i0, lane, g);
+        if constexpr (DM == 1) {
+            geoms_from_vec<kKind, P>(p, i0, load_desc_vec<P>(p, i0, lane), g);
+        } else if constexpr (DM == 2) {
+            if (have_next) {
+                geoms_from_vec<kKind, P>(p, i0, nextd, g);
+            } else {
+#pragma unroll
+                for (int j = 0; j < P; j++)
+                    g[j] = load_geom<kKind>(p, i0 + j);
+            }
+        }
 #pragma unroll
         for (int j = 0; j < P; j++) {
-            if constexpr (!(kVD && kKind != kUniformL4))
+            if constexpr (DM == 0)
                 g[j] = load_geom<kKind>(p, i0 + j);
             issue<kL4, kNT>(g[j], lane, f[j]);
+        }
+        if constexpr (DM == 2) {  // next iteration's descriptors, in flight during the finish
+            have_next = i0 + step < p.n;
+            nextd = load_desc_vec<P>(p, have_next ? i0 + step : i0, lane);
         }
         uint32_t res = 0;
 #pragma unroll
@@ -127,12 +150,31 @@ __global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
     }
 }
 
+template <int kKind, int P, bool kNT, int DM>
+static void launch_occ(const L4Params &p, uint64_t blocks, hipStream_t st) {
+    const uint32_t occ = tune().l4_occ;
+    if constexpr (P == 4 && kNT) {
+        if (occ == 7) {
+            hipLaunchKernelGGL((l4csum_kernel<kKind, P, kNT, DM, 7>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+            return;
+        }
+        if (occ == 8) {
+            hipLaunchKernelGGL((l4csum_kernel<kKind, P, kNT, DM, 8>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((l4csum_kernel<kKind, P, kNT, DM>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+}
+
 template <int kKind, int P, bool kNT>
 static void launch_variant(const L4Params &p, uint64_t blocks, hipStream_t st) {
-    if (kKind != kUniformL4 && tune().l4_descv)
-        hipLaunchKernelGGL((l4csum_kernel<kKind, P, kNT, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+    const uint32_t dm = kKind == kUniformL4 ? 0u : tune().l4_descv;
+    if (dm == 1)
+        launch_occ<kKind, P, kNT, 1>(p, blocks, st);
+    else if (dm == 2)
+        launch_occ<kKind, P, kNT, 2>(p, blocks, st);
     else
-        hipLaunchKernelGGL((l4csum_kernel<kKind, P, kNT, false>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+        launch_occ<kKind, P, kNT, 0>(p, blocks, st);
 }
 
 template <int kKind>
@@ -150,7 +192,9 @@ static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
         return WG_OK;
     const Tune &t = tune();
     const uint32_t P = t.l4_ppw;
-    const uint64_t want = (p.n + 4ull * P - 1) / (4ull * P);
+    uint64_t want = (p.n + 4ull * P - 1) / (4ull * P);
+    if (kind != kUniformL4 && t.l4_descv == 2)  // l4_iters iterations per wave (descriptor prefetch)
+        want = (want + t.l4_iters - 1) / t.l4_iters;
     uint64_t blocks = want < t.l4_blocks ? want : t.l4_blocks;
     if (blocks >= 8)
         blocks &= ~7ull;  // keep the XCD swizzle bijective

@@ -64,16 +64,19 @@ __device__ __forceinline__ void issue(const Geom &g, uint32_t lane, Front &f) {
     // (absolute-address pairing, like the interior).
     const bool v6 = g.fl & WG_PKT_V6;
     const uint32_t ao = v6 ? 8u : 12u, al = v6 ? 32u : 8u;
+    // Per-lane 32-bit offsets from a wave-uniform base (packet start, or the
+    // zero chunk for an empty packet): no per-lane 64-bit addresses.
     const bool bt = kL4 && lane < al && ao + lane < g.len;
-    const uintptr_t he = c0 < r1 ? c0 : r1;
-    const uintptr_t ts = c1 > c0 ? c1 : c0;
-    const uintptr_t xh = r0 + (lane - 32);
-    const uintptr_t xt = ts + (lane - 48);
-    const bool bh = lane >= 32 && lane < 48 && xh < he;
-    const bool btl = lane >= 48 && xt < r1;
-    const uintptr_t bp = bt ? g.a + ao + lane : (bh ? xh : (btl ? xt : zero));
-    const uint32_t par = bt ? (lane & 1u) : (uint32_t)(bp & 1u);
-    f.bv = ld8(bp) << (8u * par);
+    const uint32_t cs0 = (uint32_t)(r0 - g.a);                       // region start
+    const uint32_t heo = (uint32_t)((c0 < r1 ? c0 : r1) - g.a);      // head end
+    const uint32_t tso = (uint32_t)((c1 > c0 ? c1 : c0) - g.a);      // tail start
+    const uint32_t xh = cs0 + lane - 32u, xt = tso + lane - 48u;
+    const bool bh = lane >= 32 && lane < 48 && xh < heo;
+    const bool btl = lane >= 48 && xt < g.len;
+    const uint32_t off = bt ? ao + lane : (bh ? xh : (btl ? xt : 0u));
+    const uint32_t par = bt ? (lane & 1u) : (((uint32_t)g.a + off) & 1u);
+    const uint32_t byte = ld8((g.len ? g.a : zero) + off);
+    f.bv = (bt || bh || btl) ? byte << (8u * par) : 0u;
     f.bt = bt;
 }
 
