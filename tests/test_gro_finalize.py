@@ -150,10 +150,15 @@ def _oracle_batch(hdrs, desc):
 
 
 @pytest.mark.gpu
-def test_gpu_gro_finalize_parity(gpu):
+@pytest.mark.parametrize("lds,wide", [(1, 1), (1, 0), (0, 0)], ids=["lds-wide", "lds-narrow", "thread-loads"])
+def test_gpu_gro_finalize_parity(gpu, lds, wide):
     import torch
 
     import wireglider_amd as wg
+
+    saved = {k: wg.tune_get(k) for k in ("gro_lds", "gro_wide")}
+    wg.tune_set("gro_lds", lds)
+    wg.tune_set("gro_wide", wide)
 
     rng = np.random.default_rng(2024)
     hdrs, desc = _batch(rng, 3000)
@@ -163,6 +168,8 @@ def test_gpu_gro_finalize_parity(gpu):
     dd = torch.from_numpy(desc.view(np.uint8)).to(gpu)
     wg.gro_finalize(dh, dd)
     torch.cuda.synchronize()
+    for k, v in saved.items():
+        wg.tune_set(k, v)
     got = dh.cpu().numpy()
     got_desc = dd.cpu().numpy().view(wg.GRO_DESC_DTYPE)
     assert np.array_equal(got_desc["status"], want_st)

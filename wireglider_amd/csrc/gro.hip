@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include "wg_device.hpp"
+#include "wg_internal.hpp"
 #include "wireglider_amd.h"
 
 namespace wg {
@@ -51,21 +52,32 @@ __device__ __forceinline__ void st16_ne(uint8_t *p, uint32_t v) {  // native-ord
     }
 }
 
-__device__ __forceinline__ void gro_fast(uint8_t *h, const wg_gro_desc &d, bool v6, uint64_t l4len, uint32_t need) {
-    const uint64_t addr = (uint64_t)(uintptr_t)h;
-    const uint32_t s = (uint32_t)(addr & 15u);
-    const uintptr_t a0 = (uintptr_t)(addr - s);
-    const uintptr_t alast = (uintptr_t)((addr + need - 1) & ~15ull);
-    uint32_t W[20];
-#pragma unroll
-    for (int c = 0; c < 5; c++) {
-        const uintptr_t a = a0 + 16u * c;
-        const v4u v = ld16(a > alast ? alast : a);
-        W[4 * c] = v[0];
-        W[4 * c + 1] = v[1];
-        W[4 * c + 2] = v[2];
-        W[4 * c + 3] = v[3];
-    }
+// The finalize arithmetic on the header's aligned 16-B chunks W[0..19]
+// (chunk c = the aligned chunk at (h & ~15) + 16c, clamped onto the last one
+// holding a needed byte).
+// Stores by aligned-type pointers: the compiler emits one dword / dwordx4
+// store, and gfx950 global memory accepts the unaligned address.
+__device__ __forceinline__ void st32_u(uint8_t *p, uint32_t v) {
+    *reinterpret_cast<__attribute__((address_space(1))) uint32_t *>(reinterpret_cast<uintptr_t>(p)) = v;
+}
+__device__ __forceinline__ void st128_u(uint8_t *p, v4u v) {
+    *reinterpret_cast<__attribute__((address_space(1))) v4u *>(reinterpret_cast<uintptr_t>(p)) = v;
+}
+
+// kWide: the fields go out in two wide stores instead of four or five
+// narrow ones (stores at a 64-B lane stride are address-processing bound,
+// so instructions, not bytes, are the cost): IPv4 header bytes [0, 16)
+// (ip_len and ip_sum with the 12 unchanged bytes around them) or the IPv6
+// payload length as one dword, and for UDP the length and the seed as one
+// dword (csum_offset 6, adjacent fields).  Every byte written lies in the
+// flow's own header and the unchanged ones get their own values back.  The
+// caller writes udp->len itself when !kWide.
+template <bool kWide>
+__device__ __forceinline__ void gro_fields(uint8_t *h, const wg_gro_desc &d, bool v6, bool tcp, uint64_t l4len,
+                                           v4u k0, v4u k1, v4u k2, v4u k3, v4u k4) {
+    const uint32_t W[20] = {k0[0], k0[1], k0[2], k0[3], k1[0], k1[1], k1[2], k1[3], k2[0], k2[1],
+                            k2[2], k2[3], k3[0], k3[1], k3[2], k3[3], k4[0], k4[1], k4[2], k4[3]};
+    const uint32_t s = (uint32_t)((uintptr_t)h & 15u);
     const uint32_t q = s >> 2, sh = s & 3u;
     uint32_t R[16];
 #pragma unroll
@@ -84,12 +96,19 @@ __device__ __forceinline__ void gro_fast(uint8_t *h, const wg_gro_desc &d, bool 
         for (int m = 3; m < 16; m++)
             sip += sum16x2(keep_below(R[m], m, cs));
         const uint32_t c = ~fold16_32(sip + bswap16(T)) & 0xffffu;  // :103-106
-        st16_ne(h + 2, bswap16(T));
-        st16_ne(h + 10, c);  // native order
+        if constexpr (kWide) {
+            st128_u(h, v4u{(R[0] & 0xffffu) | (bswap16(T) << 16), R[1], (R[2] & 0xffffu) | (c << 16), R[3]});
+        } else {
+            st16_ne(h + 2, bswap16(T));
+            st16_ne(h + 10, c);  // native order
+        }
         sad = sum16x2(R[3]) + sum16x2(R[4]);
         proto = (R[2] >> 8) & 0xffu;
     } else {
-        st16_ne(h + 4, bswap16(l16));  // :95
+        if constexpr (kWide)
+            st32_u(h + 4, (R[1] & 0xffff0000u) | bswap16(l16));  // :95
+        else
+            st16_ne(h + 4, bswap16(l16));  // :95
         sad = 0;
 #pragma unroll
         for (int m = 2; m < 10; m++)
@@ -97,7 +116,24 @@ __device__ __forceinline__ void gro_fast(uint8_t *h, const wg_gro_desc &d, bool 
         proto = (R[1] >> 16) & 0xffu;
     }
     const uint32_t seed = ~fold16_32(sad + (proto << 8) + bswap16(l16)) & 0xffffu;  // :108-112
-    st16_ne(h + cs + d.csum_offset, seed);                                          // native order, :114
+    if (kWide && !tcp && d.csum_offset == 6) {
+        st32_u(h + cs + 4, bswap16(l16) | (seed << 16));  // udp->len (:85-86) + seed (:114)
+        return;
+    }
+    if (kWide && !tcp)
+        st_be16(h + cs + 4, l16);               // udp->len, :85-86
+    st16_ne(h + cs + d.csum_offset, seed);  // native order, :114
+}
+
+__device__ __forceinline__ void gro_fast(uint8_t *h, const wg_gro_desc &d, bool v6, uint64_t l4len, uint32_t need) {
+    const uint64_t addr = (uint64_t)(uintptr_t)h;
+    const uintptr_t a0 = (uintptr_t)(addr & ~15ull);
+    const uintptr_t alast = (uintptr_t)((addr + need - 1) & ~15ull);
+    auto chunk = [&](uint32_t c) {
+        const uintptr_t a = a0 + 16u * c;
+        return ld16(a > alast ? alast : a);
+    };
+    gro_fields<false>(h, d, v6, true, l4len, chunk(0), chunk(1), chunk(2), chunk(3), chunk(4));
 }
 
 // General path (header fields beyond 64 bytes): byte loop in reference order.
@@ -156,6 +192,75 @@ __global__ __launch_bounds__(256) void gro_finalize_kernel(uint8_t *hdrs, wg_gro
         reinterpret_cast<int8_t *>(desc)[i * sizeof(wg_gro_desc) + offsetof(wg_gro_desc, status)] = st;
 }
 
+// LDS-staged variant.  Thread per flow, but the header chunks are fetched
+// cooperatively: the block's 256 flows need up to 5 aligned 16-B chunks
+// each; lane L loads chunk slots L, L+256, ... (slot k = chunk k % 5 of flow
+// k / 5), so consecutive lanes read consecutive chunks of one flow and a
+// wave-instruction touches a few contiguous lines instead of 64 scattered
+// ones (thread-per-flow loads at a 64-B lane stride are address-processing
+// bound: about one cache line per cycle per CU).  The chunks go through LDS
+// to their flow's thread, which then runs the same arithmetic.
+constexpr uint32_t kGroBlock = 256, kGroChunks = 5;
+
+template <bool kWide>
+__global__ __launch_bounds__(kGroBlock) void gro_finalize_lds_kernel(uint8_t *hdrs, wg_gro_desc *desc, uint64_t n) {
+    __shared__ v4u s_chunk[kGroBlock * kGroChunks];
+    __shared__ uint64_t s_a0[kGroBlock];
+    __shared__ uint32_t s_last[kGroBlock];  // last chunk index to load, or 0xff: nothing to stage
+    const uint32_t t = threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * kGroBlock + t;
+    wg_gro_desc d{};
+    bool live = i < n, fast = false, v6 = false, tcp = false;
+    int8_t st = 0;
+    uint32_t need = 0, cs = 0, l4off = 0;
+    uint8_t *h = hdrs;
+    if (live) {
+        d = desc[i];
+        h = hdrs + d.hdr_offset;
+        const uint32_t H = d.hdr_len;
+        cs = d.csum_start;
+        l4off = cs + d.csum_offset;
+        v6 = d.flags & WG_PKT_V6;
+        tcp = d.flags & WG_PKT_TCP;
+        const uint32_t iph = v6 ? 40u : 20u;
+        if (cs < iph || cs > H || l4off < cs || l4off + 2 > H || (!tcp && cs + 8 > H))
+            st = -3;
+        else {
+            need = v6 ? 40u : cs;
+            fast = need <= kFastNeed;
+        }
+    }
+    const uintptr_t hp = reinterpret_cast<uintptr_t>(h);
+    s_a0[t] = hp & ~(uintptr_t)15;
+    s_last[t] = fast ? (uint32_t)(((hp & 15u) + need - 1) >> 4) : 0xffu;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kGroChunks; k++) {
+        const uint32_t slot = t + kGroBlock * k;
+        const uint32_t f = (slot * 52429u) >> 18;  // slot / 5 (slot < 1280)
+        const uint32_t c = slot - 5u * f;
+        const uint32_t last = s_last[f];
+        if (last != 0xffu)
+            s_chunk[slot] = ld16(s_a0[f] + 16u * (c < last ? c : last));
+    }
+    __syncthreads();
+    if (!live)
+        return;
+    if (st == 0) {
+        const uint64_t l4len = (uint64_t)(d.hdr_len - cs) + d.payload_bytes;  // :84
+        if (!tcp && !(kWide && fast))
+            st_be16(h + cs + 4, (uint32_t)l4len);  // udp->len (uint16), :85-86
+        if (fast) {
+            const v4u *k = &s_chunk[t * kGroChunks];
+            gro_fields<kWide>(h, d, v6, tcp, l4len, k[0], k[1], k[2], k[3], k[4]);
+        } else {
+            gro_slow(h, d.hdr_len, cs, l4off, d.payload_bytes, v6, l4len);
+        }
+    }
+    if (d.status != st)  // leave descriptor lines clean when the caller pre-zeroed status
+        reinterpret_cast<int8_t *>(desc)[i * sizeof(wg_gro_desc) + offsetof(wg_gro_desc, status)] = st;
+}
+
 }  // namespace wg
 
 using namespace wg;
@@ -168,7 +273,14 @@ extern "C" int wg_gro_finalize(uint8_t *dev_hdrs, wg_gro_desc *dev_desc, uint64_
     const uint64_t blocks = (n + 255) / 256;
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
-    hipLaunchKernelGGL(gro_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
-                       dev_hdrs, dev_desc, n);
+    if (tune().gro_lds && tune().gro_wide)
+        hipLaunchKernelGGL(gro_finalize_lds_kernel<true>, dim3((unsigned)blocks), dim3(kGroBlock), 0,
+                           static_cast<hipStream_t>(stream), dev_hdrs, dev_desc, n);
+    else if (tune().gro_lds)
+        hipLaunchKernelGGL(gro_finalize_lds_kernel<false>, dim3((unsigned)blocks), dim3(kGroBlock), 0,
+                           static_cast<hipStream_t>(stream), dev_hdrs, dev_desc, n);
+    else
+        hipLaunchKernelGGL(gro_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                           dev_hdrs, dev_desc, n);
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }
