@@ -262,7 +262,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                            "mixed IPv4/IPv6 x TCP/UDP, in-place finalize (wg_gro_finalize)",
                "flows_per_gpu": n, "slot_bytes": slot, "parallelism": f"shard{world}"}
         return Workload(launch, n, n, n * 24 + hdr_bytes + written + n, cfg, "weak", d_hdr,
-                        "wg::gro_finalize_kernel", rank * n, sample=sample, counts=[n] * world,
+                        "wg::gro_finalize_lds_kernel<true>", rank * n, sample=sample, counts=[n] * world,
                         metric="device-resident Mflows/s, GRO finalize (SURVEY f2)", unit="Mflows/s",
                         value_scale=1e-6, post=post)
     # config4 bimodal

@@ -6,8 +6,9 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 O=$ROOT/gpurun_out/frows_prof; mkdir -p "$O"
+WL=${@:-verify gro}
 export TMPDIR=/tmp
-for W in verify gro; do
+for W in $WL; do
   timeout -k 10 300 python3 bench.py --workload $W --steps 100 > "$O/bench_$W.json" 2> "$O/bench_$W.err" || { tail "$O/bench_$W.err"; exit 1; }
   cat "$O/bench_$W.json"
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/stats_$W" -o run --output-format csv -- python3 "$ROOT/bench.py" --workload $W --steps 100 --no-cpu-baseline > "$O/stats_$W.log" 2>&1) || { echo "stats $W failed"; exit 1; }

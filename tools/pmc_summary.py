@@ -32,7 +32,7 @@ def main():
     if "--workload" in args:
         workload = args[args.index("--workload") + 1]
     res = {"workload": workload, "bench_args": args}
-    for kern in ("l4csum_kernel", "gso_split_kernel", "verify_kernel", "gro_finalize_kernel"):
+    for kern in ("l4csum_kernel", "gso_split_kernel", "verify_kernel", "gro_finalize"):
         f = per_dispatch(str(out / "pmc_FETCH_SIZE" / "**" / "*counter_collection.csv"), kern)
         w = per_dispatch(str(out / "pmc_WRITE_SIZE" / "**" / "*counter_collection.csv"), kern)
         if not f:
@@ -47,15 +47,16 @@ def main():
             "write_bytes": wk * 1024,
             "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024,
         }
-    main_k = {"config3": "gso_split_kernel", "verify": "verify_kernel", "gro": "gro_finalize_kernel"}.get(
+    main_k = {"config3": "gso_split_kernel", "verify": "verify_kernel", "gro": "gro_finalize"}.get(
         workload, "l4csum_kernel")
     if main_k in res:
         res["hbm_bytes_per_launch"] = res[main_k]["hbm_bytes_per_launch"]
     res["correction"] = "gfx950: read bytes = 2 x FETCH_SIZE KiB x 1024 (MI355X_MICROARCH.md §HBM); write = WRITE_SIZE KiB x 1024"
     if workload == "gro":
-        res["calibration_note"] = ("gro_finalize reads 16 B/lane at a 64 B lane stride, not a coalesced stream: the x2 "
-                                   "read correction is calibrated only for coalesced 16 B/lane streams; raw "
-                                   "FETCH_SIZE is kept above")
+        res["calibration_note"] = ("gro_finalize stages its header chunks with 16 B/lane loads, consecutive lanes on "
+                                   "consecutive chunks of a flow (contiguous for the bench's 64 B slots), plus 24 B "
+                                   "descriptors: the x2 read correction is calibrated for coalesced 16 B/lane streams; "
+                                   "raw FETCH_SIZE is kept above")
     (out / f"pmc_{workload}.json").write_text(json.dumps(res, indent=1) + "\n")
     print(json.dumps(res, indent=1))
 
