@@ -183,6 +183,9 @@ int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8
  * ADDRESSES.  The reference's call sums the std::span objects instead
  * (pointer-dependent) and is not reproduced.
  * status (out): 0, or -3 when the header geometry is out of contract.
+ * Writes stay inside each flow's header: the changed fields, plus (IPv4) the
+ * unchanged bytes of header bytes [0, 16) rewritten with their own values
+ * (the fields go out as two wide stores).
  * ---------------------------------------------------------------------- */
 typedef struct wg_gro_desc {
     uint64_t hdr_offset;    /* header buffer = dev_hdrs[hdr_offset, + hdr_len) */

@@ -330,44 +330,63 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
 // and the invariant header sums into the GsoPlan; GSO_NONE + NEEDS_CSUM
 // super-buffers get both checksums in place here (:56-78).
 __global__ __launch_bounds__(256) void gso_plan_kernel(GsoParams p) {
+    constexpr int PB = 4;  // super-buffers per wave step: their descriptor and prefix loads overlap
     const uint32_t lane = lane_id();
-    const uint64_t stride = (uint64_t)gridDim.x * 4u;
-    for (uint64_t b = (uint64_t)blockIdx.x * 4u + wave_in_block(); b < p.n; b += stride) {
-        const wg_gso_desc dsc = p.desc[b];
-        Ctx c;
-        const Cls cl = classify<true>(dsc, reinterpret_cast<uintptr_t>(p.in), c);
-        GsoPlan pl{};
-        if (!cl.pass) {
-            c.id0 = (pbyte(c, 4) << 8) | pbyte(c, 5);
-            // seq0 is read after the prefix's L4 checksum field was zeroed
-            // (:149 before :152-154), which matters when the two overlap.
-            c.seq0 = 0;
-            if (c.tcp) {
-                for (uint32_t k = 0; k < 4; k++) {
-                    const uint32_t j = c.cs + 4 + k;
-                    const uint32_t bb = (j == c.l4off || j == c.l4off + 1) ? 0u : pbyte(c, j);
-                    c.seq0 |= bb << (8u * (3u - k));
-                }
-            }
-            hdr_bases(c, lane);
-            pl.hdr_len = (uint16_t)c.hdr_len;
-            pl.cs = (uint16_t)c.cs;
-            pl.l4off = (uint16_t)c.l4off;
-            pl.kind = (uint8_t)(kPlanSplit | (c.v6 ? kPlanV6 : 0u) | (c.tcp ? kPlanTcp : 0u));
-            pl.flags13 = (uint8_t)c.flags13;
-            pl.gso = (uint16_t)c.gso;
-            pl.nseg = (uint16_t)c.nseg;
-            pl.id0 = (uint16_t)c.id0;
-            pl.ip_base = (uint16_t)fold16_32(c.ip_base);
-            pl.l4h_base = (uint16_t)fold16_32(c.l4h_base);
-            pl.ps_sum = (uint16_t)fold16_32(c.ps_sum);
-            pl.seq0 = c.seq0;
-        } else if (cl.inplace) {
-            c.tcp = (cl.isv6 ? pbyte(c, 6) : pbyte(c, 9)) == 6;  // :67-70
-            do_inplace(c, lane);
+    const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
+    const uint64_t stride = (uint64_t)gridDim.x * 4u * PB;
+    for (uint64_t b0 = ((uint64_t)blockIdx.x * 4u + wave_in_block()) * PB; b0 < p.n; b0 += stride) {
+        wg_gso_desc dsc[PB];
+        Ctx c[PB];
+#pragma unroll
+        for (int k = 0; k < PB; k++)
+            dsc[k] = sload(&p.desc[b0 + k < p.n ? b0 + k : p.n - 1]);
+#pragma unroll
+        for (int k = 0; k < PB; k++) {
+            const uintptr_t in = reinterpret_cast<uintptr_t>(p.in) + dsc[k].in_offset;
+            const uint32_t L = dsc[k].in_len;
+            c[k].hb0 = ld8(L ? in + (lane < L ? lane : 0u) : zero);
+            c[k].hb1 = ld8(L ? in + (lane + 64 < L ? lane + 64 : 0u) : zero);
         }
-        if (lane == 0)
-            reinterpret_cast<GsoPlan *>(p.res)[b] = pl;
+#pragma unroll
+        for (int k = 0; k < PB; k++) {
+            const uint64_t b = b0 + k;
+            if (b >= p.n)
+                break;
+            Ctx &cc = c[k];
+            const Cls cl = classify<true, true>(dsc[k], reinterpret_cast<uintptr_t>(p.in), cc);
+            GsoPlan pl{};
+            if (!cl.pass) {
+                cc.id0 = (pbyte(cc, 4) << 8) | pbyte(cc, 5);
+                // seq0 is read after the prefix's L4 checksum field was zeroed
+                // (:149 before :152-154), which matters when the two overlap.
+                cc.seq0 = 0;
+                if (cc.tcp) {
+                    for (uint32_t q = 0; q < 4; q++) {
+                        const uint32_t j = cc.cs + 4 + q;
+                        const uint32_t bb = (j == cc.l4off || j == cc.l4off + 1) ? 0u : pbyte(cc, j);
+                        cc.seq0 |= bb << (8u * (3u - q));
+                    }
+                }
+                hdr_bases(cc, lane);
+                pl.hdr_len = (uint16_t)cc.hdr_len;
+                pl.cs = (uint16_t)cc.cs;
+                pl.l4off = (uint16_t)cc.l4off;
+                pl.kind = (uint8_t)(kPlanSplit | (cc.v6 ? kPlanV6 : 0u) | (cc.tcp ? kPlanTcp : 0u));
+                pl.flags13 = (uint8_t)cc.flags13;
+                pl.gso = (uint16_t)cc.gso;
+                pl.nseg = (uint16_t)cc.nseg;
+                pl.id0 = (uint16_t)cc.id0;
+                pl.ip_base = (uint16_t)fold16_32(cc.ip_base);
+                pl.l4h_base = (uint16_t)fold16_32(cc.l4h_base);
+                pl.ps_sum = (uint16_t)fold16_32(cc.ps_sum);
+                pl.seq0 = cc.seq0;
+            } else if (cl.inplace) {
+                cc.tcp = (cl.isv6 ? pbyte(cc, 6) : pbyte(cc, 9)) == 6;  // :67-70
+                do_inplace(cc, lane);
+            }
+            if (lane == 0)
+                reinterpret_cast<GsoPlan *>(p.res)[b] = pl;
+        }
     }
 }
 
@@ -429,7 +448,7 @@ extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64
     GsoParams p{dev_in, dev_desc, n, dev_out, dev_res, t.gso_groups};
     hipStream_t st = static_cast<hipStream_t>(stream);
     // 1. plans (into dev_res) + in-place checksums of GSO_NONE + NEEDS_CSUM
-    const uint64_t ib = (n + 3) / 4;
+    const uint64_t ib = (n + 15) / 16;  // 4 waves x 4 super-buffers per block
     hipLaunchKernelGGL(gso_plan_kernel, dim3((unsigned)(ib < 65536 ? ib : 65536)), dim3(256), 0, st, p);
     // 2. the split
     const uint64_t units = n * t.gso_groups;

@@ -207,7 +207,10 @@ __device__ __forceinline__ uint32_t ldb(const Ctx &c, uint32_t j) {
         return ld8(c.in + j);
 }
 
-template <bool kUniform>
+// kPreloaded (with kUniform): the caller has already loaded c.hb0 / c.hb1
+// (prefix bytes lane, lane + 64, as below), so several super-buffers'
+// prefix loads can be in flight at once.
+template <bool kUniform, bool kPreloaded = false>
 __device__ __forceinline__ Cls classify(const wg_gso_desc &dsc, uintptr_t in_base, Ctx &c) {
     c.in = in_base + dsc.in_offset;
     c.in_len = dsc.in_len;
@@ -224,7 +227,7 @@ __device__ __forceinline__ Cls classify(const wg_gso_desc &dsc, uintptr_t in_bas
         r.status = -3;
         return r;
     }
-    if constexpr (kUniform) {
+    if constexpr (kUniform && !kPreloaded) {
         // the whole wave loads prefix bytes 0-127 at once; every byte the
         // classification and the header work need is then a readlane
         const uint32_t lane = lane_id();
