@@ -141,11 +141,20 @@ def test_oracle_verify_desc_matches_scalar():
         assert (verdict[i], l4[i]) == V.verify(p)
 
 
+VERIFY_VARIANTS = [{"verify_dm": 0, "verify_occ": 8}, {"verify_dm": 0, "verify_occ": 0},
+                   {"verify_dm": 2, "verify_occ": 6, "l4_iters": 4}, {"verify_dm": 2, "verify_occ": 0, "l4_iters": 3}]
+
+
 @pytest.mark.gpu
-def test_gpu_verify_parity(gpu):
+@pytest.mark.parametrize("knobs", VERIFY_VARIANTS, ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()))
+def test_gpu_verify_parity(gpu, knobs):
     import torch
 
     import wireglider_amd as wga
+
+    saved = {k: wga.tune_get(k) for k in knobs}
+    for k, v in knobs.items():
+        wga.tune_set(k, v)
 
     rng = np.random.default_rng(11)
     pkts = random_verify_batch(rng, 20000)
@@ -154,6 +163,8 @@ def test_gpu_verify_parity(gpu):
     dd = torch.from_numpy(d.view(np.int64).reshape(-1, 2).copy()).to(gpu)
     verdict, l4 = wga.verify_desc(dbuf, dd)
     torch.cuda.synchronize()
+    for k, v in saved.items():
+        wga.tune_set(k, v)
     ev, el4 = oracle.verify_desc(buf, d)
     np.testing.assert_array_equal(verdict.cpu().numpy(), ev)
     np.testing.assert_array_equal(l4.cpu().numpy(), el4)

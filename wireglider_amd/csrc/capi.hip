@@ -47,6 +47,7 @@ Tune &tune_mut() {
         x.gso_spw = (uint32_t)env_u64("WG_GSO_SPW", 1);
         x.gso_groups = (uint32_t)env_u64("WG_GSO_GROUPS", 1);
         x.verify_occ = (uint32_t)env_u64("WG_VERIFY_OCC", 8);
+        x.verify_dm = (uint32_t)env_u64("WG_VERIFY_DM", 0);
         x.gro_lds = (uint32_t)env_u64("WG_GRO_LDS", 1);
         x.gro_wide = (uint32_t)env_u64("WG_GRO_WIDE", 1);
         x.gso_ablate = 0;
@@ -238,7 +239,9 @@ extern "C" int wg_tune_set(const char *key, uint64_t value) {
         t.gro_lds = (uint32_t)value;
     else if (k == "gro_wide" && value <= 1)
         t.gro_wide = (uint32_t)value;
-    else if (k == "verify_occ" && (value == 0 || value == 8))
+    else if (k == "verify_dm" && (value == 0 || value == 2))
+        t.verify_dm = (uint32_t)value;
+    else if (k == "verify_occ" && (value == 0 || value == 6 || value == 8))
         t.verify_occ = (uint32_t)value;
     else if (k == "gso_groups" && value >= 1 && value <= 64)
         t.gso_groups = (uint32_t)value;
@@ -272,6 +275,7 @@ extern "C" int wg_tune_get(const char *key, uint64_t *value) {
     else if (k == "gso_spw") *value = t.gso_spw;
     else if (k == "gso_groups") *value = t.gso_groups;
     else if (k == "verify_occ") *value = t.verify_occ;
+    else if (k == "verify_dm") *value = t.verify_dm;
     else if (k == "gro_lds") *value = t.gro_lds;
     else if (k == "gro_wide") *value = t.gro_wide;
     else if (k == "gso_ablate") *value = t.gso_ablate;

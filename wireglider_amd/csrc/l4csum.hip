@@ -232,16 +232,36 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t j) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
 }
 
-template <int P, int O = 0>  // O: waves/SIMD target (0 = compiler's choice)
+template <int P, int O = 0, int DM = 0>  // O: waves/SIMD target (0 = compiler's choice); DM: descriptor mode 0 / 2
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_kernel(
     VerifyParams p) {
     const uint32_t lane = lane_id();
-    const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
-    const uint64_t i0 = wave * P;
-    if (i0 >= p.n)
-        return;
+    const uint64_t wave0 = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
+    const uint64_t step = (uint64_t)gridDim.x * 4u * P;
     const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
+    // DM 2 (as the descriptor-batch L4 kernel): the next iteration's
+    // descriptors by one vector load, in flight during this one's finish.
+    // DM 0: one iteration per wave (the launcher covers the batch).
+    v4u nextd = v4u{0, 0, 0, 0};
+    bool have_next = false;
+    for (uint64_t i0 = wave0 * P; i0 < p.n; i0 += step) {
     uint32_t len[P], hv[P];
+    uint64_t doff[P];
+    if (DM == 2 && have_next) {
+#pragma unroll
+        for (int j = 0; j < P; j++) {
+            doff[j] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)nextd.x, j) |
+                      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)nextd.y, j) << 32);
+            len[j] = i0 + j < p.n ? (uint32_t)__builtin_amdgcn_readlane((int)nextd.z, j) : 0u;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < P; j++) {
+            const wg_pkt_desc d = p.desc[i0 + j < p.n ? i0 + j : p.n - 1];
+            doff[j] = d.offset;
+            len[j] = i0 + j < p.n ? d.len : 0u;
+        }
+    }
     Geom g[P];
     Front f[P];
     // ISSUE, before any header is decoded: header bytes 0-39 one per lane,
@@ -252,17 +272,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
     // read lies inside the descriptor's packet.)
 #pragma unroll
     for (int j = 0; j < P; j++) {
-        const uint64_t i = i0 + j < p.n ? i0 + j : p.n - 1;
-        const wg_pkt_desc d = p.desc[i];
-        const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + d.offset;
-        len[j] = i0 + j < p.n ? d.len : 0u;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + doff[j];
         const uint32_t hl = len[j] < 40u ? len[j] : 40u;
-        hv[j] = ld8(lane < hl ? a + lane : (hl ? a : zero));
+        hv[j] = ld8(hl ? a + (lane < hl ? lane : 0u) : zero);
         g[j].a = a;
         g[j].len = len[j] <= 65535u ? len[j] : 0u;  // longer packets fail the size gate (evaluator.hpp:118-121)
         g[j].cs = 40;
         g[j].fl = 0;
         issue<false, true>(g[j], lane, f[j]);
+    }
+    if constexpr (DM == 2) {
+        have_next = i0 + step < p.n;
+        const uint64_t di = (have_next ? i0 + step : i0) + (lane & (uint32_t)(P - 1));
+        nextd = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (di < p.n ? di : p.n - 1));
     }
     // decode (wave-uniform) and finish every packet
     uint32_t rv = 0, rc = 0;
@@ -330,6 +352,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
         if (p.l4)
             p.l4[i0 + lane] = (uint16_t)rc;
     }
+    if constexpr (DM == 0)
+        break;
+    }
 }
 
 }  // namespace wg
@@ -343,13 +368,26 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
     if (!dev_base || !dev_desc || !dev_verdict || (reinterpret_cast<uintptr_t>(dev_desc) & 15))
         return WG_ERR_INVALID;
     VerifyParams p{dev_base, dev_desc, dev_verdict, dev_l4, n};
+    const Tune &t = tune();
+    const bool pf = t.verify_dm == 2;
     uint64_t blocks = (n + 15) / 16;
-    if (blocks >= 8)
-        blocks = (blocks + 7) & ~7ull;
-    if (tune().verify_occ == 8)
-        hipLaunchKernelGGL((verify_kernel<4, 8>), dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), p);
+    if (pf) {
+        blocks = (blocks + t.l4_iters - 1) / t.l4_iters;
+        if (blocks >= 8)
+            blocks &= ~7ull;  // XCD swizzle bijective; the grid-stride loop covers the rest
+    } else if (blocks >= 8) {
+        blocks = (blocks + 7) & ~7ull;  // one iteration per wave: round up
+    }
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const dim3 grid((unsigned)blocks);
+    if (pf && t.verify_occ == 6)
+        hipLaunchKernelGGL((verify_kernel<4, 6, 2>), grid, dim3(256), 0, st, p);
+    else if (pf)
+        hipLaunchKernelGGL((verify_kernel<4, 0, 2>), grid, dim3(256), 0, st, p);
+    else if (t.verify_occ == 8)
+        hipLaunchKernelGGL((verify_kernel<4, 8, 0>), grid, dim3(256), 0, st, p);
     else
-        hipLaunchKernelGGL((verify_kernel<4>), dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), p);
+        hipLaunchKernelGGL((verify_kernel<4, 0, 0>), grid, dim3(256), 0, st, p);
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }
 
