@@ -158,6 +158,28 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
         def launch():
             wga.gso_split(buf, d_desc, outb, results=res)
 
+        def post():
+            # size-independent properties over the whole output: every status
+            # 0 with the expected geometry, and every segment's IPv4 header and
+            # L4 checksum verify to 0 (wg_checksum_desc / wg_l4csum_desc)
+            r = res.cpu().numpy().view(wga.GSO_RESULT_DTYPE)
+            geom_bad = int(np.count_nonzero((r["status"] != 0) | (r["out_len"] != out_len)
+                                            | (r["segment_size"] != 40 + gso)))
+            sd = np.zeros(n * nseg, dtype=wga.PKT_DESC_DTYPE)
+            base = (gd["out_offset"][:, None] + np.arange(nseg, dtype=np.uint64)[None, :] * np.uint64(40 + gso))
+            sd["offset"] = base.reshape(-1)
+            lens = np.full((n, nseg), 40 + gso, np.uint32)
+            lens[:, -1] = out_len - (nseg - 1) * (40 + gso)
+            sd["len"], sd["csum_start"], sd["flags"] = lens.reshape(-1), 20, 2
+            d_sd = torch.from_numpy(sd.view(np.uint8)).to(dev)
+            l4 = wga.calc_l4_checksum_desc(outb, d_sd)
+            sd["len"] = 20
+            ipc = wga.checksum_desc(outb, torch.from_numpy(sd.view(np.uint8)).to(dev))
+            torch.cuda.synchronize()
+            return {"result_geometry_mismatches": geom_bad, "segments_checked": int(n * nseg),
+                    "l4_verify_nonzero": int(torch.count_nonzero(l4.to(torch.int32)).item()),
+                    "ipv4_header_verify_nonzero": int(torch.count_nonzero(ipc.to(torch.int32)).item())}
+
         def sample(_npk):
             # 4,096 super-buffers (268 MB in, 300 MB out: past the host L3),
             # their GPU output and their descriptors rebased to the sample
@@ -173,7 +195,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
         alg = n * in_len + n * out_len + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES)
         return Workload(launch, n, n * in_len, alg, cfg, "weak", buf,
                         "wg::gso_plan_kernel + wg::gso_split_kernel<4,1,0> + wg::gso_finalize_kernel (one wg_gso_split call)",
-                        rank * n, sample=sample, counts=[n] * world)
+                        rank * n, sample=sample, counts=[n] * world, post=post)
     if name == "verify":
         n = 1 << 20
         seed = 0x5EED00F1

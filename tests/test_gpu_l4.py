@@ -258,3 +258,33 @@ def test_results_deterministic_across_launches(gpu):
     b = wga.calc_l4_checksum_desc(buf, desc)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+def test_long_packets(gpu):
+    """Packets past the issue phase's 2 KiB (the finish phase's long-packet
+    loop), up to the 64 KiB maximum IP packet, at odd offsets, through the
+    descriptor, verify and uniform entry points."""
+    import torch
+
+    wga = _wga()
+    rng = np.random.default_rng(65535)
+    n = 600
+    lens = rng.integers(2000, 65536, n)
+    lens[:8] = [2047, 2048, 2049, 4095, 4096, 4097, 65534, 65535]
+    offs = np.cumsum(np.concatenate([[int(rng.integers(0, 16))], lens[:-1] + rng.integers(0, 7, n - 1)]))
+    buf = rng.integers(0, 256, int(offs[-1] + lens[-1] + 16), dtype=np.uint8)
+    d = np.zeros(n, dtype=oracle.PKT_DESC)
+    d["offset"], d["len"] = offs, lens
+    d["csum_start"] = rng.choice([20, 21, 40, 41, 1000], n)
+    d["flags"] = rng.integers(0, 4, n)
+    back, view = to_dev(buf, gpu, 3)
+    out = wga.calc_l4_checksum_desc(view, desc_dev(d, gpu))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), oracle.l4_desc(buf, d))
+    seg = 65535
+    total = seg * 5 - 777
+    u = rng.integers(0, 256, total, dtype=np.uint8)
+    back, view = to_dev(u, gpu, 5)
+    out = wga.calc_l4_checksum_batch(view, seg, True, True, 40)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), oracle.l4_uniform(u, seg, 40, 3))
