@@ -26,14 +26,16 @@ def _wga():
 
 
 @pytest.fixture(params=[{"gso_ablate": 0, "gso_groups": 1}, {"gso_ablate": 32, "gso_groups": 1},
-                        {"gso_groups": 3}, {"gso_groups": 12}, {"gso_groups": 5, "gso_waves": 8}],
-                ids=["swizzled", "launch-order", "groups3", "groups12", "groups5x8"])
+                        {"gso_groups": 3}, {"gso_groups": 12}, {"gso_groups": 5, "gso_waves": 8},
+                        {"gso_groups": 3, "gso_spw": 2}, {"gso_groups": 2, "gso_spw": 0}],
+                ids=["swizzled", "launch-order", "groups3", "groups12", "groups5x8", "groups3-pairs",
+                     "groups2-serial"])
 def variant(request):
     """Every correct block -> (super-buffer, segment slot) mapping of the GSO
     kernel: one looping block per super-buffer (XCD-swizzled or in launch
     order) and several blocks per super-buffer (flat grid groups)."""
     wga = _wga()
-    saved = {k: wga.tune_get(k) for k in ("gso_ablate", "gso_groups", "gso_waves")}
+    saved = {k: wga.tune_get(k) for k in ("gso_ablate", "gso_groups", "gso_waves", "gso_spw")}
     for k, v in request.param.items():
         wga.tune_set(k, v)
     yield request.param

@@ -38,14 +38,15 @@ Tune &tune_mut() {
         x.l4_occ = (uint32_t)env_u64("WG_L4_OCC", 0);
         x.l4_iters = (uint32_t)env_u64("WG_L4_ITERS", 4);
         x.gso_blocks = env_u64("WG_GSO_BLOCKS", 1u << 23);
-        // GSO: one 4-wave block per super-buffer, each wave a ping-pong
-        // pipeline (next segment's loads in flight while this one finishes);
-        // the verify kernel at 8 waves/SIMD (64 VGPRs, no spill)
-        // (tools/ab.py, profiles/r01_ab_*.json).
+        // GSO: three 4-wave blocks per super-buffer, each wave a ping-pong
+        // pipeline (next segment's loads in flight while this one finishes;
+        // 3 groups -2.5 % vs 1 on two boxes once the per-wave setup is one
+        // scalar round trip); the verify kernel at 8 waves/SIMD (64 VGPRs,
+        // no spill) (tools/ab.py, profiles/r01_ab_*.json).
         x.gso_waves = (uint32_t)env_u64("WG_GSO_WAVES", 4);
         x.gso_split = (uint32_t)env_u64("WG_GSO_SPLIT", 1);
         x.gso_spw = (uint32_t)env_u64("WG_GSO_SPW", 1);
-        x.gso_groups = (uint32_t)env_u64("WG_GSO_GROUPS", 1);
+        x.gso_groups = (uint32_t)env_u64("WG_GSO_GROUPS", 3);
         x.verify_occ = (uint32_t)env_u64("WG_VERIFY_OCC", 8);
         x.verify_dm = (uint32_t)env_u64("WG_VERIFY_DM", 0);
         x.gro_lds = (uint32_t)env_u64("WG_GRO_LDS", 1);

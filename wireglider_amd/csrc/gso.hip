@@ -71,6 +71,12 @@ struct GsoPlan {
 };
 static_assert(sizeof(GsoPlan) == sizeof(wg_gso_result), "plan lives in the result slot");
 enum : uint32_t { kPlanV6 = 1, kPlanTcp = 2, kPlanSplit = 0x80 };
+struct PlanRaw {  // GsoPlan as dwords (little-endian field order above)
+    uint32_t w[6];
+};
+struct DescRaw {  // wg_gso_desc dwords 0-4: in_offset, out_offset, in_len
+    uint32_t w[5];
+};
 
 // Wave-uniform record loads through the constant address space: s_load.
 template <typename T>
@@ -253,36 +259,46 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
     for (uint64_t u = u0; u < units; u += gridDim.x) {
         const uint64_t b = G == 1 ? u : u / G;
         const uint32_t gw = (blockIdx.y * G + (uint32_t)(u - b * G)) * W + wave_in_block();  // segment slot
-        const GsoPlan pl = sload(reinterpret_cast<const GsoPlan *>(p.res) + b);
-        if (!(pl.kind & kPlanSplit) || gw * kStep >= pl.nseg)
+        // plan and descriptor as raw dwords: one s_load each (16-bit struct
+        // fields would become dependent vector loads), unpacked by shifts
+        const DescRaw dr = sload(reinterpret_cast<const DescRaw *>(p.desc + b));  // first 20 B of the 40-B descriptor
+        const PlanRaw pr = sload(reinterpret_cast<const PlanRaw *>(p.res) + b);
+        // all eleven dwords in one scalar round trip: without this the
+        // compiler sinks each load below the first branch that needs it
+        // and chains three waits before the first payload load
+        asm volatile("" ::"s"(pr.w[0]), "s"(pr.w[1]), "s"(pr.w[2]), "s"(pr.w[3]), "s"(pr.w[4]), "s"(pr.w[5]),
+                     "s"(dr.w[0]), "s"(dr.w[1]), "s"(dr.w[2]), "s"(dr.w[3]), "s"(dr.w[4]));
+        const uint32_t kind = (pr.w[1] >> 16) & 0xffu, nseg = pr.w[2] >> 16;
+        if (!(kind & kPlanSplit) || gw * kStep >= nseg)
             continue;  // passthrough / error (gso_plan_kernel did any in-place work) or no segment for this slot
-        const uint64_t in_off = sload(&p.desc[b].in_offset), out_off = sload(&p.desc[b].out_offset);
-        const uint32_t in_len = sload(&p.desc[b].in_len);
+        const uint64_t in_off = (uint64_t)dr.w[0] | ((uint64_t)dr.w[1] << 32);
+        const uint64_t out_off = (uint64_t)dr.w[2] | ((uint64_t)dr.w[3] << 32);
+        const uint32_t in_len = dr.w[4];
         Ctx c;
         c.in = reinterpret_cast<uintptr_t>(p.in) + in_off;
         c.in_len = in_len;
-        c.hdr_len = pl.hdr_len;
-        c.cs = pl.cs;
-        c.l4off = pl.l4off;
-        c.gso = pl.gso;
-        c.nseg = pl.nseg;
-        c.rest = in_len - pl.hdr_len;
-        c.v6 = pl.kind & kPlanV6;
-        c.tcp = pl.kind & kPlanTcp;
-        c.id0 = pl.id0;
-        c.seq0 = pl.seq0;
-        c.ip_base = pl.ip_base;
-        c.l4h_base = pl.l4h_base;
-        c.ps_sum = pl.ps_sum;
-        c.flags13 = pl.flags13;
+        c.hdr_len = pr.w[0] & 0xffffu;
+        c.cs = pr.w[0] >> 16;
+        c.l4off = pr.w[1] & 0xffffu;
+        c.gso = pr.w[2] & 0xffffu;
+        c.nseg = nseg;
+        c.rest = in_len - c.hdr_len;
+        c.v6 = kind & kPlanV6;
+        c.tcp = kind & kPlanTcp;
+        c.id0 = pr.w[3] & 0xffffu;
+        c.seq0 = pr.w[5];
+        c.ip_base = pr.w[3] >> 16;
+        c.l4h_base = pr.w[4] & 0xffffu;
+        c.ps_sum = pr.w[4] >> 16;
+        c.flags13 = pr.w[1] >> 24;
         // this lane's template bytes (used when the first header is written)
         // and field codes
         c.hb0 = ld8(c.in + (lane < c.hdr_len ? lane : 0u));
         c.hb1 = ld8(c.in + (lane + 64 < c.hdr_len ? lane + 64 : 0u));
-        c.hc0 = hdr_code(c, lane);
-        c.hc1 = hdr_code(c, lane + 64);
         const uintptr_t out_base = reinterpret_cast<uintptr_t>(p.out) + out_off;
         if constexpr (S == 0) {
+            c.hc0 = hdr_code(c, lane);
+            c.hc1 = hdr_code(c, lane + 64);
             for (uint32_t i = gw; i < c.nseg; i += gstride) {
                 SegFront A;
                 seg_issue<Abl>(c, out_base, i, lane, A);
@@ -293,6 +309,10 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
             uint32_t i = gw;
             SegFront A, B;
             seg_issue<Abl>(c, out_base, i, lane, A);
+            // the header field codes are needed only when the first header is
+            // written: computed while the first segment's loads are in flight
+            c.hc0 = hdr_code(c, lane);
+            c.hc1 = hdr_code(c, lane + 64);
             if (i + gstride > last) {  // the slot's only segment: no second slot to fill
                 seg_finish<Abl>(c, out_base, A, lane);
                 continue;
@@ -311,6 +331,8 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
                 i = i2;
             }
         } else {
+            c.hc0 = hdr_code(c, lane);
+            c.hc1 = hdr_code(c, lane + 64);
             for (uint32_t i0 = gw * S; i0 < c.nseg; i0 += gstride) {
                 SegFront f[S];
 #pragma unroll
