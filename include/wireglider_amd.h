@@ -247,7 +247,7 @@ int wg_device_count(void);
  * WG_L4_PPW, WG_L4_NT, WG_GSO_BLOCKS).  Keys: "l4_blocks" (grid cap),
  * "l4_ppw" (packets per wave iteration: 1, 2, 4, 8), "l4_nt" (0/1
  * non-temporal loads), "l4_descv" (0/1: descriptors by one vector load per
- * wave instead of scalar loads), "gso_blocks", "gso_waves" (waves per block: 4, 8, 16),
+ * wave instead of scalar loads), "gso_blocks", "gso_waves" (waves per block: 1, 2, 4, 8),
  * "gso_split" (blocks per super-buffer, 1-64), "gso_spw" (1: ping-pong pipeline of segments per wave,
  * 2: two segments issued then finished), "gso_ablate"
  * (profiling only: 1 = non-temporal payload stores; 2..7 select timing-only

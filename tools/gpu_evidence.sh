@@ -1,6 +1,6 @@
 #!/bin/bash
-# One GPU-box session: the whole -m gpu suite, bench lines for configs 3/4/5 and
-# the verify gates, rocprofv3 kernel stats and PMC HBM traffic for config 3 and
+# One GPU-box session: the whole -m gpu suite, smoke(), the default bench line
+# (config 2), bench lines for configs 3/4/5, the verify gates and GRO finalize, rocprofv3 kernel stats and PMC HBM traffic for config 3 and
 # verify.  Each GPU step has its own time limit; the first failure ends it.
 # usage: tools/gpu_evidence.sh [outdir-name]
 set -u
@@ -9,7 +9,10 @@ O=$(pwd)/gpurun_out/${1:-evidence}; mkdir -p $O
 export TMPDIR=/tmp
 ROOT=$(pwd)
 timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > $O/pytest.log 2>&1; rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
-for W in config3 verify config5 config4; do
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
+timeout -k 10 300 python3 bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail $O/bench_default.err; exit 1; }
+cat $O/bench_default.json
+for W in config3 verify config5 config4 gro; do
   timeout -k 10 300 python3 bench.py --workload $W --steps 30 > $O/bench_$W.json 2> $O/bench_$W.err || { tail $O/bench_$W.err; exit 1; }
   cat $O/bench_$W.json
 done

@@ -246,7 +246,7 @@ extern "C" int wg_tune_set(const char *key, uint64_t value) {
         t.verify_occ = (uint32_t)value;
     else if (k == "gso_groups" && value >= 1 && value <= 64)
         t.gso_groups = (uint32_t)value;
-    else if (k == "gso_waves" && (value == 4 || value == 8))
+    else if (k == "gso_waves" && (value == 1 || value == 2 || value == 4 || value == 8))
         t.gso_waves = (uint32_t)value;
     else if (k == "gso_split" && value >= 1 && value <= 64)
         t.gso_split = (uint32_t)value;

@@ -242,9 +242,9 @@ __device__ __forceinline__ void seg_finish(const Ctx &c, uintptr_t out_base, con
 // group u % G of super-buffer u / G, so the G blocks of one super-buffer are
 // consecutive in dispatch order (and, after the XCD swizzle, on one XCD).
 // Group g's waves take segment slots g*W .. g*W+W-1 of the super-buffer
-// (stride G*W); blockIdx.y (grid y) further splits the slots.  G = 1 (one
-// looping block per super-buffer) measured best; more groups mean shorter
-// waves but every wave pays the classification again.
+// (stride G*W); blockIdx.y (grid y) further splits the slots.  More groups
+// mean shorter waves, each paying the per-wave setup (plan + descriptor,
+// template bytes, field codes) again: G = 3 x W = 4 measured best.
 // S = segments per wave step: 0 one at a time (occupancy hides latency),
 // 1 ping-pong pipeline (the next segment's loads in flight while this one
 // finishes), 2 two issued then both finished.
@@ -454,6 +454,8 @@ using namespace wg;
 template <int S, int Abl>
 static void launch_split(const GsoParams &p, dim3 g, uint32_t waves, hipStream_t st) {
     switch (waves) {
+    case 1: hipLaunchKernelGGL((gso_split_kernel<1, S, Abl>), g, dim3(64), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((gso_split_kernel<2, S, Abl>), g, dim3(128), 0, st, p); break;
     case 8: hipLaunchKernelGGL((gso_split_kernel<8, S, Abl>), g, dim3(512), 0, st, p); break;
     default: hipLaunchKernelGGL((gso_split_kernel<4, S, Abl>), g, dim3(256), 0, st, p); break;
     }

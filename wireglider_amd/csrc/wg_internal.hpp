@@ -16,7 +16,7 @@ struct Tune {
     uint32_t l4_iters;    // iterations per wave in descriptor mode 2
     uint32_t l4_occ;      // waves/SIMD target of the L4 kernels at 4 packets/wave (0 = compiler's choice; 7, 8)
     uint64_t gso_blocks;  // grid cap for the GSO split kernel (one block per super-buffer)
-    uint32_t gso_waves;   // waves per block (4, 8)
+    uint32_t gso_waves;   // waves per block (1, 2, 4, 8)
     uint32_t gso_split;   // blocks per super-buffer (grid y)
     uint32_t gso_groups;  // blocks per super-buffer, consecutive in the flat grid (one-shot waves)
     uint32_t gso_spw;     // segments per wave step: 0 one at a time, 1 ping-pong pipeline, 2 pairs
