@@ -243,19 +243,31 @@ const char *wg_strerror(int code);
 /* HIP device count (0 when no GPU); never throws. */
 int wg_device_count(void);
 
-/* Launch-geometry knobs (also read once from the environment as WG_L4_BLOCKS,
- * WG_L4_PPW, WG_L4_NT, WG_GSO_BLOCKS).  Keys: "l4_blocks" (grid cap),
- * "l4_ppw" (packets per wave iteration: 1, 2, 4, 8), "l4_nt" (0/1
- * non-temporal loads), "l4_descv" (0/1: descriptors by one vector load per
- * wave instead of scalar loads), "gso_blocks", "gso_waves" (waves per block: 1, 2, 4, 8),
- * "gso_split" (blocks per super-buffer, 1-64), "gso_spw" (1: ping-pong pipeline of segments per wave,
- * 2: two segments issued then finished), "gso_ablate"
- * (profiling only: 1 = non-temporal payload stores; 2..7 select timing-only
- * GSO variants whose output is WRONG; 0 restores the default kernel).  Results never depend on the geometry
- * knobs.  Not synchronised with concurrent launches from other threads.
- * Also: "gso_groups" (1-64: blocks per super-buffer, consecutive in a flat
- * grid, so the waves of one super-buffer are short-lived and neighbours in
- * dispatch order). */
+/* Launch-geometry knobs.  Each key is also read once, at the first launch,
+ * from the environment as WG_<KEY> (e.g. WG_L4_PPW=2); the environment and
+ * wg_tune_set accept the same values and ignore / reject (WG_ERR_INVALID)
+ * anything else.  Results never depend on them (except "gso_ablate").
+ *   "l4_blocks"  grid cap of the L4 kernels (1 .. 2^20)
+ *   "l4_ppw"     packets per wave iteration (1, 2, 4, 8)
+ *   "l4_nt"      non-temporal packet loads (0, 1)
+ *   "l4_descv"   descriptor batches: 0 scalar loads, 1 one vector load per
+ *                iteration, 2 vector prefetch of the next iteration
+ *   "l4_iters"   iterations per wave in descriptor mode 2 (1 .. 64)
+ *   "l4_occ"     waves/SIMD target at 4 packets/wave (0 = compiler, 7, 8)
+ *   "gso_blocks" grid cap of the GSO split kernel (1 .. 2^23)
+ *   "gso_groups" blocks per super-buffer, consecutive in the flat grid (1 .. 64)
+ *   "gso_waves"  waves per GSO block (1, 2, 4, 8)
+ *   "gso_split"  further blocks per super-buffer in grid y (1 .. 64)
+ *   "gso_spw"    segments per wave step: 0 serial, 1 ping-pong, 2 pairs
+ *   "verify_dm"  verify descriptor mode: 0 one-shot waves, 2 prefetch
+ *   "verify_occ" verify waves/SIMD target (0 = compiler, 6, 8)
+ *   "verify_hdr" verify header bytes from the L4 byte gather (1) or a
+ *                separate byte load (0)
+ *   "gro_lds", "gro_wide"  GRO finalize: LDS-staged loads, wide field stores
+ *   "gso_ablate" profiling only: 1 = non-temporal payload stores, 32 = no XCD
+ *                swizzle (both correct); 2 = timing-only variant whose output
+ *                is WRONG; 0 restores the default kernel.
+ * Not synchronised with concurrent launches from other threads. */
 int wg_tune_set(const char *key, uint64_t value);
 /* Current value of a wg_tune_set key. */
 int wg_tune_get(const char *key, uint64_t *value);

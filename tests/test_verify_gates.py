@@ -141,7 +141,8 @@ def test_oracle_verify_desc_matches_scalar():
         assert (verdict[i], l4[i]) == V.verify(p)
 
 
-VERIFY_VARIANTS = [{"verify_dm": 0, "verify_occ": 8}, {"verify_dm": 0, "verify_occ": 0},
+VERIFY_VARIANTS = [{"verify_dm": 0, "verify_occ": 8, "verify_hdr": 1}, {"verify_dm": 0, "verify_occ": 0, "verify_hdr": 1},
+                   {"verify_dm": 0, "verify_occ": 8, "verify_hdr": 0}, {"verify_dm": 0, "verify_occ": 0, "verify_hdr": 0},
                    {"verify_dm": 2, "verify_occ": 6, "l4_iters": 4}, {"verify_dm": 2, "verify_occ": 0, "l4_iters": 3}]
 
 
@@ -169,3 +170,45 @@ def test_gpu_verify_parity(gpu, knobs):
     np.testing.assert_array_equal(verdict.cpu().numpy(), ev)
     np.testing.assert_array_equal(l4.cpu().numpy(), el4)
     assert (ev & OK == OK).mean() > 0.3 and (ev & OK != OK).mean() > 0.2  # both outcomes exercised
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("knobs", VERIFY_VARIANTS, ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()))
+def test_gpu_verify_size_gate(gpu, knobs):
+    """Packets at and past the 65535-byte size gate (evaluator.hpp:118-121):
+    the gate fails, but the V6 verdict bit still follows the version nibble;
+    mixed with maximum-size valid packets and short ones."""
+    import torch
+
+    import wireglider_amd as wga
+
+    rng = np.random.default_rng(12)
+    pkts = []
+    for v6 in (False, True):
+        for tcp in (False, True):
+            hl = (40 if v6 else 20) + (20 if tcp else 8)
+            al = 16 if v6 else 4
+            addr = lambda: rng.integers(0, 256, al, dtype=np.uint8).tobytes()  # noqa: E731
+            pay = lambda k: rng.integers(0, 256, k, dtype=np.uint8).tobytes()  # noqa: E731
+            big = pktbuild.build(v6, tcp, pay(65535 - hl), addr(), addr())  # exactly 65535 B: passes the gate
+            pkts.append(big)
+            for extra in (1, 4465, 70000 - 65535):  # past the gate
+                pkts.append(big + pay(extra))
+            small = pktbuild.build(v6, tcp, pay(1400), addr(), addr())
+            pkts += [small, small[:31], small[:33]]
+    buf, d = pack(pkts, rng)
+    saved = {k: wga.tune_get(k) for k in knobs}
+    for k, v in knobs.items():
+        wga.tune_set(k, v)
+    try:
+        verdict, l4 = wga.verify_desc(torch.from_numpy(buf).to(gpu),
+                                      torch.from_numpy(d.view(np.int64).reshape(-1, 2).copy()).to(gpu))
+        torch.cuda.synchronize()
+    finally:
+        for k, v in saved.items():
+            wga.tune_set(k, v)
+    ev, el4 = oracle.verify_desc(buf, d)
+    np.testing.assert_array_equal(verdict.cpu().numpy(), ev)
+    np.testing.assert_array_equal(l4.cpu().numpy(), el4)
+    assert np.count_nonzero(ev & V.V_V6) == sum(1 for p in pkts if p[0] >> 4 == 6)  # oversized v6 still report V6
+    assert (ev[0::7] & OK == OK).all()  # the 65535-byte packets pass

@@ -2,7 +2,9 @@
 // the host-memory path (tun / UDP buffers live in host memory).
 #include <hip/hip_runtime.h>
 
+#include <cctype>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <string>
 
@@ -12,13 +14,64 @@
 
 namespace wg {
 
-static uint64_t env_u64(const char *name, uint64_t dflt) {
-    const char *v = std::getenv(name);
-    if (!v || !*v)
-        return dflt;
-    char *end = nullptr;
-    unsigned long long x = std::strtoull(v, &end, 0);
-    return (end && *end == 0 && x > 0) ? (uint64_t)x : dflt;
+// One table of knobs: name, field, and the values it accepts.  Both the
+// environment (WG_<NAME>, read once) and wg_tune_set go through it, so a value
+// either is accepted by both or ignored / rejected by both.
+struct Knob {
+    const char *name;
+    uint64_t Tune::*f64;
+    uint32_t Tune::*f32;
+    uint64_t lo, hi;      // accepted range ...
+    const uint64_t *set;  // ... or, when non-null, one of these nset values
+    size_t nset;
+};
+
+static const uint64_t kPpw[] = {1, 2, 4, 8}, kOcc[] = {0, 7, 8}, kVOcc[] = {0, 6, 8}, kDm[] = {0, 2},
+                      kWaves[] = {1, 2, 4, 8}, kAbl[] = {0, 1, 2, 32};
+#define WG_N(a) (sizeof(a) / sizeof(a[0]))
+static const Knob kKnobs[] = {
+    {"l4_blocks", &Tune::l4_blocks, nullptr, 1, 1u << 20, nullptr, 0},
+    {"l4_ppw", nullptr, &Tune::l4_ppw, 0, 0, kPpw, WG_N(kPpw)},
+    {"l4_nt", nullptr, &Tune::l4_nt, 0, 1, nullptr, 0},
+    {"l4_descv", nullptr, &Tune::l4_descv, 0, 2, nullptr, 0},
+    {"l4_iters", nullptr, &Tune::l4_iters, 1, 64, nullptr, 0},
+    {"l4_occ", nullptr, &Tune::l4_occ, 0, 0, kOcc, WG_N(kOcc)},
+    {"gso_blocks", &Tune::gso_blocks, nullptr, 1, 1u << 23, nullptr, 0},
+    {"gso_waves", nullptr, &Tune::gso_waves, 0, 0, kWaves, WG_N(kWaves)},
+    {"gso_split", nullptr, &Tune::gso_split, 1, 64, nullptr, 0},
+    {"gso_groups", nullptr, &Tune::gso_groups, 1, 64, nullptr, 0},
+    {"gso_spw", nullptr, &Tune::gso_spw, 0, 2, nullptr, 0},
+    {"verify_dm", nullptr, &Tune::verify_dm, 0, 0, kDm, WG_N(kDm)},
+    {"verify_occ", nullptr, &Tune::verify_occ, 0, 0, kVOcc, WG_N(kVOcc)},
+    {"verify_hdr", nullptr, &Tune::verify_hdr, 0, 1, nullptr, 0},
+    {"gro_lds", nullptr, &Tune::gro_lds, 0, 1, nullptr, 0},
+    {"gro_wide", nullptr, &Tune::gro_wide, 0, 1, nullptr, 0},
+    {"gso_ablate", nullptr, &Tune::gso_ablate, 0, 0, kAbl, WG_N(kAbl)},
+};
+#undef WG_N
+
+static const Knob *find_knob(const char *key) {
+    for (const Knob &k : kKnobs)
+        if (std::strcmp(k.name, key) == 0)
+            return &k;
+    return nullptr;
+}
+
+static bool knob_set(Tune &t, const Knob &k, uint64_t v) {
+    bool ok = false;
+    if (k.set) {
+        for (size_t i = 0; i < k.nset; i++)
+            ok = ok || v == k.set[i];
+    } else {
+        ok = v >= k.lo && v <= k.hi;
+    }
+    if (!ok)
+        return false;
+    if (k.f64)
+        t.*(k.f64) = v;
+    else
+        t.*(k.f32) = (uint32_t)v;
+    return true;
 }
 
 Tune &tune_mut() {
@@ -28,30 +81,44 @@ Tune &tune_mut() {
         // wave (grid = n / (4 * ppw), i.e. no grid-stride loop), 4 packets per
         // wave, non-temporal loads: 7.26 TB/s vs 5.6 TB/s for a 2048-block
         // grid-stride launch with default-policy loads.
-        x.l4_blocks = env_u64("WG_L4_BLOCKS", 1u << 20);
-        x.l4_ppw = (uint32_t)env_u64("WG_L4_PPW", 4);
-        x.l4_nt = (uint32_t)env_u64("WG_L4_NT", 1);
+        x.l4_blocks = 1u << 20;
+        x.l4_ppw = 4;
+        x.l4_nt = 1;
         // Descriptor batches: each wave takes 4 iterations and prefetches the
         // next iteration's descriptors by one vector load during the current
         // one's finish (+3-5 % on config 5, profiles/r01_ab_session2.json).
-        x.l4_descv = (uint32_t)env_u64("WG_L4_DESCV", 2);
-        x.l4_occ = (uint32_t)env_u64("WG_L4_OCC", 0);
-        x.l4_iters = (uint32_t)env_u64("WG_L4_ITERS", 4);
-        x.gso_blocks = env_u64("WG_GSO_BLOCKS", 1u << 23);
+        x.l4_descv = 2;
+        x.l4_occ = 0;
+        x.l4_iters = 4;
+        x.gso_blocks = 1u << 23;
         // GSO: three 4-wave blocks per super-buffer, each wave a ping-pong
         // pipeline (next segment's loads in flight while this one finishes;
         // 3 groups -2.5 % vs 1 on two boxes once the per-wave setup is one
         // scalar round trip); the verify kernel at 8 waves/SIMD (64 VGPRs,
         // no spill) (tools/ab.py, profiles/r01_ab_*.json).
-        x.gso_waves = (uint32_t)env_u64("WG_GSO_WAVES", 4);
-        x.gso_split = (uint32_t)env_u64("WG_GSO_SPLIT", 1);
-        x.gso_spw = (uint32_t)env_u64("WG_GSO_SPW", 1);
-        x.gso_groups = (uint32_t)env_u64("WG_GSO_GROUPS", 3);
-        x.verify_occ = (uint32_t)env_u64("WG_VERIFY_OCC", 8);
-        x.verify_dm = (uint32_t)env_u64("WG_VERIFY_DM", 0);
-        x.gro_lds = (uint32_t)env_u64("WG_GRO_LDS", 1);
-        x.gro_wide = (uint32_t)env_u64("WG_GRO_WIDE", 1);
+        x.gso_waves = 4;
+        x.gso_split = 1;
+        x.gso_spw = 1;
+        x.gso_groups = 3;
+        x.verify_occ = 8;
+        x.verify_dm = 0;
+        x.verify_hdr = 1;
+        x.gro_lds = 1;
+        x.gro_wide = 1;
         x.gso_ablate = 0;
+        // environment overrides: WG_<KNOB> (upper case), same accepted values
+        // as wg_tune_set; anything else is ignored
+        for (const Knob &k : kKnobs) {
+            std::string env = "WG_";
+            for (const char *c = k.name; *c; c++) env += (char)std::toupper((unsigned char)*c);
+            const char *v = std::getenv(env.c_str());
+            if (!v || !*v)
+                continue;
+            char *end = nullptr;
+            const unsigned long long val = std::strtoull(v, &end, 0);
+            if (end && *end == 0)
+                knob_set(x, k, val);
+        }
         return x;
     }();
     return t;
@@ -218,69 +285,18 @@ extern "C" const char *wg_strerror(int code) {
 }
 
 extern "C" int wg_tune_set(const char *key, uint64_t value) {
-    if (!key)
-        return WG_ERR_INVALID;
-    Tune &t = tune_mut();
-    const std::string k(key);
-    if (k == "l4_blocks" && value >= 1 && value <= (1u << 20))
-        t.l4_blocks = value;
-    else if (k == "l4_ppw" && (value == 1 || value == 2 || value == 4 || value == 8))
-        t.l4_ppw = (uint32_t)value;
-    else if (k == "l4_nt" && value <= 1)
-        t.l4_nt = (uint32_t)value;
-    else if (k == "l4_iters" && value >= 1 && value <= 64)
-        t.l4_iters = (uint32_t)value;
-    else if (k == "l4_descv" && value <= 2)
-        t.l4_descv = (uint32_t)value;
-    else if (k == "l4_occ" && (value == 0 || value == 7 || value == 8))
-        t.l4_occ = (uint32_t)value;
-    else if (k == "gso_blocks" && value >= 1 && value <= (1u << 23))
-        t.gso_blocks = value;
-    else if (k == "gro_lds" && value <= 1)
-        t.gro_lds = (uint32_t)value;
-    else if (k == "gro_wide" && value <= 1)
-        t.gro_wide = (uint32_t)value;
-    else if (k == "verify_dm" && (value == 0 || value == 2))
-        t.verify_dm = (uint32_t)value;
-    else if (k == "verify_occ" && (value == 0 || value == 6 || value == 8))
-        t.verify_occ = (uint32_t)value;
-    else if (k == "gso_groups" && value >= 1 && value <= 64)
-        t.gso_groups = (uint32_t)value;
-    else if (k == "gso_waves" && (value == 1 || value == 2 || value == 4 || value == 8))
-        t.gso_waves = (uint32_t)value;
-    else if (k == "gso_split" && value >= 1 && value <= 64)
-        t.gso_split = (uint32_t)value;
-    else if (k == "gso_spw" && value <= 2)
-        t.gso_spw = (uint32_t)value;
-    else if (k == "gso_ablate" && (value <= 2 || value == 32))
-        t.gso_ablate = (uint32_t)value;
-    else
+    const Knob *k = key ? find_knob(key) : nullptr;
+    if (!k || !knob_set(tune_mut(), *k, value))
         return WG_ERR_INVALID;
     return WG_OK;
 }
 
 extern "C" int wg_tune_get(const char *key, uint64_t *value) {
-    if (!key || !value)
+    const Knob *k = key ? find_knob(key) : nullptr;
+    if (!k || !value)
         return WG_ERR_INVALID;
     const Tune &t = tune();
-    const std::string k(key);
-    if (k == "l4_blocks") *value = t.l4_blocks;
-    else if (k == "l4_ppw") *value = t.l4_ppw;
-    else if (k == "l4_nt") *value = t.l4_nt;
-    else if (k == "l4_descv") *value = t.l4_descv;
-    else if (k == "l4_occ") *value = t.l4_occ;
-    else if (k == "l4_iters") *value = t.l4_iters;
-    else if (k == "gso_blocks") *value = t.gso_blocks;
-    else if (k == "gso_waves") *value = t.gso_waves;
-    else if (k == "gso_split") *value = t.gso_split;
-    else if (k == "gso_spw") *value = t.gso_spw;
-    else if (k == "gso_groups") *value = t.gso_groups;
-    else if (k == "verify_occ") *value = t.verify_occ;
-    else if (k == "verify_dm") *value = t.verify_dm;
-    else if (k == "gro_lds") *value = t.gro_lds;
-    else if (k == "gro_wide") *value = t.gro_wide;
-    else if (k == "gso_ablate") *value = t.gso_ablate;
-    else return WG_ERR_INVALID;
+    *value = k->f64 ? t.*(k->f64) : (uint64_t)(t.*(k->f32));
     return WG_OK;
 }
 

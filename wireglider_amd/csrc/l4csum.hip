@@ -232,7 +232,10 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t j) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
 }
 
-template <int P, int O = 0, int DM = 0>  // O: waves/SIMD target (0 = compiler's choice); DM: descriptor mode 0 / 2
+// H: header bytes 0-31 ride in the L4 byte gather's idle lanes (issue<.., kHdr>)
+// and the summed region starts at byte 32 — no separate header load; else a
+// byte load of header bytes 0-39 per packet and the region from byte 40.
+template <int P, int O = 0, int DM = 0, bool H = false>  // O: waves/SIMD target (0 = compiler's choice); DM: descriptor mode 0 / 2
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_kernel(
     VerifyParams p) {
     const uint32_t lane = lane_id();
@@ -273,13 +276,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
 #pragma unroll
     for (int j = 0; j < P; j++) {
         const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + doff[j];
-        const uint32_t hl = len[j] < 40u ? len[j] : 40u;
-        hv[j] = ld8(hl ? a + (lane < hl ? lane : 0u) : zero);
         g[j].a = a;
-        g[j].len = len[j] <= 65535u ? len[j] : 0u;  // longer packets fail the size gate (evaluator.hpp:118-121)
-        g[j].cs = 40;
         g[j].fl = 0;
-        issue<false, true>(g[j], lane, f[j]);
+        if constexpr (H) {
+            // longer packets fail the size gate (evaluator.hpp:118-121): only
+            // their header bytes are read (region [32, 32) is empty)
+            g[j].len = len[j] <= 65535u ? len[j] : 32u;
+            g[j].cs = 32;
+            issue<false, true, true>(g[j], lane, f[j]);
+            hv[j] = f[j].hb;
+        } else {
+            const uint32_t hl = len[j] < 40u ? len[j] : 40u;
+            hv[j] = ld8(hl ? a + (lane < hl ? lane : 0u) : zero);
+            g[j].len = len[j] <= 65535u ? len[j] : 0u;
+            g[j].cs = 40;
+            issue<false, true>(g[j], lane, f[j]);
+        }
     }
     if constexpr (DM == 2) {
         have_next = i0 + step < p.n;
@@ -294,8 +306,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
         uint32_t v = 0;
         bool ip_ok = false, tcp = false, l4 = false, v6 = false;
         uint32_t ihs = 20, proto = 0;
-        // header byte `lane` in packet pairing (from byte 0)
-        const uint32_t hb = lane < L && lane < 40u ? hv[j] << (8u * (lane & 1u)) : 0u;
+        // header byte `lane` in packet pairing (from byte 0); zero from lane
+        // 32 (H) / 40 on and past the packet
+        constexpr uint32_t kHdrEnd = H ? 32u : 40u;
+        const uint32_t hb = lane < L && lane < kHdrEnd ? hv[j] << (8u * (lane & 1u)) : 0u;
         // IPv4 header sum over bytes 0-19
         const uint32_t hs = wave_sum_u32(lane < 20u ? hb : 0u);
         if (L >= 1) {
@@ -329,10 +343,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
             }
         }
         // calc_l4_checksum(pkt, isv6, istcp, ihs) (checksum.cpp:8-36): bytes
-        // [40, L) (issued above) + header bytes [ihs, 40) + the pseudo-header
-        // addresses (v4 12-19, v6 8-39), all in packet pairing — ihs and the
-        // address offsets are even, so that is the reference's pairing.
-        const bool inl4 = lane >= ihs;  // hb is zero from lane 40 on
+        // [E, L) (issued above; E = 32 or 40) + header bytes [ihs, E) + the
+        // pseudo-header addresses (v4 12-19, v6 8-39) below E, all in packet
+        // pairing — ihs, E and the address offsets are even, so that is the
+        // reference's pairing.  (v6 with E = 32: address bytes 32-39 are in
+        // the issued region, and its L4 region starts at 40: each counted once.)
+        const bool inl4 = lane >= ihs;  // hb is zero from lane E on
         const bool inps = v6 ? lane >= 8u : (lane >= 12u && lane < 20u);
         uint32_t s = wave_sum_u32(finish<true>(lane, f[j]) + (inl4 ? hb : 0u) + (inps ? hb : 0u));
         uint32_t c = 0;
@@ -380,7 +396,11 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
     }
     hipStream_t st = static_cast<hipStream_t>(stream);
     const dim3 grid((unsigned)blocks);
-    if (pf && t.verify_occ == 6)
+    if (!pf && t.verify_hdr && t.verify_occ == 8)
+        hipLaunchKernelGGL((verify_kernel<4, 8, 0, true>), grid, dim3(256), 0, st, p);
+    else if (!pf && t.verify_hdr)
+        hipLaunchKernelGGL((verify_kernel<4, 0, 0, true>), grid, dim3(256), 0, st, p);
+    else if (pf && t.verify_occ == 6)
         hipLaunchKernelGGL((verify_kernel<4, 6, 2>), grid, dim3(256), 0, st, p);
     else if (pf)
         hipLaunchKernelGGL((verify_kernel<4, 0, 2>), grid, dim3(256), 0, st, p);

@@ -6,7 +6,8 @@
 
 namespace wg {
 
-// Launch geometry, read once from the environment (WG_L4_BLOCKS, ...); the
+// Launch geometry, read once from the environment (WG_L4_BLOCKS, ...; the
+// accepted values are capi.hip's knob table, shared with wg_tune_set); the
 // defaults are the measured best on MI355X.
 struct Tune {
     uint64_t l4_blocks;   // grid cap for the wave-per-packet checksum kernels
@@ -22,6 +23,7 @@ struct Tune {
     uint32_t gso_spw;     // segments per wave step: 0 one at a time, 1 ping-pong pipeline, 2 pairs
     uint32_t verify_dm;   // verify kernel descriptor mode: 0 one-shot waves, 2 next-iteration prefetch (l4_iters)
     uint32_t verify_occ;  // waves/SIMD target of the verify kernel (0 = compiler's choice; 8)
+    uint32_t verify_hdr;  // 1: header bytes ride in the L4 byte gather (no separate header load)
     uint32_t gro_lds;     // 1: GRO finalize with LDS-staged cooperative header loads
     uint32_t gro_wide;    // 1: GRO finalize fields written by two wide stores (LDS variant)
     uint32_t gso_ablate;  // timing-only ablation bits (0 in production; non-zero = wrong output)

@@ -27,6 +27,7 @@ struct Front {
     v4u v0, v1;      // interior chunks lane, lane + 64 (masked to zero)
     uint32_t bv;     // gathered byte, already shifted to its pairing
     bool bt;         // bv is in TRUE pairing (pseudo-header address byte)
+    uint32_t hb;     // kHdr: packet byte `lane` (lanes 0-31), raw; else 0
     uintptr_t r0;    // start of the summed region
     uintptr_t c0;    // first aligned interior chunk
     uint32_t nint;   // interior chunk count
@@ -36,8 +37,12 @@ struct Front {
 // cs >= len).  Interior = whole aligned chunks [c0, c1); the unaligned head
 // [r0, min(c0, r1)) and tail [max(c1, c0), r1) are <= 15 bytes each.
 // Branch-free: out-of-range lanes re-read a valid chunk and are masked.
-template <bool kL4, bool kNT>
+// kHdr (plain sums only): the byte gather's otherwise idle lanes 0-31 bring
+// packet bytes 0-31 into f.hb (raw, not summed by finish) — the verify
+// kernel's header, with no extra load instruction.
+template <bool kL4, bool kNT, bool kHdr = false>
 __device__ __forceinline__ void issue(const Geom &g, uint32_t lane, Front &f) {
+    static_assert(!(kL4 && kHdr), "kHdr uses the pseudo-header lanes");
     const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
     const uintptr_t r1 = g.a + g.len;
     const uintptr_t r0 = g.cs < g.len ? g.a + g.cs : r1;
@@ -73,11 +78,13 @@ __device__ __forceinline__ void issue(const Geom &g, uint32_t lane, Front &f) {
     const uint32_t xh = cs0 + lane - 32u, xt = tso + lane - 48u;
     const bool bh = lane >= 32 && lane < 48 && xh < heo;
     const bool btl = lane >= 48 && xt < g.len;
-    const uint32_t off = bt ? ao + lane : (bh ? xh : (btl ? xt : 0u));
+    const bool bhd = kHdr && lane < 32u && lane < g.len;
+    const uint32_t off = bt ? ao + lane : (bh ? xh : (btl ? xt : (bhd ? lane : 0u)));
     const uint32_t par = bt ? (lane & 1u) : (((uint32_t)g.a + off) & 1u);
     const uint32_t byte = ld8((g.len ? g.a : zero) + off);
     f.bv = (bt || bh || btl) ? byte << (8u * par) : 0u;
     f.bt = bt;
+    f.hb = bhd ? byte : 0u;
 }
 
 // Finish phase: this lane's share of the packet's sum in TRUE pairing.
