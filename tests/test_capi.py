@@ -124,3 +124,44 @@ def test_dropin_header_compiles_and_matches_reference(tmp_path):
     exp = oracle.lib.orc_fold_complement(
         oracle.lib.orc_pseudo_header_nofold(17, src_b.ctypes.data, dst_b.ctypes.data, 4, 1480))
     assert int(p1) == exp
+
+
+def test_tune_knobs_validate_and_round_trip():
+    """wg_tune_set / wg_tune_get (host only): every documented key round
+    trips, out-of-range values are rejected and leave the knob unchanged."""
+    import wireglider_amd as wga
+
+    keys = re.findall(r'^ \*   "(\w+)"', HDR.read_text(), flags=re.M)
+    keys += re.findall(r'"(gro_wide)"', HDR.read_text())
+    assert {"l4_ppw", "gso_groups", "verify_hdr", "gro_lds", "gro_wide", "gso_ablate"} <= set(keys)
+    for k in keys:
+        v = wga.tune_get(k)
+        wga.tune_set(k, v)
+        assert wga.tune_get(k) == v
+    for k, bad in (("l4_ppw", 3), ("l4_occ", 6), ("gso_groups", 0), ("gso_groups", 65), ("verify_hdr", 2),
+                   ("gso_waves", 16), ("gso_ablate", 7)):
+        v = wga.tune_get(k)
+        with pytest.raises(Exception):
+            wga.tune_set(k, bad)
+        assert wga.tune_get(k) == v
+    with pytest.raises(Exception):
+        wga.tune_get("no_such_knob")
+    v = wga.tune_get("l4_nt")
+    wga.tune_set("l4_nt", 0)  # zero is a value, not "unset"
+    assert wga.tune_get("l4_nt") == 0
+    wga.tune_set("l4_nt", v)
+
+
+def test_tune_environment_overrides():
+    """WG_<KEY> is read once with the same validation: a valid value
+    (including 0) overrides the default, an invalid one is ignored."""
+    import os
+    import sys
+
+    code = ("import wireglider_amd as w; print(w.tune_get('l4_nt'), w.tune_get('gso_groups'), "
+            "w.tune_get('l4_ppw'), w.tune_get('verify_hdr'))")
+    env = dict(os.environ, WG_L4_NT="0", WG_GSO_GROUPS="5", WG_L4_PPW="3", WG_VERIFY_HDR="0x0")
+    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT, capture_output=True, text=True, check=True)
+    nt, groups, ppw, hdr = map(int, out.stdout.split())
+    assert (nt, groups, hdr) == (0, 5, 0)
+    assert ppw == 4  # 3 is not an accepted value: default kept
