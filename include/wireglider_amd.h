@@ -264,6 +264,8 @@ int wg_device_count(void);
  *   "verify_hdr" verify header bytes from the L4 byte gather (1) or a
  *                separate byte load (0)
  *   "gro_lds", "gro_wide"  GRO finalize: LDS-staged loads, wide field stores
+ *   "gro_chunks" 16-B header chunks staged per flow (4, 5; with 4, headers
+ *                over 48 bytes take the byte path)
  *   "gso_ablate" profiling only: 1 = non-temporal payload stores, 32 = no XCD
  *                swizzle (both correct); 2 = timing-only variant whose output
  *                is WRONG; 0 restores the default kernel.

@@ -150,15 +150,17 @@ def _oracle_batch(hdrs, desc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lds,wide", [(1, 1), (1, 0), (0, 0)], ids=["lds-wide", "lds-narrow", "thread-loads"])
-def test_gpu_gro_finalize_parity(gpu, lds, wide):
+@pytest.mark.parametrize("lds,wide,chunks", [(1, 1, 5), (1, 1, 4), (1, 0, 5), (0, 0, 5)],
+                         ids=["lds-wide", "lds-wide-4chunks", "lds-narrow", "thread-loads"])
+def test_gpu_gro_finalize_parity(gpu, lds, wide, chunks):
     import torch
 
     import wireglider_amd as wg
 
-    saved = {k: wg.tune_get(k) for k in ("gro_lds", "gro_wide")}
+    saved = {k: wg.tune_get(k) for k in ("gro_lds", "gro_wide", "gro_chunks")}
     wg.tune_set("gro_lds", lds)
     wg.tune_set("gro_wide", wide)
+    wg.tune_set("gro_chunks", chunks)
 
     rng = np.random.default_rng(2024)
     hdrs, desc = _batch(rng, 3000)

@@ -46,6 +46,7 @@ static const Knob kKnobs[] = {
     {"verify_hdr", nullptr, &Tune::verify_hdr, 0, 1, nullptr, 0},
     {"gro_lds", nullptr, &Tune::gro_lds, 0, 1, nullptr, 0},
     {"gro_wide", nullptr, &Tune::gro_wide, 0, 1, nullptr, 0},
+    {"gro_chunks", nullptr, &Tune::gro_chunks, 4, 5, nullptr, 0},
     {"gso_ablate", nullptr, &Tune::gso_ablate, 0, 0, kAbl, WG_N(kAbl)},
 };
 #undef WG_N
@@ -105,6 +106,7 @@ Tune &tune_mut() {
         x.verify_hdr = 1;
         x.gro_lds = 1;
         x.gro_wide = 1;
+        x.gro_chunks = 5;
         x.gso_ablate = 0;
         // environment overrides: WG_<KNOB> (upper case), same accepted values
         // as wg_tune_set; anything else is ignored

@@ -200,10 +200,22 @@ __global__ __launch_bounds__(256) void gro_finalize_kernel(uint8_t *hdrs, wg_gro
 // ones (thread-per-flow loads at a 64-B lane stride are address-processing
 // bound: about one cache line per cycle per CU).  The chunks go through LDS
 // to their flow's thread, which then runs the same arithmetic.
-constexpr uint32_t kGroBlock = 256, kGroChunks = 5;
+// K = chunks staged per flow: 5 covers every header the fast path takes (<= 64
+// bytes at any alignment); 4 covers <= 48 bytes (v6, v4 with up to 28 B of
+// options; longer go to the byte path) in 19 KB of LDS instead of 23 KB, i.e.
+// 8 resident blocks per CU instead of 6.
+constexpr uint32_t kGroBlock = 256;
+static __device__ v4u g_gro_zero;  // load target of slots with nothing to stage
 
-template <bool kWide>
+template <uint32_t K>
+__device__ __forceinline__ uint32_t flow_of_slot(uint32_t slot) {  // slot / K for slot < 256 * K
+    return K == 4 ? slot >> 2 : (slot * 52429u) >> 18;
+}
+
+template <bool kWide, uint32_t kGroChunks = 5>
 __global__ __launch_bounds__(kGroBlock) void gro_finalize_lds_kernel(uint8_t *hdrs, wg_gro_desc *desc, uint64_t n) {
+    static_assert(kGroChunks == 4 || kGroChunks == 5, "4 or 5 chunks per flow");
+    constexpr uint32_t kNeedMax = kGroChunks == 5 ? kFastNeed : 48u;
     __shared__ v4u s_chunk[kGroBlock * kGroChunks];
     __shared__ uint64_t s_a0[kGroBlock];
     __shared__ uint32_t s_last[kGroBlock];  // last chunk index to load, or 0xff: nothing to stage
@@ -227,22 +239,37 @@ __global__ __launch_bounds__(kGroBlock) void gro_finalize_lds_kernel(uint8_t *hd
             st = -3;
         else {
             need = v6 ? 40u : cs;
-            fast = need <= kFastNeed;
+            fast = need <= kNeedMax;
         }
     }
     const uintptr_t hp = reinterpret_cast<uintptr_t>(h);
     s_a0[t] = hp & ~(uintptr_t)15;
     s_last[t] = fast ? (uint32_t)(((hp & 15u) + need - 1) >> 4) : 0xffu;
     __syncthreads();
+    // All five loads issued before any is used, branch-free (slots of flows
+    // with nothing to stage read the zero chunk): a load inside `if` made the
+    // compiler wait for each before the next, five serial round trips.
+    uint32_t lst[kGroChunks];
+    uint64_t a0[kGroChunks];
+#pragma unroll
+    for (uint32_t k = 0; k < kGroChunks; k++) {  // every LDS read first (unconditional), then the loads
+        const uint32_t f = flow_of_slot<kGroChunks>(t + kGroBlock * k);
+        lst[k] = s_last[f];
+        a0[k] = s_a0[f];
+    }
+    v4u v[kGroChunks];
 #pragma unroll
     for (uint32_t k = 0; k < kGroChunks; k++) {
         const uint32_t slot = t + kGroBlock * k;
-        const uint32_t f = (slot * 52429u) >> 18;  // slot / 5 (slot < 1280)
-        const uint32_t c = slot - 5u * f;
-        const uint32_t last = s_last[f];
-        if (last != 0xffu)
-            s_chunk[slot] = ld16(s_a0[f] + 16u * (c < last ? c : last));
+        const uint32_t c = slot - kGroChunks * flow_of_slot<kGroChunks>(slot);
+        const uint32_t last = lst[k];
+        const uintptr_t a = last != 0xffu ? a0[k] + 16u * (c < last ? c : last)
+                                          : reinterpret_cast<uintptr_t>(&g_gro_zero);
+        v[k] = ld16(a);
     }
+#pragma unroll
+    for (uint32_t k = 0; k < kGroChunks; k++)
+        s_chunk[t + kGroBlock * k] = v[k];
     __syncthreads();
     if (!live)
         return;
@@ -252,7 +279,10 @@ __global__ __launch_bounds__(kGroBlock) void gro_finalize_lds_kernel(uint8_t *hd
             st_be16(h + cs + 4, (uint32_t)l4len);  // udp->len (uint16), :85-86
         if (fast) {
             const v4u *k = &s_chunk[t * kGroChunks];
-            gro_fields<kWide>(h, d, v6, tcp, l4len, k[0], k[1], k[2], k[3], k[4]);
+            // K = 4: header bytes >= 48 are never used (need <= 48; the
+            // v4 sum masks bytes >= csum_start), so chunk 4 may be zero
+            gro_fields<kWide>(h, d, v6, tcp, l4len, k[0], k[1], k[2], k[3],
+                              kGroChunks == 5 ? k[kGroChunks - 1] : v4u{0, 0, 0, 0});
         } else {
             gro_slow(h, d.hdr_len, cs, l4off, d.payload_bytes, v6, l4len);
         }
@@ -273,7 +303,10 @@ extern "C" int wg_gro_finalize(uint8_t *dev_hdrs, wg_gro_desc *dev_desc, uint64_
     const uint64_t blocks = (n + 255) / 256;
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
-    if (tune().gro_lds && tune().gro_wide)
+    if (tune().gro_lds && tune().gro_wide && tune().gro_chunks == 4)
+        hipLaunchKernelGGL((gro_finalize_lds_kernel<true, 4>), dim3((unsigned)blocks), dim3(kGroBlock), 0,
+                           static_cast<hipStream_t>(stream), dev_hdrs, dev_desc, n);
+    else if (tune().gro_lds && tune().gro_wide)
         hipLaunchKernelGGL(gro_finalize_lds_kernel<true>, dim3((unsigned)blocks), dim3(kGroBlock), 0,
                            static_cast<hipStream_t>(stream), dev_hdrs, dev_desc, n);
     else if (tune().gro_lds)

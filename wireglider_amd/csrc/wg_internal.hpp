@@ -26,6 +26,7 @@ struct Tune {
     uint32_t verify_hdr;  // 1: header bytes ride in the L4 byte gather (no separate header load)
     uint32_t gro_lds;     // 1: GRO finalize with LDS-staged cooperative header loads
     uint32_t gro_wide;    // 1: GRO finalize fields written by two wide stores (LDS variant)
+    uint32_t gro_chunks;  // 16-B chunks staged per flow by the LDS variant (4, 5)
     uint32_t gso_ablate;  // timing-only ablation bits (0 in production; non-zero = wrong output)
 };
 
