@@ -18,7 +18,8 @@
 // bytes in flight scale with resident waves, so everything per lane is a
 // 32-bit offset from a wave-uniform base, the per-segment header values are
 // looked up (v_writelane table + ds_bpermute) instead of selected, and the
-// GSO_NONE in-place checksum is a kernel of its own.
+// classification (plan pass) and the GSO_NONE in-place checksum (finalize
+// pass) are kernels of their own.
 #include <hip/hip_runtime.h>
 
 #include "wg_device.hpp"
@@ -62,15 +63,18 @@ __device__ __forceinline__ void st16x(uintptr_t addr, v4u v) {
 struct GsoPlan {
     uint16_t hdr_len, cs;
     uint16_t l4off;
-    uint8_t kind;  // bit 0 v6, bit 1 tcp (the unmasked :151 test), bit 7 split
-    uint8_t flags13;
+    uint8_t kind;     // kPlan* bits
+    uint8_t flags13;  // TCP flags byte of the prefix; -status when not split
     uint16_t gso, nseg;
     uint16_t id0, ip_base;  // sums folded to 16 bits (zero-preserving, congruent)
     uint16_t l4h_base, ps_sum;
     uint32_t seq0;
 };
 static_assert(sizeof(GsoPlan) == sizeof(wg_gso_result), "plan lives in the result slot");
-enum : uint32_t { kPlanV6 = 1, kPlanTcp = 2, kPlanSplit = 0x80 };
+// kind bits: the split-path family / protocol (v6, tcp: the unmasked :151
+// test), the classification's isv6 (:48) and ecn (bits 2-3), GSO_NONE +
+// NEEDS_CSUM in place, split.
+enum : uint32_t { kPlanV6 = 1, kPlanTcp = 2, kPlanEcnShift = 2, kPlanIsV6 = 0x10, kPlanInplace = 0x40, kPlanSplit = 0x80 };
 struct PlanRaw {  // GsoPlan as dwords (little-endian field order above)
     uint32_t w[6];
 };
@@ -270,7 +274,7 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
                      "s"(dr.w[0]), "s"(dr.w[1]), "s"(dr.w[2]), "s"(dr.w[3]), "s"(dr.w[4]));
         const uint32_t kind = (pr.w[1] >> 16) & 0xffu, nseg = pr.w[2] >> 16;
         if (!(kind & kPlanSplit) || gw * kStep >= nseg)
-            continue;  // passthrough / error (gso_plan_kernel did any in-place work) or no segment for this slot
+            continue;  // passthrough / error (in-place work: gso_finalize_kernel) or no segment for this slot
         const uint64_t in_off = (uint64_t)dr.w[0] | ((uint64_t)dr.w[1] << 32);
         const uint64_t out_off = (uint64_t)dr.w[2] | ((uint64_t)dr.w[3] << 32);
         const uint32_t in_len = dr.w[4];
@@ -347,103 +351,146 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
     }
 }
 
-// Plan pass, one wave per super-buffer: classification (:48-134), the
+// Plan pass, ONE THREAD per super-buffer: classification (:48-134), the
 // per-super-buffer fields (IPv4 id, TCP seq read after the :145-149 zeroing)
-// and the invariant header sums into the GsoPlan; GSO_NONE + NEEDS_CSUM
-// super-buffers get both checksums in place here (:56-78).
-__global__ __launch_bounds__(256) void gso_plan_kernel(GsoParams p) {
-    constexpr int PB = 4;  // super-buffers per wave step: their descriptor and prefix loads overlap
-    const uint32_t lane = lane_id();
-    const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
-    const uint64_t stride = (uint64_t)gridDim.x * 4u * PB;
-    for (uint64_t b0 = ((uint64_t)blockIdx.x * 4u + wave_in_block()) * PB; b0 < p.n; b0 += stride) {
-        wg_gso_desc dsc[PB];
-        Ctx c[PB];
+// and the invariant header sums into the GsoPlan.  This is scalar,
+// branchy work on a few dozen bytes; a thread does it for 64 super-buffers
+// per wave where a wave per super-buffer spent ~400 instructions of one
+// wave each (130 us for config 3, instruction-issue bound).  Each thread
+// stages its prefix (bytes [0, min(in_len, 128)), nine aligned 16-B chunks)
+// in its own LDS area, then reads bytes from there; bytes >= 128 (headers
+// past 128 bytes: rare) are loaded directly.  No barrier: a thread only
+// touches its own area.  GSO_NONE + NEEDS_CSUM super-buffers are marked
+// kPlanInplace; gso_finalize_kernel does their checksums (:56-78).
+constexpr uint32_t kPlanBlock = 256, kPreChunks = 9;
+constexpr uint32_t kPreStride = 4 * kPreChunks + 1;  // dwords per thread: odd, so threads' bytes spread over the banks
+
+__global__ __launch_bounds__(kPlanBlock) void gso_plan_kernel(GsoParams p) {
+    __shared__ uint32_t s_pre[kPlanBlock * kPreStride];
+    const uint32_t t = threadIdx.x;
+    const uint64_t b = (uint64_t)blockIdx.x * kPlanBlock + t;
+    if (b >= p.n)
+        return;
+    const wg_gso_desc dsc = p.desc[b];
+    const uintptr_t in = reinterpret_cast<uintptr_t>(p.in) + dsc.in_offset;
+    const uint32_t win = dsc.in_len < 128u ? dsc.in_len : 128u;  // staged bytes
+    const uint32_t o = (uint32_t)(in & 15u);
+    // branch-free: chunks past the window re-read its last chunk (an aligned
+    // 16-B chunk holding a byte of the buffer lies inside its page)
+    const uintptr_t base = win ? (in & ~(uintptr_t)15) : reinterpret_cast<uintptr_t>(&g_zero16);
+    const uint32_t last = win ? (o + win - 1u) >> 4 : 0u;
+    v4u ch[kPreChunks];
 #pragma unroll
-        for (int k = 0; k < PB; k++)
-            dsc[k] = sload(&p.desc[b0 + k < p.n ? b0 + k : p.n - 1]);
+    for (uint32_t k = 0; k < kPreChunks; k++)
+        ch[k] = ld16(base + 16u * (k < last ? k : last));
+    uint32_t *my = &s_pre[t * kPreStride];
 #pragma unroll
-        for (int k = 0; k < PB; k++) {
-            const uintptr_t in = reinterpret_cast<uintptr_t>(p.in) + dsc[k].in_offset;
-            const uint32_t L = dsc[k].in_len;
-            c[k].hb0 = ld8(L ? in + (lane < L ? lane : 0u) : zero);
-            c[k].hb1 = ld8(L ? in + (lane + 64 < L ? lane + 64 : 0u) : zero);
-        }
-#pragma unroll
-        for (int k = 0; k < PB; k++) {
-            const uint64_t b = b0 + k;
-            if (b >= p.n)
-                break;
-            Ctx &cc = c[k];
-            const Cls cl = classify<true, true>(dsc[k], reinterpret_cast<uintptr_t>(p.in), cc);
-            GsoPlan pl{};
-            if (!cl.pass) {
-                cc.id0 = (pbyte(cc, 4) << 8) | pbyte(cc, 5);
-                // seq0 is read after the prefix's L4 checksum field was zeroed
-                // (:149 before :152-154), which matters when the two overlap.
-                cc.seq0 = 0;
-                if (cc.tcp) {
-                    for (uint32_t q = 0; q < 4; q++) {
-                        const uint32_t j = cc.cs + 4 + q;
-                        const uint32_t bb = (j == cc.l4off || j == cc.l4off + 1) ? 0u : pbyte(cc, j);
-                        cc.seq0 |= bb << (8u * (3u - q));
-                    }
-                }
-                hdr_bases(cc, lane);
-                pl.hdr_len = (uint16_t)cc.hdr_len;
-                pl.cs = (uint16_t)cc.cs;
-                pl.l4off = (uint16_t)cc.l4off;
-                pl.kind = (uint8_t)(kPlanSplit | (cc.v6 ? kPlanV6 : 0u) | (cc.tcp ? kPlanTcp : 0u));
-                pl.flags13 = (uint8_t)cc.flags13;
-                pl.gso = (uint16_t)cc.gso;
-                pl.nseg = (uint16_t)cc.nseg;
-                pl.id0 = (uint16_t)cc.id0;
-                pl.ip_base = (uint16_t)fold16_32(cc.ip_base);
-                pl.l4h_base = (uint16_t)fold16_32(cc.l4h_base);
-                pl.ps_sum = (uint16_t)fold16_32(cc.ps_sum);
-                pl.seq0 = cc.seq0;
-            } else if (cl.inplace) {
-                cc.tcp = (cl.isv6 ? pbyte(cc, 6) : pbyte(cc, 9)) == 6;  // :67-70
-                do_inplace(cc, lane);
-            }
-            if (lane == 0)
-                reinterpret_cast<GsoPlan *>(p.res)[b] = pl;
-        }
+    for (uint32_t k = 0; k < kPreChunks; k++) {
+        my[4 * k] = ch[k].x;
+        my[4 * k + 1] = ch[k].y;
+        my[4 * k + 2] = ch[k].z;
+        my[4 * k + 3] = ch[k].w;
     }
+    const uint8_t *mb = reinterpret_cast<const uint8_t *>(my) + o;
+    auto byte = [&](uint32_t j) -> uint32_t { return j < win ? (uint32_t)mb[j] : ld8(in + j); };
+
+    Ctx c;
+    const Cls cl = classify_by(dsc, reinterpret_cast<uintptr_t>(p.in), c, byte);
+    GsoPlan pl{};
+    pl.hdr_len = (uint16_t)c.hdr_len;
+    const uint32_t cls_bits = (cl.isv6 ? kPlanIsV6 : 0u) | (cl.ecn << kPlanEcnShift);
+    if (!cl.pass) {
+        c.id0 = (byte(4) << 8) | byte(5);
+        // seq0 is read after the prefix's L4 checksum field was zeroed
+        // (:149 before :152-154), which matters when the two overlap.
+        c.seq0 = 0;
+        if (c.tcp) {
+            for (uint32_t q = 0; q < 4; q++) {
+                const uint32_t j = c.cs + 4 + q;
+                const uint32_t bb = (j == c.l4off || j == c.l4off + 1) ? 0u : byte(j);
+                c.seq0 |= bb << (8u * (3u - q));
+            }
+        }
+        hdr_bases_thread(c, byte);
+        pl.cs = (uint16_t)c.cs;
+        pl.l4off = (uint16_t)c.l4off;
+        pl.kind = (uint8_t)(kPlanSplit | cls_bits | (c.v6 ? kPlanV6 : 0u) | (c.tcp ? kPlanTcp : 0u));
+        pl.flags13 = (uint8_t)c.flags13;
+        pl.gso = (uint16_t)c.gso;
+        pl.nseg = (uint16_t)c.nseg;
+        pl.id0 = (uint16_t)c.id0;
+        pl.ip_base = (uint16_t)fold16_32(c.ip_base);
+        pl.l4h_base = (uint16_t)fold16_32(c.l4h_base);
+        pl.ps_sum = (uint16_t)fold16_32(c.ps_sum);
+        pl.seq0 = c.seq0;
+    } else {
+        // passthrough / error: the status rides in flags13 (as -status)
+        const bool tcp = cl.inplace && (cl.isv6 ? byte(6) : byte(9)) == 6;  // :67-70
+        pl.cs = (uint16_t)c.cs;
+        pl.l4off = (uint16_t)c.l4off;
+        pl.kind = (uint8_t)(cls_bits | (cl.inplace ? kPlanInplace : 0u) | (c.v6 ? kPlanV6 : 0u) |
+                            (tcp ? kPlanTcp : 0u));
+        pl.flags13 = (uint8_t)(-cl.status);
+    }
+    reinterpret_cast<GsoPlan *>(p.res)[b] = pl;
 }
 
-// Finalize (same stream, after the main kernel): the PacketBatch record per
-// super-buffer, and the reference's in-place zeroing of the input prefix's
-// ip_sum / L4 checksum field (:145-149) — only once every block of the main
-// kernel has read that prefix, hence a separate launch.
+// Finalize (same stream, after the split kernel), thread per super-buffer
+// from its plan: the PacketBatch record, and the reference's in-place zeroing
+// of the input prefix's ip_sum / L4 checksum field (:145-149) — only once
+// every block of the split kernel has read that prefix, hence a separate
+// launch.  Then each wave checksums its GSO_NONE + NEEDS_CSUM super-buffers
+// in place (:56-78), one at a time, the whole wave per super-buffer.
 __global__ __launch_bounds__(256) void gso_finalize_kernel(GsoParams p) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < p.n; b += stride) {
-        const wg_gso_desc dsc = p.desc[b];
-        Ctx c;
-        const Cls cl = classify<false>(dsc, reinterpret_cast<uintptr_t>(p.in), c);
+    const uint32_t lane = lane_id();
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = b < p.n;
+    GsoPlan pl{};
+    uint64_t in_off = 0;
+    uint32_t in_len = 0;
+    if (live) {
+        pl = reinterpret_cast<const GsoPlan *>(p.res)[b];
+        in_off = p.desc[b].in_offset;
+        in_len = p.desc[b].in_len;
+    }
+    const uint32_t kind = pl.kind;
+    const uintptr_t in = reinterpret_cast<uintptr_t>(p.in) + in_off;
+    if (live) {
+        const bool split = kind & kPlanSplit;
         wg_gso_result r;
-        r.out_len = cl.pass ? c.in_len : (uint64_t)c.rest + (uint64_t)c.nseg * c.hdr_len;
-        r.segment_size = cl.pass ? c.in_len : c.hdr_len + c.gso;
-        r.hdr_len = (uint16_t)c.hdr_len;
-        r.isv6 = (uint8_t)cl.isv6;
-        r.ecn = (uint8_t)cl.ecn;
-        r.status = (int8_t)cl.status;
-        r.passthrough = cl.pass ? 1 : 0;
+        const int status = split ? 0 : -(int)pl.flags13;
+        r.hdr_len = pl.hdr_len;
+        r.isv6 = (kind & kPlanIsV6) ? 1 : 0;
+        r.ecn = (uint8_t)((kind >> kPlanEcnShift) & 3u);
+        r.status = (int8_t)status;
+        r.passthrough = split ? 0 : 1;
+        r.out_len = split ? (uint64_t)(in_len - pl.hdr_len) + (uint64_t)pl.nseg * pl.hdr_len : (status ? 0 : in_len);
+        r.segment_size = split ? (uint32_t)pl.hdr_len + pl.gso : (status ? 0u : in_len);
         for (int k = 0; k < 6; k++) r.pad[k] = 0;
-        if (cl.status != 0) {
-            r.out_len = 0;
-            r.segment_size = 0;
-        }
         p.res[b] = r;
-        if (!cl.pass) {
-            if (!c.v6) {
-                st8(c.in + 10, 0);
-                st8(c.in + 11, 0);
+        if (split) {
+            if (!(kind & kPlanV6)) {
+                st8(in + 10, 0);
+                st8(in + 11, 0);
             }
-            st8(c.in + c.l4off, 0);
-            st8(c.in + c.l4off + 1, 0);
+            st8(in + pl.l4off, 0);
+            st8(in + pl.l4off + 1, 0);
         }
+    }
+    uint64_t todo = __ballot(live && (kind & kPlanInplace));
+    while (todo) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(todo);
+        todo &= todo - 1;
+        Ctx c;
+        c.in = (uintptr_t)__builtin_amdgcn_readlane((int)(uint32_t)in, (int)j) |
+               ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(in >> 32), (int)j) << 32);
+        c.in_len = (uint32_t)__builtin_amdgcn_readlane((int)in_len, (int)j);
+        c.cs = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pl.cs, (int)j);
+        c.l4off = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pl.l4off, (int)j);
+        const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)kind, (int)j);
+        c.v6 = kj & kPlanV6;
+        c.tcp = kj & kPlanTcp;
+        do_inplace(c, lane);
     }
 }
 
@@ -471,9 +518,11 @@ extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64
     const Tune &t = tune();
     GsoParams p{dev_in, dev_desc, n, dev_out, dev_res, t.gso_groups};
     hipStream_t st = static_cast<hipStream_t>(stream);
-    // 1. plans (into dev_res) + in-place checksums of GSO_NONE + NEEDS_CSUM
-    const uint64_t ib = (n + 15) / 16;  // 4 waves x 4 super-buffers per block
-    hipLaunchKernelGGL(gso_plan_kernel, dim3((unsigned)(ib < 65536 ? ib : 65536)), dim3(256), 0, st, p);
+    // 1. plans (into dev_res), thread per super-buffer
+    const uint64_t pb = (n + kPlanBlock - 1) / kPlanBlock;
+    if (pb > 0x7fffffffull)
+        return WG_ERR_INVALID;
+    hipLaunchKernelGGL(gso_plan_kernel, dim3((unsigned)pb), dim3(kPlanBlock), 0, st, p);
     // 2. the split
     const uint64_t units = n * t.gso_groups;
     uint64_t blocks = units < t.gso_blocks ? units : t.gso_blocks;
@@ -493,8 +542,7 @@ extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64
     }
     if (hipGetLastError() != hipSuccess)
         return WG_ERR_LAUNCH;
-    // 3. PacketBatch records + the input prefix zeroing
-    const uint64_t fb = (n + 255) / 256;
-    hipLaunchKernelGGL(gso_finalize_kernel, dim3((unsigned)(fb < 65536 ? fb : 65536)), dim3(256), 0, st, p);
+    // 3. PacketBatch records + the input prefix zeroing + in-place checksums
+    hipLaunchKernelGGL(gso_finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }

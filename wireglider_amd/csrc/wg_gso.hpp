@@ -31,11 +31,6 @@ struct GsoParams {
     uint32_t groups;  // blocks per super-buffer (flat grid: block u -> super-buffer u / groups)
 };
 
-// Wave-uniform byte load (every lane reads the same address).
-__device__ __forceinline__ uint32_t ubyte_u(uintptr_t a) {
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)ld8(a));
-}
-
 struct Ctx {
     uintptr_t in;
     uint32_t in_len, cs, l4off, hdr_len, gso, nseg;
@@ -43,24 +38,14 @@ struct Ctx {
     uint32_t id0, seq0;
     bool v6, tcp;
     // Per-super-buffer header sums over the bytes that do NOT change from
-    // segment to segment (computed once by each wave, hdr_bases()):
+    // segment to segment (hdr_bases_thread(), in the plan pass):
     uint32_t ip_base;   // IPv4 header [0, cs) minus len/id, ip_sum = 0 (pairing from byte 0)
     uint32_t l4h_base;  // L4 header [cs, hdr_len) minus seq/flags (TCP) or len (UDP) (pairing from cs)
     uint32_t ps_sum;    // pseudo-header addresses
     uint32_t flags13;   // TCP flags byte of the prefix
-    uint32_t hb0, hb1;  // this lane's prefix bytes lane, lane + 64 (one load for the whole wave)
+    uint32_t hb0, hb1;  // split kernel: this lane's prefix bytes lane, lane + 64
     uint32_t hc0, hc1;  // per-segment field code of prefix bytes lane, lane + 64 (hdr_code)
 };
-
-// Prefix byte j, wave-uniform: from the registers of the one prefix load
-// when j < 128, else a direct load.
-__device__ __forceinline__ uint32_t pbyte(const Ctx &c, uint32_t j) {
-    if (j < 64)
-        return (uint32_t)__builtin_amdgcn_readlane((int)c.hb0, (int)j);
-    if (j < 128)
-        return (uint32_t)__builtin_amdgcn_readlane((int)c.hb1, (int)(j - 64));
-    return ubyte_u(c.in + j);
-}
 
 // Is prefix byte j one of the per-segment L4 header fields?
 __device__ __forceinline__ bool l4_varying(const Ctx &c, uint32_t j) {
@@ -104,13 +89,18 @@ __device__ __forceinline__ uint32_t hdr_code(const Ctx &c, uint32_t j) {
     return kFldTmpl;
 }
 
-// One pass over the prefix per wave: exact integer sums of the invariant
-// header bytes (the reference's values after the :145-149 zeroing).
-__device__ void hdr_bases(Ctx &c, uint32_t lane) {
+// Exact integer sums of the invariant header bytes (the reference's values
+// after the :145-149 zeroing), by ONE thread over its super-buffer's prefix
+// bytes (`byte(j)`, j < hdr_len): IPv4 header [0, cs) without len / id /
+// ip_sum, L4 header [cs, hdr_len) without its checksum and per-segment
+// fields, and the pseudo-header addresses.  Every total stays below 2^32
+// (at most 32,768 16-bit words), so the later 16-bit folds are exact.
+template <class ByteFn>
+__device__ __forceinline__ void hdr_bases_thread(Ctx &c, ByteFn byte) {
     const uint32_t ao = c.v6 ? 8u : 12u, al = c.v6 ? 32u : 8u;
     uint32_t ip = 0, l4 = 0, ps = 0;
-    for (uint32_t j = lane; j < c.hdr_len; j += 64) {
-        uint32_t b = j < 64 ? c.hb0 : (j < 128 ? c.hb1 : ld8(c.in + j));
+    for (uint32_t j = 0; j < c.hdr_len; j++) {
+        uint32_t b = byte(j);
         if ((!c.v6 && (j == 10 || j == 11)) || j == c.l4off || j == c.l4off + 1)
             b = 0;
         if (j < c.cs) {
@@ -122,13 +112,11 @@ __device__ void hdr_bases(Ctx &c, uint32_t lane) {
         if (j >= ao && j < ao + al)
             ps += b << (8u * ((j - ao) & 1u));
     }
-    c.hc0 = hdr_code(c, lane);
-    c.hc1 = hdr_code(c, lane + 64);
-    c.ip_base = wave_sum_u32(ip);
-    c.l4h_base = wave_sum_u32(l4);
-    c.ps_sum = wave_sum_u32(ps);
+    c.ip_base = ip;
+    c.l4h_base = l4;
+    c.ps_sum = ps;
     const uint32_t j13 = c.cs + 13;
-    c.flags13 = (c.tcp && j13 < c.hdr_len && j13 != c.l4off && j13 != c.l4off + 1) ? pbyte(c, j13) : 0u;
+    c.flags13 = (c.tcp && j13 < c.hdr_len && j13 != c.l4off && j13 != c.l4off + 1) ? byte(j13) : 0u;
 }
 
 __device__ __forceinline__ void st8(uintptr_t addr, uint32_t b) {
@@ -191,27 +179,17 @@ __device__ void do_inplace(const Ctx &c, uint32_t lane) {
     }
 }
 
-// Classification of one super-buffer (mirrors :48-134 and the oracle).
-// kUniform: called by a whole wave (wave-uniform byte loads).
+// Classification of one super-buffer (mirrors :48-134 and the oracle), by
+// one thread (gso_plan_kernel).
 struct Cls {
     int status;
     bool pass, inplace;
     uint32_t isv6, ecn;
 };
 
-template <bool kUniform>
-__device__ __forceinline__ uint32_t ldb(const Ctx &c, uint32_t j) {
-    if constexpr (kUniform)
-        return pbyte(c, j);
-    else
-        return ld8(c.in + j);
-}
-
-// kPreloaded (with kUniform): the caller has already loaded c.hb0 / c.hb1
-// (prefix bytes lane, lane + 64, as below), so several super-buffers'
-// prefix loads can be in flight at once.
-template <bool kUniform, bool kPreloaded = false>
-__device__ __forceinline__ Cls classify(const wg_gso_desc &dsc, uintptr_t in_base, Ctx &c) {
+// byte(j): prefix byte j of the super-buffer (only called for j < in_len).
+template <class ByteFn>
+__device__ __forceinline__ Cls classify_by(const wg_gso_desc &dsc, uintptr_t in_base, Ctx &c, ByteFn byte) {
     c.in = in_base + dsc.in_offset;
     c.in_len = dsc.in_len;
     c.cs = dsc.vnet.csum_start;
@@ -227,20 +205,13 @@ __device__ __forceinline__ Cls classify(const wg_gso_desc &dsc, uintptr_t in_bas
         r.status = -3;
         return r;
     }
-    if constexpr (kUniform && !kPreloaded) {
-        // the whole wave loads prefix bytes 0-127 at once; every byte the
-        // classification and the header work need is then a readlane
-        const uint32_t lane = lane_id();
-        c.hb0 = ld8(c.in + (lane < c.in_len ? lane : 0u));
-        c.hb1 = ld8(c.in + (lane + 64 < c.in_len ? lane + 64 : 0u));
-    }
-    r.isv6 = (ldb<kUniform>(c, 0) >> 4) == 6;  // :48
+    r.isv6 = (byte(0) >> 4) == 6;  // :48
     const uint32_t iph_min = r.isv6 ? 40u : 20u;
     if (c.in_len < iph_min) {
         r.status = -3;
         return r;
     }
-    r.ecn = r.isv6 ? ((ldb<kUniform>(c, 1) >> 4) & 3u) : (ldb<kUniform>(c, 1) & 3u);  // :49-53
+    r.ecn = r.isv6 ? ((byte(1) >> 4) & 3u) : (byte(1) & 3u);  // :49-53
     c.v6 = r.isv6;
     const uint32_t g = gtype & ~kGsoEcn;  // :55
     bool seg = false;
@@ -255,7 +226,7 @@ __device__ __forceinline__ Cls classify(const wg_gso_desc &dsc, uintptr_t in_bas
         if (c.cs > c.in_len) {
             r.status = -3;
         } else if (c.in_len - c.cs >= 20) {                                        // :91
-            const uint32_t thlen = 4u * (ldb<kUniform>(c, c.cs + 12) >> 4);  // doff, :100
+            const uint32_t thlen = 4u * (byte(c.cs + 12) >> 4);  // doff, :100
             if (thlen >= 20) {                                                    // :101
                 c.hdr_len = c.cs + thlen;                                         // :110
                 seg = true;
