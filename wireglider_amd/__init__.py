@@ -23,6 +23,9 @@ from pathlib import Path
 
 _PKG = Path(__file__).resolve().parent
 LIB_PATH = _PKG / "lib" / "libwireglider_amd.so"
+# A/B tooling only (tools/ab_builds.sh): load another build of the same library.
+if os.environ.get("WG_LIB"):
+    LIB_PATH = Path(os.environ["WG_LIB"]).resolve()
 
 WG_OK = 0
 WG_PKT_V6 = 0x01

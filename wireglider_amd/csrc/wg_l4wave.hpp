@@ -28,7 +28,7 @@ struct Front {
     uint32_t bv;     // gathered byte, already shifted to its pairing
     bool bt;         // bv is in TRUE pairing (pseudo-header address byte)
     uint32_t hb;     // kHdr: packet byte `lane` (lanes 0-31), raw; else 0
-    uintptr_t r0;    // start of the summed region
+    uint32_t r0odd;  // the summed region starts at an odd address
     uintptr_t c0;    // first aligned interior chunk
     uint32_t nint;   // interior chunk count
 };
@@ -37,6 +37,11 @@ struct Front {
 // cs >= len).  Interior = whole aligned chunks [c0, c1); the unaligned head
 // [r0, min(c0, r1)) and tail [max(c1, c0), r1) are <= 15 bytes each.
 // Branch-free: out-of-range lanes re-read a valid chunk and are masked.
+// The geometry is 32-bit offsets from the packet start (alignment depends
+// only on the address's low bits): 64-bit scalar compares have no SALU form
+// on gfx9 and cost a VALU compare plus exec bookkeeping each, and the scalar
+// unit (one per CU) is what the per-packet work is bound by.  Requires
+// len < 2^32 - 32.
 // kHdr (plain sums only): the byte gather's otherwise idle lanes 0-31 bring
 // packet bytes 0-31 into f.hb (raw, not summed by finish) — the verify
 // kernel's header, with no extra load instruction.
@@ -44,12 +49,14 @@ template <bool kL4, bool kNT, bool kHdr = false>
 __device__ __forceinline__ void issue(const Geom &g, uint32_t lane, Front &f) {
     static_assert(!(kL4 && kHdr), "kHdr uses the pseudo-header lanes");
     const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
-    const uintptr_t r1 = g.a + g.len;
-    const uintptr_t r0 = g.cs < g.len ? g.a + g.cs : r1;
-    const uintptr_t c0 = (r0 + 15) & ~(uintptr_t)15;
-    const uintptr_t c1 = r1 & ~(uintptr_t)15;
-    const uint32_t nint = c1 > c0 ? (uint32_t)((c1 - c0) >> 4) : 0u;
-    f.r0 = r0;
+    const uint32_t alo = (uint32_t)g.a;
+    const uint32_t o0 = g.cs < g.len ? g.cs : g.len;                // r0 - a
+    const uint32_t oc0 = ((alo + o0 + 15u) & ~15u) - alo;           // c0 - a, in [o0, o0 + 15]
+    const uint32_t b1 = ((alo + g.len) & ~15u) - alo + 16u;         // c1 - a + 16 (c1 - a >= -15)
+    const uint32_t b0 = oc0 + 16u;
+    const uint32_t nint = b1 > b0 ? (b1 - b0) >> 4 : 0u;
+    const uintptr_t c0 = g.a + oc0;
+    f.r0odd = (alo + o0) & 1u;
     f.c0 = c0;
     f.nint = nint;
     // wave-uniform base and clamp, per-lane 32-bit offset
@@ -72,15 +79,14 @@ __device__ __forceinline__ void issue(const Geom &g, uint32_t lane, Front &f) {
     // Per-lane 32-bit offsets from a wave-uniform base (packet start, or the
     // zero chunk for an empty packet): no per-lane 64-bit addresses.
     const bool bt = kL4 && lane < al && ao + lane < g.len;
-    const uint32_t cs0 = (uint32_t)(r0 - g.a);                       // region start
-    const uint32_t heo = (uint32_t)((c0 < r1 ? c0 : r1) - g.a);      // head end
-    const uint32_t tso = (uint32_t)((c1 > c0 ? c1 : c0) - g.a);      // tail start
-    const uint32_t xh = cs0 + lane - 32u, xt = tso + lane - 48u;
+    const uint32_t heo = oc0 < g.len ? oc0 : g.len;   // head end
+    const uint32_t tso = nint ? b1 - 16u : oc0;       // tail start
+    const uint32_t xh = o0 + lane - 32u, xt = tso + lane - 48u;
     const bool bh = lane >= 32 && lane < 48 && xh < heo;
     const bool btl = lane >= 48 && xt < g.len;
     const bool bhd = kHdr && lane < 32u && lane < g.len;
     const uint32_t off = bt ? ao + lane : (bh ? xh : (btl ? xt : (bhd ? lane : 0u)));
-    const uint32_t par = bt ? (lane & 1u) : (((uint32_t)g.a + off) & 1u);
+    const uint32_t par = bt ? (lane & 1u) : ((alo + off) & 1u);
     const uint32_t byte = ld8((g.len ? g.a : zero) + off);
     f.bv = (bt || bh || btl) ? byte << (8u * par) : 0u;
     f.bt = bt;
@@ -112,7 +118,7 @@ __device__ __forceinline__ uint32_t finish(uint32_t lane, const Front &f) {
     if (!f.bt)
         acc.add(f.bv);
     uint32_t s = fold16(acc.value());
-    if (f.r0 & 1u)  // region pairs from an odd address: swap its folded sum
+    if (f.r0odd)  // region pairs from an odd address: swap its folded sum
         s = bswap16(s);
     return s + (f.bt ? f.bv : 0u);
 }
