@@ -124,7 +124,7 @@ def test_desc_random(gpu, knobs):
     import torch
 
     wga = _wga()
-    saved = {k: wga.tune_get(k) for k in ("l4_occ", "l4_descv", "l4_iters", "l4_ppw")}
+    saved = {k: wga.tune_get(k) for k in ("l4_occ", "l4_descv", "l4_iters", "l4_ppw", "l4_blocks")}
     for k, v in knobs.items():
         wga.tune_set(k, v)
     rng = np.random.default_rng(1234)
