@@ -270,3 +270,61 @@ def test_config3_full_size_properties(gpu):
         assert st == 0
         np.testing.assert_array_equal(d_out[b * out_stride:b * out_stride + out_len].cpu().numpy(), o_out)
         np.testing.assert_array_equal(d_in[b * in_stride:b * in_stride + in_len].cpu().numpy(), o_in)
+
+
+def test_high_addresses(gpu):
+    """Super-buffers spread over a 4.3 GB input, so their addresses take both
+    values of bit 31 and cross the 4 GiB line: in-place (GSO_NONE +
+    NEEDS_CSUM), split TCP and UDP cases each at several far offsets.  (An
+    address narrowed through a signed 32-bit lane read once turned into a
+    wild pointer only for buffers above such a line.)"""
+    import torch
+
+    wga = _wga()
+    rng = np.random.default_rng(4242)
+    span = (1 << 32) + (1 << 22)
+    d_in = torch.zeros(span, dtype=torch.uint8, device=gpu)
+    # bases at least 3 x 4 KiB apart (three cases of < 4 KiB each per base)
+    offs = [0, 3 << 29, (1 << 31) - 6144, (1 << 31) + 16384, 3 << 30, (1 << 32) - 12288, (1 << 32) + 16384]
+    cases = []
+    for k, base in enumerate(offs):
+        for kind in range(3):
+            o = base + kind * 4096 + int(rng.integers(0, 16))
+            isv6 = bool((k + kind) & 1)
+            if kind == 2:
+                p = pktbuild.build(isv6, False, rng.integers(0, 256, 1400, dtype=np.uint8).tobytes(),
+                                   *(2 * [bytes(16 if isv6 else 4)]), fill_l4=False)
+                vnet = dict(flags=1, gso_type=5, gso_size=500, csum_start=40 if isv6 else 20, csum_offset=6)
+            else:
+                p = pktbuild.build(isv6, True, rng.integers(0, 256, 1800, dtype=np.uint8).tobytes(),
+                                   *(2 * [bytes(16 if isv6 else 4)]), seq=7, fill_l4=False)
+                vnet = dict(flags=1, gso_type=(0 if kind == 0 else (4 if isv6 else 1)), gso_size=700,
+                            csum_start=40 if isv6 else 20, csum_offset=16)
+            cases.append((o, p, vnet))
+    n = len(cases)
+    desc = np.zeros(n, dtype=wga.GSO_DESC_DTYPE)
+    cap = 4096
+    for k, (o, p, vnet) in enumerate(cases):
+        desc[k]["in_offset"], desc[k]["out_offset"] = o, k * cap
+        desc[k]["in_len"], desc[k]["out_cap"] = len(p), cap
+        for f in ("flags", "gso_type", "gso_size", "csum_start", "csum_offset"):
+            desc[k]["vnet"][f] = vnet[f]
+        d_in[o:o + len(p)] = torch.from_numpy(np.frombuffer(p, np.uint8).copy()).to(gpu)
+    d_out = torch.full((n * cap,), 0xA5, dtype=torch.uint8, device=gpu)
+    d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(gpu)
+    d_res = wga.gso_split(d_in, d_desc, d_out)
+    torch.cuda.synchronize()
+    g_out = d_out.cpu().numpy()
+    g_res = d_res.cpu().numpy().view(wga.GSO_RESULT_DTYPE)
+    for k, (o, p, vnet) in enumerate(cases):
+        st, o_in, o_out, vafter, res = oracle.gso_split(np.frombuffer(p, np.uint8), vnet, cap)
+        r = g_res[k]
+        assert int(r["status"]) == st == 0, k
+        assert int(r["out_len"]) == res["out_len"], k
+        np.testing.assert_array_equal(d_in[o:o + len(p)].cpu().numpy(), o_in, err_msg=f"case {k} input after")
+        assert int(r["passthrough"]) == res["passthrough"], k
+        if not res["passthrough"]:
+            np.testing.assert_array_equal(g_out[k * cap:k * cap + res["out_len"]], o_out[:res["out_len"]],
+                                          err_msg=f"case {k} output")
+    del d_in
+    torch.cuda.empty_cache()

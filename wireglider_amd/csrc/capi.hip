@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cctype>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -127,6 +128,20 @@ Tune &tune_mut() {
 }
 
 const Tune &tune() { return tune_mut(); }
+
+bool debug_sync(hipStream_t st, const char *kernel) {
+    static const bool on = [] {
+        const char *v = std::getenv("WG_DEBUG_SYNC");
+        return v && *v == '1';
+    }();
+    if (!on)
+        return true;
+    const hipError_t e = hipStreamSynchronize(st);
+    if (e == hipSuccess)
+        return true;
+    std::fprintf(stderr, "wireglider_amd: %s failed: %s\n", kernel, hipGetErrorString(e));
+    return false;
+}
 
 // Per-host-thread device workspace for the host-memory path.  Grows to the
 // largest batch seen; freed at thread exit.

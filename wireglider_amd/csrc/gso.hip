@@ -482,7 +482,9 @@ __global__ __launch_bounds__(256) void gso_finalize_kernel(GsoParams p) {
         const uint32_t j = (uint32_t)__builtin_ctzll(todo);
         todo &= todo - 1;
         Ctx c;
-        c.in = (uintptr_t)__builtin_amdgcn_readlane((int)(uint32_t)in, (int)j) |
+        // through uint32_t: readlane returns int, and int -> uintptr_t would
+        // sign-extend an address whose bit 31 is set
+        c.in = (uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)in, (int)j) |
                ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(in >> 32), (int)j) << 32);
         c.in_len = (uint32_t)__builtin_amdgcn_readlane((int)in_len, (int)j);
         c.cs = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pl.cs, (int)j);
@@ -523,6 +525,8 @@ extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64
     if (pb > 0x7fffffffull)
         return WG_ERR_INVALID;
     hipLaunchKernelGGL(gso_plan_kernel, dim3((unsigned)pb), dim3(kPlanBlock), 0, st, p);
+    if (!debug_sync(st, "gso_plan_kernel"))
+        return WG_ERR_LAUNCH;
     // 2. the split
     const uint64_t units = n * t.gso_groups;
     uint64_t blocks = units < t.gso_blocks ? units : t.gso_blocks;
@@ -540,9 +544,11 @@ extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64
         default: launch_split<0, 0>(p, g, t.gso_waves, st); break;
         }
     }
-    if (hipGetLastError() != hipSuccess)
+    if (hipGetLastError() != hipSuccess || !debug_sync(st, "gso_split_kernel"))
         return WG_ERR_LAUNCH;
     // 3. PacketBatch records + the input prefix zeroing + in-place checksums
     hipLaunchKernelGGL(gso_finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
+    if (!debug_sync(st, "gso_finalize_kernel"))
+        return WG_ERR_LAUNCH;
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }

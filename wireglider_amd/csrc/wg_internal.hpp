@@ -33,4 +33,9 @@ struct Tune {
 const Tune &tune();
 Tune &tune_mut();
 
+// Debugging aid: with WG_DEBUG_SYNC=1 in the environment, synchronise the
+// stream after a launch and report a failing kernel by name on stderr.
+// Returns false when the kernel failed.
+bool debug_sync(hipStream_t st, const char *kernel);
+
 }  // namespace wg
