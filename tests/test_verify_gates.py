@@ -212,3 +212,35 @@ def test_gpu_verify_size_gate(gpu, knobs):
     np.testing.assert_array_equal(l4.cpu().numpy(), el4)
     assert np.count_nonzero(ev & V.V_V6) == sum(1 for p in pkts if p[0] >> 4 == 6)  # oversized v6 still report V6
     assert (ev[0::7] & OK == OK).all()  # the 65535-byte packets pass
+
+
+@pytest.mark.gpu
+def test_gpu_verify_high_addresses(gpu):
+    """Packets placed on both sides of bit 31 and of 4 GiB in a 4.3 GB batch
+    buffer (64-bit descriptor offsets, lane-level address arithmetic)."""
+    import torch
+
+    import wireglider_amd as wga
+
+    rng = np.random.default_rng(31)
+    pkts = random_verify_batch(rng, 48)
+    span = (1 << 32) + (1 << 22)
+    big = torch.zeros(span, dtype=torch.uint8, device=gpu)
+    # 10 slots of 3,100 B per base (packets < 3,100 B); the bases far enough
+    # apart that no two packets overlap, two of them straddling bit 31 / 4 GiB
+    bases = [0, (1 << 31) - 15500, (1 << 31) + 16000, (1 << 32) - 15500, (1 << 32) + 16000]
+    d = np.zeros(len(pkts), dtype=oracle.PKT_DESC)
+    host_buf, hd = pack(pkts, rng)  # compact copy for the oracle
+    assert max(len(p) for p in pkts) + 16 < 3100
+    for k, p in enumerate(pkts):
+        o = bases[k % len(bases)] + (k // len(bases)) * 3100 + int(rng.integers(0, 16))
+        d[k]["offset"], d[k]["len"] = o, len(p)
+        if len(p):
+            big[o:o + len(p)] = torch.from_numpy(np.frombuffer(p, np.uint8).copy()).to(gpu)
+    verdict, l4 = wga.verify_desc(big, torch.from_numpy(d.view(np.int64).reshape(-1, 2).copy()).to(gpu))
+    torch.cuda.synchronize()
+    ev, el4 = oracle.verify_desc(host_buf, hd)
+    np.testing.assert_array_equal(verdict.cpu().numpy(), ev)
+    np.testing.assert_array_equal(l4.cpu().numpy(), el4)
+    del big
+    torch.cuda.empty_cache()
