@@ -185,3 +185,28 @@ def test_gpu_gro_finalize_empty(gpu):
     import wireglider_amd as wg
 
     wg.gro_finalize(torch.zeros(0, dtype=torch.uint8, device=gpu), torch.zeros(0, dtype=torch.uint8, device=gpu))
+
+
+@pytest.mark.gpu
+def test_gpu_gro_finalize_high_addresses(gpu):
+    """The same ragged batch placed so its flows straddle bit 31 and 4 GiB of
+    a 4.3 GB header buffer (64-bit header offsets, staged-chunk addresses)."""
+    import torch
+
+    import wireglider_amd as wg
+
+    rng = np.random.default_rng(2031)
+    hdrs, desc = _batch(rng, 3000)
+    want, want_st = _oracle_batch(hdrs, desc)
+    big = torch.zeros((1 << 32) + (1 << 22), dtype=torch.uint8, device=gpu)
+    for base in ((1 << 31) - hdrs.size // 2 + 3, (1 << 32) - hdrs.size // 2 + 9):
+        d = desc.copy()
+        d["hdr_offset"] += base
+        big[base:base + hdrs.size] = torch.from_numpy(hdrs).to(gpu)
+        dd = torch.from_numpy(d.view(np.uint8).copy()).to(gpu)
+        wg.gro_finalize(big, dd)
+        torch.cuda.synchronize()
+        assert np.array_equal(dd.cpu().numpy().view(wg.GRO_DESC_DTYPE)["status"], want_st)
+        assert np.array_equal(big[base:base + hdrs.size].cpu().numpy(), want)
+    del big
+    torch.cuda.empty_cache()
