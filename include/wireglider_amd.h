@@ -138,6 +138,9 @@ int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_desc, uint64_
  *   - the input prefix's ip_sum and L4 checksum field are zeroed in place
  *     (:145-149), and GSO_NONE + NEEDS_CSUM packets are checksummed in
  *     place (:56-78).
+ * Contract: in_len <= 65,535 for super-buffers that are split or checksummed
+ * in place (tun delivers at most 64 KiB; the IP length fields are 16-bit);
+ * longer ones get status -3 and are left untouched.
  * ---------------------------------------------------------------------- */
 
 /* Native-order mirror of struct virtio_net_hdr (linux/virtio_net.h). */

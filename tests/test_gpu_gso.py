@@ -328,3 +328,35 @@ def test_high_addresses(gpu):
                                           err_msg=f"case {k} output")
     del d_in
     torch.cuda.empty_cache()
+
+
+def test_oversize_super_buffers(gpu):
+    """in_len > 65,535 (out of contract: tun never delivers it) -> status -3
+    for split and in-place candidates, input untouched; passthrough types
+    still pass through.  Documented in include/wireglider_amd.h."""
+    import torch
+
+    wga = _wga()
+    rng = np.random.default_rng(5)
+    p4 = pktbuild.build(False, True, rng.integers(0, 256, 70000, dtype=np.uint8).tobytes(),
+                        pktbuild.ipv4_addr("10.0.0.1"), pktbuild.ipv4_addr("10.0.0.2"), fill_l4=False)
+    cases = [(1, 1), (0, 1), (3, 1), (0, 0)]  # (gso_type, flags): TCPv4 split, in place, passthrough x2
+    n = len(cases)
+    desc = np.zeros(n, dtype=wga.GSO_DESC_DTYPE)
+    cap = 200000
+    for k, (gt, fl) in enumerate(cases):
+        desc[k]["in_offset"], desc[k]["out_offset"] = k * 80000, k * cap
+        desc[k]["in_len"], desc[k]["out_cap"] = len(p4), cap
+        desc[k]["vnet"]["flags"], desc[k]["vnet"]["gso_type"] = fl, gt
+        desc[k]["vnet"]["gso_size"], desc[k]["vnet"]["csum_start"], desc[k]["vnet"]["csum_offset"] = 1000, 20, 16
+    inbuf = np.zeros(n * 80000, np.uint8)
+    for k in range(n):
+        inbuf[k * 80000:k * 80000 + len(p4)] = np.frombuffer(p4, np.uint8)
+    d_in = torch.from_numpy(inbuf.copy()).to(gpu)
+    d_out = torch.zeros(n * cap, dtype=torch.uint8, device=gpu)
+    res = wga.gso_split(d_in, torch.from_numpy(desc.view(np.uint8).copy()).to(gpu), d_out)
+    torch.cuda.synchronize()
+    r = res.cpu().numpy().view(wga.GSO_RESULT_DTYPE)
+    assert list(r["status"]) == [-3, -3, 0, 0]
+    assert list(r["passthrough"][2:]) == [1, 1] and list(r["out_len"][2:]) == [len(p4)] * 2
+    np.testing.assert_array_equal(d_in.cpu().numpy(), inbuf)

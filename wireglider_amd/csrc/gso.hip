@@ -395,7 +395,15 @@ __global__ __launch_bounds__(kPlanBlock) void gso_plan_kernel(GsoParams p) {
     auto byte = [&](uint32_t j) -> uint32_t { return j < win ? (uint32_t)mb[j] : ld8(in + j); };
 
     Ctx c;
-    const Cls cl = classify_by(dsc, reinterpret_cast<uintptr_t>(p.in), c, byte);
+    Cls cl = classify_by(dsc, reinterpret_cast<uintptr_t>(p.in), c, byte);
+    // Super-buffers longer than 65,535 bytes (tun never delivers one: the IP
+    // length fields are 16-bit) are out of contract for splitting and in-place
+    // checksumming: status -3 rather than 16-bit plan fields that wrap.
+    if (dsc.in_len > 65535u && (!cl.pass || cl.inplace)) {
+        cl.status = -3;
+        cl.pass = true;
+        cl.inplace = false;
+    }
     GsoPlan pl{};
     pl.hdr_len = (uint16_t)c.hdr_len;
     const uint32_t cls_bits = (cl.isv6 ? kPlanIsV6 : 0u) | (cl.ecn << kPlanEcnShift);
