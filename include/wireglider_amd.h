@@ -46,8 +46,10 @@ extern "C" {
 
 /*
  * One packet of a variable-length batch.  16 bytes, 16-byte aligned array.
- * The packet is dev_base[offset, offset + len).  Replaces the per-call
- * (span, isv6, istcp, csum_start) arguments of calc_l4_checksum.
+ * The packet is dev_base[offset, offset + len), len < 2^32 - 32 (the
+ * kernels compute a packet's geometry in 32-bit offsets from its start).
+ * Replaces the per-call (span, isv6, istcp, csum_start) arguments of
+ * calc_l4_checksum.
  */
 typedef struct wg_pkt_desc {
     uint64_t offset;
