@@ -310,10 +310,48 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
         end = int(offs[npk - 1] + lens[npk - 1])
         return buf[:end].cpu().numpy(), out[:npk].cpu().numpy(), ("desc", raw[:npk])
 
+    def post():
+        """the small-only and large-only sub-batches
+        (same buffer, the descriptors of one size class) and the whole batch,
+        under the default wave-per-packet kernel and the thread-per-packet one
+        (knob l4_small), timed like the main line (back-to-back launches
+        between one event pair on the launch stream), each checked bit-exact
+        against the main line's results."""
+        sub = {}
+        saved = wga.tune_get("l4_small")
+        host_out = out.cpu().numpy()
+        for name, size in (("small_64B", 64), ("large_9000B", 9000), ("mixed", None)):
+            idx = np.nonzero(lens == size)[0] if size else np.arange(n)
+            d_sub = torch.from_numpy(raw[idx]).to(dev)
+            o_sub = torch.empty(len(idx), dtype=torch.uint16, device=dev)
+            nbytes = int(lens[idx].sum())
+            alg = nbytes + 18 * len(idx)  # bytes read + u16 written + 16-B descriptor
+            for kname, small in (("wave_per_packet", 0), ("thread_per_packet", 1)):
+                wga.tune_set("l4_small", small)
+                for _ in range(10):
+                    wga.calc_l4_checksum_desc(buf, d_sub, out=o_sub)
+                reps = 30
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
+                e0.record()
+                for _ in range(reps):
+                    wga.calc_l4_checksum_desc(buf, d_sub, out=o_sub)
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / reps
+                same = bool(np.array_equal(o_sub.cpu().numpy(), host_out[idx]))
+                sub.setdefault(name, {"packets": int(len(idx))})[kname] = {
+                    "kernel_ms": round(ms, 5), "GiB_s": round(nbytes / (ms * 1e-3) / 2**30, 1),
+                    "Mpps": round(len(idx) / (ms * 1e-3) / 1e6, 1),
+                    "roofline_frac": round(alg / (ms * 1e-3) / 8e12, 4), "bit_exact_vs_main_line": same}
+            del d_sub, o_sub
+        wga.tune_set("l4_small", saved)
+        return {"sub_batches": sub}
+
     cfg = {"workload": "config4: 4,194,304 IPv4/UDP packets, 64 B / 9000 B 50/50, packed, descriptor batch",
            "packets_per_gpu": n, "layout": "descriptor", "parallelism": f"shard{world}"}
     return Workload(launch, n, total, total + 2 * n + 16 * n, cfg, "weak", buf, "wg::l4csum_kernel<1,4,nt>",
-                    rank * n, out, desc, sample, [n] * world)
+                    rank * n, out, desc, sample, [n] * world, post=post)
 
 
 def settle(torch, fn, seconds: float) -> int:

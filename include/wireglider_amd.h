@@ -259,6 +259,9 @@ int wg_device_count(void);
  *                iteration, 2 vector prefetch of the next iteration
  *   "l4_iters"   iterations per wave in descriptor mode 2 (1 .. 64)
  *   "l4_occ"     waves/SIMD target at 4 packets/wave (0 = compiler, 7, 8)
+ *   "l4_small"   descriptor batches by the thread-per-packet kernel: a
+ *                packet of <= 64 B summed in one lane, longer ones by the
+ *                wave (0, 1)
  *   "gso_blocks" grid cap of the GSO split kernel (1 .. 2^23)
  *   "gso_groups" blocks per super-buffer, consecutive in the flat grid (1 .. 64)
  *   "gso_waves"  waves per GSO block (1, 2, 4, 8)

@@ -113,7 +113,8 @@ def test_uniform_geometry_sweep(gpu, seg, occ):
 
 
 DESC_VARIANTS = [{"l4_occ": 0}, {"l4_occ": 7}, {"l4_occ": 8}, {"l4_descv": 1}, {"l4_descv": 2, "l4_iters": 2},
-                 {"l4_descv": 2, "l4_iters": 3, "l4_occ": 0}, {"l4_descv": 2, "l4_iters": 8, "l4_ppw": 2}]
+                 {"l4_descv": 2, "l4_iters": 3, "l4_occ": 0}, {"l4_descv": 2, "l4_iters": 8, "l4_ppw": 2},
+                 {"l4_small": 1}, {"l4_small": 1, "l4_nt": 0}]
 
 
 @pytest.mark.parametrize("knobs", DESC_VARIANTS, ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()))
@@ -124,7 +125,8 @@ def test_desc_random(gpu, knobs):
     import torch
 
     wga = _wga()
-    saved = {k: wga.tune_get(k) for k in ("l4_occ", "l4_descv", "l4_iters", "l4_ppw", "l4_blocks")}
+    saved = {k: wga.tune_get(k) for k in ("l4_occ", "l4_descv", "l4_iters", "l4_ppw", "l4_blocks", "l4_small",
+                                          "l4_nt")}
     for k, v in knobs.items():
         wga.tune_set(k, v)
     rng = np.random.default_rng(1234)
@@ -148,6 +150,48 @@ def test_desc_random(gpu, knobs):
     torch.cuda.synchronize()
     for k, v in saved.items():
         wga.tune_set(k, v)
+    np.testing.assert_array_equal(out.cpu().numpy(), oracle.l4_desc(buf, d))
+    np.testing.assert_array_equal(plain.cpu().numpy(), oracle.checksum_desc(buf, d))
+
+
+@pytest.mark.parametrize("small", [0, 1])
+@pytest.mark.parametrize("seed", [5, 6])
+def test_desc_small_packets(gpu, small, seed):
+    """Batches of mostly small packets (0-130 B, every alignment, csum_start
+    inside, at and past the end, truncated pseudo-header addresses) with a few
+    long ones mixed in: the thread-per-packet kernel's lane path (<= 64 B),
+    its wave path (the rest) and the wave-per-packet kernel agree with the
+    oracle."""
+    import torch
+
+    wga = _wga()
+    saved = wga.tune_get("l4_small")
+    wga.tune_set("l4_small", small)
+    rng = np.random.default_rng(seed)
+    n = 30001
+    lens = rng.integers(0, 131, n)
+    lens[::53] = rng.integers(131, 3000, lens[::53].size)
+    lens[::211] = 0
+    lens[7::97] = 64
+    lens[8::97] = 65
+    offs = np.cumsum(np.concatenate([[int(rng.integers(0, 16))], lens[:-1] + rng.integers(0, 17, n - 1)]))
+    total = int(offs[-1] + lens[-1] + 16)
+    buf = rng.integers(0, 256, total, dtype=np.uint8)
+    buf[offs[::31, None] + np.arange(8)] = 0  # some all-zero leading bytes
+    d = np.zeros(n, dtype=oracle.PKT_DESC)
+    d["offset"] = offs
+    d["len"] = lens
+    d["csum_start"] = rng.choice([0, 1, 19, 20, 21, 40, 41, 63, 64, 65], n)
+    d["csum_start"][::9] = lens[::9]
+    d["flags"] = rng.integers(0, 4, n)
+    zl = np.nonzero(lens == 0)[0][:5]
+    d["offset"][zl[:2]] = total - 16  # empty packets at the very end of the buffer
+    back, view = to_dev(buf, gpu, 0)
+    dd = desc_dev(d, gpu)
+    out = wga.calc_l4_checksum_desc(view, dd)
+    plain = wga.checksum_desc(view, dd)
+    torch.cuda.synchronize()
+    wga.tune_set("l4_small", saved)
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.l4_desc(buf, d))
     np.testing.assert_array_equal(plain.cpu().numpy(), oracle.checksum_desc(buf, d))
 

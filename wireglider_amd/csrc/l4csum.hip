@@ -187,10 +187,147 @@ static void launch_kind(const L4Params &p, uint64_t blocks, uint32_t P, bool nt,
     }
 }
 
+// ---------------------------------------------------------------------------
+// Small-packet descriptor kernel (knob l4_small; SURVEY §8(d) config 4's
+// small-packet stress).  A wave per packet spends ~150 wave-instructions
+// (half of them on the CU's one scalar unit) on a 64-B packet, so 64-B
+// batches are issue-bound at ~6 % of the HBM roofline.  Here a THREAD takes
+// one descriptor: a packet of <= kSmallMax bytes is summed in its own lane
+// from (at most) five aligned 16-B chunks, masked per dword to the summed
+// region and to the pseudo-header address bytes; the lanes whose packet is
+// longer are then taken by the whole wave, two at a time, through the same
+// issue / finish machinery as l4csum_kernel.  Same arithmetic model
+// (wg_device.hpp): absolute-address pairing, one byte swap of a folded sum
+// whose pairing starts at an odd address.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSmallMax = 64;  // bytes: five aligned 16-B chunks at any alignment
+
+// Bytes of the dword at relative position p (a multiple of 4) that lie in [lo, hi).
+__device__ __forceinline__ uint32_t dword_mask(uint32_t p, uint32_t lo, uint32_t hi) {
+    const int a = (int)lo - (int)p, b = (int)hi - (int)p;
+    const uint32_t mh = b >= 4 ? ~0u : (b <= 0 ? 0u : (1u << (8 * b)) - 1u);
+    const uint32_t ml = a >= 4 ? ~0u : (a <= 0 ? 0u : (1u << (8 * a)) - 1u);
+    return mh & ~ml;
+}
+
+__device__ __forceinline__ uint32_t half_sum(uint32_t w) { return (w & 0xffffu) + (w >> 16); }
+
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t j) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
+}
+
+template <int kKind, bool kNT>
+__global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
+    constexpr bool kL4 = kKind != kDescPlain;
+    const uint32_t lane = lane_id();
+    const uint64_t i = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 256u + threadIdx.x;
+    const bool live = i < p.n;
+    const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0));
+    const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + (live ? off : 0u);
+    const uint32_t len = live ? dv.z : 0u;
+    const uint32_t cs = kL4 && live ? (dv.w & 0xffffu) : 0u;
+    const uint32_t fl = live ? (dv.w >> 16) & 0xffu : 0u;
+    const bool small = len <= kSmallMax;
+
+    // ---- thread path: the packet's aligned chunks, all five issued at once
+    const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
+    const uintptr_t a0 = a & ~(uintptr_t)15;
+    const uintptr_t alast = (a + len - 1) & ~(uintptr_t)15;
+    const bool any = small && len;
+    v4u W[5];
+#pragma unroll
+    for (uint32_t c = 0; c < 5; c++) {
+        const uintptr_t ca = a0 + 16u * c;
+        W[c] = ld16x<kNT>(any ? (ca > alast ? alast : ca) : zero);  // clamped chunks are masked below
+    }
+    const uint32_t s = (uint32_t)(a & 15u);
+    const uint32_t o0 = cs < len ? cs : len;
+    const bool v6 = fl & WG_PKT_V6;
+    const uint32_t ao = v6 ? 8u : 12u, al = v6 ? 32u : 8u;
+    const uint32_t aend = ao + al < len ? ao + al : len;  // address bytes past the packet end are absent
+    uint32_t sr = 0, sq = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < 5; c++) {
+#pragma unroll
+        for (uint32_t d = 0; d < 4; d++) {
+            const uint32_t pos = 16u * c + 4u * d, w = W[c][d];
+            sr += half_sum(w & dword_mask(pos, s + o0, s + len));
+            if (kL4)
+                sq += half_sum(w & dword_mask(pos, s + ao, s + (aend > ao ? aend : ao)));
+        }
+    }
+    sr = fold16_32(sr);
+    if ((s + o0) & 1u)  // the region pairs from an odd address
+        sr = bswap16(sr);
+    uint32_t res = 0;
+    {
+        uint32_t t = sr;
+        if (kL4) {
+            sq = fold16_32(sq);
+            if (s & 1u)  // the addresses pair from the packet start (an even offset)
+                sq = bswap16(sq);
+            const uint32_t proto = (fl & WG_PKT_TCP) ? 6u : 17u;
+            t += sq + (proto << 8) + bswap16((len - cs) & 0xffffu);  // checksum.hpp:111-114, checksum.cpp:23,33
+        }
+        res = ~fold16_32(t) & 0xffffu;
+    }
+
+    // ---- wave path: the longer packets of this wave, two at a time
+    uint64_t m = __ballot(live && !small);
+    const uint32_t alo = (uint32_t)a, ahi = (uint32_t)((uint64_t)a >> 32);
+    while (m) {
+        Geom g[2];
+        uint32_t jj[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const bool have = m != 0;
+            const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
+            m = have ? m & (m - 1) : m;
+            jj[k] = have ? j : 64u;
+            g[k].a = have ? (uintptr_t)(((uint64_t)rdl(ahi, j) << 32) | rdl(alo, j)) : reinterpret_cast<uintptr_t>(p.base);
+            g[k].len = have ? rdl(len, j) : 0u;
+            g[k].cs = have ? rdl(cs, j) : 0u;
+            g[k].fl = have ? rdl(fl, j) : 0u;
+        }
+        Front f[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+            issue<kL4, kNT>(g[k], lane, f[k]);
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            uint32_t t = wave_sum_u32(finish<kNT>(lane, f[k]));
+            if (kL4) {
+                const uint32_t proto = (g[k].fl & WG_PKT_TCP) ? 6u : 17u;
+                t += (proto << 8) + bswap16((g[k].len - g[k].cs) & 0xffffu);
+            }
+            if (lane == jj[k])
+                res = ~fold16_32(t) & 0xffffu;
+        }
+    }
+    if (live)
+        p.out[i] = (uint16_t)res;
+}
+
 static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
     if (p.n == 0)
         return WG_OK;
     const Tune &t = tune();
+    if (kind != kUniformL4 && t.l4_small) {
+        const uint64_t blocks = (p.n + 255) / 256;
+        if (blocks > 0x7fffffffull)
+            return WG_ERR_INVALID;
+        const dim3 grid((unsigned)blocks), blk(256);
+        if (kind == kDescL4 && t.l4_nt)
+            hipLaunchKernelGGL((l4csum_small_kernel<kDescL4, true>), grid, blk, 0, st, p);
+        else if (kind == kDescL4)
+            hipLaunchKernelGGL((l4csum_small_kernel<kDescL4, false>), grid, blk, 0, st, p);
+        else if (t.l4_nt)
+            hipLaunchKernelGGL((l4csum_small_kernel<kDescPlain, true>), grid, blk, 0, st, p);
+        else
+            hipLaunchKernelGGL((l4csum_small_kernel<kDescPlain, false>), grid, blk, 0, st, p);
+        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+    }
     const uint32_t P = t.l4_ppw;
     uint64_t want = (p.n + 4ull * P - 1) / (4ull * P);
     if (kind != kUniformL4 && t.l4_descv == 2)  // l4_iters iterations per wave (descriptor prefetch)
