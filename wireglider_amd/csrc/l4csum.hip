@@ -216,7 +216,7 @@ __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t j) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
 }
 
-template <int kKind, bool kNT>
+template <int kKind, bool kNT, int Q>  // Q: long packets the wave takes at a time (2, 4)
 __global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
     constexpr bool kL4 = kKind != kDescPlain;
     const uint32_t lane = lane_id();
@@ -231,56 +231,59 @@ __global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
     const bool small = len <= kSmallMax;
 
     // ---- thread path: the packet's aligned chunks, all five issued at once
-    const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
-    const uintptr_t a0 = a & ~(uintptr_t)15;
-    const uintptr_t alast = (a + len - 1) & ~(uintptr_t)15;
-    const bool any = small && len;
-    v4u W[5];
-#pragma unroll
-    for (uint32_t c = 0; c < 5; c++) {
-        const uintptr_t ca = a0 + 16u * c;
-        W[c] = ld16x<kNT>(any ? (ca > alast ? alast : ca) : zero);  // clamped chunks are masked below
-    }
-    const uint32_t s = (uint32_t)(a & 15u);
-    const uint32_t o0 = cs < len ? cs : len;
-    const bool v6 = fl & WG_PKT_V6;
-    const uint32_t ao = v6 ? 8u : 12u, al = v6 ? 32u : 8u;
-    const uint32_t aend = ao + al < len ? ao + al : len;  // address bytes past the packet end are absent
-    uint32_t sr = 0, sq = 0;
-#pragma unroll
-    for (uint32_t c = 0; c < 5; c++) {
-#pragma unroll
-        for (uint32_t d = 0; d < 4; d++) {
-            const uint32_t pos = 16u * c + 4u * d, w = W[c][d];
-            sr += half_sum(w & dword_mask(pos, s + o0, s + len));
-            if (kL4)
-                sq += half_sum(w & dword_mask(pos, s + ao, s + (aend > ao ? aend : ao)));
-        }
-    }
-    sr = fold16_32(sr);
-    if ((s + o0) & 1u)  // the region pairs from an odd address
-        sr = bswap16(sr);
+    // (skipped by waves whose packets are all long: uniform branch)
     uint32_t res = 0;
-    {
-        uint32_t t = sr;
-        if (kL4) {
-            sq = fold16_32(sq);
-            if (s & 1u)  // the addresses pair from the packet start (an even offset)
-                sq = bswap16(sq);
-            const uint32_t proto = (fl & WG_PKT_TCP) ? 6u : 17u;
-            t += sq + (proto << 8) + bswap16((len - cs) & 0xffffu);  // checksum.hpp:111-114, checksum.cpp:23,33
+    if (__ballot(live && small)) {
+        const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
+        const uintptr_t a0 = a & ~(uintptr_t)15;
+        const uintptr_t alast = (a + len - 1) & ~(uintptr_t)15;
+        const bool any = small && len;
+        v4u W[5];
+#pragma unroll
+        for (uint32_t c = 0; c < 5; c++) {
+            const uintptr_t ca = a0 + 16u * c;
+            W[c] = ld16x<kNT>(any ? (ca > alast ? alast : ca) : zero);  // clamped chunks are masked below
         }
-        res = ~fold16_32(t) & 0xffffu;
+        const uint32_t s = (uint32_t)(a & 15u);
+        const uint32_t o0 = cs < len ? cs : len;
+        const bool v6 = fl & WG_PKT_V6;
+        const uint32_t ao = v6 ? 8u : 12u, al = v6 ? 32u : 8u;
+        const uint32_t aend = ao + al < len ? ao + al : len;  // address bytes past the packet end are absent
+        uint32_t sr = 0, sq = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < 5; c++) {
+#pragma unroll
+            for (uint32_t d = 0; d < 4; d++) {
+                const uint32_t pos = 16u * c + 4u * d, w = W[c][d];
+                sr += half_sum(w & dword_mask(pos, s + o0, s + len));
+                if (kL4)
+                    sq += half_sum(w & dword_mask(pos, s + ao, s + (aend > ao ? aend : ao)));
+            }
+        }
+        sr = fold16_32(sr);
+        if ((s + o0) & 1u)  // the region pairs from an odd address
+            sr = bswap16(sr);
+        {
+            uint32_t t = sr;
+            if (kL4) {
+                sq = fold16_32(sq);
+                if (s & 1u)  // the addresses pair from the packet start (an even offset)
+                    sq = bswap16(sq);
+                const uint32_t proto = (fl & WG_PKT_TCP) ? 6u : 17u;
+                t += sq + (proto << 8) + bswap16((len - cs) & 0xffffu);  // checksum.hpp:111-114, checksum.cpp:23,33
+            }
+            res = ~fold16_32(t) & 0xffffu;
+        }
     }
 
-    // ---- wave path: the longer packets of this wave, two at a time
+    // ---- wave path: the longer packets of this wave, Q at a time
     uint64_t m = __ballot(live && !small);
     const uint32_t alo = (uint32_t)a, ahi = (uint32_t)((uint64_t)a >> 32);
     while (m) {
-        Geom g[2];
-        uint32_t jj[2];
+        Geom g[Q];
+        uint32_t jj[Q];
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < Q; k++) {
             const bool have = m != 0;
             const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
             m = have ? m & (m - 1) : m;
@@ -290,12 +293,12 @@ __global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
             g[k].cs = have ? rdl(cs, j) : 0u;
             g[k].fl = have ? rdl(fl, j) : 0u;
         }
-        Front f[2];
+        Front f[Q];
 #pragma unroll
-        for (int k = 0; k < 2; k++)
+        for (int k = 0; k < Q; k++)
             issue<kL4, kNT>(g[k], lane, f[k]);
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < Q; k++) {
             uint32_t t = wave_sum_u32(finish<kNT>(lane, f[k]));
             if (kL4) {
                 const uint32_t proto = (g[k].fl & WG_PKT_TCP) ? 6u : 17u;
@@ -309,6 +312,19 @@ __global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
         p.out[i] = (uint16_t)res;
 }
 
+template <int kKind>
+static void launch_small(const L4Params &p, uint64_t blocks, bool nt, bool q4, hipStream_t st) {
+    const dim3 grid((unsigned)blocks), blk(256);
+    if (nt && q4)
+        hipLaunchKernelGGL((l4csum_small_kernel<kKind, true, 4>), grid, blk, 0, st, p);
+    else if (nt)
+        hipLaunchKernelGGL((l4csum_small_kernel<kKind, true, 2>), grid, blk, 0, st, p);
+    else if (q4)
+        hipLaunchKernelGGL((l4csum_small_kernel<kKind, false, 4>), grid, blk, 0, st, p);
+    else
+        hipLaunchKernelGGL((l4csum_small_kernel<kKind, false, 2>), grid, blk, 0, st, p);
+}
+
 static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
     if (p.n == 0)
         return WG_OK;
@@ -317,15 +333,10 @@ static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
         const uint64_t blocks = (p.n + 255) / 256;
         if (blocks > 0x7fffffffull)
             return WG_ERR_INVALID;
-        const dim3 grid((unsigned)blocks), blk(256);
-        if (kind == kDescL4 && t.l4_nt)
-            hipLaunchKernelGGL((l4csum_small_kernel<kDescL4, true>), grid, blk, 0, st, p);
-        else if (kind == kDescL4)
-            hipLaunchKernelGGL((l4csum_small_kernel<kDescL4, false>), grid, blk, 0, st, p);
-        else if (t.l4_nt)
-            hipLaunchKernelGGL((l4csum_small_kernel<kDescPlain, true>), grid, blk, 0, st, p);
+        if (kind == kDescL4)
+            launch_small<kDescL4>(p, blocks, t.l4_nt != 0, t.l4_small == 2, st);
         else
-            hipLaunchKernelGGL((l4csum_small_kernel<kDescPlain, false>), grid, blk, 0, st, p);
+            launch_small<kDescPlain>(p, blocks, t.l4_nt != 0, t.l4_small == 2, st);
         return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
     }
     const uint32_t P = t.l4_ppw;
