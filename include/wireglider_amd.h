@@ -261,7 +261,9 @@ int wg_device_count(void);
  *   "l4_occ"     waves/SIMD target at 4 packets/wave (0 = compiler, 7, 8)
  *   "l4_small"   descriptor batches by the thread-per-packet kernel: a
  *                packet of <= 64 B summed in one lane, longer ones by the
- *                wave, 2 (1) or 4 (2) at a time; 0 = wave-per-packet kernel
+ *                wave, 2 (1) or 4 (2) at a time; 3: a lane quad per
+ *                descriptor, long packets 4 at a time; 4: as 3, the lane
+ *                loads in flight during the long packets; 0 = wave-per-packet
  *   "gso_blocks" grid cap of the GSO split kernel (1 .. 2^23)
  *   "gso_groups" blocks per super-buffer, consecutive in the flat grid (1 .. 64)
  *   "gso_waves"  waves per GSO block (1, 2, 4, 8)

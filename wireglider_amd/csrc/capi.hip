@@ -37,7 +37,7 @@ static const Knob kKnobs[] = {
     {"l4_descv", nullptr, &Tune::l4_descv, 0, 2, nullptr, 0},
     {"l4_iters", nullptr, &Tune::l4_iters, 1, 64, nullptr, 0},
     {"l4_occ", nullptr, &Tune::l4_occ, 0, 0, kOcc, WG_N(kOcc)},
-    {"l4_small", nullptr, &Tune::l4_small, 0, 2, nullptr, 0},
+    {"l4_small", nullptr, &Tune::l4_small, 0, 4, nullptr, 0},
     {"gso_blocks", &Tune::gso_blocks, nullptr, 1, 1u << 23, nullptr, 0},
     {"gso_waves", nullptr, &Tune::gso_waves, 0, 0, kWaves, WG_N(kWaves)},
     {"gso_split", nullptr, &Tune::gso_split, 1, 64, nullptr, 0},

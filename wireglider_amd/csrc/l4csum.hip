@@ -216,11 +216,18 @@ __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t j) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
 }
 
-template <int kKind, bool kNT, int Q>  // Q: long packets the wave takes at a time (2, 4)
+// G: lanes per descriptor.  G = 1: a lane loads all five chunks; G = 4: a
+// quad shares one descriptor, lane q of the quad loads chunks q and (q = 0)
+// chunk 4, and the quad's partial sums meet by DPP — a wave then carries 16
+// descriptors instead of 64, so its serial walk over the long packets is as
+// short as the wave-per-packet kernel's four iterations.
+template <int kKind, bool kNT, int Q, int G, bool kLate = false>  // Q: long packets the wave takes at a time (2, 4)
 __global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
+    static_assert(G == 1 || G == 4, "lanes per descriptor");
     constexpr bool kL4 = kKind != kDescPlain;
     const uint32_t lane = lane_id();
-    const uint64_t i = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 256u + threadIdx.x;
+    const uint32_t q = lane & (uint32_t)(G - 1);
+    const uint64_t i = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * (256u / G) + threadIdx.x / G;
     const bool live = i < p.n;
     const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0));
     const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
@@ -230,54 +237,72 @@ __global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
     const uint32_t fl = live ? (dv.w >> 16) & 0xffu : 0u;
     const bool small = len <= kSmallMax;
 
-    // ---- thread path: the packet's aligned chunks, all five issued at once
-    // (skipped by waves whose packets are all long: uniform branch)
+    // ---- lane path: the packet's aligned chunks, all issued at once.
+    // kLate: the loads go out before the wave path and are summed after it,
+    // so they fly under the long packets' loads; otherwise loaded and summed
+    // here, skipped by waves whose packets are all long (uniform branch).
     uint32_t res = 0;
-    if (__ballot(live && small)) {
+    const bool any_small = __ballot(live && small) != 0;
+    constexpr uint32_t kC = G == 1 ? 5u : 2u;  // chunks per lane
+    v4u W[kC];
+    uint32_t cidx[kC];
+    const uint32_t s = (uint32_t)(a & 15u);
+    auto load_chunks = [&]() {
         const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
         const uintptr_t a0 = a & ~(uintptr_t)15;
         const uintptr_t alast = (a + len - 1) & ~(uintptr_t)15;
         const bool any = small && len;
-        v4u W[5];
 #pragma unroll
-        for (uint32_t c = 0; c < 5; c++) {
-            const uintptr_t ca = a0 + 16u * c;
-            W[c] = ld16x<kNT>(any ? (ca > alast ? alast : ca) : zero);  // clamped chunks are masked below
+        for (uint32_t k = 0; k < kC; k++) {
+            cidx[k] = G == 1 ? k : q + 4u * k;  // G = 4: chunks q and q + 4 (< 5 only for q = 0)
+            const uintptr_t ca = a0 + 16u * cidx[k];
+            const bool use = any && cidx[k] < 5u;
+            W[k] = ld16x<kNT>(use ? (ca > alast ? alast : ca) : zero);  // clamped chunks are masked below
         }
-        const uint32_t s = (uint32_t)(a & 15u);
+    };
+    auto sum_chunks = [&]() {
         const uint32_t o0 = cs < len ? cs : len;
         const bool v6 = fl & WG_PKT_V6;
         const uint32_t ao = v6 ? 8u : 12u, al = v6 ? 32u : 8u;
         const uint32_t aend = ao + al < len ? ao + al : len;  // address bytes past the packet end are absent
         uint32_t sr = 0, sq = 0;
 #pragma unroll
-        for (uint32_t c = 0; c < 5; c++) {
+        for (uint32_t k = 0; k < kC; k++) {
 #pragma unroll
             for (uint32_t d = 0; d < 4; d++) {
-                const uint32_t pos = 16u * c + 4u * d, w = W[c][d];
+                const uint32_t pos = 16u * cidx[k] + 4u * d, w = W[k][d];
                 sr += half_sum(w & dword_mask(pos, s + o0, s + len));
                 if (kL4)
                     sq += half_sum(w & dword_mask(pos, s + ao, s + (aend > ao ? aend : ao)));
             }
         }
+        if (G > 1) {  // the quad's partial sums (each < 2^20: no overflow)
+            sr = group_sum_u32<4>(sr);
+            sq = group_sum_u32<4>(sq);
+        }
         sr = fold16_32(sr);
         if ((s + o0) & 1u)  // the region pairs from an odd address
             sr = bswap16(sr);
-        {
-            uint32_t t = sr;
-            if (kL4) {
-                sq = fold16_32(sq);
-                if (s & 1u)  // the addresses pair from the packet start (an even offset)
-                    sq = bswap16(sq);
-                const uint32_t proto = (fl & WG_PKT_TCP) ? 6u : 17u;
-                t += sq + (proto << 8) + bswap16((len - cs) & 0xffffu);  // checksum.hpp:111-114, checksum.cpp:23,33
-            }
-            res = ~fold16_32(t) & 0xffffu;
+        uint32_t t = sr;
+        if (kL4) {
+            sq = fold16_32(sq);
+            if (s & 1u)  // the addresses pair from the packet start (an even offset)
+                sq = bswap16(sq);
+            const uint32_t proto = (fl & WG_PKT_TCP) ? 6u : 17u;
+            t += sq + (proto << 8) + bswap16((len - cs) & 0xffffu);  // checksum.hpp:111-114, checksum.cpp:23,33
         }
+        if (small)
+            res = ~fold16_32(t) & 0xffffu;
+    };
+    if (kLate) {
+        load_chunks();
+    } else if (any_small) {
+        load_chunks();
+        sum_chunks();
     }
 
     // ---- wave path: the longer packets of this wave, Q at a time
-    uint64_t m = __ballot(live && !small);
+    uint64_t m = __ballot(live && !small && q == 0);
     const uint32_t alo = (uint32_t)a, ahi = (uint32_t)((uint64_t)a >> 32);
     while (m) {
         Geom g[Q];
@@ -308,21 +333,28 @@ __global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
                 res = ~fold16_32(t) & 0xffffu;
         }
     }
-    if (live)
+    if (kLate && any_small)
+        sum_chunks();
+    if (live && q == 0)
         p.out[i] = (uint16_t)res;
 }
 
-template <int kKind>
-static void launch_small(const L4Params &p, uint64_t blocks, bool nt, bool q4, hipStream_t st) {
+template <int kKind, bool kNT>
+static int launch_small(const L4Params &p, uint32_t mode, hipStream_t st) {
+    const uint32_t per_block = mode >= 3 ? 64u : 256u;  // descriptors per 256-thread block
+    const uint64_t blocks = (p.n + per_block - 1) / per_block;
+    if (blocks > 0x7fffffffull)
+        return WG_ERR_INVALID;
     const dim3 grid((unsigned)blocks), blk(256);
-    if (nt && q4)
-        hipLaunchKernelGGL((l4csum_small_kernel<kKind, true, 4>), grid, blk, 0, st, p);
-    else if (nt)
-        hipLaunchKernelGGL((l4csum_small_kernel<kKind, true, 2>), grid, blk, 0, st, p);
-    else if (q4)
-        hipLaunchKernelGGL((l4csum_small_kernel<kKind, false, 4>), grid, blk, 0, st, p);
+    if (mode == 4)
+        hipLaunchKernelGGL((l4csum_small_kernel<kKind, kNT, 4, 4, true>), grid, blk, 0, st, p);
+    else if (mode == 3)
+        hipLaunchKernelGGL((l4csum_small_kernel<kKind, kNT, 4, 4>), grid, blk, 0, st, p);
+    else if (mode == 2)
+        hipLaunchKernelGGL((l4csum_small_kernel<kKind, kNT, 4, 1>), grid, blk, 0, st, p);
     else
-        hipLaunchKernelGGL((l4csum_small_kernel<kKind, false, 2>), grid, blk, 0, st, p);
+        hipLaunchKernelGGL((l4csum_small_kernel<kKind, kNT, 2, 1>), grid, blk, 0, st, p);
+    return WG_OK;
 }
 
 static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
@@ -330,13 +362,14 @@ static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
         return WG_OK;
     const Tune &t = tune();
     if (kind != kUniformL4 && t.l4_small) {
-        const uint64_t blocks = (p.n + 255) / 256;
-        if (blocks > 0x7fffffffull)
-            return WG_ERR_INVALID;
+        int rc;
         if (kind == kDescL4)
-            launch_small<kDescL4>(p, blocks, t.l4_nt != 0, t.l4_small == 2, st);
+            rc = t.l4_nt ? launch_small<kDescL4, true>(p, t.l4_small, st) : launch_small<kDescL4, false>(p, t.l4_small, st);
         else
-            launch_small<kDescPlain>(p, blocks, t.l4_nt != 0, t.l4_small == 2, st);
+            rc = t.l4_nt ? launch_small<kDescPlain, true>(p, t.l4_small, st)
+                         : launch_small<kDescPlain, false>(p, t.l4_small, st);
+        if (rc != WG_OK)
+            return rc;
         return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
     }
     const uint32_t P = t.l4_ppw;
