@@ -346,6 +346,37 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                     "roofline_frac": round(alg / (ms * 1e-3) / 8e12, 4), "bit_exact_vs_main_line": same}
             del d_sub, o_sub
         wga.tune_set("l4_small", saved)
+        # a uniform PacketBatch of 64-B segments (same packet count as the
+        # 64-B sub-batch): the small-packet kernel is chosen from segment_size
+        n64 = int((lens == 64).sum())
+        b64 = torch.empty(n64 * 64, dtype=torch.uint8, device=dev)
+        wga.synth_fill(b64, seed ^ 64)
+        wga.synth_headers(b64, wga.synth_desc_stride(n64, 64, 64, 0, seed, 0, device=dev), seed, 0)
+        o64 = torch.empty(n64, dtype=torch.uint16, device=dev)
+        su = wga.tune_get("l4_small_uniform")
+        res = {}
+        ref = None
+        for kname, knob in (("wave_per_packet", 0), ("small_kernel_quad", 1), ("small_kernel_lane", 2)):
+            wga.tune_set("l4_small_uniform", knob)
+            for _ in range(10):
+                wga.calc_l4_checksum_batch(b64, 64, False, False, 20, out=o64)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(30):
+                wga.calc_l4_checksum_batch(b64, 64, False, False, 20, out=o64)
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / 30
+            got = o64.cpu().numpy()
+            ref = got if ref is None else ref
+            res[kname] = {"kernel_ms": round(ms, 5), "GiB_s": round(n64 * 64 / (ms * 1e-3) / 2**30, 1),
+                          "Mpps": round(n64 / (ms * 1e-3) / 1e6, 1),
+                          "roofline_frac": round(n64 * 66 / (ms * 1e-3) / 8e12, 4),
+                          "bit_exact_vs_wave_kernel": bool(np.array_equal(got, ref))}
+        wga.tune_set("l4_small_uniform", su)
+        sub["uniform_64B"] = {"packets": n64, **res}
+        del b64, o64
         return {"sub_batches": sub}
 
     cfg = {"workload": "config4: 4,194,304 IPv4/UDP packets, 64 B / 9000 B 50/50, packed, descriptor batch",

@@ -264,6 +264,9 @@ int wg_device_count(void);
  *                wave, 2 (1) or 4 (2) at a time; 3: a lane quad per
  *                descriptor, long packets 4 at a time; 4: as 3, the lane
  *                loads in flight during the long packets; 0 = wave-per-packet
+ *   "l4_small_uniform" uniform batches with segment_size <= 64 by the
+ *                small-packet kernel, a lane quad (1) or a lane (2) per
+ *                segment, or by the wave-per-packet kernel (0)
  *   "gso_blocks" grid cap of the GSO split kernel (1 .. 2^23)
  *   "gso_groups" blocks per super-buffer, consecutive in the flat grid (1 .. 64)
  *   "gso_waves"  waves per GSO block (1, 2, 4, 8)

@@ -154,6 +154,36 @@ def test_desc_random(gpu, knobs):
     np.testing.assert_array_equal(plain.cpu().numpy(), oracle.checksum_desc(buf, d))
 
 
+@pytest.mark.parametrize("knob", [0, 1, 2])
+@pytest.mark.parametrize("seg", [1, 2, 3, 15, 16, 17, 20, 33, 40, 47, 60, 63, 64, 65])
+def test_uniform_small_segments(gpu, seg, knob):
+    """PacketBatches of small segments (<= 64 B go to the small-packet kernel
+    unless l4_small_uniform = 0), every alignment, short last segment."""
+    import torch
+
+    wga = _wga()
+    saved = wga.tune_get("l4_small_uniform")
+    wga.tune_set("l4_small_uniform", knob)
+    rng = np.random.default_rng(1000 + seg)
+    try:
+        for trial in range(8):
+            nseg = int(rng.integers(1, 3000))
+            total = max(1, seg * nseg - int(rng.integers(0, seg)))
+            buf = rng.integers(0, 256, total, dtype=np.uint8)
+            if trial == 0:
+                buf[:] = 0  # all-zero segments
+            pad = int(rng.integers(0, 16))
+            cs = int(rng.choice([0, 1, 7, 12, 20, 21, 40, 41, seg, seg + 3]))
+            flags = int(rng.integers(0, 4))
+            back, view = to_dev(buf, gpu, pad)
+            out = wga.calc_l4_checksum_batch(view, seg, bool(flags & 1), bool(flags & 2), cs)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(out.cpu().numpy(), oracle.l4_uniform(buf, seg, cs, flags),
+                                          err_msg=f"seg={seg} total={total} pad={pad} cs={cs} flags={flags}")
+    finally:
+        wga.tune_set("l4_small_uniform", saved)
+
+
 @pytest.mark.parametrize("small", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("seed", [5, 6])
 def test_desc_small_packets(gpu, small, seed):

@@ -229,12 +229,23 @@ __global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
     const uint32_t q = lane & (uint32_t)(G - 1);
     const uint64_t i = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * (256u / G) + threadIdx.x / G;
     const bool live = i < p.n;
-    const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0));
-    const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + (live ? off : 0u);
-    const uint32_t len = live ? dv.z : 0u;
-    const uint32_t cs = kL4 && live ? (dv.w & 0xffffu) : 0u;
-    const uint32_t fl = live ? (dv.w >> 16) & 0xffu : 0u;
+    uintptr_t a;
+    uint32_t len, cs, fl;
+    if constexpr (kKind == kUniformL4) {  // PacketBatch segment i (include/util/packets.hpp:23-36)
+        const uint64_t off = live ? i * (uint64_t)p.seg : 0u;
+        const uint64_t rem = p.total_len - off;
+        a = reinterpret_cast<uintptr_t>(p.base) + off;
+        len = live ? (rem < p.seg ? (uint32_t)rem : p.seg) : 0u;
+        cs = live ? p.cs : 0u;
+        fl = live ? p.flags : 0u;
+    } else {
+        const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0));
+        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+        a = reinterpret_cast<uintptr_t>(p.base) + (live ? off : 0u);
+        len = live ? dv.z : 0u;
+        cs = kL4 && live ? (dv.w & 0xffffu) : 0u;
+        fl = live ? (dv.w >> 16) & 0xffu : 0u;
+    }
     const bool small = len <= kSmallMax;
 
     // ---- lane path: the packet's aligned chunks, all issued at once.
@@ -361,6 +372,14 @@ static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
     if (p.n == 0)
         return WG_OK;
     const Tune &t = tune();
+    if (kind == kUniformL4 && p.seg <= kSmallMax && t.l4_small_uniform) {
+        // every segment is small: the small-packet kernel, no trade-off
+        const uint32_t mode = t.l4_small_uniform == 2 ? 2u : 3u;  // 1: lane quad per segment, 2: lane per segment
+        const int rc = t.l4_nt ? launch_small<kUniformL4, true>(p, mode, st) : launch_small<kUniformL4, false>(p, mode, st);
+        if (rc != WG_OK)
+            return rc;
+        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+    }
     if (kind != kUniformL4 && t.l4_small) {
         int rc;
         if (kind == kDescL4)
