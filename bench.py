@@ -217,7 +217,43 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
             okbits = 0x03
             bad = int(((verdict & okbits) != okbits).sum().item()) + int(torch.count_nonzero(l4.to(torch.int32)).item())
             v6 = int(((verdict & 0x10) != 0).sum().item())
-            return {"verify_failures": bad, "v6_packets": v6, "v6_expected": int((flags & 1).sum().item())}
+            info = {"verify_failures": bad, "v6_packets": v6, "v6_expected": int((flags & 1).sum().item())}
+            # small packets: the same batch shape with 64-B packets (valid,
+            # mixed v4/v6 x TCP/UDP), wave-per-packet vs lane-per-descriptor
+            # kernel (knob verify_small), bit-exact against each other
+            b64 = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+            wga.synth_fill(b64, seed ^ 64)
+            d64 = wga.synth_desc_stride(n, 64, 64, 1, seed, 0, device=dev)
+            wga.synth_headers(b64, d64, seed, 0)
+            wga.store_l4csum(b64, d64, wga.calc_l4_checksum_desc(b64, d64))
+            v64 = torch.empty(n, dtype=torch.uint8, device=dev)
+            l64 = torch.empty(n, dtype=torch.uint16, device=dev)
+            saved = wga.tune_get("verify_small")
+            small, ref = {}, None
+            for kname, knob in (("wave_per_packet", 0), ("lane_per_descriptor", 1)):
+                wga.tune_set("verify_small", knob)
+                for _ in range(10):
+                    wga.verify_desc(b64, d64, verdict=v64, l4=l64)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
+                e0.record()
+                for _ in range(30):
+                    wga.verify_desc(b64, d64, verdict=v64, l4=l64)
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / 30
+                got = (v64.cpu().numpy(), l64.cpu().numpy())
+                ref = got if ref is None else ref
+                small[kname] = {"kernel_ms": round(ms, 5), "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
+                                "GiB_s": round(n * 64 / (ms * 1e-3) / 2**30, 1),
+                                "roofline_frac": round(n * (64 + 16 + 3) / (ms * 1e-3) / 8e12, 4),
+                                "all_pass": bool(((got[0] & 3) == 3).all() and not got[1].any()),
+                                "bit_exact_vs_wave_kernel": bool(np.array_equal(got[0], ref[0])
+                                                                 and np.array_equal(got[1], ref[1]))}
+            wga.tune_set("verify_small", saved)
+            info["small_64B"] = {"packets": n, **small}
+            del b64, d64, v64, l64
+            return info
 
         def sample(npk):
             d = desc[:npk].cpu().numpy()

@@ -432,41 +432,19 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t j) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
 }
 
-// H: header bytes 0-31 ride in the L4 byte gather's idle lanes (issue<.., kHdr>)
-// and the summed region starts at byte 32 — no separate header load; else a
-// byte load of header bytes 0-39 per packet and the region from byte 40.
-template <int P, int O = 0, int DM = 0, bool H = false>  // O: waves/SIMD target (0 = compiler's choice); DM: descriptor mode 0 / 2
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_kernel(
-    VerifyParams p) {
-    const uint32_t lane = lane_id();
-    const uint64_t wave0 = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
-    const uint64_t step = (uint64_t)gridDim.x * 4u * P;
+// One group of P packets by the whole wave: ISSUE (header bytes and the
+// packet bytes from 32 / 40 on), then `mid` (the caller's descriptor
+// prefetch), then decode + finish; packet j's verdict and L4 result land in
+// lane tgt[j]'s rv / rc.  Shared by verify_kernel and the long packets of
+// verify_small_kernel.
+template <int P, bool H, typename Mid>
+__device__ __forceinline__ void verify_group(const uint8_t *base, const uint64_t *doff, const uint32_t *len,
+                                             const uint32_t *tgt, uint32_t lane, uint32_t &rv, uint32_t &rc,
+                                             Mid mid) {
     const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
-    // DM 2 (as the descriptor-batch L4 kernel): the next iteration's
-    // descriptors by one vector load, in flight during this one's finish.
-    // DM 0: one iteration per wave (the launcher covers the batch).
-    v4u nextd = v4u{0, 0, 0, 0};
-    bool have_next = false;
-    for (uint64_t i0 = wave0 * P; i0 < p.n; i0 += step) {
-    uint32_t len[P], hv[P];
-    uint64_t doff[P];
-    if (DM == 2 && have_next) {
-#pragma unroll
-        for (int j = 0; j < P; j++) {
-            doff[j] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)nextd.x, j) |
-                      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)nextd.y, j) << 32);
-            len[j] = i0 + j < p.n ? (uint32_t)__builtin_amdgcn_readlane((int)nextd.z, j) : 0u;
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < P; j++) {
-            const wg_pkt_desc d = p.desc[i0 + j < p.n ? i0 + j : p.n - 1];
-            doff[j] = d.offset;
-            len[j] = i0 + j < p.n ? d.len : 0u;
-        }
-    }
     Geom g[P];
     Front f[P];
+    uint32_t hv[P];
     // ISSUE, before any header is decoded: header bytes 0-39 one per lane,
     // and bytes [40, len) — inside the L4 region for IPv4 (ihs 20) and IPv6
     // (ihs 40) alike — through the L4 wave's issue phase.  Decoding first
@@ -475,7 +453,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
     // read lies inside the descriptor's packet.)
 #pragma unroll
     for (int j = 0; j < P; j++) {
-        const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + doff[j];
+        const uintptr_t a = reinterpret_cast<uintptr_t>(base) + doff[j];
         g[j].a = a;
         g[j].fl = 0;
         if constexpr (H) {
@@ -493,13 +471,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
             issue<false, true>(g[j], lane, f[j]);
         }
     }
-    if constexpr (DM == 2) {
-        have_next = i0 + step < p.n;
-        const uint64_t di = (have_next ? i0 + step : i0) + (lane & (uint32_t)(P - 1));
-        nextd = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (di < p.n ? di : p.n - 1));
-    }
+    mid();
     // decode (wave-uniform) and finish every packet
-    uint32_t rv = 0, rc = 0;
 #pragma unroll
     for (int j = 0; j < P; j++) {
         const uint32_t L = len[j];
@@ -558,11 +531,58 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
             if (c == 0)
                 v |= WG_VERDICT_L4_OK;
         }
-        if (lane == (uint32_t)j) {
+        if (lane == tgt[j]) {
             rv = v;
             rc = c;
         }
     }
+}
+
+// H: header bytes 0-31 ride in the L4 byte gather's idle lanes (issue<.., kHdr>)
+// and the summed region starts at byte 32 — no separate header load; else a
+// byte load of header bytes 0-39 per packet and the region from byte 40.
+template <int P, int O = 0, int DM = 0, bool H = false>  // O: waves/SIMD target (0 = compiler's choice); DM: descriptor mode 0 / 2
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_kernel(
+    VerifyParams p) {
+    const uint32_t lane = lane_id();
+    const uint64_t wave0 = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
+    const uint64_t step = (uint64_t)gridDim.x * 4u * P;
+    const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
+    // DM 2 (as the descriptor-batch L4 kernel): the next iteration's
+    // descriptors by one vector load, in flight during this one's finish.
+    // DM 0: one iteration per wave (the launcher covers the batch).
+    v4u nextd = v4u{0, 0, 0, 0};
+    bool have_next = false;
+    for (uint64_t i0 = wave0 * P; i0 < p.n; i0 += step) {
+    uint32_t len[P];
+    uint64_t doff[P];
+    if (DM == 2 && have_next) {
+#pragma unroll
+        for (int j = 0; j < P; j++) {
+            doff[j] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)nextd.x, j) |
+                      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)nextd.y, j) << 32);
+            len[j] = i0 + j < p.n ? (uint32_t)__builtin_amdgcn_readlane((int)nextd.z, j) : 0u;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < P; j++) {
+            const wg_pkt_desc d = p.desc[i0 + j < p.n ? i0 + j : p.n - 1];
+            doff[j] = d.offset;
+            len[j] = i0 + j < p.n ? d.len : 0u;
+        }
+    }
+    uint32_t rv = 0, rc = 0;
+    uint32_t tgt[P];
+#pragma unroll
+    for (int j = 0; j < P; j++)
+        tgt[j] = (uint32_t)j;
+    verify_group<P, H>(p.base, doff, len, tgt, lane, rv, rc, [&]() {
+        if constexpr (DM == 2) {
+            have_next = i0 + step < p.n;
+            const uint64_t di = (have_next ? i0 + step : i0) + (lane & (uint32_t)(P - 1));
+            nextd = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (di < p.n ? di : p.n - 1));
+        }
+    });
     if (lane < (uint32_t)P && i0 + lane < p.n) {
         p.verdict[i0 + lane] = (uint8_t)rv;
         if (p.l4)
@@ -577,6 +597,126 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
 
 using namespace wg;
 
+// Small-packet verify (knob verify_small; the same split as
+// l4csum_small_kernel): a lane per descriptor.  A packet of <= kSmallMax
+// bytes is decoded and summed in its lane from its five aligned 16-B chunks,
+// funnel-shifted (v_alignbyte) into 16 packet-relative dwords R[0..15] with
+// the bytes past the packet zeroed, so every gate field sits at a static
+// byte position and every summed range (header [0, 20), L4 [ihs, len), the
+// addresses) starts at an even packet offset: packet pairing throughout, as
+// the reference pairs them.  The wave then takes the lanes with longer
+// packets Q at a time through verify_group.
+__device__ __forceinline__ uint32_t bytes_below(uint32_t w, uint32_t m, uint32_t lim) {
+    const int k = (int)lim - 4 * (int)m;  // bytes of dword m at packet positions < lim
+    return k >= 4 ? w : (k <= 0 ? 0u : (w & ((1u << (8 * k)) - 1u)));
+}
+
+template <int Q>
+__global__ __launch_bounds__(256) void verify_small_kernel(VerifyParams p) {
+    const uint32_t lane = lane_id();
+    const uint64_t i = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 256u + threadIdx.x;
+    const bool live = i < p.n;
+    const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0));
+    const uint32_t len = live ? dv.z : 0u;
+    const uint32_t olo = live ? dv.x : 0u, ohi = live ? dv.y : 0u;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)ohi << 32) | olo);
+    const bool small = len <= kSmallMax;
+    uint32_t rv = 0, rc = 0;
+    if (__ballot(live && small)) {
+        const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
+        const uintptr_t a0 = a & ~(uintptr_t)15;
+        const uintptr_t alast = (a + len - 1) & ~(uintptr_t)15;
+        const bool any = small && len;
+        v4u W[5];
+#pragma unroll
+        for (uint32_t c = 0; c < 5; c++) {
+            const uintptr_t ca = a0 + 16u * c;
+            W[c] = ld16(any ? (ca > alast ? alast : ca) : zero);  // clamped chunks lie past the packet: zeroed below
+        }
+        const uint32_t Wd[20] = {W[0][0], W[0][1], W[0][2], W[0][3], W[1][0], W[1][1], W[1][2], W[1][3],
+                                 W[2][0], W[2][1], W[2][2], W[2][3], W[3][0], W[3][1], W[3][2], W[3][3],
+                                 W[4][0], W[4][1], W[4][2], W[4][3]};
+        const uint32_t s = (uint32_t)(a & 15u), q4 = s >> 2, sh = s & 3u;
+        uint32_t R[16];
+#pragma unroll
+        for (uint32_t m = 0; m < 16; m++) {
+            const uint32_t lo = q4 == 0 ? Wd[m] : q4 == 1 ? Wd[m + 1] : q4 == 2 ? Wd[m + 2] : Wd[m + 3];
+            const uint32_t hi = q4 == 0 ? Wd[m + 1] : q4 == 1 ? Wd[m + 2] : q4 == 2 ? Wd[m + 3] : Wd[m + 4];
+            R[m] = bytes_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, len);
+        }
+        uint32_t v = 0, c = 0;
+        if (len >= 1) {
+            const uint32_t b0 = R[0] & 0xffu;
+            const bool v6 = (b0 >> 4) == 6;
+            if (v6)
+                v |= WG_VERDICT_V6;
+            const uint32_t ihs = v6 ? 40u : 20u;
+            bool ip_ok = false;
+            uint32_t proto = 0;
+            if (len >= ihs) {  // evaluator.hpp:118-121 (len <= 64 here)
+                if (!v6) {
+                    const uint32_t hs = half_sum(R[0]) + half_sum(R[1]) + half_sum(R[2]) + half_sum(R[3]) +
+                                        half_sum(R[4]);
+                    ip_ok = (b0 & 0xfu) == 5u &&                                  // ip_hl, evaluator.cpp:19
+                            len == bswap16(R[0] >> 16) &&                          // ip_len, :21
+                            (bswap16(R[1] >> 16) & ~0x4000u) == 0 &&              // ip_off & ~IP_DF, :24
+                            fold16_32(hs) == 0xffffu;                             // checksum == 0, :27
+                    proto = (R[2] >> 8) & 0xffu;
+                } else {
+                    ip_ok = len - 40u == bswap16(R[1] & 0xffffu);  // ip6_plen, :47
+                    proto = (R[1] >> 16) & 0xffu;
+                }
+            }
+            bool l4 = false;
+            if (ip_ok) {
+                v |= WG_VERDICT_IP_OK;
+                if (proto == 6u) {
+                    v |= WG_VERDICT_TCP;
+                    l4 = len - ihs > 20u;  // evaluator.hpp:61
+                } else if (proto == 17u) {
+                    v |= WG_VERDICT_UDP;
+                    l4 = len - ihs > 8u;  // evaluator.hpp:91
+                }
+            }
+            if (l4) {  // calc_l4_checksum(pkt, isv6, istcp, ihs), checksum.cpp:8-36
+                uint32_t sum = (proto << 8) + bswap16((len - ihs) & 0xffffu);
+#pragma unroll
+                for (uint32_t m = 2; m < 16; m++) {
+                    const bool in_l4 = 4u * m >= ihs;
+                    const bool in_addr = v6 ? m < 10u : (m == 3u || m == 4u);  // v6 bytes 8-39, v4 12-19
+                    sum += (in_l4 ? half_sum(R[m]) : 0u) + (in_addr ? half_sum(R[m]) : 0u);
+                }
+                c = ~fold16_32(sum) & 0xffffu;
+                if (c == 0)
+                    v |= WG_VERDICT_L4_OK;
+            }
+        }
+        rv = v;
+        rc = c;
+    }
+    // the longer packets of this wave, Q at a time
+    uint64_t m = __ballot(live && !small);
+    while (m) {
+        uint64_t doff[Q];
+        uint32_t ln[Q], tgt[Q];
+#pragma unroll
+        for (int k = 0; k < Q; k++) {
+            const bool have = m != 0;
+            const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
+            m = have ? m & (m - 1) : m;
+            tgt[k] = have ? j : 64u;
+            doff[k] = have ? (((uint64_t)rdl(ohi, j) << 32) | rdl(olo, j)) : 0u;
+            ln[k] = have ? rdl(len, j) : 0u;
+        }
+        verify_group<Q, true>(p.base, doff, ln, tgt, lane, rv, rc, [] {});
+    }
+    if (live) {
+        p.verdict[i] = (uint8_t)rv;
+        if (p.l4)
+            p.l4[i] = (uint16_t)rc;
+    }
+}
+
 extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_desc, uint64_t n,
                               uint8_t *dev_verdict, uint16_t *dev_l4, void *stream) {
     if (!n)
@@ -585,6 +725,14 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
         return WG_ERR_INVALID;
     VerifyParams p{dev_base, dev_desc, dev_verdict, dev_l4, n};
     const Tune &t = tune();
+    if (t.verify_small) {
+        const uint64_t sb = (n + 255) / 256;
+        if (sb > 0x7fffffffull)
+            return WG_ERR_INVALID;
+        hipLaunchKernelGGL((verify_small_kernel<4>), dim3((unsigned)sb), dim3(256), 0, static_cast<hipStream_t>(stream),
+                           p);
+        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+    }
     const bool pf = t.verify_dm == 2;
     uint64_t blocks = (n + 15) / 16;
     if (pf) {
