@@ -392,8 +392,11 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
         su = wga.tune_get("l4_small_uniform")
         res = {}
         ref = None
-        for kname, knob in (("wave_per_packet", 0), ("small_kernel_quad", 1), ("small_kernel_lane", 2)):
+        nt0 = wga.tune_get("l4_nt")
+        for kname, knob, nt in (("wave_per_packet", 0, nt0), ("small_kernel_quad", 1, nt0),
+                                ("small_kernel_lane", 2, nt0)):
             wga.tune_set("l4_small_uniform", knob)
+            wga.tune_set("l4_nt", nt)
             for _ in range(10):
                 wga.calc_l4_checksum_batch(b64, 64, False, False, 20, out=o64)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -411,6 +414,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                           "roofline_frac": round(n64 * 66 / (ms * 1e-3) / 8e12, 4),
                           "bit_exact_vs_wave_kernel": bool(np.array_equal(got, ref))}
         wga.tune_set("l4_small_uniform", su)
+        wga.tune_set("l4_nt", nt0)
         sub["uniform_64B"] = {"packets": n64, **res}
         del b64, o64
         return {"sub_batches": sub}
