@@ -634,6 +634,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
 
 using namespace wg;
 
+namespace wg {
+
 // Small-packet verify (knob verify_small; the same split as
 // l4csum_small_kernel): a lane per descriptor.  A packet of <= kSmallMax
 // bytes is decoded and summed in its lane from its five aligned 16-B chunks,
@@ -749,6 +751,8 @@ __global__ __launch_bounds__(256) void verify_small_kernel(VerifyParams p) {
             p.l4[i] = (uint16_t)rc;
     }
 }
+
+}  // namespace wg
 
 extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_desc, uint64_t n,
                               uint8_t *dev_verdict, uint16_t *dev_l4, void *stream) {
