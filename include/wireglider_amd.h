@@ -276,8 +276,9 @@ int wg_device_count(void);
  *   "verify_occ" verify waves/SIMD target (0 = compiler, 6, 8)
  *   "verify_hdr" verify header bytes from the L4 byte gather (1) or a
  *                separate byte load (0)
- *   "verify_small" verify by the lane-per-descriptor kernel: packets of
- *                <= 64 B decoded in one lane, longer ones by the wave (0, 1)
+ *   "verify_small" verify by the small-packet kernel: packets of <= 64 B
+ *                decoded in one lane (1) or redundantly in a lane quad (2),
+ *                longer ones by the wave; 0 = wave-per-packet kernel
  *   "gro_lds", "gro_wide"  GRO finalize: LDS-staged loads, wide field stores
  *   "gro_chunks" 16-B header chunks staged per flow (4, 5; with 4, headers
  *                over 48 bytes take the byte path)

@@ -646,10 +646,15 @@ namespace wg {
 // the reference pairs them.  The wave then takes the lanes with longer
 // packets Q at a time through verify_group.
 
-template <int Q>
+// G = 4: a lane quad per descriptor, every lane of it decoding the same
+// packet (its loads hit the same addresses): a wave owns 16 descriptors, so
+// its serial walk over the long packets is 4 groups instead of 16.
+template <int Q, int G = 1>
 __global__ __launch_bounds__(256) void verify_small_kernel(VerifyParams p) {
+    static_assert(G == 1 || G == 4, "lanes per descriptor");
     const uint32_t lane = lane_id();
-    const uint64_t i = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 256u + threadIdx.x;
+    const uint32_t q = lane & (uint32_t)(G - 1);
+    const uint64_t i = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * (256u / G) + threadIdx.x / G;
     const bool live = i < p.n;
     const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0));
     const uint32_t len = live ? dv.z : 0u;
@@ -730,7 +735,7 @@ __global__ __launch_bounds__(256) void verify_small_kernel(VerifyParams p) {
         rc = c;
     }
     // the longer packets of this wave, Q at a time
-    uint64_t m = __ballot(live && !small);
+    uint64_t m = __ballot(live && !small && q == 0);
     while (m) {
         uint64_t doff[Q];
         uint32_t ln[Q], tgt[Q];
@@ -745,7 +750,7 @@ __global__ __launch_bounds__(256) void verify_small_kernel(VerifyParams p) {
         }
         verify_group<Q, true>(p.base, doff, ln, tgt, lane, rv, rc, [] {});
     }
-    if (live) {
+    if (live && q == 0) {
         p.verdict[i] = (uint8_t)rv;
         if (p.l4)
             p.l4[i] = (uint16_t)rc;
@@ -763,11 +768,16 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
     VerifyParams p{dev_base, dev_desc, dev_verdict, dev_l4, n};
     const Tune &t = tune();
     if (t.verify_small) {
-        const uint64_t sb = (n + 255) / 256;
+        const uint64_t per_block = t.verify_small == 2 ? 64u : 256u;  // descriptors per 256-thread block
+        const uint64_t sb = (n + per_block - 1) / per_block;
         if (sb > 0x7fffffffull)
             return WG_ERR_INVALID;
-        hipLaunchKernelGGL((verify_small_kernel<4>), dim3((unsigned)sb), dim3(256), 0, static_cast<hipStream_t>(stream),
-                           p);
+        if (t.verify_small == 2)
+            hipLaunchKernelGGL((verify_small_kernel<4, 4>), dim3((unsigned)sb), dim3(256), 0,
+                               static_cast<hipStream_t>(stream), p);
+        else
+            hipLaunchKernelGGL((verify_small_kernel<4>), dim3((unsigned)sb), dim3(256), 0,
+                               static_cast<hipStream_t>(stream), p);
         return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
     }
     const bool pf = t.verify_dm == 2;
