@@ -191,14 +191,16 @@ static void launch_kind(const L4Params &p, uint64_t blocks, uint32_t P, bool nt,
 // Small-packet descriptor kernel (knob l4_small; SURVEY §8(d) config 4's
 // small-packet stress).  A wave per packet spends ~150 wave-instructions
 // (half of them on the CU's one scalar unit) on a 64-B packet, so 64-B
-// batches are issue-bound at ~6 % of the HBM roofline.  Here a THREAD takes
-// one descriptor: a packet of <= kSmallMax bytes is summed in its own lane
-// from (at most) five aligned 16-B chunks, masked per dword to the summed
-// region and to the pseudo-header address bytes; the lanes whose packet is
-// longer are then taken by the whole wave, two at a time, through the same
-// issue / finish machinery as l4csum_kernel.  Same arithmetic model
-// (wg_device.hpp): absolute-address pairing, one byte swap of a folded sum
-// whose pairing starts at an odd address.
+// batches are issue-bound at ~6 % of the HBM roofline.  Here a lane (or a
+// lane quad, G below) takes one descriptor: a packet of <= kSmallMax bytes is
+// summed from (at most) five aligned 16-B chunks — by a lane as 16
+// packet-relative dwords funnel-shifted out of them, by a quad as masked
+// absolute dwords — over the summed region and the pseudo-header address
+// bytes; the lanes whose packet is longer are then taken by the whole wave,
+// Q at a time, through the same issue / finish machinery as l4csum_kernel.
+// Uniform PacketBatches with segment_size <= kSmallMax use it too (every
+// segment is small).  Same arithmetic model (wg_device.hpp): one byte swap of
+// a folded sum whose pairing starts at an odd position.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSmallMax = 64;  // bytes: five aligned 16-B chunks at any alignment
 
