@@ -587,7 +587,7 @@ def post_checks(torch, wga, wl: Workload, world: int, dev):
     if wl.out is None:
         return info
     torch.cuda.synchronize()
-    h = wdist.allreduce_hash(wdist.result_hash(wl.out, wl.first_index))
+    h = wdist.allreduce_hash(wdist.result_hash(wl.out, wl.first_index), device=dev)
     info["result_hash"] = h
     t0 = time.perf_counter()
     full = wdist.gather_results(wl.out, wl.counts)

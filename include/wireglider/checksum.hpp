@@ -12,10 +12,11 @@
 // Placement: the header-inline pieces stay header-inline and run
 // where the caller runs (each is a 20-40 byte fixed-size sum; a device launch
 // would cost more than it saves).  calc_l4_checksum — the reference's only
-// out-of-line symbol (checksum.cpp:8) — is exported by libwireglider_amd.so
-// and goes to the MI355X through the C ABI (include/wireglider_amd.h).  Batch
-// callers should use the wireglider::gpu:: entry points below, which take
-// whole PacketBatch-shaped batches in device memory.
+// out-of-line symbol (checksum.cpp:8) — is exported by libwireglider_amd.so;
+// a per-call caller gets its answer on the CPU (host::calc_l4_checksum), and
+// batch callers use the wireglider::gpu:: entry points below, which take
+// whole PacketBatch-shaped batches in device memory to the MI355X through the
+// C ABI (include/wireglider_amd.h).
 //
 // No boost / fastcsum dependency: the nofold and fold primitives are this
 // repository's own (clean-room) with the same contract.
@@ -173,11 +174,48 @@ static inline uint16_t checksum(std::span<const uint8_t> b, uint64_t initial) {
     return checksum_impl::fold_complement(checksum_impl::checksum_nofold(b, initial));
 }
 
+namespace host {
+
+// checksum.cpp:8-36 on the calling CPU: the pseudo-header over the addresses
+// (v4 bytes 12-19, v6 8-39; :14-28) with l4Len = (uint16_t)(len - csum_start)
+// (:23,33), seeded into checksum(ippkt[csum_start:]) (:35).  Inputs the
+// reference leaves undefined (a packet shorter than its addresses, or than
+// csum_start) get the GPU kernels' definition: bytes past the packet are
+// absent (zero) and the summed region is empty — so host and device agree on
+// every input.
+inline uint16_t calc_l4_checksum(std::span<const uint8_t> p, bool isv6, bool istcp, uint16_t csum_start) {
+    using namespace checksum_impl;
+    const uint8_t proto = istcp ? 6 : 17;
+    const size_t ao = isv6 ? 8 : 12, al = isv6 ? 16 : 4;
+    const uint16_t l4len = static_cast<uint16_t>(p.size() - csum_start);
+    const uint8_t *a = p.data() + ao;
+    std::array<uint8_t, 32> pad{};
+    if (p.size() < ao + 2 * al) {  // out of contract: missing address bytes are absent
+        if (p.size() > ao)
+            std::memcpy(pad.data(), p.data() + ao, p.size() - ao);
+        a = pad.data();
+    }
+    const uint64_t ph =
+        isv6 ? pseudo_header_checksum_nofold(proto, std::span<const uint8_t, 16>(a, 16),
+                                             std::span<const uint8_t, 16>(a + 16, 16), l4len)
+             : pseudo_header_checksum_nofold(proto, std::span<const uint8_t, 4>(a, 4),
+                                             std::span<const uint8_t, 4>(a + 4, 4), l4len);
+    const size_t o0 = csum_start < p.size() ? csum_start : p.size();
+    return checksum(p.subspan(o0), ph);
+}
+
+}  // namespace host
+
 // include/netio/checksum.hpp:151 / checksum.cpp:8 — exported by
-// libwireglider_amd.so; computed on the GPU (one-packet batch through the
-// host-memory path).  Aborts with a message if no GPU / the engine fails:
-// the reference has no error channel and a wrong checksum must never be
-// returned silently.
+// libwireglider_amd.so with the reference's mangled name.  Per-call callers
+// (worker/offload.cpp:75,202, include/worker/evaluator.hpp:64,93) use its
+// return value immediately, one packet at a time, so it computes on the
+// calling CPU (host::calc_l4_checksum above: ~0.1 us for 1500 B, against
+// tens of us for a device round trip).  WG_PERCALL=gpu in the environment
+// sends each call through the host-memory GPU path instead (tests, latency
+// measurement); if that path fails (no device, runtime error) the call is
+// answered on the host — never an abort, never a different checksum.  Batches
+// go to the GPU through wireglider::gpu:: below.
 uint16_t calc_l4_checksum(std::span<const uint8_t> thispkt, bool isv6, bool istcp, uint16_t csum_start);
 
 namespace gpu {

@@ -251,7 +251,7 @@ int wg_device_count(void);
 /* Launch-geometry knobs.  Each key is also read once, at the first launch,
  * from the environment as WG_<KEY> (e.g. WG_L4_PPW=2); the environment and
  * wg_tune_set accept the same values and ignore / reject (WG_ERR_INVALID)
- * anything else.  Results never depend on them (except "gso_ablate").
+ * anything else.  Results never depend on them.
  *   "l4_blocks"  grid cap of the L4 kernels (1 .. 2^20)
  *   "l4_ppw"     packets per wave iteration (1, 2, 4, 8)
  *   "l4_nt"      non-temporal packet loads (0, 1)
@@ -282,10 +282,9 @@ int wg_device_count(void);
  *   "gro_lds", "gro_wide"  GRO finalize: LDS-staged loads, wide field stores
  *   "gro_chunks" 16-B header chunks staged per flow (4, 5; with 4, headers
  *                over 48 bytes take the byte path)
- *   "gso_ablate" profiling only: 1 = non-temporal payload stores, 32 = no XCD
- *                swizzle (both correct); 2 = timing-only variant whose output
- *                is WRONG; 0 restores the default kernel.
- * Not synchronised with concurrent launches from other threads. */
+ *   "gso_ablate" GSO A/B variants: 1 = non-temporal payload stores, 32 = no
+ *                XCD swizzle (both correct); 0 = the default kernel.
+ * Thread-safe: each launch reads one consistent snapshot of the knobs. */
 int wg_tune_set(const char *key, uint64_t value);
 /* Current value of a wg_tune_set key. */
 int wg_tune_get(const char *key, uint64_t *value);

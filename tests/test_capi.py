@@ -139,11 +139,13 @@ def test_tune_knobs_validate_and_round_trip():
         wga.tune_set(k, v)
         assert wga.tune_get(k) == v
     for k, bad in (("l4_ppw", 3), ("l4_occ", 6), ("gso_groups", 0), ("gso_groups", 65), ("verify_hdr", 2),
-                   ("gso_waves", 16), ("gso_ablate", 7)):
+                   ("gso_waves", 16), ("gso_ablate", 7), ("gso_ablate", 2)):
         v = wga.tune_get(k)
         with pytest.raises(Exception):
             wga.tune_set(k, bad)
         assert wga.tune_get(k) == v
+    # the library ships no wrong-output variant (round-1 gso_ablate = 2 removed)
+    assert wga.lib.wg_tune_set(b"gso_ablate", 2) == -1
     with pytest.raises(Exception):
         wga.tune_get("no_such_knob")
     v = wga.tune_get("l4_nt")
@@ -160,8 +162,10 @@ def test_tune_environment_overrides():
 
     code = ("import wireglider_amd as w; print(w.tune_get('l4_nt'), w.tune_get('gso_groups'), "
             "w.tune_get('l4_ppw'), w.tune_get('verify_hdr'))")
-    env = dict(os.environ, WG_L4_NT="0", WG_GSO_GROUPS="5", WG_L4_PPW="3", WG_VERIFY_HDR="0x0")
+    code += "; print(w.tune_get('gso_ablate'))"
+    env = dict(os.environ, WG_L4_NT="0", WG_GSO_GROUPS="5", WG_L4_PPW="3", WG_VERIFY_HDR="0x0", WG_GSO_ABLATE="2")
     out = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT, capture_output=True, text=True, check=True)
-    nt, groups, ppw, hdr = map(int, out.stdout.split())
+    nt, groups, ppw, hdr, abl = map(int, out.stdout.split())
     assert (nt, groups, hdr) == (0, 5, 0)
+    assert abl == 0  # WG_GSO_ABLATE=2 is not an accepted value: ignored
     assert ppw == 4  # 3 is not an accepted value: default kept

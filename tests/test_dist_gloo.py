@@ -17,6 +17,14 @@ import torch.multiprocessing as mp
 from wireglider_amd import dist as wdist
 
 
+BIG_OFFSET = (1 << 39) + 12345
+
+
+def exact_hash(values, offset: int) -> int:
+    """The hash's definition in Python integers (no overflow possible)."""
+    return sum((offset + 1 + i) * (int(x) + 1) for i, x in enumerate(values)) % wdist.HASH_MOD
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -58,9 +66,11 @@ def _worker(rank, world, port, n, q):
         local = torch.from_numpy(oracle.l4_desc(buf, d[lo:hi], threads=1).astype(np.int32)).to(torch.uint16)
         full = wdist.gather_results(local, [b - a for a, b in bounds])
         h = wdist.allreduce_hash(wdist.result_hash(local, lo))
+        # far from zero: per-rank hashes near 2^61 must not overflow the reduction
+        h_big = wdist.allreduce_hash(wdist.result_hash(local, lo + BIG_OFFSET))
         t = wdist.max_over_ranks(float(rank + 1))
         if rank == 0:
-            q.put((full.numpy().astype(np.uint16).tobytes(), h, t, bounds))
+            q.put((full.numpy().astype(np.uint16).tobytes(), h, h_big, t, bounds))
     finally:
         dist.destroy_process_group()
 
@@ -76,7 +86,7 @@ def test_sharded_equals_single_process(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
     for p in procs:
         p.start()
-    full_bytes, h, t, bounds = q.get(timeout=240)
+    full_bytes, h, h_big, t, bounds = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -84,7 +94,8 @@ def test_sharded_equals_single_process(world):
     ref = oracle.l4_desc(buf, d)
     got = np.frombuffer(full_bytes, dtype=np.uint16)
     np.testing.assert_array_equal(got, ref)
-    assert h == wdist.result_hash(torch.from_numpy(ref.astype(np.int32)), 0).item() % wdist.HASH_MOD
+    assert h == wdist.result_hash(torch.from_numpy(ref.astype(np.int32)), 0) == exact_hash(ref, 0)
+    assert h_big == exact_hash(ref, BIG_OFFSET)
     assert t == float(world)
     # byte balance: each shard within one max-size packet of the mean
     per = [int(d["len"][a:b].astype(np.int64).sum()) for a, b in bounds]
@@ -109,6 +120,25 @@ def test_shard_bounds_properties():
 
 def test_hash_is_split_invariant():
     v = torch.randint(0, 65536, (1000,), dtype=torch.int32).to(torch.uint16)
-    whole = wdist.result_hash(v, 0).item()
-    parts = (wdist.result_hash(v[:300], 0) + wdist.result_hash(v[300:], 300)).item() % wdist.HASH_MOD
-    assert whole == parts
+    whole = wdist.result_hash(v, 0)
+    parts = (wdist.result_hash(v[:300], 0) + wdist.result_hash(v[300:], 300)) % wdist.HASH_MOD
+    assert whole == parts == exact_hash(v.to(torch.int32).numpy(), 0)
+
+
+def test_hash_exact_at_large_shards_and_offsets():
+    """Shard sizes and offsets where a plain int64 sum of (index * value)
+    would wrap (2^22 packets per rank at 8 ranks): block sums and
+    20-bit index halves keep it exact."""
+    rng = np.random.default_rng(3)
+    v = torch.from_numpy(rng.integers(60000, 65536, 1 << 22).astype(np.int32)).to(torch.uint16)
+    for off in (0, 7 << 22, (1 << 39) + 1):
+        vv = v.to(torch.int64) + 1
+        i = torch.arange(vv.numel(), dtype=torch.int64)
+        # exact reference: sum (off+1+i) v_i = (off+1) sum v_i + sum i v_i, each
+        # int64 sum < 2^61 here, combined as Python integers
+        ref = ((off + 1) * int(vv.sum()) + int((vv * i).sum())) % wdist.HASH_MOD
+        assert wdist.result_hash(v, off) == ref
+    # split invariance across a 2^24 block boundary
+    w = v[: (1 << 22)]
+    assert (wdist.result_hash(w[:12345], 5 << 30) + wdist.result_hash(w[12345:], (5 << 30) + 12345)) % \
+        wdist.HASH_MOD == wdist.result_hash(w, 5 << 30)

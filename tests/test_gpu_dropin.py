@@ -1,8 +1,12 @@
 """The C++ drop-in end to end on the GPU: a program compiled against
 include/wireglider/checksum.hpp and linked to libwireglider_amd.so through the
-reference's symbol wireglider::calc_l4_checksum (checksum.cpp:8) returns the
+reference's symbol wireglider::calc_l4_checksum (checksum.cpp:8), with
+WG_PERCALL=gpu (every call through the host-memory GPU path), returns the
 RFC textbook checksum for every packet, and verify-to-zero holds for the
-reference test's packets (tests/test-checksum.cpp:53-82)."""
+reference test's packets (tests/test-checksum.cpp:53-82).  The per-call
+latency of both placements is printed for DESIGN.md."""
+import json
+import os
 import struct
 import subprocess
 from pathlib import Path
@@ -45,7 +49,26 @@ def test_dropin_calc_l4_checksum_on_gpu(gpu, tmp_path):
         recs.append((p, isv6, istcp, cs))
         exp.append(textbook.l4_checksum_native(p, isv6, istcp, cs))
     blob = b"".join(struct.pack("<IBBH", len(p), v6, tcp, cs) + p for p, v6, tcp, cs in recs)
-    r = subprocess.run([str(exe)], input=blob, capture_output=True, timeout=300)
+    r = subprocess.run([str(exe)], input=blob, capture_output=True, timeout=300,
+                       env=dict(os.environ, WG_PERCALL="gpu"))
     assert r.returncode == 0, r.stderr.decode()
     got = [int(x, 16) for x in r.stdout.decode().split()]
     assert got == exp
+
+
+def test_percall_latency_both_placements(gpu, tmp_path):
+    exe = tmp_path / "percall_latency"
+    lib = ROOT / "wireglider_amd" / "lib"
+    subprocess.run(["g++", "-std=c++20", "-O2", f"-I{ROOT / 'include'}",
+                    str(ROOT / "tests" / "cpp" / "percall_latency.cpp"), f"-L{lib}", "-lwireglider_amd",
+                    f"-Wl,-rpath,{lib}", "-o", str(exe)], check=True)
+    res = {}
+    for mode, reps in (("host", 20000), ("gpu", 500)):
+        env = {k: v for k, v in os.environ.items() if k != "WG_PERCALL"}
+        if mode == "gpu":
+            env["WG_PERCALL"] = "gpu"
+        r = subprocess.run([str(exe), str(reps)], capture_output=True, text=True, timeout=300, env=env, check=True)
+        res[mode] = json.loads(r.stdout)
+    print("percall_latency", json.dumps(res))
+    assert res["host"]["results"] == res["gpu"]["results"]  # same answers from both placements
+    assert res["host"]["ns_per_call_1500B"] < res["gpu"]["ns_per_call_1500B"]

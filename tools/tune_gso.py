@@ -43,13 +43,13 @@ def main():
              "GBps_med": round(alg / (statistics.median(t) * 1e-3) / 1e9, 1)} for v, t in res.items()]
     rows.sort(key=lambda r: r["ms_med"])
     out = {"workload": "config3", "alg_bytes": alg, "variants": rows}
-    # ablations (timing only) and a torch device-to-device copy of the same bytes
+    # A/B variants and a torch device-to-device copy of the same bytes
     best = rows[0]
     wga.tune_set("gso_waves", 4)
     wga.tune_set("gso_spw", best["spw"])
     wga.tune_set("gso_groups", best["groups"])
     abl = {}
-    for a in (0, 1, 2, 32):
+    for a in (0, 1, 32):
         wga.tune_set("gso_ablate", a)
         launch()
         ts = []
@@ -63,7 +63,7 @@ def main():
             ts += [e0.elapsed_time(e1) for e0, e1 in ev]
         abl[a] = round(statistics.median(ts), 3)
     wga.tune_set("gso_ablate", 0)
-    out["ablation_ms"] = {"0 real": abl[0], "1 nt stores (correct variant)": abl[1], "2 no byte stores": abl[2],
+    out["ablation_ms"] = {"0 real": abl[0], "1 nt stores (correct variant)": abl[1],
                           "32 launch-order blocks (correct variant)": abl[32]}
     src = torch.empty(17_179_869_184 // 16 * 16 // 2, dtype=torch.int16, device=dev)
     dst = torch.empty_like(src)

@@ -148,11 +148,29 @@ def _torch():
     return torch
 
 
-def _stream_ptr(stream) -> int | None:
+def _stream_ptr(stream, tensor=None) -> int | None:
+    """The launch stream: `stream`, else the current stream of the device
+    that holds `tensor` (not of whichever device happens to be current)."""
     torch = _torch()
     if stream is None:
-        stream = torch.cuda.current_stream()
+        stream = torch.cuda.current_stream(tensor.device if tensor is not None else None)
     return stream.cuda_stream
+
+
+def _on(t):
+    """Launch on the device that holds `t` (HIP launches go to the current
+    device)."""
+    return _torch().cuda.device(t.device)
+
+
+def _check_out(out, n: int, dtype, like, name: str) -> None:
+    """A caller-supplied output must hold n elements of `dtype` on the same
+    device: an undersized tensor would be an out-of-bounds device write."""
+    _require_cuda(out, name)
+    if out.dtype != dtype or out.device != like.device:
+        raise WireGliderError(f"{name}: expected {dtype} on {like.device}, got {out.dtype} on {out.device}")
+    if out.numel() < n:
+        raise WireGliderError(f"{name}: {out.numel()} elements, the batch needs {n}")
 
 
 def _require_cuda(t, name: str):
@@ -179,9 +197,11 @@ def calc_l4_checksum_batch(batch, segment_size: int, isv6: bool, istcp: bool, cs
     n = nr_segments(batch.numel(), segment_size)
     if out is None:
         out = torch.empty(n, dtype=torch.uint16, device=batch.device)
+    _check_out(out, n, torch.uint16, batch, "out")
     flags = (WG_PKT_V6 if isv6 else 0) | (WG_PKT_TCP if istcp else 0)
-    rc = lib.wg_l4csum_uniform(batch.data_ptr(), batch.numel(), segment_size, csum_start, flags,
-                               out.data_ptr(), _stream_ptr(stream))
+    with _on(batch):
+        rc = lib.wg_l4csum_uniform(batch.data_ptr(), batch.numel(), segment_size, csum_start, flags,
+                                   out.data_ptr(), _stream_ptr(stream, batch))
     _check(rc, "wg_l4csum_uniform")
     return out
 
@@ -195,7 +215,9 @@ def calc_l4_checksum_desc(base, desc, out=None, stream=None):
     n = desc.numel() * desc.element_size() // PKT_DESC_BYTES
     if out is None:
         out = torch.empty(n, dtype=torch.uint16, device=base.device)
-    rc = lib.wg_l4csum_desc(base.data_ptr(), desc.data_ptr(), n, out.data_ptr(), _stream_ptr(stream))
+    _check_out(out, n, torch.uint16, base, "out")
+    with _on(base):
+        rc = lib.wg_l4csum_desc(base.data_ptr(), desc.data_ptr(), n, out.data_ptr(), _stream_ptr(stream, base))
     _check(rc, "wg_l4csum_desc")
     return out
 
@@ -208,7 +230,9 @@ def checksum_desc(base, desc, out=None, stream=None):
     n = desc.numel() * desc.element_size() // PKT_DESC_BYTES
     if out is None:
         out = torch.empty(n, dtype=torch.uint16, device=base.device)
-    rc = lib.wg_checksum_desc(base.data_ptr(), desc.data_ptr(), n, out.data_ptr(), _stream_ptr(stream))
+    _check_out(out, n, torch.uint16, base, "out")
+    with _on(base):
+        rc = lib.wg_checksum_desc(base.data_ptr(), desc.data_ptr(), n, out.data_ptr(), _stream_ptr(stream, base))
     _check(rc, "wg_checksum_desc")
     return out
 
@@ -229,10 +253,12 @@ def verify_desc(base, desc, with_l4: bool = True, stream=None, verdict=None, l4=
         verdict = torch.empty(n, dtype=torch.uint8, device=base.device)
     if l4 is None and with_l4:
         l4 = torch.empty(n, dtype=torch.uint16, device=base.device)
-    if verdict.numel() < n or (l4 is not None and l4.numel() < n):
-        raise ValueError("verify_desc: output tensors shorter than the descriptor batch")
-    rc = lib.wg_verify_desc(base.data_ptr(), desc.data_ptr(), n, verdict.data_ptr(),
-                            l4.data_ptr() if l4 is not None else None, _stream_ptr(stream))
+    _check_out(verdict, n, torch.uint8, base, "verdict")
+    if l4 is not None:
+        _check_out(l4, n, torch.uint16, base, "l4")
+    with _on(base):
+        rc = lib.wg_verify_desc(base.data_ptr(), desc.data_ptr(), n, verdict.data_ptr(),
+                                l4.data_ptr() if l4 is not None else None, _stream_ptr(stream, base))
     _check(rc, "wg_verify_desc")
     return verdict, l4
 
@@ -246,8 +272,12 @@ def gso_split(inbuf, gso_desc, outbuf, results=None, stream=None):
     n = gso_desc.numel() * gso_desc.element_size() // GSO_DESC_BYTES
     if results is None:
         results = torch.zeros(n * GSO_RESULT_BYTES, dtype=torch.uint8, device=inbuf.device)
-    rc = lib.wg_gso_split(inbuf.data_ptr(), gso_desc.data_ptr(), n, outbuf.data_ptr(),
-                          results.data_ptr(), _stream_ptr(stream))
+    _check_out(results, n * GSO_RESULT_BYTES, torch.uint8, inbuf, "results")
+    if gso_desc.device != inbuf.device or outbuf.device != inbuf.device:
+        raise WireGliderError("gso_split: inbuf, gso_desc and outbuf must be on one device")
+    with _on(inbuf):
+        rc = lib.wg_gso_split(inbuf.data_ptr(), gso_desc.data_ptr(), n, outbuf.data_ptr(),
+                              results.data_ptr(), _stream_ptr(stream, inbuf))
     _check(rc, "wg_gso_split")
     return results
 
@@ -259,7 +289,11 @@ def gro_finalize(hdrs, gro_desc, stream=None):
     for t, nm in ((hdrs, "hdrs"), (gro_desc, "gro_desc")):
         _require_cuda(t, nm)
     n = gro_desc.numel() * gro_desc.element_size() // GRO_DESC_BYTES
-    _check(lib.wg_gro_finalize(hdrs.data_ptr(), gro_desc.data_ptr(), n, _stream_ptr(stream)), "wg_gro_finalize")
+    if gro_desc.device != hdrs.device:
+        raise WireGliderError("gro_finalize: hdrs and gro_desc must be on one device")
+    with _on(hdrs):
+        rc = lib.wg_gro_finalize(hdrs.data_ptr(), gro_desc.data_ptr(), n, _stream_ptr(stream, hdrs))
+    _check(rc, "wg_gro_finalize")
 
 
 def calc_l4_checksum_host(buf: bytes | bytearray | memoryview, segment_size: int, isv6: bool,
@@ -284,29 +318,33 @@ def calc_l4_checksum_host(buf: bytes | bytearray | memoryview, segment_size: int
 
 def synth_fill(buf, seed: int, counter_base: int = 0, stream=None) -> None:
     _require_cuda(buf, "buf")
-    _check(lib.wg_synth_fill(buf.data_ptr(), buf.numel() * buf.element_size(), seed, counter_base,
-                             _stream_ptr(stream)), "wg_synth_fill")
+    with _on(buf):
+        _check(lib.wg_synth_fill(buf.data_ptr(), buf.numel() * buf.element_size(), seed, counter_base,
+                                 _stream_ptr(stream, buf)), "wg_synth_fill")
 
 
 def synth_headers(base, desc, seed: int, index_base: int = 0, stream=None) -> None:
     n = desc.numel() * desc.element_size() // PKT_DESC_BYTES
-    _check(lib.wg_synth_headers(base.data_ptr(), desc.data_ptr(), n, seed, index_base,
-                                _stream_ptr(stream)), "wg_synth_headers")
+    with _on(base):
+        _check(lib.wg_synth_headers(base.data_ptr(), desc.data_ptr(), n, seed, index_base,
+                                    _stream_ptr(stream, base)), "wg_synth_headers")
 
 
 def synth_desc_stride(n: int, stride: int, length: int, mode: int, seed: int, index_base: int = 0,
                       device=None, stream=None):
     torch = _torch()
     desc = torch.empty((n, 2), dtype=torch.int64, device=device or "cuda")
-    _check(lib.wg_synth_desc_stride(desc.data_ptr(), n, stride, length, mode, seed, index_base,
-                                    _stream_ptr(stream)), "wg_synth_desc_stride")
+    with _on(desc):
+        _check(lib.wg_synth_desc_stride(desc.data_ptr(), n, stride, length, mode, seed, index_base,
+                                        _stream_ptr(stream, desc)), "wg_synth_desc_stride")
     return desc
 
 
 def store_l4csum(base, desc, csum, stream=None) -> None:
     n = desc.numel() * desc.element_size() // PKT_DESC_BYTES
-    _check(lib.wg_store_l4csum(base.data_ptr(), desc.data_ptr(), n, csum.data_ptr(),
-                               _stream_ptr(stream)), "wg_store_l4csum")
+    with _on(base):
+        _check(lib.wg_store_l4csum(base.data_ptr(), desc.data_ptr(), n, csum.data_ptr(),
+                                   _stream_ptr(stream, base)), "wg_store_l4csum")
 
 
 def tune_set(key: str, value: int) -> None:
@@ -322,14 +360,17 @@ def tune_get(key: str) -> int:
 
 def probe_read(buf, out, kib_per_wave: int = 4, stream=None) -> None:
     """Launch the read-roofline probe over a device buffer."""
-    _check(lib.wg_probe_read(buf.data_ptr(), buf.numel() * buf.element_size(), out.data_ptr(), kib_per_wave, 0,
-                             _stream_ptr(stream)), "wg_probe_read")
+    with _on(buf):
+        _check(lib.wg_probe_read(buf.data_ptr(), buf.numel() * buf.element_size(), out.data_ptr(), kib_per_wave, 0,
+                                 _stream_ptr(stream, buf)), "wg_probe_read")
 
 
 def probe_copy(src, dst, kib_per_wave: int = 2, stream=None) -> None:
     """Launch the copy-roofline probe (dst = src) over device buffers."""
     n = min(src.numel() * src.element_size(), dst.numel() * dst.element_size())
-    _check(lib.wg_probe_copy(src.data_ptr(), dst.data_ptr(), n, kib_per_wave, _stream_ptr(stream)), "wg_probe_copy")
+    with _on(src):
+        _check(lib.wg_probe_copy(src.data_ptr(), dst.data_ptr(), n, kib_per_wave, _stream_ptr(stream, src)),
+               "wg_probe_copy")
 
 
 def device_count() -> int:

@@ -28,7 +28,7 @@ struct Knob {
 };
 
 static const uint64_t kPpw[] = {1, 2, 4, 8}, kOcc[] = {0, 7, 8}, kVOcc[] = {0, 6, 8}, kDm[] = {0, 2},
-                      kWaves[] = {1, 2, 4, 8}, kAbl[] = {0, 1, 2, 32};
+                      kWaves[] = {1, 2, 4, 8}, kAbl[] = {0, 1, 32};
 #define WG_N(a) (sizeof(a) / sizeof(a[0]))
 static const Knob kKnobs[] = {
     {"l4_blocks", &Tune::l4_blocks, nullptr, 1, 1u << 20, nullptr, 0},
@@ -79,7 +79,11 @@ static bool knob_set(Tune &t, const Knob &k, uint64_t v) {
     return true;
 }
 
-Tune &tune_mut() {
+// The knob table's storage.  Guarded by g_tune_mu: wg_tune_set may run
+// while other host threads launch, so launches take a snapshot (tune()).
+static std::mutex g_tune_mu;
+
+static Tune &tune_storage() {
     static Tune t = [] {
         Tune x;
         // Measured on MI355X (tools/tune_l4.py, profiles/): one iteration per
@@ -133,7 +137,12 @@ Tune &tune_mut() {
     return t;
 }
 
-const Tune &tune() { return tune_mut(); }
+// One consistent copy of every knob per launch: a concurrent wg_tune_set is
+// seen entirely or not at all, never half-applied (and never a data race).
+Tune tune() {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    return tune_storage();
+}
 
 bool debug_sync(hipStream_t st, const char *kernel) {
     static const bool on = [] {
@@ -309,16 +318,17 @@ extern "C" const char *wg_strerror(int code) {
 
 extern "C" int wg_tune_set(const char *key, uint64_t value) {
     const Knob *k = key ? find_knob(key) : nullptr;
-    if (!k || !knob_set(tune_mut(), *k, value))
+    if (!k)
         return WG_ERR_INVALID;
-    return WG_OK;
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    return knob_set(tune_storage(), *k, value) ? WG_OK : WG_ERR_INVALID;
 }
 
 extern "C" int wg_tune_get(const char *key, uint64_t *value) {
     const Knob *k = key ? find_knob(key) : nullptr;
     if (!k || !value)
         return WG_ERR_INVALID;
-    const Tune &t = tune();
+    const Tune t = tune();
     *value = k->f64 ? t.*(k->f64) : (uint64_t)(t.*(k->f32));
     return WG_OK;
 }

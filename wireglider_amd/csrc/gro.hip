@@ -303,13 +303,14 @@ extern "C" int wg_gro_finalize(uint8_t *dev_hdrs, wg_gro_desc *dev_desc, uint64_
     const uint64_t blocks = (n + 255) / 256;
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
-    if (tune().gro_lds && tune().gro_wide && tune().gro_chunks == 4)
+    const Tune t = tune();
+    if (t.gro_lds && t.gro_wide && t.gro_chunks == 4)
         hipLaunchKernelGGL((gro_finalize_lds_kernel<true, 4>), dim3((unsigned)blocks), dim3(kGroBlock), 0,
                            static_cast<hipStream_t>(stream), dev_hdrs, dev_desc, n);
-    else if (tune().gro_lds && tune().gro_wide)
+    else if (t.gro_lds && t.gro_wide)
         hipLaunchKernelGGL(gro_finalize_lds_kernel<true>, dim3((unsigned)blocks), dim3(kGroBlock), 0,
                            static_cast<hipStream_t>(stream), dev_hdrs, dev_desc, n);
-    else if (tune().gro_lds)
+    else if (t.gro_lds)
         hipLaunchKernelGGL(gro_finalize_lds_kernel<false>, dim3((unsigned)blocks), dim3(kGroBlock), 0,
                            static_cast<hipStream_t>(stream), dev_hdrs, dev_desc, n);
     else

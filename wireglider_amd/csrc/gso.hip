@@ -38,14 +38,13 @@ __device__ __forceinline__ void st16_nt(uintptr_t addr, v4u v) {
     __builtin_nontemporal_store(v, reinterpret_cast<__attribute__((address_space(1))) v4u *>(addr));
 }
 
-// Variant bits (wg_tune_set("gso_ablate")): 1 = non-temporal payload
-// stores (a correct variant; default-policy stores measured faster because
-// the segment-edge byte stores then merge with the chunk stores in L2).
-// 32 = blocks -> super-buffers in launch order instead of XCD-swizzled (a
-// correct variant; the swizzle keeps consecutive super-buffers on one XCD).
-// Timing-only (WRONG output, to price one part of the kernel, guide §5.4
-// rule 17): 2 = no byte stores (header / payload head & tail).
-enum : int { kAblNtStore = 1, kAblNoByteStores = 2, kAblNoSwizzle = 32 };
+// Variant bits (wg_tune_set("gso_ablate")), both correct: 1 = non-temporal
+// payload stores (default-policy stores measured faster because the
+// segment-edge byte stores then merge with the chunk stores in L2); 32 =
+// blocks -> super-buffers in launch order instead of XCD-swizzled (the
+// swizzle keeps consecutive super-buffers on one XCD).  Timing-only
+// ablations with wrong output live in tools/exp, never in this library.
+enum : int { kAblNtStore = 1, kAblNoSwizzle = 32 };
 
 template <int A>
 __device__ __forceinline__ void st16x(uintptr_t addr, v4u v) {
@@ -178,8 +177,7 @@ __device__ __forceinline__ void seg_finish(const Ctx &c, uintptr_t out_base, con
     }
     const uint32_t eo = edge_off(g, lane);
     if (eo != kNoEdge) {
-        if (!(Abl & kAblNoByteStores))
-            st8(g.oa + eo, f.pb);
+        st8(g.oa + eo, f.pb);
         acc.add(f.pb << (8u * (((uint32_t)g.oa + eo) & 1u)));
     }
 
@@ -201,10 +199,6 @@ __device__ __forceinline__ void seg_finish(const Ctx &c, uintptr_t out_base, con
     uint32_t T = wave_sum_u32(lp) + l4h + c.ps_sum;
     T += ((c.tcp ? 6u : 17u) << 8) + bswap16((pktlen - c.cs) & 0xffffu);
     const uint32_t l4cs = ~fold16_32(T) & 0xffffu;
-    if (Abl & kAblNoByteStores) {
-        if (lane == 0 && l4cs == 0x12345u) st8(g.seg, 0);  // keep the sums live
-        return;
-    }
     // write the header prefix: each byte is the prefix byte or one byte of a
     // per-segment value, by its field code (checksums in native order,
     // :185-186, :203-204).  The values go into lanes 1-7 of one VGPR and
@@ -525,7 +519,7 @@ extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64
     if (!dev_in || !dev_desc || !dev_out || !dev_res || (reinterpret_cast<uintptr_t>(dev_desc) & 7) ||
         (reinterpret_cast<uintptr_t>(dev_res) & 7))
         return WG_ERR_INVALID;
-    const Tune &t = tune();
+    const Tune t = tune();
     GsoParams p{dev_in, dev_desc, n, dev_out, dev_res, t.gso_groups};
     hipStream_t st = static_cast<hipStream_t>(stream);
     // 1. plans (into dev_res), thread per super-buffer
@@ -541,9 +535,8 @@ extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64
     if (blocks >= 8)
         blocks &= ~7ull;  // the XCD swizzle wants a multiple of 8 (the grid-stride loop covers the rest)
     const dim3 g((unsigned)blocks, t.gso_split);
-    switch (t.gso_ablate) {  // A/B variants (1, 32 correct; 2 timing-only)
+    switch (t.gso_ablate) {  // correct A/B variants
     case 1: launch_split<0, 1>(p, g, 4, st); break;
-    case 2: launch_split<0, 2>(p, g, 4, st); break;
     case 32: launch_split<0, 32>(p, g, 4, st); break;
     default:
         switch (t.gso_spw) {

@@ -410,7 +410,7 @@ static int launch_small(const L4Params &p, uint32_t mode, hipStream_t st) {
 static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
     if (p.n == 0)
         return WG_OK;
-    const Tune &t = tune();
+    const Tune t = tune();
     if (kind == kUniformL4 && p.seg <= kSmallMax && t.l4_small_uniform) {
         // every segment is small: the small-packet kernel, no trade-off
         const uint32_t mode = t.l4_small_uniform == 2 ? 2u : 3u;  // 1: lane quad per segment, 2: lane per segment
@@ -768,7 +768,7 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
     if (!dev_base || !dev_desc || !dev_verdict || (reinterpret_cast<uintptr_t>(dev_desc) & 15))
         return WG_ERR_INVALID;
     VerifyParams p{dev_base, dev_desc, dev_verdict, dev_l4, n};
-    const Tune &t = tune();
+    const Tune t = tune();
     if (t.verify_small) {
         const uint64_t per_block = t.verify_small == 2 ? 64u : 256u;  // descriptors per 256-thread block
         const uint64_t sb = (n + per_block - 1) / per_block;

@@ -30,11 +30,12 @@ struct Tune {
     uint32_t gro_lds;     // 1: GRO finalize with LDS-staged cooperative header loads
     uint32_t gro_wide;    // 1: GRO finalize fields written by two wide stores (LDS variant)
     uint32_t gro_chunks;  // 16-B chunks staged per flow by the LDS variant (4, 5)
-    uint32_t gso_ablate;  // timing-only ablation bits (0 in production; non-zero = wrong output)
+    uint32_t gso_ablate;  // GSO A/B variants (1 non-temporal stores, 32 no XCD swizzle; both correct)
 };
 
-const Tune &tune();
-Tune &tune_mut();
+// A snapshot of the knobs (copied under the knob mutex: wg_tune_set may run
+// concurrently on another host thread).
+Tune tune();
 
 // Debugging aid: with WG_DEBUG_SYNC=1 in the environment, synchronise the
 // stream after a launch and report a failing kernel by name on stderr.

@@ -48,26 +48,43 @@ def shard_bounds_by_bytes(lengths: Sequence[int], world: int) -> list[tuple[int,
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
 
-def result_hash(results, global_offset: int):
+def result_hash(results, global_offset: int) -> int:
     """Order-independent hash of a shard of uint16 results: sum over packets
-    of (global_index + 1) * (value + 1) mod 2^61-1, as an int64 tensor; the
-    all-reduced (SUM then mod) hash equals the hash of the whole array."""
+    of (global_index + 1) * (value + 1) mod 2^61-1.  The per-rank hashes add
+    (mod 2^61-1) to the hash of the whole array.
+
+    Exact for any shard size and offset below 2^40: the index is split into
+    20-bit halves, so each int64 product is < 2^17 * 2^20, and the shard is
+    summed in blocks of 2^24 packets (block sums < 2^61); the blocks are
+    combined as Python integers."""
     import torch
 
-    v = results.to(torch.int64) + 1
-    idx = torch.arange(global_offset + 1, global_offset + 1 + v.numel(), dtype=torch.int64, device=v.device)
-    # products < 2^16 * 2^40 for batches below 2^40 packets: no overflow
-    return ((v * idx) % HASH_MOD).sum() % HASH_MOD
+    v = results.reshape(-1).to(torch.int64) + 1
+    total = 0
+    blk = 1 << 24
+    for s0 in range(0, v.numel(), blk):
+        vb = v[s0 : s0 + blk]
+        idx = torch.arange(global_offset + 1 + s0, global_offset + 1 + s0 + vb.numel(), dtype=torch.int64,
+                           device=v.device)
+        lo = int((vb * (idx & 0xFFFFF)).sum().item())
+        hi = int((vb * (idx >> 20)).sum().item())
+        total = (total + lo + (hi << 20)) % HASH_MOD
+    return total
 
 
-def allreduce_hash(local_hash, group=None):
+def allreduce_hash(local_hash: int, group=None, device=None) -> int:
+    """Sum of the ranks' hashes mod 2^61-1.  Each hash is < 2^61, so eight of
+    them would overflow an int64 all-reduce: the 31-bit halves are reduced
+    separately (sums < 2^34) and recombined here."""
     import torch
     import torch.distributed as dist
 
-    t = local_hash.clone().reshape(1)
-    if dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-    return int(t.item()) % HASH_MOD
+    h = int(local_hash)
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return h % HASH_MOD
+    t = torch.tensor([h & 0x7FFFFFFF, h >> 31], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return (int(t[0].item()) + (int(t[1].item()) << 31)) % HASH_MOD
 
 
 def gather_results(local, counts: Sequence[int], group=None):
