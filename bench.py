@@ -7,11 +7,17 @@ batch already resident in HBM (reference: calc_l4_checksum, checksum.cpp:8-36,
 once per segment of a PacketBatch, include/worker/offload.hpp:19-29).
 
 Workloads (--workload; BASELINE.json configs):
+  config1            checksum(buf, 0) over 16,384 x 64 KiB random buffers
+                     (configs[0], tests/test-checksum.cpp:11-17 shape): the
+                     CPU baseline on 1 core and all cores beside
+                     wg_checksum_desc on the same bytes.
   config2 (default)  1,048,576 x 1500 B IPv4/UDP per GPU, uniform PacketBatch
                      (configs[1]); N GPUs = N independent shards, weak
                      scaling, no data-path collective.
   config3            262,144 x 64 KiB GSO super-buffers -> 45 x 1460 B TCP
                      segments per GPU (configs[2]), fused split + checksums.
+  config3udp         the same super-buffers as UDP_L4 (gso_type 5, 8-B UDP
+                     header) -> 45 x 1472 B UDP segments.
   config4            4,194,304 bimodal 64 B / 9000 B IPv4/UDP (configs[3]).
   config5            16,777,216 x 1500 B mixed v4/v6 x TCP/UDP split across
                      the N GPUs (configs[4]); strong scaling.
@@ -24,10 +30,17 @@ Workloads (--workload; BASELINE.json configs):
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2]
   torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N
+ranks itself (torch.distributed.run, one process per GPU) before touching the
+GPU and exits with their status; every rank checks that the process group
+holds exactly N ranks.
 Rank 0 prints ONE JSON line.  Outside the timed region: a GPU verify pass
 (store the checksums, re-run in verify mode, every result must be 0),
 an RCCL all-gather of the results (timed separately) and an order-independent
-result hash; rank 0 at N=1 also times the CPU oracle on a sample.
+result hash; rank 0 at N=1 also times the CPU oracle on a sample.  Unless
+--no-strong, the line also carries `strong_scaling`: BASELINE config 5
+(16,777,216 x 1500 B mixed, split across the N ranks) timed the same way, so
+the driver's 1/2/4/8 runs give a weak (config 2) and a strong (config 5) curve.
 """
 from __future__ import annotations
 
@@ -53,8 +66,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="config2", choices=["config2", "config3", "config4", "config5", "verify", "gro"])
+    ap.add_argument("--workload", default="config2",
+                    choices=["config1", "config2", "config3", "config3udp", "config4", "config5", "verify", "gro"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-strong", action="store_true", help="skip the config 5 strong-scaling companion")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall seconds of the CPU baseline sample")
     ap.add_argument("--settle-seconds", type=float, default=0.3,
                     help="untimed back-to-back launches before the warmup (clock/memory settle)")
@@ -133,27 +148,31 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                   for r in range(world)]
         return Workload(launch, n, n * SEG, n * SEG + 2 * n + 16 * n, cfg, "strong", buf,
                         "wg::l4csum_kernel<1,4,nt>", lo, out, desc, sample, counts)
-    if name == "config3":
+    if name in ("config3", "config3udp"):
+        udp = name == "config3udp"
         n, in_stride, out_stride = 1 << 18, 65536, 73216  # outbuf stride of worker/encap.cpp:26
-        in_len, gso = 65535, 1460
+        in_len = 65535
+        # TCPV4 (doff 5, ACK|PSH): 40-B headers, gso_size 1460; UDP_L4 (gso_type 5,
+        # worker/offload.cpp:113-115,197-199): 28-B headers, gso_size 1472
+        hdr, gso, pflags = (28, 1472, 0) if udp else (40, 1460, 2)
         seed = 0x5EED0003
         buf = torch.empty(n * in_stride, dtype=torch.uint8, device=dev)
         wga.synth_fill(buf, seed, counter_base=rank * n * in_stride)
         pd = np.zeros(n, dtype=wga.PKT_DESC_DTYPE)
         pd["offset"] = np.arange(n, dtype=np.uint64) * in_stride
-        pd["len"], pd["csum_start"], pd["flags"] = in_len, 20, 2  # IPv4 + TCP (doff 5, ACK|PSH)
+        pd["len"], pd["csum_start"], pd["flags"] = in_len, 20, pflags
         wga.synth_headers(buf, torch.from_numpy(pd.view(np.uint8).copy()).to(dev), seed, rank * n)
         gd = np.zeros(n, dtype=wga.GSO_DESC_DTYPE)
         gd["in_offset"] = pd["offset"]
         gd["out_offset"] = np.arange(n, dtype=np.uint64) * out_stride
         gd["in_len"], gd["out_cap"] = in_len, out_stride
-        gd["vnet"]["flags"], gd["vnet"]["gso_type"], gd["vnet"]["gso_size"] = 1, 1, gso
-        gd["vnet"]["csum_start"], gd["vnet"]["csum_offset"] = 20, 16
+        gd["vnet"]["flags"], gd["vnet"]["gso_type"], gd["vnet"]["gso_size"] = 1, (5 if udp else 1), gso
+        gd["vnet"]["csum_start"], gd["vnet"]["csum_offset"] = 20, (6 if udp else 16)
         d_desc = torch.from_numpy(gd.view(np.uint8).copy()).to(dev)
         outb = torch.empty(n * out_stride, dtype=torch.uint8, device=dev)
         res = torch.empty(n * wga.GSO_RESULT_BYTES, dtype=torch.uint8, device=dev)
-        nseg = (in_len - 40 + gso - 1) // gso
-        out_len = in_len - 40 + nseg * 40
+        nseg = (in_len - hdr + gso - 1) // gso
+        out_len = in_len - hdr + nseg * hdr
 
         def launch():
             wga.gso_split(buf, d_desc, outb, results=res)
@@ -164,13 +183,13 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
             # L4 checksum verify to 0 (wg_checksum_desc / wg_l4csum_desc)
             r = res.cpu().numpy().view(wga.GSO_RESULT_DTYPE)
             geom_bad = int(np.count_nonzero((r["status"] != 0) | (r["out_len"] != out_len)
-                                            | (r["segment_size"] != 40 + gso)))
+                                            | (r["segment_size"] != hdr + gso)))
             sd = np.zeros(n * nseg, dtype=wga.PKT_DESC_DTYPE)
-            base = (gd["out_offset"][:, None] + np.arange(nseg, dtype=np.uint64)[None, :] * np.uint64(40 + gso))
+            base = (gd["out_offset"][:, None] + np.arange(nseg, dtype=np.uint64)[None, :] * np.uint64(hdr + gso))
             sd["offset"] = base.reshape(-1)
-            lens = np.full((n, nseg), 40 + gso, np.uint32)
-            lens[:, -1] = out_len - (nseg - 1) * (40 + gso)
-            sd["len"], sd["csum_start"], sd["flags"] = lens.reshape(-1), 20, 2
+            lens = np.full((n, nseg), hdr + gso, np.uint32)
+            lens[:, -1] = out_len - (nseg - 1) * (hdr + gso)
+            sd["len"], sd["csum_start"], sd["flags"] = lens.reshape(-1), 20, pflags
             d_sd = torch.from_numpy(sd.view(np.uint8)).to(dev)
             l4 = wga.calc_l4_checksum_desc(outb, d_sd)
             sd["len"] = 20
@@ -188,14 +207,45 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
             return (buf[: k * in_stride].cpu().numpy(), outb[: k * out_stride].cpu().numpy(),
                     ("gso", gk, k * out_stride))
 
-        cfg = {"workload": "config3: 262,144 x 64 KiB GSO super-buffers (IPv4/TCP, 65535 B) -> 45 x 1460 B "
-                           "segments each, fused copy + header fix-up + IPv4/TCP checksums",
-               "super_buffers_per_gpu": n, "gso_size": gso, "segments_per_buffer": nseg,
-               "parallelism": f"shard{world}"}
+        proto = ("UDP_L4, IPv4/UDP, 65535 B) -> 45 x 1472 B UDP segments each"
+                 if udp else "IPv4/TCP, 65535 B) -> 45 x 1460 B segments each")
+        cfg = {"workload": f"{name}: 262,144 x 64 KiB GSO super-buffers ({proto}, fused copy + header "
+                           "fix-up + IPv4/L4 checksums",
+               "super_buffers_per_gpu": n, "gso_size": gso, "gso_type": "UDP_L4" if udp else "TCPV4",
+               "segments_per_buffer": nseg, "parallelism": f"shard{world}"}
         alg = n * in_len + n * out_len + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES)
         return Workload(launch, n, n * in_len, alg, cfg, "weak", buf,
                         "wg::gso_plan_kernel + wg::gso_split_kernel<4,1,0> + wg::gso_finalize_kernel (one wg_gso_split call)",
                         rank * n, sample=sample, counts=[n] * world, post=post)
+    if name == "config1":
+        # tests/test-checksum.cpp:11-17: checksum(create_packet(n), 0) on random
+        # buffers; BASELINE configs[0] at 64 KiB, 16,384 buffers (1 GiB,
+        # past the host LLC), SURVEY §8(d).  On the GPU the same bytes go
+        # through wg_checksum_desc (checksum(span, 0) per descriptor).
+        n, size = 16384, 65536
+        seed = 0x5EED0001
+        buf = torch.empty(n * size, dtype=torch.uint8, device=dev)
+        wga.synth_fill(buf, seed, counter_base=rank * n * size)
+        pd = np.zeros(n, dtype=wga.PKT_DESC_DTYPE)
+        pd["offset"] = np.arange(n, dtype=np.uint64) * size
+        pd["len"] = size
+        desc = torch.from_numpy(pd.view(np.uint8).copy()).to(dev)
+        out = torch.empty(n, dtype=torch.uint16, device=dev)
+
+        def launch():
+            wga.checksum_desc(buf, desc, out=out)
+
+        def sample(npk):
+            k = min(n, npk)
+            return buf[: k * size].cpu().numpy(), out[:k].cpu().numpy(), ("checksum", pd[:k].copy())
+
+        cfg = {"workload": "config1: checksum(buf, 0) over 16,384 x 64 KiB random buffers per GPU "
+                           "(tests/test-checksum.cpp:11-17 shape; BASELINE configs[0]), descriptor batch",
+               "buffers_per_gpu": n, "buffer_bytes": size, "layout": "descriptor", "parallelism": f"shard{world}"}
+        return Workload(launch, n, n * size, n * size + 2 * n + 16 * n, cfg, "weak", buf,
+                        "wg::l4csum_kernel<2,4,nt> (plain checksum, descriptor mode 2)", rank * n, sample=sample,
+                        counts=[n] * world,
+                        metric="device-resident GiB/s, checksum(span, 0) over 64 KiB buffers (BASELINE config 1 shape)")
     if name == "verify":
         n = 1 << 20
         seed = 0x5EED00F1
@@ -469,7 +519,8 @@ def cpu_baseline(sample_fn, seconds: float):
     # host's last-level cache (EPYC 9575F: 256 MB L3) between repetitions.
     npk = 1 << 19
     host, gpu_out, kind = sample_fn(npk)
-    threads = oracle.default_threads()
+    cores = oracle.host_cores()
+    threads = cores["threads"]
     if kind[0] == "uniform":
         _, seg, cs, fl = kind
         exp = oracle.l4_uniform(host, seg, cs, fl, threads)
@@ -519,16 +570,36 @@ def cpu_baseline(sample_fn, seconds: float):
         d = kind[1]
         hdr_after, st = oracle.gro_finalize_desc(host, d, threads)
         exp = np.concatenate([hdr_after.astype(np.int64), st.astype(np.int64)])
+        # timed: the C call only, in place on working copies made outside the
+        # timed region (finalize is idempotent: re-running it on finalized
+        # headers rewrites the same bytes)
+        hw, dw = oracle.gro_working_copies(host, d)
         t0 = time.perf_counter()
-        oracle.gro_finalize_desc(host, d, 1)
+        oracle.gro_finalize_desc_inplace(hw, dw, 1)
         t_1core = time.perf_counter() - t0
         reps = max(1, int(seconds * threads / max(t_1core, 1e-6)))
         t0 = time.perf_counter()
         for _ in range(reps):
-            oracle.gro_finalize_desc(host, d, threads)
+            oracle.gro_finalize_desc_inplace(hw, dw, threads)
         t_all = (time.perf_counter() - t0) / reps
+        if not (np.array_equal(hw, hdr_after) and np.array_equal(dw["status"], st)):
+            gpu_out = None  # the timed in-place runs must reproduce the checked answer
         nbytes = d.size  # flows
         gpu_out = np.concatenate([gpu_out[0].astype(np.int64), gpu_out[1].astype(np.int64)])
+    elif kind[0] == "checksum":
+        # checksum(buf, 0) per buffer (BASELINE config 1)
+        d = kind[1]
+        exp = oracle.checksum_desc(host, d, threads)
+        t0 = time.perf_counter()
+        oracle.checksum_desc(host, d, 1)
+        t_1core = time.perf_counter() - t0
+        reps = max(1, int(seconds * threads / max(t_1core, 1e-6)))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            oracle.checksum_desc(host, d, threads)
+        t_all = (time.perf_counter() - t0) / reps
+        nbytes = int(np.ascontiguousarray(d).view(oracle.PKT_DESC)["len"].astype(np.int64).sum())
+        npk = d.size
     else:
         d = kind[1]
         exp = oracle.l4_desc(host, d, threads)
@@ -548,7 +619,9 @@ def cpu_baseline(sample_fn, seconds: float):
         cpu_model = "unknown"
     scale, unit = (1e-6, "Mflows/s") if kind[0] == "gro" else (2.0**-30, "GiB/s")
     what = {"verify": "decap verify gates restatement (orc_verify)", "gro": "GRO finalize restatement",
-            "gso": "do_tun_gso_split restatement, output bytes compared"}.get(kind[0], "calc_l4_checksum restatement")
+            "gso": "do_tun_gso_split restatement, output bytes compared",
+            "checksum": "checksum(span, 0) restatement"}.get(kind[0], "calc_l4_checksum restatement")
+    nofold = "AVX2 vector nofold (oracle/csum_oracle.c nofold_avx2)" if oracle.have_avx2() else "scalar nofold"
     return {
         "value": nbytes / t_all * scale,
         "unit": unit,
@@ -556,9 +629,11 @@ def cpu_baseline(sample_fn, seconds: float):
         "kind": "port",
         "value_1core": nbytes / t_1core * scale,
         "cpu_model": cpu_model,
+        "host_cores": cores,
         "sample": f"first {npk} units of the same batch, oracle/csum_oracle.c "
-                  f"({what}), {threads} pthreads, ~{seconds:.1f} s wall; "
-                  f"bit-exact vs GPU: {parity}",
+                  f"({what}; {nofold} for spans >= 256 B), {threads} pthreads "
+                  f"(sched_getaffinity {cores['affinity']}, cgroup quota {cores['cgroup_quota_cpus']}), "
+                  f"~{seconds:.1f} s wall; bit-exact vs GPU: {parity}",
         "parity_with_gpu": parity,
     }
 
@@ -606,47 +681,50 @@ def post_checks(torch, wga, wl: Workload, world: int, dev):
     return info
 
 
-def main():
-    args = parse()
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: start N ranks under
+    torch.distributed.run (rendezvous on 127.0.0.1) and return their exit
+    status.  Runs before anything touches the GPU (torch.cuda.device_count()
+    does not initialise it on this image), so the children own the devices."""
+    import socket
+    import subprocess
+
     import torch
+
+    backend = os.environ.get("WG_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and ndev < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but {ndev} GPU(s) visible (RCCL needs one GPU per rank; "
+              "WG_DIST_BACKEND=gloo rehearses ranks sharing a GPU)", file=sys.stderr)
+        return 2
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def time_steps(torch, wl: Workload, args, world: int, dev) -> dict:
+    """The timed region: barrier + synchronize, exactly K back-to-back
+    launches with ONE HIP event pair on the launch stream at its two ends,
+    synchronize + barrier; max over ranks.  Returns wall / kernel times."""
     import torch.distributed as dist
 
-    import wireglider_amd as wga
     from wireglider_amd import dist as wdist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
-    # one process per GPU; WG_DIST_BACKEND=gloo (with ranks sharing a GPU)
-    # only rehearses the multi-rank logic on a one-GPU box
-    backend = os.environ.get("WG_DIST_BACKEND", "nccl")
-    local = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-
-    wl = build_workload(wga, torch, args.workload, rank, world, dev)
-    torch.cuda.synchronize()
-    settled = settle(torch, wl.launch, args.settle_seconds)
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
+    settled = settle(torch, wl.launch, args.settle_seconds)
     for _ in range(args.warmup):
         wl.launch()
     barrier()
-
-    # Timed region: exactly K back-to-back launches, one HIP event pair on
-    # the launch stream at its two ends (device time per launch = the pair /
-    # K).  Events between the launches would each add a serialising marker:
+    # Events between the launches would each add a serialising marker:
     # ~6 us per step, 3 % of config 2 (repo:tools/gap_probe.py).
     stream = torch.cuda.current_stream()
     e_start, e_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -664,23 +742,86 @@ def main():
     # pair around each launch, which also stops neighbouring launches from
     # overlapping at their boundaries.
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    for a, b in evs:
-        a.record(stream)
+    for x, y in evs:
+        x.record(stream)
         wl.launch()
-        b.record(stream)
+        y.record(stream)
     torch.cuda.synchronize()
-    kern_ms_isolated = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    kern_ms_isolated = sum(x.elapsed_time(y) for x, y in evs) / args.steps
     wall = wdist.max_over_ranks(t1 - t0, dev)
-    kern_ms_max = wdist.max_over_ranks(kern_ms, dev)
+    per_rank = wdist.all_gather_floats([kern_ms, t1 - t0, float(wl.payload_bytes)], dev)
+    total_payload = sum(r[2] for r in per_rank)
+    return {"settled": settled, "wall": wall, "kern_ms": kern_ms, "kern_ms_isolated": kern_ms_isolated,
+            "kern_ms_per_rank": [round(r[0], 5) for r in per_rank],
+            "wall_s_per_rank": [round(r[1], 6) for r in per_rank],
+            "kern_ms_max": max(r[0] for r in per_rank), "total_payload": total_payload}
+
+
+def strong_scaling(torch, wga, args, rank: int, world: int, dev) -> dict:
+    """BASELINE config 5 (16,777,216 x 1500 B mixed v4/v6 x TCP/UDP, split
+    across the ranks) timed like the main line: whole-job GiB/s
+    = all ranks' packet bytes / max-over-ranks wall time."""
+    from wireglider_amd import dist as wdist
+
+    wl = build_workload(wga, torch, "config5", rank, world, dev)
+    torch.cuda.synchronize()
+    t = time_steps(torch, wl, args, world, dev)
+    h = wdist.allreduce_hash(wdist.result_hash(wl.out, wl.first_index), device=dev)
+    out = {
+        "workload": wl.cfg["workload"], "scaling": "strong", "packets_total": wl.cfg["packets_total"],
+        "packets_per_rank": wl.counts,
+        "value": round(t["total_payload"] * args.steps / t["wall"] * 2.0**-30, 3), "unit": "GiB/s",
+        "ms_per_step": round(t["wall"] / args.steps * 1e3, 5),
+        "kernel_ms_per_rank": t["kern_ms_per_rank"],
+        "roofline_frac_rank0": round(wl.alg_bytes / (t["kern_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        # order-independent hash of all 16 M results: the same at every world
+        # size when the sharded job is bit-exact
+        "result_hash": h,
+    }
+    del wl
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    import torch
+    import torch.distributed as dist
+
+    import wireglider_amd as wga
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; WG_DIST_BACKEND=gloo (with ranks sharing a GPU)
+    # only rehearses the multi-rank logic on a one-GPU box
+    backend = os.environ.get("WG_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     if world > 1:
-        tot = torch.tensor([wl.payload_bytes], dtype=torch.float64, device=dev)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        total_payload = float(tot[0])
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+        got = dist.get_world_size()
     else:
-        total_payload = float(wl.payload_bytes)
+        got = 1
+    if got != args.gpus:
+        print(f"bench.py: process group has {got} rank(s) but --gpus {args.gpus}", file=sys.stderr)
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(3)
+
+    wl = build_workload(wga, torch, args.workload, rank, world, dev)
+    torch.cuda.synchronize()
+    t = time_steps(torch, wl, args, world, dev)
+    wall, kern_ms = t["wall"], t["kern_ms"]
 
     ms_per_step = wall / args.steps * 1e3
-    value = total_payload * args.steps / wall * wl.value_scale
+    value = t["total_payload"] * args.steps / wall * wl.value_scale
     achieved = wl.alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args.workload)
     read_peak = measured_read_peak(torch, wga, wl.buf) if rank == 0 else None
@@ -691,21 +832,28 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl.sample is not None:
         cpu = cpu_baseline(wl.sample, args.cpu_seconds)
     post = post_checks(torch, wga, wl, world, dev)
+    meta = {"metric": wl.metric or "device-resident GiB/s, L4 checksum over packet batch; 1/2/4/8 MI355X",
+            "unit": wl.unit, "scaling": wl.scaling, "config": wl.cfg, "kernel": wl.kernel, "alg_bytes": wl.alg_bytes}
+    del wl
+    torch.cuda.empty_cache()
+    strong = None if args.no_strong else strong_scaling(torch, wga, args, rank, world, dev)
     line = {
-        "metric": wl.metric or "device-resident GiB/s, L4 checksum over packet batch; 1/2/4/8 MI355X",
+        "metric": meta["metric"],
         "value": round(value, 3),
-        "unit": wl.unit,
-        "n_gpus": world,
+        "unit": meta["unit"],
+        "n_gpus": got,
         "steps": args.steps,
         "warmup": args.warmup,
-        "settle_launches": settled,
+        "settle_launches": t["settled"],
         "ms_per_step": round(ms_per_step, 5),
         "higher_is_better": True,
-        "scaling": wl.scaling,
+        "scaling": meta["scaling"],
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (device-generated, seeded; BASELINE config shapes)",
-        "config": wl.cfg,
+        "config": meta["config"],
+        "distributed": {"backend": backend if world > 1 else None, "world_size": got,
+                        "kernel_ms_per_rank": t["kern_ms_per_rank"], "wall_s_per_rank": t["wall_s_per_rank"]},
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved, 2),
@@ -713,19 +861,21 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": wl.kernel,
-            "alg_bytes_per_launch": wl.alg_bytes,
+            "kernel": meta["kernel"],
+            "alg_bytes_per_launch": meta["alg_bytes"],
             "traffic_source": f"profiles/pmc_{args.workload}.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)",
             "measured_read_peak": round(read_peak, 1) if read_peak else None,
             "frac_of_measured_read_peak": round(achieved / read_peak, 4) if read_peak else None,
             "kernel_ms_avg": round(kern_ms, 5),
-            "kernel_ms_avg_max_over_ranks": round(kern_ms_max, 5),
+            "kernel_ms_avg_max_over_ranks": round(t["kern_ms_max"], 5),
             "kernel_ms_source": "HIP events at the two ends of the timed region on the launch stream / K "
                                 "(back-to-back launches)",
-            "kernel_ms_isolated": round(kern_ms_isolated, 5),
+            "kernel_ms_isolated": round(t["kern_ms_isolated"], 5),
         },
         "post_checks": post,
     }
+    if strong is not None:
+        line["strong_scaling"] = strong
     if rank == 0:
         line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)

@@ -56,7 +56,7 @@ static inline uint64_t add_eac(uint64_t a, uint64_t b) {
  * byte, then an end-around-carry add of `initial`.  The accumulator is
  * congruent to (initial + sum of LE 16-bit words) mod 0xFFFF and is zero only
  * when initial and every byte are zero, so it folds to the reference value. */
-uint64_t orc_nofold(const uint8_t *b, size_t n, uint64_t initial) {
+uint64_t orc_nofold_scalar(const uint8_t *b, size_t n, uint64_t initial) {
     uint64_t acc = 0;
     size_t i = 0;
     for (; i + 4 <= n; i += 4) {
@@ -73,6 +73,80 @@ uint64_t orc_nofold(const uint8_t *b, size_t n, uint64_t initial) {
     if (n - i == 1)
         acc += b[i]; /* low byte on little-endian (checksum.hpp:69-77) */
     return add_eac(acc, initial);
+}
+
+/* The AVX2 arm of the same dispatch (include/netio/checksum.hpp:88-91:
+ * fastcsum_nofold_vec256_align when AVX2 is available and the span is long).
+ * fastcsum is un-vendored, so this is this repository's own
+ * vector kernel with the same contract: per 32-B load, each 64-bit lane is
+ * split into its two LE 32-bit words (mask / shift) and both are added into
+ * 64-bit accumulator lanes (no lane can overflow below 2^31 iterations), so
+ * the result is congruent mod 0xFFFF to the scalar sum and zero only when
+ * every byte is.  It is the CPU BASELINE's nofold (bench.py cpu_baseline);
+ * tests/test_oracle_golden.py pins it to the reference goldens and to
+ * orc_nofold_scalar. */
+#include <immintrin.h>
+
+__attribute__((target("avx2"))) static uint64_t nofold_avx2(const uint8_t *b, size_t n, uint64_t initial) {
+    const __m256i m32 = _mm256_set1_epi64x(0xffffffffll);
+    __m256i a0 = _mm256_setzero_si256(), a1 = _mm256_setzero_si256();
+    __m256i a2 = _mm256_setzero_si256(), a3 = _mm256_setzero_si256();
+    __m256i b0 = _mm256_setzero_si256(), b1 = _mm256_setzero_si256();
+    __m256i b2 = _mm256_setzero_si256(), b3 = _mm256_setzero_si256();
+    while (n >= 128) {  /* two independent accumulator sets: 8 add chains in flight */
+        const __m256i v0 = _mm256_loadu_si256((const __m256i *)b);
+        const __m256i v1 = _mm256_loadu_si256((const __m256i *)(b + 32));
+        const __m256i v2 = _mm256_loadu_si256((const __m256i *)(b + 64));
+        const __m256i v3 = _mm256_loadu_si256((const __m256i *)(b + 96));
+        a0 = _mm256_add_epi64(a0, _mm256_and_si256(v0, m32));
+        a1 = _mm256_add_epi64(a1, _mm256_srli_epi64(v0, 32));
+        a2 = _mm256_add_epi64(a2, _mm256_and_si256(v1, m32));
+        a3 = _mm256_add_epi64(a3, _mm256_srli_epi64(v1, 32));
+        b0 = _mm256_add_epi64(b0, _mm256_and_si256(v2, m32));
+        b1 = _mm256_add_epi64(b1, _mm256_srli_epi64(v2, 32));
+        b2 = _mm256_add_epi64(b2, _mm256_and_si256(v3, m32));
+        b3 = _mm256_add_epi64(b3, _mm256_srli_epi64(v3, 32));
+        b += 128;
+        n -= 128;
+    }
+    a0 = _mm256_add_epi64(a0, b0);
+    a1 = _mm256_add_epi64(a1, b1);
+    a2 = _mm256_add_epi64(a2, b2);
+    a3 = _mm256_add_epi64(a3, b3);
+    while (n >= 64) {
+        const __m256i v0 = _mm256_loadu_si256((const __m256i *)b);
+        const __m256i v1 = _mm256_loadu_si256((const __m256i *)(b + 32));
+        a0 = _mm256_add_epi64(a0, _mm256_and_si256(v0, m32));
+        a1 = _mm256_add_epi64(a1, _mm256_srli_epi64(v0, 32));
+        a2 = _mm256_add_epi64(a2, _mm256_and_si256(v1, m32));
+        a3 = _mm256_add_epi64(a3, _mm256_srli_epi64(v1, 32));
+        b += 64;
+        n -= 64;
+    }
+    const __m256i t = _mm256_add_epi64(_mm256_add_epi64(a0, a1), _mm256_add_epi64(a2, a3));
+    uint64_t lanes[4];
+    _mm256_storeu_si256((__m256i *)lanes, t);
+    uint64_t acc = add_eac(add_eac(lanes[0], lanes[1]), add_eac(lanes[2], lanes[3]));
+    /* the < 64-byte tail: 64 is even, so its pairing is unchanged */
+    return orc_nofold_scalar(b, n, add_eac(acc, initial));
+}
+
+static int g_have_avx2 = -1;
+
+uint64_t orc_nofold(const uint8_t *b, size_t n, uint64_t initial) {
+    if (n >= 256) {
+        if (g_have_avx2 < 0)
+            g_have_avx2 = __builtin_cpu_supports("avx2") ? 1 : 0;
+        if (g_have_avx2)
+            return nofold_avx2(b, n, initial);
+    }
+    return orc_nofold_scalar(b, n, initial);
+}
+
+int orc_have_avx2(void) {
+    if (g_have_avx2 < 0)
+        g_have_avx2 = __builtin_cpu_supports("avx2") ? 1 : 0;
+    return g_have_avx2;
 }
 
 /* fastcsum_fold_complement: 64 -> 32 -> 16 with end-around carry, then ~. */

@@ -35,6 +35,11 @@ uint16_t orc_checksum_ref1(const uint8_t *data, size_t size);
  * of the native (LE) words of b, pairing relative to b[0], odd tail byte
  * as the low byte, added to `initial` with end-around carry. */
 uint64_t orc_nofold(const uint8_t *b, size_t n, uint64_t initial);
+/* The two arms of orc_nofold's dispatch (n >= 256 and AVX2: the vector arm,
+ * like checksum.hpp:88-91's vec256 branch): the scalar arm on its own, and
+ * whether this CPU takes the vector arm. */
+uint64_t orc_nofold_scalar(const uint8_t *b, size_t n, uint64_t initial);
+int orc_have_avx2(void);
 
 /* fastcsum_fold_complement contract (include/netio/checksum.hpp:127,148):
  * fold 64 -> 16 bits with end-around carry, then one's complement. */

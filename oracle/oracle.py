@@ -53,6 +53,10 @@ def _load():
     lib.orc_checksum_ref1.argtypes = [vp, sz]
     lib.orc_nofold.restype = u64
     lib.orc_nofold.argtypes = [vp, sz, u64]
+    lib.orc_nofold_scalar.restype = u64
+    lib.orc_nofold_scalar.argtypes = [vp, sz, u64]
+    lib.orc_have_avx2.restype = i32
+    lib.orc_have_avx2.argtypes = []
     lib.orc_fold_complement.restype = u16
     lib.orc_fold_complement.argtypes = [u64]
     lib.orc_checksum.restype = u16
@@ -87,11 +91,37 @@ def _load():
 lib = _load()
 
 
+def _cgroup_cpu_quota() -> float | None:
+    """CPUs granted by the cgroup CPU controller (v2 cpu.max or v1
+    cfs_quota/period), or None when unlimited / not visible."""
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except Exception:
+        pass
+    try:
+        q = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
+        per = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+        return None if q <= 0 else q / per
+    except Exception:
+        return None
+
+
+def host_cores() -> dict:
+    """The host cores this process may run on: the scheduler affinity mask
+    (os.sched_getaffinity), capped by a cgroup CPU quota when one is set.
+    `threads` is what the CPU baseline uses; the other fields say why."""
+    import math
+
+    aff = len(os.sched_getaffinity(0))
+    quota = _cgroup_cpu_quota()
+    used = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
+    return {"threads": used, "affinity": aff, "cgroup_quota_cpus": quota, "cpu_count": os.cpu_count(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
 def default_threads() -> int:
-    env = os.environ.get("OMP_NUM_THREADS")
-    if env and env.isdigit():
-        return max(1, int(env))
-    return max(1, min(16, os.cpu_count() or 1))
+    return host_cores()["threads"]
 
 
 def _u8(buf) -> np.ndarray:
@@ -113,6 +143,15 @@ def checksum(buf, initial: int = 0) -> int:
 def nofold(buf, initial: int = 0) -> int:
     a = _u8(buf)
     return int(lib.orc_nofold(a.ctypes.data, a.size, initial))
+
+
+def nofold_scalar(buf, initial: int = 0) -> int:
+    a = _u8(buf)
+    return int(lib.orc_nofold_scalar(a.ctypes.data, a.size, initial))
+
+
+def have_avx2() -> bool:
+    return bool(lib.orc_have_avx2())
 
 
 def fold_complement(x: int) -> int:
@@ -193,6 +232,20 @@ def gro_finalize_desc(hdrs: np.ndarray, desc: np.ndarray, threads: int | None = 
         raise ValueError("gro_finalize_desc: descriptor past the header buffer")
     lib.orc_gro_finalize_desc(a.ctypes.data, d.ctypes.data, d.size, threads or default_threads())
     return a, d["status"].copy()
+
+
+def gro_working_copies(hdrs: np.ndarray, desc: np.ndarray):
+    """Mutable copies of a GRO batch for gro_finalize_desc_inplace (made
+    outside any timed region)."""
+    return (np.array(_u8(hdrs), copy=True),
+            np.array(np.ascontiguousarray(desc).view(GRO_DESC).reshape(-1), copy=True))
+
+
+def gro_finalize_desc_inplace(hdrs: np.ndarray, desc: np.ndarray, threads: int | None = None) -> None:
+    """Batched GRO finalize in place (headers and status), the C call only:
+    the CPU baseline's timed leg."""
+    assert hdrs.flags["C_CONTIGUOUS"] and desc.dtype == GRO_DESC and desc.flags["C_CONTIGUOUS"]
+    lib.orc_gro_finalize_desc(hdrs.ctypes.data, desc.ctypes.data, desc.size, threads or default_threads())
 
 
 def gso_split(inbuf: np.ndarray, vnet: dict, out_cap: int):

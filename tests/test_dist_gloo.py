@@ -69,8 +69,9 @@ def _worker(rank, world, port, n, q):
         # far from zero: per-rank hashes near 2^61 must not overflow the reduction
         h_big = wdist.allreduce_hash(wdist.result_hash(local, lo + BIG_OFFSET))
         t = wdist.max_over_ranks(float(rank + 1))
+        per = wdist.all_gather_floats([float(rank), 0.5 * rank])
         if rank == 0:
-            q.put((full.numpy().astype(np.uint16).tobytes(), h, h_big, t, bounds))
+            q.put((full.numpy().astype(np.uint16).tobytes(), h, h_big, t, bounds, per))
     finally:
         dist.destroy_process_group()
 
@@ -86,7 +87,7 @@ def test_sharded_equals_single_process(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
     for p in procs:
         p.start()
-    full_bytes, h, h_big, t, bounds = q.get(timeout=240)
+    full_bytes, h, h_big, t, bounds, per = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -97,6 +98,7 @@ def test_sharded_equals_single_process(world):
     assert h == wdist.result_hash(torch.from_numpy(ref.astype(np.int32)), 0) == exact_hash(ref, 0)
     assert h_big == exact_hash(ref, BIG_OFFSET)
     assert t == float(world)
+    assert per == [[float(r), 0.5 * r] for r in range(world)]  # per-rank bench times, in rank order
     # byte balance: each shard within one max-size packet of the mean
     per = [int(d["len"][a:b].astype(np.int64).sum()) for a, b in bounds]
     assert max(per) - min(per) <= 2 * int(d["len"].max())
@@ -142,3 +144,20 @@ def test_hash_exact_at_large_shards_and_offsets():
     w = v[: (1 << 22)]
     assert (wdist.result_hash(w[:12345], 5 << 30) + wdist.result_hash(w[12345:], (5 << 30) + 12345)) % \
         wdist.HASH_MOD == wdist.result_hash(w, 5 << 30)
+
+
+def test_bench_refuses_more_ranks_than_gpus():
+    """bench.py --gpus 2 with RCCL and fewer visible GPUs exits non-zero
+    before touching a device (the parent never initialises the GPU)."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "WG_DIST_BACKEND")}
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("this host has >= 2 GPUs")
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--steps", "1"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2, r.stderr
+    assert "GPU(s) visible" in r.stderr

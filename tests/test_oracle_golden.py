@@ -127,3 +127,28 @@ def test_nofold_initial_zero_semantics():
         s = init + words
         exp = 0xFFFF if s == 0 else (~(1 + (s - 1) % 0xFFFF)) & 0xFFFF
         assert oracle.checksum(b, init) == exp
+
+
+def test_vector_nofold_arm_pinned(golden):
+    """The AVX2 arm of orc_nofold (the CPU baseline's fastcsum-class path,
+    include/netio/checksum.hpp:88-91) against the reference goldens and the
+    scalar arm: every length 256..1500 of create_packet, the 65536-B golden,
+    all-0xFF carry buffers, zero buffers, odd offsets and non-zero initials."""
+    assert oracle.have_avx2(), "the oracle's vector arm needs AVX2 (x86-64-v3) on this host"
+    s = golden["stream"]
+    for n in range(256, 1501):
+        assert oracle.checksum(s[:n], 0) == golden["random"][n - 1], n
+    assert oracle.checksum(s, 0) == golden["r65536"]
+    rng = np.random.default_rng(11)
+    for _ in range(400):
+        n = int(rng.integers(256, 70000))
+        o = int(rng.integers(0, 64))
+        init = int(rng.integers(0, 2**64, dtype=np.uint64)) if rng.random() < 0.5 else 0
+        buf = s[o:o + n] if o + n <= s.size else rng.integers(0, 256, n, dtype=np.uint8)
+        if rng.random() < 0.2:
+            buf = np.full(n, 0xFF, np.uint8)
+        assert oracle.fold_complement(oracle.nofold(buf, init)) == oracle.fold_complement(
+            oracle.nofold_scalar(buf, init))
+    assert oracle.checksum(np.zeros(4096, np.uint8), 0) == 0xFFFF
+    for n in (256, 257, 4095, 65536):
+        assert oracle.checksum(carry_packet(n), 0) == oracle.checksum_ref1(carry_packet(n))

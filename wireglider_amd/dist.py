@@ -112,3 +112,20 @@ def max_over_ranks(x: float, device=None, group=None) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
+
+
+def all_gather_floats(values: Sequence[float], device=None, group=None) -> list[list[float]]:
+    """Every rank's list of floats (same length on every rank), in rank
+    order; [values] without a process group.  bench.py reports per-rank kernel
+    and wall times with it (stragglers show up there, not in the max)."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return [list(map(float, values))]
+    if dist.get_backend(group) == "gloo":
+        device = "cpu"
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, t, group=group)
+    return [p.cpu().tolist() for p in parts]
