@@ -412,7 +412,8 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
             o_sub = torch.empty(len(idx), dtype=torch.uint16, device=dev)
             nbytes = int(lens[idx].sum())
             alg = nbytes + 18 * len(idx)  # bytes read + u16 written + 16-B descriptor
-            for kname, small in (("wave_per_packet", 0), ("thread_per_packet", 1), ("thread_per_packet_q4", 2), ("quad_per_packet_q4", 3), ("quad_late", 4)):
+            for kname, small in (("wave_per_packet", 0), ("thread_per_packet", 1), ("thread_per_packet_q4", 2),
+                                 ("quad_per_packet_q4", 3), ("quad_late", 4), ("split_roles", 5)):
                 wga.tune_set("l4_small", small)
                 for _ in range(10):
                     wga.calc_l4_checksum_desc(buf, d_sub, out=o_sub)

@@ -259,11 +259,13 @@ int wg_device_count(void);
  *                iteration, 2 vector prefetch of the next iteration
  *   "l4_iters"   iterations per wave in descriptor mode 2 (1 .. 64)
  *   "l4_occ"     waves/SIMD target at 4 packets/wave (0 = compiler, 7, 8)
- *   "l4_small"   descriptor batches by the thread-per-packet kernel: a
- *                packet of <= 64 B summed in one lane, longer ones by the
- *                wave, 2 (1) or 4 (2) at a time; 3: a lane quad per
- *                descriptor, long packets 4 at a time; 4: as 3, the lane
- *                loads in flight during the long packets; 0 = wave-per-packet
+ *   "l4_small"   descriptor-batch kernel: 5 (default) split roles — groups
+ *                of 4 descriptors whose packets are all <= 64 B are summed a
+ *                lane per packet, every other group wave-per-packet; 0 =
+ *                wave-per-packet for all; 1-4 the thread-per-packet variants
+ *                (a lane per descriptor, long packets 2 (1) or 4 (2) at a
+ *                time; 3: a lane quad per descriptor; 4: as 3, lane loads in
+ *                flight during the long packets)
  *   "l4_small_uniform" uniform batches with segment_size <= 64 by the
  *                small-packet kernel, a lane quad (1) or a lane (2) per
  *                segment, or by the wave-per-packet kernel (0)

@@ -114,7 +114,8 @@ def test_uniform_geometry_sweep(gpu, seg, occ):
 
 DESC_VARIANTS = [{"l4_occ": 0}, {"l4_occ": 7}, {"l4_occ": 8}, {"l4_descv": 1}, {"l4_descv": 2, "l4_iters": 2},
                  {"l4_descv": 2, "l4_iters": 3, "l4_occ": 0}, {"l4_descv": 2, "l4_iters": 8, "l4_ppw": 2},
-                 {"l4_small": 1}, {"l4_small": 2}, {"l4_small": 3}, {"l4_small": 4}, {"l4_small": 1, "l4_nt": 0}]
+                 {"l4_small": 0}, {"l4_small": 1}, {"l4_small": 2}, {"l4_small": 3}, {"l4_small": 4},
+                 {"l4_small": 1, "l4_nt": 0}, {"l4_small": 5}, {"l4_small": 5, "l4_nt": 0}]
 
 
 @pytest.mark.parametrize("knobs", DESC_VARIANTS, ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()))
@@ -184,7 +185,7 @@ def test_uniform_small_segments(gpu, seg, knob):
         wga.tune_set("l4_small_uniform", saved)
 
 
-@pytest.mark.parametrize("small", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("small", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("seed", [5, 6])
 def test_desc_small_packets(gpu, small, seed):
     """Batches of mostly small packets (0-130 B, every alignment, csum_start

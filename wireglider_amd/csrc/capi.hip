@@ -37,7 +37,7 @@ static const Knob kKnobs[] = {
     {"l4_descv", nullptr, &Tune::l4_descv, 0, 2, nullptr, 0},
     {"l4_iters", nullptr, &Tune::l4_iters, 1, 64, nullptr, 0},
     {"l4_occ", nullptr, &Tune::l4_occ, 0, 0, kOcc, WG_N(kOcc)},
-    {"l4_small", nullptr, &Tune::l4_small, 0, 4, nullptr, 0},
+    {"l4_small", nullptr, &Tune::l4_small, 0, 5, nullptr, 0},
     {"l4_small_uniform", nullptr, &Tune::l4_small_uniform, 0, 2, nullptr, 0},
     {"gso_blocks", &Tune::gso_blocks, nullptr, 1, 1u << 23, nullptr, 0},
     {"gso_waves", nullptr, &Tune::gso_waves, 0, 0, kWaves, WG_N(kWaves)},
@@ -98,7 +98,12 @@ static Tune &tune_storage() {
         // one's finish (+3-5 % on config 5, profiles/r01_ab_session2.json).
         x.l4_descv = 2;
         x.l4_occ = 0;
-        x.l4_small = 0;
+        // Descriptor batches: the split-role kernel (l4_small = 5): small
+        // packets of all-small groups a lane each, the rest wave-per-packet.
+        // Config 4's 64-B sub-batch 0.336 -> 0.061 ms (35 % of the roofline);
+        // config 5 and config 4's mixed batch within 0.6 % of the
+        // wave-per-packet kernel (interleaved A/B, profiles/r02_small_ab.json).
+        x.l4_small = 5;
         x.l4_small_uniform = 2;  // lane per segment: 64-B PacketBatch 0.342 -> 0.043 ms (quad 0.074)
         x.l4_iters = 4;
         x.gso_blocks = 1u << 23;

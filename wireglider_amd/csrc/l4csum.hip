@@ -33,6 +33,7 @@ struct L4Params {
     uint32_t seg;
     uint32_t cs;
     uint32_t flags;
+    uint64_t quarter;  // l4csum_split_kernel: descriptors per quarter of the batch (a multiple of 4)
 };
 
 enum Kind : int { kUniformL4 = 0, kDescL4 = 1, kDescPlain = 2 };
@@ -229,6 +230,98 @@ __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t j) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
 }
 
+// The lane path for one packet of <= kSmallMax bytes at a (length len):
+// its five aligned 16-B chunks (default cache policy: a small packet's 128-B
+// lines are shared with its neighbours' lanes, and non-temporal loads fetched
+// them again — 64-B PacketBatch 42.9 -> 24.3 us), clamped onto the last
+// chunk the packet touches; `use` false -> the zero chunk.
+__device__ __forceinline__ void lane_chunks(uintptr_t a, uint32_t len, bool use, v4u W[5]) {
+    const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
+    const uintptr_t a0 = a & ~(uintptr_t)15;
+    const uintptr_t alast = (a + len - 1) & ~(uintptr_t)15;
+#pragma unroll
+    for (uint32_t k = 0; k < 5; k++) {
+        const uintptr_t ca = a0 + 16u * k;
+        W[k] = ld16(use ? (ca > alast ? alast : ca) : zero);  // clamped chunks are masked below
+    }
+}
+
+// ... summed: the chunks funnel-shifted into 16 packet-relative dwords
+// (bytes past the packet zeroed), so the region and address masks are
+// per-dword constants of len / csum_start and the addresses static dwords.
+// Returns the pre-complement folded sum t (region, byte-swapped when it pairs
+// from an odd packet offset, + pseudo-header when kL4); the caller's result
+// is ~fold16_32(t).
+template <bool kL4>
+__device__ __forceinline__ uint32_t lane_sum(const v4u W[5], uintptr_t a, uint32_t len, uint32_t cs, uint32_t fl) {
+    const uint32_t o0 = cs < len ? cs : len;
+    const bool v6 = fl & WG_PKT_V6;
+    const uint32_t Wd[20] = {W[0][0], W[0][1], W[0][2], W[0][3], W[1][0], W[1][1], W[1][2],
+                             W[1][3], W[2][0], W[2][1], W[2][2], W[2][3], W[3][0], W[3][1],
+                             W[3][2], W[3][3], W[4][0], W[4][1], W[4][2], W[4][3]};
+    const uint32_t s = (uint32_t)(a & 15u), q4 = s >> 2, sh = s & 3u;
+    uint32_t sr = 0, sq = 0;
+#pragma unroll
+    for (uint32_t m = 0; m < 16; m++) {
+        const uint32_t lo = q4 == 0 ? Wd[m] : q4 == 1 ? Wd[m + 1] : q4 == 2 ? Wd[m + 2] : Wd[m + 3];
+        const uint32_t hi = q4 == 0 ? Wd[m + 1] : q4 == 1 ? Wd[m + 2] : q4 == 2 ? Wd[m + 3] : Wd[m + 4];
+        const uint32_t r = bytes_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, len);
+        sr += half_sum(bytes_from(r, m, o0));
+        if (kL4) {
+            const bool in_addr = v6 ? (m >= 2u && m < 10u) : (m == 3u || m == 4u);  // v6 8-39, v4 12-19
+            sq += in_addr ? half_sum(r) : 0u;
+        }
+    }
+    sr = fold16_32(sr);
+    if (o0 & 1u)  // packet pairing; the region pairs from an odd offset
+        sr = bswap16(sr);
+    uint32_t t = sr;
+    if (kL4) {
+        const uint32_t proto = (fl & WG_PKT_TCP) ? 6u : 17u;
+        t += fold16_32(sq) + (proto << 8) + bswap16((len - cs) & 0xffffu);  // checksum.hpp:111-114, checksum.cpp:23,33
+    }
+    return t;
+}
+
+// The wave path: the packets of the lanes in mask m (lane j's packet at a,
+// length len, csum_start cs, flags fl), Q at a time through the issue /
+// finish machinery of l4csum_kernel (all Q packets' loads in flight before
+// the first wait); packet j's result lands in lane j's res.
+template <bool kL4, bool kNT, int Q>
+__device__ __forceinline__ void wave_long(uint64_t m, uintptr_t a, uint32_t len, uint32_t cs, uint32_t fl,
+                                          const uint8_t *base, uint32_t lane, uint32_t &res) {
+    const uint32_t alo = (uint32_t)a, ahi = (uint32_t)((uint64_t)a >> 32);
+    while (m) {
+        Geom g[Q];
+        uint32_t jj[Q];
+#pragma unroll
+        for (int k = 0; k < Q; k++) {
+            const bool have = m != 0;
+            const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
+            m = have ? m & (m - 1) : m;
+            jj[k] = have ? j : 64u;
+            g[k].a = have ? (uintptr_t)(((uint64_t)rdl(ahi, j) << 32) | rdl(alo, j)) : reinterpret_cast<uintptr_t>(base);
+            g[k].len = have ? rdl(len, j) : 0u;
+            g[k].cs = have ? rdl(cs, j) : 0u;
+            g[k].fl = have ? rdl(fl, j) : 0u;
+        }
+        Front f[Q];
+#pragma unroll
+        for (int k = 0; k < Q; k++)
+            issue<kL4, kNT>(g[k], lane, f[k]);
+#pragma unroll
+        for (int k = 0; k < Q; k++) {
+            uint32_t t = wave_sum_u32(finish<kNT>(lane, f[k]));
+            if (kL4) {
+                const uint32_t proto = (g[k].fl & WG_PKT_TCP) ? 6u : 17u;
+                t += (proto << 8) + bswap16((g[k].len - g[k].cs) & 0xffffu);
+            }
+            if (lane == jj[k])
+                res = ~fold16_32(t) & 0xffffu;
+        }
+    }
+}
+
 // G: lanes per descriptor.  G = 1: a lane loads all five chunks; G = 4: a
 // quad shares one descriptor, lane q of the quad loads chunks q and (q = 0)
 // chunk 4, and the quad's partial sums meet by DPP — a wave then carries 16
@@ -272,6 +365,10 @@ __global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
     uint32_t cidx[kC];
     const uint32_t s = (uint32_t)(a & 15u);
     auto load_chunks = [&]() {
+        if constexpr (G == 1) {
+            lane_chunks(a, len, small && len, W);
+            return;
+        }
         const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
         const uintptr_t a0 = a & ~(uintptr_t)15;
         const uintptr_t alast = (a + len - 1) & ~(uintptr_t)15;
@@ -289,33 +386,19 @@ __global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
         }
     };
     auto sum_chunks = [&]() {
+        if constexpr (G == 1) {
+            const uint32_t t = lane_sum<kL4>(W, a, len, cs, fl);
+            if (small)
+                res = ~fold16_32(t) & 0xffffu;
+            return;
+        }
         const uint32_t o0 = cs < len ? cs : len;
         const bool v6 = fl & WG_PKT_V6;
         const uint32_t ao = v6 ? 8u : 12u, al = v6 ? 32u : 8u;
         const uint32_t aend = ao + al < len ? ao + al : len;  // address bytes past the packet end are absent
         uint32_t sr = 0, sq = 0;
         uint32_t rodd;  // the region's pairing is odd relative to the summed dwords
-        if constexpr (G == 1) {
-            // funnel-shift the chunks into 16 packet-relative dwords (bytes
-            // past the packet zeroed): the masks become per-dword constants
-            // of len / o0, and the addresses static dwords
-            const uint32_t Wd[20] = {W[0][0], W[0][1], W[0][2], W[0][3], W[1][0], W[1][1], W[1][2],
-                                     W[1][3], W[2][0], W[2][1], W[2][2], W[2][3], W[3][0], W[3][1],
-                                     W[3][2], W[3][3], W[4][0], W[4][1], W[4][2], W[4][3]};
-            const uint32_t q4 = s >> 2, sh = s & 3u;
-#pragma unroll
-            for (uint32_t m = 0; m < 16; m++) {
-                const uint32_t lo = q4 == 0 ? Wd[m] : q4 == 1 ? Wd[m + 1] : q4 == 2 ? Wd[m + 2] : Wd[m + 3];
-                const uint32_t hi = q4 == 0 ? Wd[m + 1] : q4 == 1 ? Wd[m + 2] : q4 == 2 ? Wd[m + 3] : Wd[m + 4];
-                const uint32_t r = bytes_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, len);
-                sr += half_sum(bytes_from(r, m, o0));
-                if (kL4) {
-                    const bool in_addr = v6 ? (m >= 2u && m < 10u) : (m == 3u || m == 4u);  // v6 8-39, v4 12-19
-                    sq += in_addr ? half_sum(r) : 0u;
-                }
-            }
-            rodd = o0 & 1u;  // packet pairing; the addresses start at an even offset
-        } else {
+        {
 #pragma unroll
             for (uint32_t k = 0; k < kC; k++) {
 #pragma unroll
@@ -352,51 +435,91 @@ __global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
     }
 
     // ---- wave path: the longer packets of this wave, Q at a time
-    uint64_t m = __ballot(live && !small && q == 0);
-    const uint32_t alo = (uint32_t)a, ahi = (uint32_t)((uint64_t)a >> 32);
-    while (m) {
-        Geom g[Q];
-        uint32_t jj[Q];
-#pragma unroll
-        for (int k = 0; k < Q; k++) {
-            const bool have = m != 0;
-            const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
-            m = have ? m & (m - 1) : m;
-            jj[k] = have ? j : 64u;
-            g[k].a = have ? (uintptr_t)(((uint64_t)rdl(ahi, j) << 32) | rdl(alo, j)) : reinterpret_cast<uintptr_t>(p.base);
-            g[k].len = have ? rdl(len, j) : 0u;
-            g[k].cs = have ? rdl(cs, j) : 0u;
-            g[k].fl = have ? rdl(fl, j) : 0u;
-        }
-        Front f[Q];
-#pragma unroll
-        for (int k = 0; k < Q; k++)
-            issue<kL4, kNT>(g[k], lane, f[k]);
-#pragma unroll
-        for (int k = 0; k < Q; k++) {
-            uint32_t t = wave_sum_u32(finish<kNT>(lane, f[k]));
-            if (kL4) {
-                const uint32_t proto = (g[k].fl & WG_PKT_TCP) ? 6u : 17u;
-                t += (proto << 8) + bswap16((g[k].len - g[k].cs) & 0xffffu);
-            }
-            if (lane == jj[k])
-                res = ~fold16_32(t) & 0xffffu;
-        }
-    }
+    wave_long<kL4, kNT, Q>(__ballot(live && !small && q == 0), a, len, cs, fl, p.base, lane, res);
     if (kLate && any_small)
         sum_chunks();
     if (live && q == 0)
         p.out[i] = (uint16_t)res;
 }
 
+// Split-role descriptor kernel (knob l4_small = 5).  Descriptors come in
+// groups of 4 consecutive ones; the batch is cut into 4 quarters of Q
+// descriptors, and block b owns the 16 at [q*Q + 16b, q*Q + 16b + 16) of each
+// quarter q (64 in all).  Its wave k owns one group per quarter,
+// [q*Q + 16b + 4k, +4): 16 descriptors a quarter batch apart, like the
+// wave-per-packet kernel's grid-stride iterations (consecutive packets per
+// wave measured 3-4 % slower).
+//  * WAVE role (every wave): every packet of its groups that hold a packet
+//    longer than kSmallMax, 4 at a time through the wave-per-packet
+//    machinery; small packets among long ones ride along in their issue
+//    phase at next to no cost (config 4's mixed batch measured +2.5 % when
+//    they went to the lane role instead).
+//  * LANE role (wave 0): the block's all-small groups, a lane per packet,
+//    summed from its 5 aligned chunks (4 KiB of loads in flight per wave).
+// Wave 0 loads the block's 64 descriptors (lane l = descriptor
+// (l >> 4) * Q + 16b + (l & 15); its own groups are lanes with (l & 15) < 4),
+// waves 1-3 their 16: every descriptor read once from HBM.  An all-small
+// batch keeps a lane per packet (waves 1-3 leave after one descriptor load),
+// an all-long one keeps the short 16-packet waves with every descriptor in
+// one vector load.  One launch, no host knowledge of the mix.
+template <int kKind, bool kNT>
+__global__ __launch_bounds__(256) void l4csum_split_kernel(L4Params p) {
+    constexpr bool kL4 = kKind != kDescPlain;
+    const uint32_t lane = lane_id();
+    const uint32_t wib = wave_in_block();
+    const uint64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
+    const uint64_t Q = p.quarter;
+    // lane -> (quarter, offset in the block's 16 of that quarter)
+    const uint32_t qq = wib == 0 ? lane >> 4 : (lane >> 2) & 3u;
+    const uint32_t oo = wib == 0 ? lane & 15u : 4u * wib + (lane & 3u);
+    const uint64_t i = (uint64_t)qq * Q + 16u * blk + oo;
+    const bool live = (wib == 0 || lane < 16u) && 16u * blk < Q && i < p.n;
+    const v4u d = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : p.n - 1));
+    const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + (live ? off : 0u);
+    const uint32_t len = live ? d.z : 0u;
+    const uint32_t cs = kL4 && live ? (d.w & 0xffffu) : 0u;
+    const uint32_t fl = live ? (d.w >> 16) & 0xffu : 0u;
+    // groups are 4 consecutive lanes in both layouts
+    const uint64_t gl = __ballot(live && len > kSmallMax);
+    const bool grp_long = ((gl >> (lane & ~3u)) & 0xfu) != 0;
+    // ---- wave role: this wave's groups that hold a long packet
+    const bool own = wib == 0 ? (lane & 15u) < 4u : true;
+    const bool mine = live && own && grp_long;
+    uint32_t res = 0;
+    wave_long<kL4, kNT, 4>(__ballot(mine), a, len, cs, fl, p.base, lane, res);
+    if (mine)
+        p.out[i] = (uint16_t)res;
+    // ---- lane role (wave 0): the block's all-small groups
+    const bool small = wib == 0 && live && !grp_long;
+    if (__ballot(small)) {  // wave-uniform; never true on waves 1-3
+        v4u W[5];
+        lane_chunks(a, len, small && len, W);
+        const uint32_t t = lane_sum<kL4>(W, a, small ? len : 0u, cs, fl);
+        if (small)
+            p.out[i] = (uint16_t)(~fold16_32(t) & 0xffffu);
+    }
+}
+
 template <int kKind, bool kNT>
 static int launch_small(const L4Params &p, uint32_t mode, hipStream_t st) {
     const uint32_t per_block = mode >= 3 ? 64u : 256u;  // descriptors per 256-thread block
-    const uint64_t blocks = (p.n + per_block - 1) / per_block;
+    uint64_t blocks = (p.n + per_block - 1) / per_block;
+    L4Params q = p;
+    if (mode == 5) {
+        // quarters of Q descriptors (a multiple of 16: block b owns
+        // [q*Q + 16b, +16) of each quarter, whole 4-descriptor groups); 4 Q >= n
+        q.quarter = ((p.n + 3) / 4 + 15) & ~15ull;
+        blocks = q.quarter / 16;
+        if (blocks >= 8)
+            blocks = (blocks + 7) & ~7ull;  // XCD swizzle bijective; surplus blocks have no live lane
+    }
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
     const dim3 grid((unsigned)blocks), blk(256);
-    if (mode == 4)
+    if (mode == 5)
+        hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT>), grid, blk, 0, st, q);
+    else if (mode == 4)
         hipLaunchKernelGGL((l4csum_small_kernel<kKind, kNT, 4, 4, true>), grid, blk, 0, st, p);
     else if (mode == 3)
         hipLaunchKernelGGL((l4csum_small_kernel<kKind, kNT, 4, 4>), grid, blk, 0, st, p);

@@ -15,7 +15,7 @@ struct Tune {
     uint32_t l4_nt;       // 1: non-temporal packet loads
     uint32_t l4_descv;    // descriptor mode: 0 scalar loads, 1 vector load, 2 vector prefetch of the next iteration
     uint32_t l4_iters;    // iterations per wave in descriptor mode 2
-    uint32_t l4_small;    // 1: descriptor batches by the thread-per-packet kernel (packets <= 64 B in a lane)
+    uint32_t l4_small;    // descriptor-batch kernel: 5 split roles (default), 0 wave-per-packet, 1-4 thread-per-packet variants
     uint32_t l4_small_uniform;  // 1: uniform batches with segment_size <= 64 by the small-packet kernel
     uint32_t l4_occ;      // waves/SIMD target of the L4 kernels at 4 packets/wave (0 = compiler's choice; 7, 8)
     uint64_t gso_blocks;  // grid cap for the GSO split kernel (one block per super-buffer)
