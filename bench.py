@@ -95,6 +95,7 @@ class Workload:
     unit: str = "GiB/s"
     value_scale: float = 2.0**-30     # metric value = payload units/s x value_scale
     post: Optional[Callable] = None   # workload-specific post-check
+    probe_run: int = 0                # packet size for the kernel-shaped read probe (0: contiguous only)
 
 
 def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workload:
@@ -120,7 +121,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                "packets_per_gpu": n, "segment_size": SEG, "csum_start": 20, "layout": "uniform",
                "parallelism": f"shard{world} (independent packet shards, no data-path collective)"}
         return Workload(launch, n, n * SEG, n * SEG + 2 * n, cfg, "weak", buf, "wg::l4csum_kernel<0,4,nt>",
-                        rank * n, out, desc, sample, [n] * world)
+                        rank * n, out, desc, sample, [n] * world, probe_run=SEG)
     if name == "config5":
         from wireglider_amd import dist as wdist
 
@@ -147,7 +148,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
         counts = [wdist.shard_bounds(total, world, r)[1] - wdist.shard_bounds(total, world, r)[0]
                   for r in range(world)]
         return Workload(launch, n, n * SEG, n * SEG + 2 * n + 16 * n, cfg, "strong", buf,
-                        "wg::l4csum_kernel<1,4,nt>", lo, out, desc, sample, counts)
+                        "wg::l4csum_split_kernel<1,nt> (l4_small=5)", lo, out, desc, sample, counts, probe_run=SEG)
     if name in ("config3", "config3udp"):
         udp = name == "config3udp"
         n, in_stride, out_stride = 1 << 18, 65536, 73216  # outbuf stride of worker/encap.cpp:26
@@ -243,7 +244,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                            "(tests/test-checksum.cpp:11-17 shape; BASELINE configs[0]), descriptor batch",
                "buffers_per_gpu": n, "buffer_bytes": size, "layout": "descriptor", "parallelism": f"shard{world}"}
         return Workload(launch, n, n * size, n * size + 2 * n + 16 * n, cfg, "weak", buf,
-                        "wg::l4csum_kernel<2,4,nt> (plain checksum, descriptor mode 2)", rank * n, sample=sample,
+                        "wg::l4csum_split_kernel<2,nt> (plain checksum, l4_small=5)", rank * n, sample=sample,
                         counts=[n] * world,
                         metric="device-resident GiB/s, checksum(span, 0) over 64 KiB buffers (BASELINE config 1 shape)")
     if name == "verify":
@@ -316,7 +317,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                            "checksums stored, evaluate_packet checksum gates (wg_verify_desc)",
                "packets_per_gpu": n, "segment_size": SEG, "layout": "descriptor", "parallelism": f"shard{world}"}
         return Workload(launch, n, n * SEG, n * SEG + 16 * n + n + 2 * n, cfg, "weak", buf,
-                        "wg::verify_kernel<4>", rank * n, sample=sample, counts=[n] * world,
+                        "wg::verify_kernel<4>", rank * n, sample=sample, counts=[n] * world, probe_run=SEG,
                         metric="device-resident GiB/s, decap verify gates over packet batch (SURVEY f1)",
                         post=post)
     if name == "gro":
@@ -472,7 +473,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
 
     cfg = {"workload": "config4: 4,194,304 IPv4/UDP packets, 64 B / 9000 B 50/50, packed, descriptor batch",
            "packets_per_gpu": n, "layout": "descriptor", "parallelism": f"shard{world}"}
-    return Workload(launch, n, total, total + 2 * n + 16 * n, cfg, "weak", buf, "wg::l4csum_kernel<1,4,nt>",
+    return Workload(launch, n, total, total + 2 * n + 16 * n, cfg, "weak", buf, "wg::l4csum_split_kernel<1,nt> (l4_small=5)",
                     rank * n, out, desc, sample, [n] * world, post=post)
 
 
@@ -490,23 +491,30 @@ def settle(torch, fn, seconds: float) -> int:
     return k
 
 
-def measured_read_peak(torch, wga, buf, iters: int = 30) -> float:
-    """Read-roofline probe over the batch buffer itself: the same bytes,
-    read by the same access structure with no checksum work (GB/s)."""
+def measured_read_peak(torch, wga, buf, iters: int = 30, run_bytes: int = 0) -> dict:
+    """Read-roofline probe over the batch buffer itself: the same bytes, read
+    with no checksum work (GB/s) — contiguous one-shot waves of 2/4/8 KiB,
+    and, for batches of <= 2 KiB packets (run_bytes), the L4 kernel's own
+    issue structure (4 packets per wave, two 16-B loads per lane each).  The
+    best of them is the ceiling."""
     acc = torch.zeros(1, dtype=torch.int64, device=buf.device)
     n = min(buf.numel(), 4 << 30) // 16 * 16
     view = buf[:n]
-    best = 0.0
-    for kib in (2, 4, 8):
-        settle(torch, lambda: wga.probe_read(view, acc, kib), 0.05)
+    variants = [(f"contiguous_{k}KiB", k, 0) for k in (2, 4, 8)]
+    if 0 < run_bytes <= 2048:
+        variants.append((f"runs_{run_bytes}B_x4_per_wave", 1, run_bytes))
+    rates = {}
+    for name, kib, run in variants:
+        nb = n if not run else n // run * run
+        settle(torch, lambda: wga.probe_read(view, acc, kib, run_bytes=run), 0.05)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(iters):
-            wga.probe_read(view, acc, kib)
+            wga.probe_read(view, acc, kib, run_bytes=run)
         e1.record()
         torch.cuda.synchronize()
-        best = max(best, n * iters / (e0.elapsed_time(e1) * 1e-3) / 1e9)
-    return best
+        rates[name] = round(nb * iters / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+    return {"best": max(rates.values()), "variants": rates}
 
 
 def cpu_baseline(sample_fn, seconds: float):
@@ -825,7 +833,8 @@ def main():
     value = t["total_payload"] * args.steps / wall * wl.value_scale
     achieved = wl.alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args.workload)
-    read_peak = measured_read_peak(torch, wga, wl.buf) if rank == 0 else None
+    probe = measured_read_peak(torch, wga, wl.buf, run_bytes=wl.probe_run) if rank == 0 else None
+    read_peak = probe["best"] if probe else None
     # The CPU baseline samples the batch as the timed launches saw it, so it
     # runs before post_checks (whose verify pass stores the checksums into the
     # packets).
@@ -866,6 +875,7 @@ def main():
             "alg_bytes_per_launch": meta["alg_bytes"],
             "traffic_source": f"profiles/pmc_{args.workload}.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)",
             "measured_read_peak": round(read_peak, 1) if read_peak else None,
+            "read_probe_variants": probe["variants"] if probe else None,
             "frac_of_measured_read_peak": round(achieved / read_peak, 4) if read_peak else None,
             "kernel_ms_avg": round(kern_ms, 5),
             "kernel_ms_avg_max_over_ranks": round(t["kern_ms_max"], 5),

@@ -205,13 +205,30 @@ typedef struct wg_gro_desc {
 int wg_gro_finalize(uint8_t *dev_hdrs, wg_gro_desc *dev_desc, uint64_t n, void *stream);
 
 /* ------------------------------------------------------------------------
- * Host-memory path: the batch starts and ends in host
- * memory.  Pinned staging + hipMemcpyAsync H2D -> kernel -> D2H on the
- * engine's per-thread stream; synchronous.  Uses a per-thread device
- * workspace that grows to the largest batch seen.
+ * Host-memory path: the batch starts and ends in host memory
+ * (tun read buffers, worker/encap.cpp:74-97; UDP GRO recvmsg buffers,
+ * worker/decap.cpp:16-28,90-156).  Synchronous.  The batch is cut into
+ * ~32 MiB chunks of whole segments that flow through a per-thread pipeline of
+ * three device slots on two streams: chunk k+1's hipMemcpyAsync H2D runs
+ * under chunk k's kernel and result copy; results gather in a pinned buffer
+ * and reach host_out once at the end.  host_base may be pageable (the HIP
+ * runtime stages it) or pinned (wg_host_alloc: DMA straight from it).  The
+ * workspace (streams, events, device slots, pinned results) is per calling
+ * thread, reused across calls, and freed at thread exit or by
+ * wg_host_release().  Rate: PCIe-bound, never the metric.
  * ---------------------------------------------------------------------- */
 int wg_l4csum_uniform_host(const uint8_t *host_base, uint64_t total_len, uint32_t segment_size,
                            uint16_t csum_start, uint32_t flags, uint16_t *host_out);
+
+/* Free the calling thread's host-path workspace now (it is rebuilt on the
+ * next wg_l4csum_uniform_host call).  Always WG_OK. */
+int wg_host_release(void);
+
+/* Pinned (page-locked) host memory for packet I/O buffers — the reference's
+ * per-thread tun / UDP buffers allocated this way are DMA'd by the host path
+ * without runtime staging.  wg_host_free(NULL) is a no-op. */
+int wg_host_alloc(void **ptr, uint64_t bytes);
+int wg_host_free(void *ptr);
 
 /* ------------------------------------------------------------------------
  * Synthetic batches (benchmark / test data, written on the device; not part
@@ -292,11 +309,16 @@ int wg_tune_set(const char *key, uint64_t value);
 int wg_tune_get(const char *key, uint64_t *value);
 
 /* Read-roofline probe (benchmark support): streams dev[0, nbytes) with
- * non-temporal 16-B loads, one-shot waves of `kib_per_wave` (1/2/4/8)
- * contiguous KiB each, and adds a folded sum into *dev_out.  Its bandwidth
- * is the measured read ceiling the checksum kernels are compared against. */
+ * non-temporal 16-B loads and folds the bytes into a sum that is stored to
+ * *dev_out only in a case real data never hits.  run_bytes = 0: one-shot
+ * waves of `kib_per_wave` (1/2/4/8) contiguous KiB each.  run_bytes in
+ * [1, 2048]: the L4 kernel's own issue structure on a uniform batch of
+ * run_bytes-byte segments (4 segments per one-shot wave, two 64-lane 16-B
+ * loads per segment, all in flight at once), over nbytes / run_bytes whole
+ * segments.  Its bandwidth is the measured read ceiling the checksum kernels
+ * are compared against. */
 int wg_probe_read(const uint8_t *dev, uint64_t nbytes, uint64_t *dev_out, uint32_t kib_per_wave,
-                  uint32_t reserved, void *stream);
+                  uint32_t run_bytes, void *stream);
 
 /* Copy-roofline probe: dst[0, nbytes) = src[0, nbytes) by one-shot waves of
  * `kib_per_wave` (1/2/4) KiB, non-temporal loads and stores; the measured

@@ -62,6 +62,9 @@ def test_invalid_args_rejected_without_gpu():
     assert wga.lib.wg_l4csum_uniform(None, 100, 1500, 20, 0, None, None) == -1
     assert wga.lib.wg_l4csum_uniform(1, 100, 0, 20, 0, 1, None) == -1
     assert wga.lib.wg_l4csum_desc(16, 17, 1, 16, None) == -1
+    # the kernel-shaped read probe takes segments of at most 2 KiB
+    assert wga.lib.wg_probe_read(16, 1 << 20, 16, 1, 4096, None) == -1
+    assert wga.lib.wg_probe_read(16, 100, 16, 1, 1500, None) == -1
 
 
 DROPIN_TEST = r"""

@@ -363,3 +363,65 @@ def test_long_packets(gpu):
     out = wga.calc_l4_checksum_batch(view, seg, True, True, 40)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.l4_uniform(u, seg, 40, 3))
+
+
+def test_read_probe_variants_run(gpu):
+    """The read probes (bench.py's measured ceiling) over odd sizes: the
+    contiguous and the kernel-shaped (segment runs) variants launch, finish
+    and never store for real data; out-of-contract run sizes are rejected."""
+    import torch
+
+    wga = _wga()
+    buf = torch.empty(1500 * 1001 + 16, dtype=torch.uint8, device=gpu)
+    wga.synth_fill(buf, 3)
+    acc = torch.zeros(1, dtype=torch.int64, device=gpu)
+    for kib, run in ((1, 0), (2, 0), (8, 0), (1, 1500), (1, 64), (1, 2048), (1, 17)):
+        wga.probe_read(buf, acc, kib, run_bytes=run)
+    torch.cuda.synchronize()
+    assert int(acc.item()) == 0
+    with pytest.raises(Exception):
+        wga.probe_read(buf, acc, 1, run_bytes=4096)
+
+
+def test_host_pipeline_multichunk(gpu):
+    """wg_l4csum_uniform_host's chunked two-stream pipeline:
+    batches spanning many ~32 MiB chunks and more chunks than device slots,
+    odd totals with a short last segment, a segment larger than a chunk,
+    pageable and pinned (wg_host_alloc) inputs, two host threads at once,
+    and a rebuild after wg_host_release — every result against the oracle."""
+    import threading
+
+    wga = _wga()
+    rng = np.random.default_rng(4242)
+    cases = [(1500, 1500 * 70001 - 777), (64, 64 * 1_200_001 + 5), (9000, 9000 * 12000 + 1),
+             ((33 << 20) + 7, ((33 << 20) + 7) * 2 + 12345)]
+    for seg, total in cases:
+        buf = rng.integers(0, 256, total, dtype=np.uint8)
+        cs, fl = int(rng.choice([20, 21, 40])), int(rng.integers(0, 4))
+        got = wga.calc_l4_checksum_host(buf, seg, bool(fl & 1), bool(fl & 2), cs)
+        np.testing.assert_array_equal(got, oracle.l4_uniform(buf, seg, cs, fl), err_msg=f"seg={seg} total={total}")
+    # pinned input
+    pb = wga.PinnedBuffer(1500 * 50000 + 3)
+    pb.array[:] = rng.integers(0, 256, pb.nbytes, dtype=np.uint8)
+    got = wga.calc_l4_checksum_host(pb.array, 1500, False, True, 20)
+    np.testing.assert_array_equal(got, oracle.l4_uniform(pb.array, 1500, 20, 2))
+    pb.close()
+    # two threads, each with its own pipeline, concurrently
+    bufs = [rng.integers(0, 256, 1500 * 40000 + k, dtype=np.uint8) for k in (11, 13)]
+    res = [None, None]
+
+    def work(k):
+        for _ in range(3):
+            res[k] = wga.calc_l4_checksum_host(bufs[k], 1500, bool(k), False, 20)
+        wga.host_release()
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in (0, 1)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for k in (0, 1):
+        np.testing.assert_array_equal(res[k], oracle.l4_uniform(bufs[k], 1500, 20, k))
+    wga.host_release()
+    got = wga.calc_l4_checksum_host(bufs[0], 1500, False, False, 20)  # rebuilt after release
+    np.testing.assert_array_equal(got, oracle.l4_uniform(bufs[0], 1500, 20, 0))

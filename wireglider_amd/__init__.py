@@ -41,6 +41,9 @@ EXPORTED_SYMBOLS = (
     "wg_gso_split",
     "wg_gro_finalize",
     "wg_l4csum_uniform_host",
+    "wg_host_release",
+    "wg_host_alloc",
+    "wg_host_free",
     "wg_synth_fill",
     "wg_synth_headers",
     "wg_synth_desc_stride",
@@ -108,6 +111,9 @@ def _load() -> ctypes.CDLL:
 
         "wg_gro_finalize": (i32, [u8p, vp, u64, vp]),
         "wg_l4csum_uniform_host": (i32, [u8p, u64, u32, u16, u32, vp]),
+        "wg_host_release": (i32, []),
+        "wg_host_alloc": (i32, [ctypes.POINTER(ctypes.c_void_p), u64]),
+        "wg_host_free": (i32, [vp]),
         "wg_synth_fill": (i32, [u8p, u64, u64, u64, vp]),
         "wg_synth_headers": (i32, [u8p, vp, u64, u64, u64, vp]),
         "wg_synth_desc_stride": (i32, [vp, u64, u64, u32, i32, u64, u64, vp]),
@@ -311,6 +317,36 @@ def calc_l4_checksum_host(buf: bytes | bytearray | memoryview, segment_size: int
     return out
 
 
+def host_release() -> None:
+    """Free this thread's host-path workspace (rebuilt on next use)."""
+    _check(lib.wg_host_release(), "wg_host_release")
+
+
+class PinnedBuffer:
+    """Pinned host memory from wg_host_alloc (the engine's packet I/O
+    buffers), exposed as a numpy uint8 array; freed by close() / GC."""
+
+    def __init__(self, nbytes: int):
+        import numpy as np
+
+        self._p = ctypes.c_void_p()
+        _check(lib.wg_host_alloc(ctypes.byref(self._p), nbytes), "wg_host_alloc")
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self._p.value))
+
+    def close(self) -> None:
+        if self._p is not None and self._p.value:
+            self.array = None
+            _check(lib.wg_host_free(self._p), "wg_host_free")
+        self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 # ---------------------------------------------------------------------------
 # synthetic batches (bench / tests)
 # ---------------------------------------------------------------------------
@@ -358,11 +394,12 @@ def tune_get(key: str) -> int:
     return int(v.value)
 
 
-def probe_read(buf, out, kib_per_wave: int = 4, stream=None) -> None:
-    """Launch the read-roofline probe over a device buffer."""
+def probe_read(buf, out, kib_per_wave: int = 4, stream=None, run_bytes: int = 0) -> None:
+    """Launch the read-roofline probe over a device buffer (run_bytes > 0:
+    the L4 kernel's issue structure over run_bytes-byte segments)."""
     with _on(buf):
-        _check(lib.wg_probe_read(buf.data_ptr(), buf.numel() * buf.element_size(), out.data_ptr(), kib_per_wave, 0,
-                                 _stream_ptr(stream, buf)), "wg_probe_read")
+        _check(lib.wg_probe_read(buf.data_ptr(), buf.numel() * buf.element_size(), out.data_ptr(), kib_per_wave,
+                                 run_bytes, _stream_ptr(stream, buf)), "wg_probe_read")
 
 
 def probe_copy(src, dst, kib_per_wave: int = 2, stream=None) -> None:

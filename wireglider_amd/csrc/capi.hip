@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
 
@@ -163,56 +164,110 @@ bool debug_sync(hipStream_t st, const char *kernel) {
     return false;
 }
 
-// Per-host-thread device workspace for the host-memory path.  Grows to the
-// largest batch seen; freed at thread exit.
-struct HostCtx {
+// Host-memory path: per host thread, a pipeline of kSlots
+// device chunk buffers on two streams.  Chunk k's H2D copy (stream h2d)
+// waits only for the kernel that last used its slot; its kernel and the D2H
+// of its results (stream exec) wait for its copy — so chunk k+1's copy runs
+// under chunk k's kernel and result copy.  Results land in a pinned buffer
+// and are copied to the caller's array once at the end (2 B per packet), so
+// no D2H targets pageable memory mid-pipeline (a pageable D2H synchronises).
+// Device memory is reused across calls and grows only with the chunk size.
+struct HostPipe {
+    static constexpr int kSlots = 3;
     int device = -1;
-    hipStream_t stream = nullptr;
-    uint8_t *dbuf = nullptr;
-    size_t dcap = 0;
-    uint16_t *dout = nullptr;
-    size_t ocap = 0;
-    ~HostCtx() {
-        if (device < 0)
-            return;
-        hipSetDevice(device);
-        if (dbuf) hipFree(dbuf);
-        if (dout) hipFree(dout);
-        if (stream) hipStreamDestroy(stream);
-    }
+    hipStream_t h2d = nullptr, exec = nullptr;
+    hipEvent_t copied[kSlots] = {}, done[kSlots] = {};
+    uint8_t *dbuf[kSlots] = {};
+    uint16_t *dres[kSlots] = {};
+    size_t slot_bytes = 0, slot_res = 0;
+    uint16_t *hres = nullptr;  // pinned
+    size_t hres_cap = 0;
+    void release();
+    ~HostPipe();
 };
 
-static thread_local HostCtx g_host;
+// Set by an atexit handler (registered when the first pipeline is built):
+// thread-exit destructors that run after it must not call into a HIP runtime
+// that may already be torn down — the process is ending and the driver
+// reclaims the memory anyway.
+static std::atomic<bool> g_exiting{false};
 
-static int host_ctx_reserve(size_t bytes, size_t outs) {
-    HostCtx &c = g_host;
-    if (c.device < 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess)
-            return WG_ERR_NODEV;
-        if (hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess)
-            return WG_ERR_RUNTIME;
-        c.device = dev;
+void HostPipe::release() {
+    if (device < 0)
+        return;
+    hipSetDevice(device);
+    for (int k = 0; k < kSlots; k++) {
+        if (dbuf[k]) hipFree(dbuf[k]);
+        if (dres[k]) hipFree(dres[k]);
+        if (copied[k]) hipEventDestroy(copied[k]);
+        if (done[k]) hipEventDestroy(done[k]);
+        dbuf[k] = nullptr;
+        dres[k] = nullptr;
+        copied[k] = done[k] = nullptr;
     }
-    if (bytes > c.dcap) {
-        if (c.dbuf) hipFree(c.dbuf);
-        c.dbuf = nullptr;
-        size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes;
-        if (hipMalloc(&c.dbuf, cap) != hipSuccess) {
-            c.dcap = 0;
+    if (hres) hipHostFree(hres);
+    if (h2d) hipStreamDestroy(h2d);
+    if (exec) hipStreamDestroy(exec);
+    hres = nullptr;
+    h2d = exec = nullptr;
+    hres_cap = slot_bytes = slot_res = 0;
+    device = -1;
+}
+
+HostPipe::~HostPipe() {
+    if (!g_exiting.load())
+        release();
+}
+
+static thread_local HostPipe g_pipe;
+
+static int pipe_init(HostPipe &c) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        return WG_ERR_NODEV;
+    if (c.device == dev)
+        return WG_OK;
+    c.release();  // first use on this thread, or the thread switched devices
+    static std::once_flag once;
+    std::call_once(once, [] { std::atexit([] { g_exiting.store(true); }); });
+    c.device = dev;
+    if (hipStreamCreateWithFlags(&c.h2d, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c.exec, hipStreamNonBlocking) != hipSuccess)
+        return WG_ERR_RUNTIME;
+    for (int k = 0; k < HostPipe::kSlots; k++)
+        if (hipEventCreateWithFlags(&c.copied[k], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c.done[k], hipEventDisableTiming) != hipSuccess)
             return WG_ERR_RUNTIME;
+    return WG_OK;
+}
+
+static int pipe_reserve(HostPipe &c, size_t slot_bytes, size_t slot_res, size_t total_res) {
+    if (slot_bytes > c.slot_bytes || slot_res > c.slot_res) {
+        if (hipStreamSynchronize(c.exec) != hipSuccess || hipStreamSynchronize(c.h2d) != hipSuccess)
+            return WG_ERR_RUNTIME;
+        const size_t nb = slot_bytes > c.slot_bytes ? slot_bytes : c.slot_bytes;
+        const size_t nr = slot_res > c.slot_res ? slot_res : c.slot_res;
+        for (int k = 0; k < HostPipe::kSlots; k++) {
+            if (c.dbuf[k]) hipFree(c.dbuf[k]);
+            if (c.dres[k]) hipFree(c.dres[k]);
+            c.dbuf[k] = nullptr;
+            c.dres[k] = nullptr;
         }
-        c.dcap = cap;
+        c.slot_bytes = c.slot_res = 0;
+        for (int k = 0; k < HostPipe::kSlots; k++)
+            if (hipMalloc(&c.dbuf[k], nb) != hipSuccess || hipMalloc(&c.dres[k], nr * sizeof(uint16_t)) != hipSuccess)
+                return WG_ERR_RUNTIME;
+        c.slot_bytes = nb;
+        c.slot_res = nr;
     }
-    if (outs > c.ocap) {
-        if (c.dout) hipFree(c.dout);
-        c.dout = nullptr;
-        size_t cap = outs < 4096 ? 4096 : outs;
-        if (hipMalloc(&c.dout, cap * sizeof(uint16_t)) != hipSuccess) {
-            c.ocap = 0;
+    if (total_res > c.hres_cap) {
+        if (c.hres) hipHostFree(c.hres);
+        c.hres = nullptr;
+        c.hres_cap = 0;
+        const size_t cap = total_res < 4096 ? 4096 : total_res;
+        if (hipHostMalloc(reinterpret_cast<void **>(&c.hres), cap * sizeof(uint16_t), hipHostMallocDefault) != hipSuccess)
             return WG_ERR_RUNTIME;
-        }
-        c.ocap = cap;
+        c.hres_cap = cap;
     }
     return WG_OK;
 }
@@ -243,6 +298,38 @@ __global__ __launch_bounds__(256) void probe_read_kernel(const uint8_t *dev, uin
     const uint32_t s = wave_sum_u32(fold16(acc.value()));
     // Keep the loads live without a contended atomic: a data-dependent store
     // that (for any real data) never fires.
+    if (lane == 0 && s == 0xFFFFFFFFu) *out = s;
+}
+
+// Read probe with the packet kernels' issue structure: one-shot waves, each
+// reading P = 4 runs of `run` bytes (consecutive runs = consecutive
+// packets of a uniform batch), every run as two 64-lane 16-B loads (the
+// aligned chunks covering it, clamped onto its last chunk — duplicate lanes
+// coalesce), all 8 loads issued before the first use, non-temporal.  The
+// same bytes and the same load pattern as l4csum_kernel on a PacketBatch of
+// run-byte segments, with none of its work: its rate bounds that kernel.
+template <int P>
+__global__ __launch_bounds__(256) void probe_read_runs_kernel(const uint8_t *dev, uint64_t nruns, uint32_t run,
+                                                              uint64_t *out) {
+    const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
+    const uint64_t r0 = wave * P;
+    if (r0 >= nruns)
+        return;
+    const uint32_t lane = lane_id();
+    v4u v[2 * P];
+#pragma unroll
+    for (int j = 0; j < P; j++) {
+        const uint64_t r = r0 + j < nruns ? r0 + j : nruns - 1;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(dev) + r * run;
+        const uintptr_t c0 = a & ~(uintptr_t)15;
+        const uint32_t last = (uint32_t)(((a + run - 1) & ~(uintptr_t)15) - c0) >> 4;
+        v[2 * j] = ld16_nt(c0 + 16u * (lane < last ? lane : last));
+        v[2 * j + 1] = ld16_nt(c0 + 16u * (lane + 64 < last ? lane + 64 : last));
+    }
+    Acc acc;
+#pragma unroll
+    for (int j = 0; j < 2 * P; j++) acc.add4(v[j]);
+    const uint32_t s = wave_sum_u32(fold16(acc.value()));
     if (lane == 0 && s == 0xFFFFFFFFu) *out = s;
 }
 
@@ -291,10 +378,19 @@ extern "C" int wg_probe_copy(const uint8_t *src, uint8_t *dst, uint64_t nbytes, 
 }
 
 extern "C" int wg_probe_read(const uint8_t *dev, uint64_t nbytes, uint64_t *dev_out, uint32_t kib_per_wave,
-                             uint32_t unused, void *stream) {
-    (void)unused;
+                             uint32_t run_bytes, void *stream) {
     if (!dev || !dev_out || (reinterpret_cast<uintptr_t>(dev) & 15) || nbytes < 16) return WG_ERR_INVALID;
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (run_bytes) {  // the packet kernels' structure: 4 runs of run_bytes per wave
+        if (run_bytes > 2048 || nbytes < run_bytes) return WG_ERR_INVALID;
+        const uint64_t nruns = nbytes / run_bytes;
+        uint64_t blocks = (nruns + 15) / 16;
+        if (blocks >= 8) blocks = (blocks + 7) & ~7ull;
+        if (blocks > 0x7fffffffull) return WG_ERR_INVALID;
+        hipLaunchKernelGGL(probe_read_runs_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, st, dev, nruns, run_bytes,
+                           dev_out);
+        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+    }
     const uint64_t nch = nbytes >> 4;
     const uint32_t U = kib_per_wave == 2 || kib_per_wave == 4 || kib_per_wave == 8 ? kib_per_wave : 1;
     uint64_t blocks = (nch + 256ull * U - 1) / (256ull * U);
@@ -345,6 +441,10 @@ extern "C" int wg_device_count(void) {
     return n;
 }
 
+// Chunk size of the host pipeline: whole segments, ~32 MiB (H2D ~0.6 ms at
+// PCIe Gen5 rates, long enough to amortise three launches per chunk).
+static constexpr uint64_t kHostChunkBytes = 32ull << 20;
+
 extern "C" int wg_l4csum_uniform_host(const uint8_t *host_base, uint64_t total_len, uint32_t segment_size,
                                       uint16_t csum_start, uint32_t flags, uint16_t *host_out) {
     if (!segment_size || (total_len && (!host_base || !host_out)))
@@ -353,17 +453,65 @@ extern "C" int wg_l4csum_uniform_host(const uint8_t *host_base, uint64_t total_l
         return WG_OK;
     if (wg_device_count() <= 0)
         return WG_ERR_NODEV;
-    const uint64_t n = (total_len + segment_size - 1) / segment_size;
-    int rc = host_ctx_reserve((size_t)total_len, (size_t)n);
+    HostPipe &c = g_pipe;
+    int rc = pipe_init(c);
     if (rc != WG_OK)
         return rc;
-    HostCtx &c = g_host;
-    if (hipMemcpyAsync(c.dbuf, host_base, total_len, hipMemcpyHostToDevice, c.stream) != hipSuccess)
-        return WG_ERR_RUNTIME;
-    rc = wg_l4csum_uniform(c.dbuf, total_len, segment_size, csum_start, flags, c.dout, c.stream);
+    const uint64_t nseg_total = (total_len + segment_size - 1) / segment_size;
+    uint64_t per = kHostChunkBytes / segment_size;  // segments per chunk
+    if (per == 0)
+        per = 1;
+    const uint64_t chunk = per * segment_size;
+    const uint64_t slot_bytes = chunk < total_len ? chunk : total_len;
+    rc = pipe_reserve(c, (size_t)slot_bytes, (size_t)(per < nseg_total ? per : nseg_total), (size_t)nseg_total);
     if (rc != WG_OK)
         return rc;
-    if (hipMemcpyAsync(host_out, c.dout, n * sizeof(uint16_t), hipMemcpyDeviceToHost, c.stream) != hipSuccess)
+    for (uint64_t off = 0, k = 0; off < total_len; off += chunk, k++) {
+        const int slot = (int)(k % HostPipe::kSlots);
+        const uint64_t len = total_len - off < chunk ? total_len - off : chunk;
+        const uint64_t first = off / segment_size, nseg = (len + segment_size - 1) / segment_size;
+        // the slot's previous kernel must have read its bytes
+        if (k >= (uint64_t)HostPipe::kSlots && hipStreamWaitEvent(c.h2d, c.done[slot], 0) != hipSuccess)
+            return WG_ERR_RUNTIME;
+        if (hipMemcpyAsync(c.dbuf[slot], host_base + off, len, hipMemcpyHostToDevice, c.h2d) != hipSuccess ||
+            hipEventRecord(c.copied[slot], c.h2d) != hipSuccess ||
+            hipStreamWaitEvent(c.exec, c.copied[slot], 0) != hipSuccess)
+            return WG_ERR_RUNTIME;
+        rc = wg_l4csum_uniform(c.dbuf[slot], len, segment_size, csum_start, flags, c.dres[slot], c.exec);
+        if (rc != WG_OK)
+            return rc;
+        if (hipMemcpyAsync(c.hres + first, c.dres[slot], nseg * sizeof(uint16_t), hipMemcpyDeviceToHost, c.exec) !=
+                hipSuccess ||
+            hipEventRecord(c.done[slot], c.exec) != hipSuccess)
+            return WG_ERR_RUNTIME;
+    }
+    if (hipStreamSynchronize(c.exec) != hipSuccess)
         return WG_ERR_RUNTIME;
-    return hipStreamSynchronize(c.stream) == hipSuccess ? WG_OK : WG_ERR_RUNTIME;
+    std::memcpy(host_out, c.hres, nseg_total * sizeof(uint16_t));
+    return WG_OK;
+}
+
+extern "C" int wg_host_release(void) {
+    if (g_pipe.device >= 0) {
+        hipSetDevice(g_pipe.device);
+        hipStreamSynchronize(g_pipe.exec);
+        hipStreamSynchronize(g_pipe.h2d);
+    }
+    g_pipe.release();
+    return WG_OK;
+}
+
+extern "C" int wg_host_alloc(void **ptr, uint64_t bytes) {
+    if (!ptr || !bytes)
+        return WG_ERR_INVALID;
+    *ptr = nullptr;
+    if (wg_device_count() <= 0)
+        return WG_ERR_NODEV;
+    return hipHostMalloc(ptr, bytes, hipHostMallocDefault) == hipSuccess ? WG_OK : WG_ERR_RUNTIME;
+}
+
+extern "C" int wg_host_free(void *ptr) {
+    if (!ptr)
+        return WG_OK;
+    return hipHostFree(ptr) == hipSuccess ? WG_OK : WG_ERR_RUNTIME;
 }
