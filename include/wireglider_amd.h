@@ -208,7 +208,7 @@ int wg_gro_finalize(uint8_t *dev_hdrs, wg_gro_desc *dev_desc, uint64_t n, void *
  * Host-memory path: the batch starts and ends in host memory
  * (tun read buffers, worker/encap.cpp:74-97; UDP GRO recvmsg buffers,
  * worker/decap.cpp:16-28,90-156).  Synchronous.  The batch is cut into
- * ~32 MiB chunks of whole segments that flow through a per-thread pipeline of
+ * chunks of whole segments (~host_chunk_mb MiB) that flow through a per-thread pipeline of
  * three device slots on two streams: chunk k+1's hipMemcpyAsync H2D runs
  * under chunk k's kernel and result copy; results gather in a pinned buffer
  * and reach host_out once at the end.  host_base may be pageable (the HIP
@@ -301,6 +301,7 @@ int wg_device_count(void);
  *   "gro_lds", "gro_wide"  GRO finalize: LDS-staged loads, wide field stores
  *   "gro_chunks" 16-B header chunks staged per flow (4, 5; with 4, headers
  *                over 48 bytes take the byte path)
+ *   "host_chunk_mb" wg_l4csum_uniform_host chunk size in MiB (1 .. 4096)
  *   "gso_ablate" GSO A/B variants: 1 = non-temporal payload stores, 32 = no
  *                XCD swizzle (both correct); 0 = the default kernel.
  * Thread-safe: each launch reads one consistent snapshot of the knobs. */

@@ -16,8 +16,10 @@ On BASELINE config 2 bytes (1,048,576 x 1500 B), one process:
   h2d_torch_pinned  : torch's tensor.copy_(pinned, non_blocking=True) from that
                       buffer — round 1's "h2d_only", which came out slower than
                       the whole library path
-Every rate is bytes / wall time of 5 repetitions after one warm-up; each
-library result is checked against the first.
+The pipeline runs at chunk sizes 8 MiB .. 2 GiB (knob host_chunk_mb; 2 GiB =
+one chunk, no overlap).  Every rate is bytes / wall time of 5 repetitions
+after one warm-up; every library result is checked against the device batch
+entry point's.
 """
 import ctypes
 import json
@@ -57,10 +59,14 @@ def main():
         return {"ms": round(dt * 1e3, 3), "GBps": round(nbytes / dt / 1e9, 2), "GiBps": round(nbytes / dt / 2**30, 2)}
 
     out = {"batch_bytes": nbytes}
-    for name, arr in (("pipeline_pageable", pageable), ("pipeline_pinned", pinned.array)):
-        got = wga.calc_l4_checksum_host(arr, seg, False, False, 20)
-        assert np.array_equal(got, dev_ref), name
-        out[name] = rate(lambda: wga.calc_l4_checksum_host(arr, seg, False, False, 20))
+    chunk0 = wga.tune_get("host_chunk_mb")
+    for mb in (8, 32, 128, 512, 2048):
+        wga.tune_set("host_chunk_mb", mb)
+        for name, arr in (("pipeline_pageable", pageable), ("pipeline_pinned", pinned.array)):
+            got = wga.calc_l4_checksum_host(arr, seg, False, False, 20)
+            assert np.array_equal(got, dev_ref), name
+            out[f"{name}_chunk{mb}MiB"] = rate(lambda: wga.calc_l4_checksum_host(arr, seg, False, False, 20))
+    wga.tune_set("host_chunk_mb", chunk0)
 
     hip = ctypes.CDLL("libamdhip64.so")
     hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]

@@ -53,6 +53,7 @@ static const Knob kKnobs[] = {
     {"gro_wide", nullptr, &Tune::gro_wide, 0, 1, nullptr, 0},
     {"gro_chunks", nullptr, &Tune::gro_chunks, 4, 5, nullptr, 0},
     {"gso_ablate", nullptr, &Tune::gso_ablate, 0, 0, kAbl, WG_N(kAbl)},
+    {"host_chunk_mb", nullptr, &Tune::host_chunk_mb, 1, 4096, nullptr, 0},
 };
 #undef WG_N
 
@@ -125,6 +126,9 @@ static Tune &tune_storage() {
         x.gro_wide = 1;
         x.gro_chunks = 5;
         x.gso_ablate = 0;
+        // host pipeline chunk: 128-512 MiB reach 97-98 % of the raw H2D rate
+        // (8 MiB: 70 %, per-chunk overheads; profiles/r02_host_path.json)
+        x.host_chunk_mb = 256;
         // environment overrides: WG_<KNOB> (upper case), same accepted values
         // as wg_tune_set; anything else is ignored
         for (const Knob &k : kKnobs) {
@@ -441,9 +445,6 @@ extern "C" int wg_device_count(void) {
     return n;
 }
 
-// Chunk size of the host pipeline: whole segments, ~32 MiB (H2D ~0.6 ms at
-// PCIe Gen5 rates, long enough to amortise three launches per chunk).
-static constexpr uint64_t kHostChunkBytes = 32ull << 20;
 
 extern "C" int wg_l4csum_uniform_host(const uint8_t *host_base, uint64_t total_len, uint32_t segment_size,
                                       uint16_t csum_start, uint32_t flags, uint16_t *host_out) {
@@ -458,7 +459,8 @@ extern "C" int wg_l4csum_uniform_host(const uint8_t *host_base, uint64_t total_l
     if (rc != WG_OK)
         return rc;
     const uint64_t nseg_total = (total_len + segment_size - 1) / segment_size;
-    uint64_t per = kHostChunkBytes / segment_size;  // segments per chunk
+    // whole segments per chunk, ~host_chunk_mb MiB (knob)
+    uint64_t per = ((uint64_t)tune().host_chunk_mb << 20) / segment_size;
     if (per == 0)
         per = 1;
     const uint64_t chunk = per * segment_size;
