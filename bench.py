@@ -281,7 +281,8 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
             l64 = torch.empty(n, dtype=torch.uint16, device=dev)
             saved = wga.tune_get("verify_small")
             small, ref = {}, None
-            for kname, knob in (("wave_per_packet", 0), ("lane_per_descriptor", 1), ("quad_per_descriptor", 2)):
+            for kname, knob in (("wave_per_packet", 0), ("lane_per_descriptor", 1), ("quad_per_descriptor", 2),
+                                ("split_roles", 3)):
                 wga.tune_set("verify_small", knob)
                 for _ in range(10):
                     wga.verify_desc(b64, d64, verdict=v64, l4=l64)

@@ -297,7 +297,9 @@ int wg_device_count(void);
  *                separate byte load (0)
  *   "verify_small" verify by the small-packet kernel: packets of <= 64 B
  *                decoded in one lane (1) or redundantly in a lane quad (2),
- *                longer ones by the wave; 0 = wave-per-packet kernel
+ *                longer ones by the wave; 3 = split roles (all-small groups
+ *                of 4 descriptors a lane per packet, the rest by the wave);
+ *                0 = wave-per-packet kernel (default)
  *   "gro_lds", "gro_wide"  GRO finalize: LDS-staged loads, wide field stores
  *   "gro_chunks" 16-B header chunks staged per flow (4, 5; with 4, headers
  *                over 48 bytes take the byte path)

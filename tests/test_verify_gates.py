@@ -144,7 +144,8 @@ def test_oracle_verify_desc_matches_scalar():
 VERIFY_VARIANTS = [{"verify_dm": 0, "verify_occ": 8, "verify_hdr": 1}, {"verify_dm": 0, "verify_occ": 0, "verify_hdr": 1},
                    {"verify_dm": 0, "verify_occ": 8, "verify_hdr": 0}, {"verify_dm": 0, "verify_occ": 0, "verify_hdr": 0},
                    {"verify_dm": 2, "verify_occ": 6, "l4_iters": 4}, {"verify_dm": 2, "verify_occ": 0, "l4_iters": 3},
-                   {"verify_small": 1}, {"verify_small": 2}]
+                   {"verify_small": 0}, {"verify_small": 1}, {"verify_small": 2}, {"verify_small": 3},
+                   {"verify_small": 3, "verify_occ": 0}]
 
 
 @pytest.mark.gpu

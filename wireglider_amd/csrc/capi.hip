@@ -48,7 +48,7 @@ static const Knob kKnobs[] = {
     {"verify_dm", nullptr, &Tune::verify_dm, 0, 0, kDm, WG_N(kDm)},
     {"verify_occ", nullptr, &Tune::verify_occ, 0, 0, kVOcc, WG_N(kVOcc)},
     {"verify_hdr", nullptr, &Tune::verify_hdr, 0, 1, nullptr, 0},
-    {"verify_small", nullptr, &Tune::verify_small, 0, 2, nullptr, 0},
+    {"verify_small", nullptr, &Tune::verify_small, 0, 3, nullptr, 0},
     {"gro_lds", nullptr, &Tune::gro_lds, 0, 1, nullptr, 0},
     {"gro_wide", nullptr, &Tune::gro_wide, 0, 1, nullptr, 0},
     {"gro_chunks", nullptr, &Tune::gro_chunks, 4, 5, nullptr, 0},

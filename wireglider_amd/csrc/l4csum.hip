@@ -774,6 +774,104 @@ namespace wg {
 // G = 4: a lane quad per descriptor, every lane of it decoding the same
 // packet (its loads hit the same addresses): a wave owns 16 descriptors, so
 // its serial walk over the long packets is 4 groups instead of 16.
+// The packets of the lanes in mask m (lane j: offset ohi:olo, length len),
+// Q at a time through verify_group; packet j's verdict / L4 result land in
+// lane j's rv / rc.
+template <int Q>
+__device__ __forceinline__ void verify_mask(uint64_t m, uint32_t olo, uint32_t ohi, uint32_t len, const uint8_t *base,
+                                            uint32_t lane, uint32_t &rv, uint32_t &rc) {
+    while (m) {
+        uint64_t doff[Q];
+        uint32_t ln[Q], tgt[Q];
+#pragma unroll
+        for (int k = 0; k < Q; k++) {
+            const bool have = m != 0;
+            const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
+            m = have ? m & (m - 1) : m;
+            tgt[k] = have ? j : 64u;
+            doff[k] = have ? (((uint64_t)rdl(ohi, j) << 32) | rdl(olo, j)) : 0u;
+            ln[k] = have ? rdl(len, j) : 0u;
+        }
+        verify_group<Q, true>(base, doff, ln, tgt, lane, rv, rc, [] {});
+    }
+}
+
+// The lane path of the small-packet verify kernels: packet (a, len), len <=
+// kSmallMax, decoded and checked in one lane; verdict bits into rv, the L4
+// result into rc.
+__device__ __forceinline__ void verify_lane(uintptr_t a, uint32_t len, bool use, uint32_t &rv, uint32_t &rc) {
+    const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
+    const uintptr_t a0 = a & ~(uintptr_t)15;
+    const uintptr_t alast = (a + len - 1) & ~(uintptr_t)15;
+    const bool any = use && len;
+    v4u W[5];
+#pragma unroll
+    for (uint32_t c = 0; c < 5; c++) {
+        const uintptr_t ca = a0 + 16u * c;
+        W[c] = ld16(any ? (ca > alast ? alast : ca) : zero);  // clamped chunks lie past the packet: zeroed below
+    }
+    const uint32_t Wd[20] = {W[0][0], W[0][1], W[0][2], W[0][3], W[1][0], W[1][1], W[1][2], W[1][3],
+                             W[2][0], W[2][1], W[2][2], W[2][3], W[3][0], W[3][1], W[3][2], W[3][3],
+                             W[4][0], W[4][1], W[4][2], W[4][3]};
+    const uint32_t s = (uint32_t)(a & 15u), q4 = s >> 2, sh = s & 3u;
+    uint32_t R[16];
+#pragma unroll
+    for (uint32_t m = 0; m < 16; m++) {
+        const uint32_t lo = q4 == 0 ? Wd[m] : q4 == 1 ? Wd[m + 1] : q4 == 2 ? Wd[m + 2] : Wd[m + 3];
+        const uint32_t hi = q4 == 0 ? Wd[m + 1] : q4 == 1 ? Wd[m + 2] : q4 == 2 ? Wd[m + 3] : Wd[m + 4];
+        R[m] = bytes_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, len);
+    }
+    uint32_t v = 0, c = 0;
+    if (len >= 1) {
+        const uint32_t b0 = R[0] & 0xffu;
+        const bool v6 = (b0 >> 4) == 6;
+        if (v6)
+            v |= WG_VERDICT_V6;
+        const uint32_t ihs = v6 ? 40u : 20u;
+        bool ip_ok = false;
+        uint32_t proto = 0;
+        if (len >= ihs) {  // evaluator.hpp:118-121 (len <= 64 here)
+            if (!v6) {
+                const uint32_t hs = half_sum(R[0]) + half_sum(R[1]) + half_sum(R[2]) + half_sum(R[3]) +
+                                    half_sum(R[4]);
+                ip_ok = (b0 & 0xfu) == 5u &&                                  // ip_hl, evaluator.cpp:19
+                        len == bswap16(R[0] >> 16) &&                          // ip_len, :21
+                        (bswap16(R[1] >> 16) & ~0x4000u) == 0 &&              // ip_off & ~IP_DF, :24
+                        fold16_32(hs) == 0xffffu;                             // checksum == 0, :27
+                proto = (R[2] >> 8) & 0xffu;
+            } else {
+                ip_ok = len - 40u == bswap16(R[1] & 0xffffu);  // ip6_plen, :47
+                proto = (R[1] >> 16) & 0xffu;
+            }
+        }
+        bool l4 = false;
+        if (ip_ok) {
+            v |= WG_VERDICT_IP_OK;
+            if (proto == 6u) {
+                v |= WG_VERDICT_TCP;
+                l4 = len - ihs > 20u;  // evaluator.hpp:61
+            } else if (proto == 17u) {
+                v |= WG_VERDICT_UDP;
+                l4 = len - ihs > 8u;  // evaluator.hpp:91
+            }
+        }
+        if (l4) {  // calc_l4_checksum(pkt, isv6, istcp, ihs), checksum.cpp:8-36
+            uint32_t sum = (proto << 8) + bswap16((len - ihs) & 0xffffu);
+#pragma unroll
+            for (uint32_t m = 2; m < 16; m++) {
+                const bool in_l4 = 4u * m >= ihs;
+                const bool in_addr = v6 ? m < 10u : (m == 3u || m == 4u);  // v6 bytes 8-39, v4 12-19
+                sum += (in_l4 ? half_sum(R[m]) : 0u) + (in_addr ? half_sum(R[m]) : 0u);
+            }
+            c = ~fold16_32(sum) & 0xffffu;
+            if (c == 0)
+                v |= WG_VERDICT_L4_OK;
+        }
+    }
+    rv = v;
+    rc = c;
+}
+
 template <int Q, int G = 1>
 __global__ __launch_bounds__(256) void verify_small_kernel(VerifyParams p) {
     static_assert(G == 1 || G == 4, "lanes per descriptor");
@@ -787,95 +885,49 @@ __global__ __launch_bounds__(256) void verify_small_kernel(VerifyParams p) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)ohi << 32) | olo);
     const bool small = len <= kSmallMax;
     uint32_t rv = 0, rc = 0;
-    if (__ballot(live && small)) {
-        const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
-        const uintptr_t a0 = a & ~(uintptr_t)15;
-        const uintptr_t alast = (a + len - 1) & ~(uintptr_t)15;
-        const bool any = small && len;
-        v4u W[5];
-#pragma unroll
-        for (uint32_t c = 0; c < 5; c++) {
-            const uintptr_t ca = a0 + 16u * c;
-            W[c] = ld16(any ? (ca > alast ? alast : ca) : zero);  // clamped chunks lie past the packet: zeroed below
-        }
-        const uint32_t Wd[20] = {W[0][0], W[0][1], W[0][2], W[0][3], W[1][0], W[1][1], W[1][2], W[1][3],
-                                 W[2][0], W[2][1], W[2][2], W[2][3], W[3][0], W[3][1], W[3][2], W[3][3],
-                                 W[4][0], W[4][1], W[4][2], W[4][3]};
-        const uint32_t s = (uint32_t)(a & 15u), q4 = s >> 2, sh = s & 3u;
-        uint32_t R[16];
-#pragma unroll
-        for (uint32_t m = 0; m < 16; m++) {
-            const uint32_t lo = q4 == 0 ? Wd[m] : q4 == 1 ? Wd[m + 1] : q4 == 2 ? Wd[m + 2] : Wd[m + 3];
-            const uint32_t hi = q4 == 0 ? Wd[m + 1] : q4 == 1 ? Wd[m + 2] : q4 == 2 ? Wd[m + 3] : Wd[m + 4];
-            R[m] = bytes_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, len);
-        }
-        uint32_t v = 0, c = 0;
-        if (len >= 1) {
-            const uint32_t b0 = R[0] & 0xffu;
-            const bool v6 = (b0 >> 4) == 6;
-            if (v6)
-                v |= WG_VERDICT_V6;
-            const uint32_t ihs = v6 ? 40u : 20u;
-            bool ip_ok = false;
-            uint32_t proto = 0;
-            if (len >= ihs) {  // evaluator.hpp:118-121 (len <= 64 here)
-                if (!v6) {
-                    const uint32_t hs = half_sum(R[0]) + half_sum(R[1]) + half_sum(R[2]) + half_sum(R[3]) +
-                                        half_sum(R[4]);
-                    ip_ok = (b0 & 0xfu) == 5u &&                                  // ip_hl, evaluator.cpp:19
-                            len == bswap16(R[0] >> 16) &&                          // ip_len, :21
-                            (bswap16(R[1] >> 16) & ~0x4000u) == 0 &&              // ip_off & ~IP_DF, :24
-                            fold16_32(hs) == 0xffffu;                             // checksum == 0, :27
-                    proto = (R[2] >> 8) & 0xffu;
-                } else {
-                    ip_ok = len - 40u == bswap16(R[1] & 0xffffu);  // ip6_plen, :47
-                    proto = (R[1] >> 16) & 0xffu;
-                }
-            }
-            bool l4 = false;
-            if (ip_ok) {
-                v |= WG_VERDICT_IP_OK;
-                if (proto == 6u) {
-                    v |= WG_VERDICT_TCP;
-                    l4 = len - ihs > 20u;  // evaluator.hpp:61
-                } else if (proto == 17u) {
-                    v |= WG_VERDICT_UDP;
-                    l4 = len - ihs > 8u;  // evaluator.hpp:91
-                }
-            }
-            if (l4) {  // calc_l4_checksum(pkt, isv6, istcp, ihs), checksum.cpp:8-36
-                uint32_t sum = (proto << 8) + bswap16((len - ihs) & 0xffffu);
-#pragma unroll
-                for (uint32_t m = 2; m < 16; m++) {
-                    const bool in_l4 = 4u * m >= ihs;
-                    const bool in_addr = v6 ? m < 10u : (m == 3u || m == 4u);  // v6 bytes 8-39, v4 12-19
-                    sum += (in_l4 ? half_sum(R[m]) : 0u) + (in_addr ? half_sum(R[m]) : 0u);
-                }
-                c = ~fold16_32(sum) & 0xffffu;
-                if (c == 0)
-                    v |= WG_VERDICT_L4_OK;
-            }
-        }
-        rv = v;
-        rc = c;
-    }
+    if (__ballot(live && small))
+        verify_lane(a, len, small, rv, rc);
     // the longer packets of this wave, Q at a time
-    uint64_t m = __ballot(live && !small && q == 0);
-    while (m) {
-        uint64_t doff[Q];
-        uint32_t ln[Q], tgt[Q];
-#pragma unroll
-        for (int k = 0; k < Q; k++) {
-            const bool have = m != 0;
-            const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
-            m = have ? m & (m - 1) : m;
-            tgt[k] = have ? j : 64u;
-            doff[k] = have ? (((uint64_t)rdl(ohi, j) << 32) | rdl(olo, j)) : 0u;
-            ln[k] = have ? rdl(len, j) : 0u;
-        }
-        verify_group<Q, true>(p.base, doff, ln, tgt, lane, rv, rc, [] {});
-    }
+    verify_mask<Q>(__ballot(live && !small && q == 0), olo, ohi, len, p.base, lane, rv, rc);
     if (live && q == 0) {
+        p.verdict[i] = (uint8_t)rv;
+        if (p.l4)
+            p.l4[i] = (uint16_t)rc;
+    }
+}
+
+// Split-role verify kernel (knob verify_small = 3; the layout and the role
+// split of l4csum_split_kernel): block b owns the 16 descriptors at
+// [q*Q + 16b, +16) of each quarter q; groups of 4 consecutive descriptors
+// whose packets are all <= kSmallMax bytes are decoded a lane per packet by
+// wave 0, every other group by its wave through verify_group, 4 at a time.
+template <int O = 0>  // O: waves/SIMD target (0 = compiler's choice)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_split_kernel(VerifyParams p, uint64_t Q) {
+    const uint32_t lane = lane_id();
+    const uint32_t wib = wave_in_block();
+    const uint64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
+    const uint32_t qq = wib == 0 ? lane >> 4 : (lane >> 2) & 3u;
+    const uint32_t oo = wib == 0 ? lane & 15u : 4u * wib + (lane & 3u);
+    const uint64_t i = (uint64_t)qq * Q + 16u * blk + oo;
+    const bool live = (wib == 0 || lane < 16u) && 16u * blk < Q && i < p.n;
+    const v4u d = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : p.n - 1));
+    const uint32_t len = live ? d.z : 0u;
+    const uint32_t olo = live ? d.x : 0u, ohi = live ? d.y : 0u;
+    const uint64_t gl = __ballot(live && len > kSmallMax);
+    const bool grp_long = ((gl >> (lane & ~3u)) & 0xfu) != 0;
+    const bool own = wib == 0 ? (lane & 15u) < 4u : true;
+    const bool mine = live && own && grp_long;
+    uint32_t rv = 0, rc = 0;
+    verify_mask<4>(__ballot(mine), olo, ohi, len, p.base, lane, rv, rc);
+    const bool small = wib == 0 && live && !grp_long;
+    if (__ballot(small)) {  // wave-uniform; never true on waves 1-3
+        uint32_t sv = 0, sc = 0;
+        verify_lane(reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)ohi << 32) | olo), small ? len : 0u, small, sv,
+                    sc);
+        rv = small ? sv : rv;
+        rc = small ? sc : rc;
+    }
+    if (mine || small) {
         p.verdict[i] = (uint8_t)rv;
         if (p.l4)
             p.l4[i] = (uint16_t)rc;
@@ -892,6 +944,21 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
         return WG_ERR_INVALID;
     VerifyParams p{dev_base, dev_desc, dev_verdict, dev_l4, n};
     const Tune t = tune();
+    if (t.verify_small == 3) {
+        const uint64_t Q = ((n + 3) / 4 + 15) & ~15ull;  // as l4csum_split_kernel's quarters
+        uint64_t sb = Q / 16;
+        if (sb >= 8)
+            sb = (sb + 7) & ~7ull;
+        if (sb > 0x7fffffffull)
+            return WG_ERR_INVALID;
+        if (t.verify_occ == 8)
+            hipLaunchKernelGGL(verify_split_kernel<8>, dim3((unsigned)sb), dim3(256), 0,
+                               static_cast<hipStream_t>(stream), p, Q);
+        else
+            hipLaunchKernelGGL(verify_split_kernel<0>, dim3((unsigned)sb), dim3(256), 0,
+                               static_cast<hipStream_t>(stream), p, Q);
+        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+    }
     if (t.verify_small) {
         const uint64_t per_block = t.verify_small == 2 ? 64u : 256u;  // descriptors per 256-thread block
         const uint64_t sb = (n + per_block - 1) / per_block;
