@@ -304,6 +304,8 @@ int wg_device_count(void);
  *   "gro_chunks" 16-B header chunks staged per flow (4, 5; with 4, headers
  *                over 48 bytes take the byte path)
  *   "host_chunk_mb" wg_l4csum_uniform_host chunk size in MiB (1 .. 4096)
+ *   "l4_unroll"  descriptor batches: 16-B loads in flight per lane while
+ *                streaming a packet's bytes past its first 2 KiB (4, 8)
  *   "gso_ablate" GSO A/B variants: 1 = non-temporal payload stores, 32 = no
  *                XCD swizzle (both correct); 0 = the default kernel.
  * Thread-safe: each launch reads one consistent snapshot of the knobs. */

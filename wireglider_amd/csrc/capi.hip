@@ -29,7 +29,8 @@ struct Knob {
 };
 
 static const uint64_t kPpw[] = {1, 2, 4, 8}, kOcc[] = {0, 7, 8}, kVOcc[] = {0, 6, 8}, kDm[] = {0, 2},
-                      kWaves[] = {1, 2, 4, 8}, kAbl[] = {0, 1, 32};
+                      kWaves[] = {1, 2, 4, 8}, kAbl[] = {0, 1, 32},
+                      kUnroll[] = {4, 8};
 #define WG_N(a) (sizeof(a) / sizeof(a[0]))
 static const Knob kKnobs[] = {
     {"l4_blocks", &Tune::l4_blocks, nullptr, 1, 1u << 20, nullptr, 0},
@@ -54,6 +55,7 @@ static const Knob kKnobs[] = {
     {"gro_chunks", nullptr, &Tune::gro_chunks, 4, 5, nullptr, 0},
     {"gso_ablate", nullptr, &Tune::gso_ablate, 0, 0, kAbl, WG_N(kAbl)},
     {"host_chunk_mb", nullptr, &Tune::host_chunk_mb, 1, 4096, nullptr, 0},
+    {"l4_unroll", nullptr, &Tune::l4_unroll, 0, 0, kUnroll, WG_N(kUnroll)},
 };
 #undef WG_N
 
@@ -129,6 +131,11 @@ static Tune &tune_storage() {
         // host pipeline chunk: 128-512 MiB reach 97-98 % of the raw H2D rate
         // (8 MiB: 70 %, per-chunk overheads; profiles/r02_host_path.json)
         x.host_chunk_mb = 256;
+        // descriptor batches: 8 loads in flight per lane on a long packet's
+        // rest (5 waves/SIMD instead of 6): config 4 -1.4 %, config 1 (64 KiB
+        // buffers) -26 %, config 5 (no long packets) unchanged
+        // (profiles/r02_unroll_ab.json)
+        x.l4_unroll = 8;
         // environment overrides: WG_<KNOB> (upper case), same accepted values
         // as wg_tune_set; anything else is ignored
         for (const Knob &k : kKnobs) {

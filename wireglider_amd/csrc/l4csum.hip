@@ -287,7 +287,7 @@ __device__ __forceinline__ uint32_t lane_sum(const v4u W[5], uintptr_t a, uint32
 // length len, csum_start cs, flags fl), Q at a time through the issue /
 // finish machinery of l4csum_kernel (all Q packets' loads in flight before
 // the first wait); packet j's result lands in lane j's res.
-template <bool kL4, bool kNT, int Q>
+template <bool kL4, bool kNT, int Q, int U = 4>
 __device__ __forceinline__ void wave_long(uint64_t m, uintptr_t a, uint32_t len, uint32_t cs, uint32_t fl,
                                           const uint8_t *base, uint32_t lane, uint32_t &res) {
     const uint32_t alo = (uint32_t)a, ahi = (uint32_t)((uint64_t)a >> 32);
@@ -311,7 +311,7 @@ __device__ __forceinline__ void wave_long(uint64_t m, uintptr_t a, uint32_t len,
             issue<kL4, kNT>(g[k], lane, f[k]);
 #pragma unroll
         for (int k = 0; k < Q; k++) {
-            uint32_t t = wave_sum_u32(finish<kNT>(lane, f[k]));
+            uint32_t t = wave_sum_u32(finish<kNT, U>(lane, f[k]));
             if (kL4) {
                 const uint32_t proto = (g[k].fl & WG_PKT_TCP) ? 6u : 17u;
                 t += (proto << 8) + bswap16((g[k].len - g[k].cs) & 0xffffu);
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
 // batch keeps a lane per packet (waves 1-3 leave after one descriptor load),
 // an all-long one keeps the short 16-packet waves with every descriptor in
 // one vector load.  One launch, no host knowledge of the mix.
-template <int kKind, bool kNT>
+template <int kKind, bool kNT, int U = 4>  // U: loads in flight per lane on a long packet's rest
 __global__ __launch_bounds__(256) void l4csum_split_kernel(L4Params p) {
     constexpr bool kL4 = kKind != kDescPlain;
     const uint32_t lane = lane_id();
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(256) void l4csum_split_kernel(L4Params p) {
     const bool own = wib == 0 ? (lane & 15u) < 4u : true;
     const bool mine = live && own && grp_long;
     uint32_t res = 0;
-    wave_long<kL4, kNT, 4>(__ballot(mine), a, len, cs, fl, p.base, lane, res);
+    wave_long<kL4, kNT, 4, U>(__ballot(mine), a, len, cs, fl, p.base, lane, res);
     if (mine)
         p.out[i] = (uint16_t)res;
     // ---- lane role (wave 0): the block's all-small groups
@@ -517,7 +517,9 @@ static int launch_small(const L4Params &p, uint32_t mode, hipStream_t st) {
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
     const dim3 grid((unsigned)blocks), blk(256);
-    if (mode == 5)
+    if (mode == 5 && tune().l4_unroll == 8)
+        hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 8>), grid, blk, 0, st, q);
+    else if (mode == 5)
         hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT>), grid, blk, 0, st, q);
     else if (mode == 4)
         hipLaunchKernelGGL((l4csum_small_kernel<kKind, kNT, 4, 4, true>), grid, blk, 0, st, p);

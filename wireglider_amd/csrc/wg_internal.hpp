@@ -31,6 +31,7 @@ struct Tune {
     uint32_t gro_wide;    // 1: GRO finalize fields written by two wide stores (LDS variant)
     uint32_t gro_chunks;  // 16-B chunks staged per flow by the LDS variant (4, 5)
     uint32_t host_chunk_mb;  // host-memory pipeline chunk size, MiB
+    uint32_t l4_unroll;   // split kernel: loads in flight per lane on a long packet's rest (4, 8)
     uint32_t gso_ablate;  // GSO A/B variants (1 non-temporal stores, 32 no XCD swizzle; both correct)
 };
 

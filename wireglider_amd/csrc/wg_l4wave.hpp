@@ -94,26 +94,31 @@ __device__ __forceinline__ void issue(const Geom &g, uint32_t lane, Front &f) {
 }
 
 // Finish phase: this lane's share of the packet's sum in TRUE pairing.
-template <bool kNT>
+// U: loads in flight per lane while streaming a long packet's rest (4 or 8).
+template <bool kNT, int U = 4>
 __device__ __forceinline__ uint32_t finish(uint32_t lane, const Front &f) {
+    static_assert(U == 4 || U == 8, "loads in flight");
     Acc acc;
     acc.add4(f.v0);
     acc.add4(f.v1);
-    if (f.nint > 128) {  // long packet (> ~2 KiB): stream the rest, 4 loads in flight
+    if (f.nint > 128) {  // long packet (> ~2 KiB): stream the rest, U loads in flight
         const uintptr_t q = f.c0;
-        uint32_t k = lane + 128;
-        for (; k + 192 < f.nint; k += 256) {
-            v4u a0 = ld16x<kNT>(q + 16ull * k);
-            v4u a1 = ld16x<kNT>(q + 16ull * (k + 64));
-            v4u a2 = ld16x<kNT>(q + 16ull * (k + 128));
-            v4u a3 = ld16x<kNT>(q + 16ull * (k + 192));
-            acc.add4(a0);
-            acc.add4(a1);
-            acc.add4(a2);
-            acc.add4(a3);
+        const uint32_t last = f.nint - 1;
+        // wave-uniform trip count: every round issues U loads (lanes past the
+        // end re-read the last chunk and are masked), so the remainder is one
+        // round trip too
+        for (uint32_t k0 = 128; k0 < f.nint; k0 += 64 * U) {
+            v4u a[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t k = k0 + 64 * u + lane;
+                a[u] = ld16x<kNT>(q + 16ull * (k < last ? k : last));
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (k0 + 64 * u + lane < f.nint)
+                    acc.add4(a[u]);
         }
-        for (; k < f.nint; k += 64)
-            acc.add4(ld16x<kNT>(q + 16ull * k));
     }
     if (!f.bt)
         acc.add(f.bv);
