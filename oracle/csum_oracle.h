@@ -181,4 +181,23 @@ double orc_time_l4_uniform(const uint8_t *base, uint64_t total_len, uint32_t seg
 }
 #endif
 
+/* ---- data-message AEAD, oracle/aead_oracle.c ---------- */
+/* RejectAfterMessages (include/proto/proto.hpp:36) */
+#define ORC_REJECT_AFTER_MESSAGES (UINT64_MAX - (1ull << 13))
+void orc_chacha20_block(const uint8_t key[32], uint32_t counter, const uint8_t nonce[12], uint8_t out[64]);
+void orc_chacha20_xor(const uint8_t key[32], uint32_t counter, const uint8_t nonce[12], const uint8_t *in,
+                      uint8_t *out, size_t len);
+void orc_poly1305(const uint8_t key[32], const uint8_t *msg, size_t len, uint8_t tag[16]);
+void orc_aead_encrypt(const uint8_t key[32], const uint8_t nonce[12], const uint8_t *aad, size_t aad_len,
+                      const uint8_t *pt, size_t len, uint8_t *ct, uint8_t tag[16]);
+int orc_aead_decrypt(const uint8_t key[32], const uint8_t nonce[12], const uint8_t *aad, size_t aad_len,
+                     const uint8_t *ct, size_t len, const uint8_t tag[16], uint8_t *pt);
+size_t orc_wg_encrypt(const uint8_t key[32], uint32_t receiver_index, uint64_t counter, const uint8_t *pt, size_t len,
+                      uint8_t *out);
+int orc_wg_decrypt(const uint8_t key[32], const uint8_t *msg, size_t msg_len, uint8_t *out);
+void orc_wg_encrypt_batch(const uint8_t key[32], uint32_t receiver_index, uint64_t counter0, const uint8_t *in,
+                          uint64_t total_len, uint32_t segment_size, uint8_t *out);
+void orc_wg_decrypt_batch(const uint8_t key[32], const uint8_t *in, uint64_t total_len, uint32_t segment_size,
+                          uint8_t *out, int8_t *status);
+
 #endif

@@ -83,6 +83,22 @@ def _load():
     lib.orc_gro_finalize_desc.argtypes = [vp, vp, u64, i32]
     lib.orc_gso_split_desc.restype = None
     lib.orc_gso_split_desc.argtypes = [vp, vp, u64, vp, vp, i32]
+    lib.orc_chacha20_block.restype = None
+    lib.orc_chacha20_block.argtypes = [vp, u32, vp, vp]
+    lib.orc_poly1305.restype = None
+    lib.orc_poly1305.argtypes = [vp, vp, sz, vp]
+    lib.orc_aead_encrypt.restype = None
+    lib.orc_aead_encrypt.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp]
+    lib.orc_aead_decrypt.restype = i32
+    lib.orc_aead_decrypt.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp]
+    lib.orc_wg_encrypt.restype = sz
+    lib.orc_wg_encrypt.argtypes = [vp, u32, u64, vp, sz, vp]
+    lib.orc_wg_decrypt.restype = i32
+    lib.orc_wg_decrypt.argtypes = [vp, vp, sz, vp]
+    lib.orc_wg_encrypt_batch.restype = None
+    lib.orc_wg_encrypt_batch.argtypes = [vp, u32, u64, vp, u64, u32, vp]
+    lib.orc_wg_decrypt_batch.restype = None
+    lib.orc_wg_decrypt_batch.argtypes = [vp, vp, u64, u32, vp, vp]
     lib.orc_time_l4_uniform.restype = ctypes.c_double
     lib.orc_time_l4_uniform.argtypes = [vp, u64, u32, u16, u32, vp, i32, i32]
     return lib
@@ -290,3 +306,84 @@ def time_l4_uniform(buf: np.ndarray, segment_size: int, csum_start: int, flags: 
     out = np.empty(n, dtype=np.uint16)
     return float(lib.orc_time_l4_uniform(a.ctypes.data, a.size, segment_size, csum_start, flags,
                                          out.ctypes.data, threads, reps))
+
+
+# ---------------------------------------------------------------------------
+# data-message AEAD: oracle/aead_oracle.c
+# ---------------------------------------------------------------------------
+REJECT_AFTER_MESSAGES = (1 << 64) - 1 - (1 << 13)  # include/proto/proto.hpp:36
+
+
+def _b(x) -> np.ndarray:
+    return np.ascontiguousarray(np.frombuffer(bytes(x), dtype=np.uint8) if not isinstance(x, np.ndarray) else x,
+                                dtype=np.uint8)
+
+
+def chacha20_block(key: bytes, counter: int, nonce: bytes) -> bytes:
+    out = np.zeros(64, np.uint8)
+    k, n = _b(key), _b(nonce)
+    lib.orc_chacha20_block(k.ctypes.data, counter, n.ctypes.data, out.ctypes.data)
+    return out.tobytes()
+
+
+def poly1305(key: bytes, msg: bytes) -> bytes:
+    out = np.zeros(16, np.uint8)
+    k, m = _b(key), _b(msg)
+    lib.orc_poly1305(k.ctypes.data, m.ctypes.data, m.size, out.ctypes.data)
+    return out.tobytes()
+
+
+def aead_encrypt(key: bytes, nonce: bytes, aad: bytes, pt: bytes):
+    k, n, a, p = _b(key), _b(nonce), _b(aad), _b(pt)
+    ct = np.zeros(max(p.size, 1), np.uint8)
+    tag = np.zeros(16, np.uint8)
+    lib.orc_aead_encrypt(k.ctypes.data, n.ctypes.data, a.ctypes.data, a.size, p.ctypes.data, p.size, ct.ctypes.data,
+                         tag.ctypes.data)
+    return ct[: p.size].tobytes(), tag.tobytes()
+
+
+def aead_decrypt(key: bytes, nonce: bytes, aad: bytes, ct: bytes, tag: bytes):
+    k, n, a, c, t = _b(key), _b(nonce), _b(aad), _b(ct), _b(tag)
+    pt = np.full(max(c.size, 1), 0xEE, np.uint8)
+    rc = lib.orc_aead_decrypt(k.ctypes.data, n.ctypes.data, a.ctypes.data, a.size, c.ctypes.data, c.size,
+                              t.ctypes.data, pt.ctypes.data)
+    return rc, pt[: c.size].tobytes()
+
+
+def wg_encrypt(key: bytes, receiver_index: int, counter: int, pt: bytes) -> bytes:
+    k, p = _b(key), _b(pt)
+    out = np.zeros(16 + (p.size + 15) // 16 * 16 + 16, np.uint8)
+    n = lib.orc_wg_encrypt(k.ctypes.data, receiver_index, counter, p.ctypes.data, p.size, out.ctypes.data)
+    return out[:n].tobytes()
+
+
+def wg_decrypt(key: bytes, msg: bytes):
+    k, m = _b(key), _b(msg)
+    out = np.full(max(m.size - 32, 1), 0xEE, np.uint8)
+    rc = lib.orc_wg_decrypt(k.ctypes.data, m.ctypes.data, m.size, out.ctypes.data)
+    return rc, out[: max(m.size - 32, 0)].tobytes()
+
+
+def wg_encrypt_batch(key: bytes, receiver_index: int, counter0: int, buf: np.ndarray, segment_size: int) -> np.ndarray:
+    """Every segment of a PacketBatch into consecutive data messages at the
+    stride expected_encrypt_size(segment_size) (worker/encap.cpp:136-141)."""
+    k, a = _b(key), _u8(buf)
+    n = (a.size + segment_size - 1) // segment_size
+    stride = 16 + (segment_size + 15) // 16 * 16 + 16
+    last = a.size - (n - 1) * segment_size if n else 0
+    out = np.zeros(max((n - 1) * stride + 16 + (last + 15) // 16 * 16 + 16, 1) if n else 1, np.uint8)
+    lib.orc_wg_encrypt_batch(k.ctypes.data, receiver_index, counter0, a.ctypes.data, a.size, segment_size,
+                             out.ctypes.data)
+    return out[: (n - 1) * stride + 16 + (last + 15) // 16 * 16 + 16] if n else out[:0]
+
+
+def wg_decrypt_batch(key: bytes, buf: np.ndarray, segment_size: int):
+    """Every message of a GRO batch (worker/decap_ref.cpp:78-86); plaintext i at
+    i * (segment_size - 32); status 0 / -1 per message."""
+    k, a = _b(key), _u8(buf)
+    n = (a.size + segment_size - 1) // segment_size
+    ostride = max(segment_size - 32, 0)
+    out = np.full(max(n * ostride, 1), 0xEE, np.uint8)
+    st = np.zeros(max(n, 1), np.int8)
+    lib.orc_wg_decrypt_batch(k.ctypes.data, a.ctypes.data, a.size, segment_size, out.ctypes.data, st.ctypes.data)
+    return out[: n * ostride], st[:n]
