@@ -205,6 +205,40 @@ typedef struct wg_gro_desc {
 int wg_gro_finalize(uint8_t *dev_hdrs, wg_gro_desc *dev_desc, uint64_t n, void *stream);
 
 /* ------------------------------------------------------------------------
+ * Data-message AEAD, batched: Peer::encrypt / Peer::decrypt
+ * (proto/proto.cpp:544-583, 496-523) over crypto_aead_chacha20poly1305_ietf
+ * (RFC 8439) for the batches the workers build.  `key` is the session's
+ * 32-byte key in HOST memory (passed by value to the kernel).
+ *
+ * wg_aead_encrypt_batch: every segment of a PacketBatch (dev_in, total_len,
+ * segment_size <= 65535; the last segment may be short), as
+ * worker/encap.cpp:136-141 calls Peer::encrypt for each: message i =
+ * DataHeader {4, receiver_index, counter0 + i} (little-endian) ||
+ * ChaCha20-Poly1305(key, nonce = 0^4 || le64(counter), no AAD, plaintext
+ * zero-padded to 16) || 16-B tag, written at dev_out + i * stride with
+ * stride = 16 + round_up(segment_size, 16) + 16
+ * (Peer::expected_encrypt_size, include/proto/proto.hpp:266-269); dev_out
+ * 16-byte aligned.  dev_status (nullable): -1 for a packet whose counter is
+ * >= RejectAfterMessages (EncryptError::NoSession; nothing written), else 0.
+ *
+ * wg_aead_decrypt_batch: every message of a batch of equal-size data
+ * messages (a UDP GRO batch, worker/decap_ref.cpp:78-86; the last may be
+ * short): plaintext i (message length - 32 bytes, the padding included, as
+ * the reference's outsize) at dev_out + i * (segment_size - 32);
+ * dev_status[i] = 0, or -1 when Peer::decrypt rejects it: shorter than the
+ * 16-B header or than header + tag, counter > RejectAfterMessages (plaintext
+ * left untouched), or a tag that does not verify (plaintext zeroed, as
+ * libsodium does).  The replay window (session->replay.try_advance,
+ * proto.cpp:519-520) stays with the caller: it is a sequential per-session
+ * state update over the accepted counters.
+ * ---------------------------------------------------------------------- */
+int wg_aead_encrypt_batch(const uint8_t *dev_in, uint64_t total_len, uint32_t segment_size, const uint8_t key[32],
+                          uint32_t receiver_index, uint64_t counter0, uint8_t *dev_out, int8_t *dev_status,
+                          void *stream);
+int wg_aead_decrypt_batch(const uint8_t *dev_in, uint64_t total_len, uint32_t segment_size, const uint8_t key[32],
+                          uint8_t *dev_out, int8_t *dev_status, void *stream);
+
+/* ------------------------------------------------------------------------
  * Host-memory path: the batch starts and ends in host memory
  * (tun read buffers, worker/encap.cpp:74-97; UDP GRO recvmsg buffers,
  * worker/decap.cpp:16-28,90-156).  Synchronous.  The batch is cut into

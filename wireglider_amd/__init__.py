@@ -40,6 +40,8 @@ EXPORTED_SYMBOLS = (
     "wg_verify_desc",
     "wg_gso_split",
     "wg_gro_finalize",
+    "wg_aead_encrypt_batch",
+    "wg_aead_decrypt_batch",
     "wg_l4csum_uniform_host",
     "wg_host_release",
     "wg_host_alloc",
@@ -110,6 +112,8 @@ def _load() -> ctypes.CDLL:
         "wg_gso_split": (i32, [u8p, vp, u64, u8p, vp, vp]),
 
         "wg_gro_finalize": (i32, [u8p, vp, u64, vp]),
+        "wg_aead_encrypt_batch": (i32, [u8p, u64, u32, ctypes.c_char_p, u32, u64, u8p, vp, vp]),
+        "wg_aead_decrypt_batch": (i32, [u8p, u64, u32, ctypes.c_char_p, u8p, vp, vp]),
         "wg_l4csum_uniform_host": (i32, [u8p, u64, u32, u16, u32, vp]),
         "wg_host_release": (i32, []),
         "wg_host_alloc": (i32, [ctypes.POINTER(ctypes.c_void_p), u64]),
@@ -300,6 +304,60 @@ def gro_finalize(hdrs, gro_desc, stream=None):
     with _on(hdrs):
         rc = lib.wg_gro_finalize(hdrs.data_ptr(), gro_desc.data_ptr(), n, _stream_ptr(stream, hdrs))
     _check(rc, "wg_gro_finalize")
+
+
+def aead_message_stride(segment_size: int) -> int:
+    """Peer::expected_encrypt_size(segment_size) (include/proto/proto.hpp:266-269)."""
+    return 16 + (segment_size + 15) // 16 * 16 + 16
+
+
+def aead_encrypt_batch(batch, segment_size: int, key: bytes, receiver_index: int, counter0: int, out=None,
+                       status=None, stream=None):
+    """Peer::encrypt (proto/proto.cpp:544-583) for every segment of a
+    PacketBatch (worker/encap.cpp:136-141): message i at i * stride of `out`
+    (uint8 device tensor), counter counter0 + i.  Returns (out, status)."""
+    torch = _torch()
+    _require_cuda(batch, "batch")
+    if len(key) != 32:
+        raise WireGliderError("key must be 32 bytes")
+    n = nr_segments(batch.numel(), segment_size)
+    last = batch.numel() - (n - 1) * segment_size if n else 0
+    need = (n - 1) * aead_message_stride(segment_size) + aead_message_stride(last) if n else 0
+    if out is None:
+        out = torch.empty(max(need, 1), dtype=torch.uint8, device=batch.device)
+    _check_out(out, need, torch.uint8, batch, "out")
+    if status is None:
+        status = torch.empty(max(n, 1), dtype=torch.int8, device=batch.device)
+    _check_out(status, n, torch.int8, batch, "status")
+    with _on(batch):
+        rc = lib.wg_aead_encrypt_batch(batch.data_ptr(), batch.numel(), segment_size, bytes(key), receiver_index,
+                                       counter0 & (2**64 - 1), out.data_ptr(), status.data_ptr(),
+                                       _stream_ptr(stream, batch))
+    _check(rc, "wg_aead_encrypt_batch")
+    return out, status
+
+
+def aead_decrypt_batch(msgs, segment_size: int, key: bytes, out=None, status=None, stream=None):
+    """Peer::decrypt (proto/proto.cpp:496-523) for every message of a batch
+    of equal-size data messages (worker/decap_ref.cpp:78-86): plaintext i at
+    i * (segment_size - 32) of `out`.  Returns (out, status)."""
+    torch = _torch()
+    _require_cuda(msgs, "msgs")
+    if len(key) != 32:
+        raise WireGliderError("key must be 32 bytes")
+    n = nr_segments(msgs.numel(), segment_size)
+    need = n * max(segment_size - 32, 0)
+    if out is None:
+        out = torch.empty(max(need, 1), dtype=torch.uint8, device=msgs.device)
+    _check_out(out, need, torch.uint8, msgs, "out")
+    if status is None:
+        status = torch.empty(max(n, 1), dtype=torch.int8, device=msgs.device)
+    _check_out(status, n, torch.int8, msgs, "status")
+    with _on(msgs):
+        rc = lib.wg_aead_decrypt_batch(msgs.data_ptr(), msgs.numel(), segment_size, bytes(key), out.data_ptr(),
+                                       status.data_ptr(), _stream_ptr(stream, msgs))
+    _check(rc, "wg_aead_decrypt_batch")
+    return out, status
 
 
 def calc_l4_checksum_host(buf: bytes | bytearray | memoryview, segment_size: int, isv6: bool,

@@ -1,0 +1,579 @@
+// aead.hip — batched WireGuard data-message AEAD on MI355X (gfx950), SURVEY §8 f4.
+//
+// Per packet this is Peer::encrypt / Peer::decrypt (reference
+// proto/proto.cpp:544-583, 496-523) over crypto_aead_chacha20poly1305_ietf
+// (libsodium, i.e. RFC 8439), for the batches the workers build:
+//   encap: every segment of a PacketBatch into consecutive data messages
+//          (worker/encap.cpp:136-141; counter = encrypt_nonce++ per call);
+//   decap: every message of a UDP GRO batch (worker/decap_ref.cpp:78-86).
+//
+// Layout: a group of G lanes (G = 32: two packets per wave; G = 64: one,
+// in passes of 63 blocks for packets past 4 KiB) per packet.  Group lane 0
+// computes ChaCha20 block 0 (the Poly1305 key), writes the DataHeader and
+// handles the length block; lane g >= 1 computes keystream block g (counter
+// g) for the 64 bytes [64(g-1), 64g) of the padded payload, XORs and stores
+// them.  Poly1305 runs in the lanes too: lane g Horner-evaluates its (up to)
+// four 16-B ciphertext blocks with r, multiplies the result by r^(blocks
+// after it + 1) — a suffix product of r^(n_j) over the later lanes, log2(G)
+// cross-lane steps — and the group sums the products (26-bit limbs, so the
+// sum of 64 products stays below 2^32 per limb) before lane 0 reduces mod
+// 2^130 - 5 and adds s.  ChaCha20 and Poly1305 are integer-VALU work (~1,000
+// and ~700 instructions per 64-B block lane), so this kernel is bound by
+// VALU issue, not HBM.
+#include <hip/hip_runtime.h>
+
+#include "wg_device.hpp"
+#include "wg_internal.hpp"
+#include "wireglider_amd.h"
+
+namespace wg {
+
+// ---------------------------------------------------------------------------
+// ChaCha20 block function (RFC 8439 §2.3)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+
+#define WG_QR(a, b, c, d)                                                                                            \
+    a += b; d ^= a; d = rotl(d, 16);                                                                                 \
+    c += d; b ^= c; b = rotl(b, 12);                                                                                 \
+    a += b; d ^= a; d = rotl(d, 8);                                                                                  \
+    c += d; b ^= c; b = rotl(b, 7);
+
+struct AeadKey {
+    uint32_t k[8];
+};
+
+__device__ __forceinline__ void chacha20_block(const AeadKey &key, uint32_t ctr, uint32_t n0, uint32_t n1, uint32_t n2,
+                                               uint32_t out[16]) {
+    uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
+    uint32_t x4 = key.k[0], x5 = key.k[1], x6 = key.k[2], x7 = key.k[3];
+    uint32_t x8 = key.k[4], x9 = key.k[5], x10 = key.k[6], x11 = key.k[7];
+    uint32_t x12 = ctr, x13 = n0, x14 = n1, x15 = n2;
+#pragma unroll 2
+    for (int i = 0; i < 10; i++) {
+        WG_QR(x0, x4, x8, x12);
+        WG_QR(x1, x5, x9, x13);
+        WG_QR(x2, x6, x10, x14);
+        WG_QR(x3, x7, x11, x15);
+        WG_QR(x0, x5, x10, x15);
+        WG_QR(x1, x6, x11, x12);
+        WG_QR(x2, x7, x8, x13);
+        WG_QR(x3, x4, x9, x14);
+    }
+    out[0] = x0 + 0x61707865u;
+    out[1] = x1 + 0x3320646eu;
+    out[2] = x2 + 0x79622d32u;
+    out[3] = x3 + 0x6b206574u;
+    out[4] = x4 + key.k[0];
+    out[5] = x5 + key.k[1];
+    out[6] = x6 + key.k[2];
+    out[7] = x7 + key.k[3];
+    out[8] = x8 + key.k[4];
+    out[9] = x9 + key.k[5];
+    out[10] = x10 + key.k[6];
+    out[11] = x11 + key.k[7];
+    out[12] = x12 + ctr;
+    out[13] = x13 + n0;
+    out[14] = x14 + n1;
+    out[15] = x15 + n2;
+}
+#undef WG_QR
+
+// ---------------------------------------------------------------------------
+// Poly1305 arithmetic mod 2^130 - 5 in five 26-bit limbs (RFC 8439 §2.5)
+// ---------------------------------------------------------------------------
+struct L5 {
+    uint32_t v[5];
+};
+
+__device__ __forceinline__ L5 l5_one() { return L5{{1u, 0u, 0u, 0u, 0u}}; }
+__device__ __forceinline__ L5 l5_zero() { return L5{{0u, 0u, 0u, 0u, 0u}}; }
+
+// 16 little-endian bytes (four dwords) + 2^128 * hibit as limbs
+__device__ __forceinline__ L5 l5_from_words(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t hibit) {
+    L5 a;
+    a.v[0] = w0 & 0x3ffffffu;
+    a.v[1] = ((w0 >> 26) | (w1 << 6)) & 0x3ffffffu;
+    a.v[2] = ((w1 >> 20) | (w2 << 12)) & 0x3ffffffu;
+    a.v[3] = ((w2 >> 14) | (w3 << 18)) & 0x3ffffffu;
+    a.v[4] = (w3 >> 8) | (hibit << 24);
+    return a;
+}
+
+__device__ __forceinline__ L5 l5_add(const L5 &a, const L5 &b) {
+    L5 c;
+#pragma unroll
+    for (int i = 0; i < 5; i++) c.v[i] = a.v[i] + b.v[i];
+    return c;
+}
+
+// a * b mod p, partially reduced (limbs < 2^26 + a little); inputs with
+// limbs below ~2^27 (the products then stay below 2^58 after five terms).
+__device__ __forceinline__ L5 l5_mul(const L5 &a, const L5 &b) {
+    const uint32_t b0 = b.v[0], b1 = b.v[1], b2 = b.v[2], b3 = b.v[3], b4 = b.v[4];
+    const uint32_t s1 = b1 * 5u, s2 = b2 * 5u, s3 = b3 * 5u, s4 = b4 * 5u;
+    const uint32_t a0 = a.v[0], a1 = a.v[1], a2 = a.v[2], a3 = a.v[3], a4 = a.v[4];
+    uint64_t d0 = (uint64_t)a0 * b0 + (uint64_t)a1 * s4 + (uint64_t)a2 * s3 + (uint64_t)a3 * s2 + (uint64_t)a4 * s1;
+    uint64_t d1 = (uint64_t)a0 * b1 + (uint64_t)a1 * b0 + (uint64_t)a2 * s4 + (uint64_t)a3 * s3 + (uint64_t)a4 * s2;
+    uint64_t d2 = (uint64_t)a0 * b2 + (uint64_t)a1 * b1 + (uint64_t)a2 * b0 + (uint64_t)a3 * s4 + (uint64_t)a4 * s3;
+    uint64_t d3 = (uint64_t)a0 * b3 + (uint64_t)a1 * b2 + (uint64_t)a2 * b1 + (uint64_t)a3 * b0 + (uint64_t)a4 * s4;
+    uint64_t d4 = (uint64_t)a0 * b4 + (uint64_t)a1 * b3 + (uint64_t)a2 * b2 + (uint64_t)a3 * b1 + (uint64_t)a4 * b0;
+    L5 h;
+    uint32_t c = (uint32_t)(d0 >> 26);
+    h.v[0] = (uint32_t)d0 & 0x3ffffffu;
+    d1 += c;
+    c = (uint32_t)(d1 >> 26);
+    h.v[1] = (uint32_t)d1 & 0x3ffffffu;
+    d2 += c;
+    c = (uint32_t)(d2 >> 26);
+    h.v[2] = (uint32_t)d2 & 0x3ffffffu;
+    d3 += c;
+    c = (uint32_t)(d3 >> 26);
+    h.v[3] = (uint32_t)d3 & 0x3ffffffu;
+    d4 += c;
+    c = (uint32_t)(d4 >> 26);
+    h.v[4] = (uint32_t)d4 & 0x3ffffffu;
+    h.v[0] += c * 5u;
+    c = h.v[0] >> 26;
+    h.v[0] &= 0x3ffffffu;
+    h.v[1] += c;
+    return h;
+}
+
+// Shuffles within groups of G lanes (ds_bpermute).
+template <int G>
+__device__ __forceinline__ uint32_t grp_down(uint32_t v, uint32_t lane, uint32_t off) {
+    const uint32_t g = lane & (G - 1u);
+    const uint32_t src = g + off < (uint32_t)G ? lane + off : lane;
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+template <int G>
+__device__ __forceinline__ L5 l5_down(const L5 &a, uint32_t lane, uint32_t off) {
+    L5 b;
+#pragma unroll
+    for (int i = 0; i < 5; i++) b.v[i] = grp_down<G>(a.v[i], lane, off);
+    return b;
+}
+template <int G>
+__device__ __forceinline__ uint32_t grp_sum(uint32_t v, uint32_t lane) {
+#pragma unroll
+    for (uint32_t off = 1; off < (uint32_t)G; off <<= 1)
+        v += (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane ^ off) << 2), (int)v);
+    return v;
+}
+
+// Carry-normalise (value unchanged mod p): every limb < 2^26 but limb 1,
+// which may exceed it by a few units.  Limbs in must be < 2^32 - 2^29.
+__device__ __forceinline__ L5 l5_norm(L5 h) {
+    uint32_t c;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        c = h.v[0] >> 26; h.v[0] &= 0x3ffffffu; h.v[1] += c;
+        c = h.v[1] >> 26; h.v[1] &= 0x3ffffffu; h.v[2] += c;
+        c = h.v[2] >> 26; h.v[2] &= 0x3ffffffu; h.v[3] += c;
+        c = h.v[3] >> 26; h.v[3] &= 0x3ffffffu; h.v[4] += c;
+        c = h.v[4] >> 26; h.v[4] &= 0x3ffffffu; h.v[0] += c * 5u;
+    }
+    c = h.v[0] >> 26; h.v[0] &= 0x3ffffffu; h.v[1] += c;
+    return h;
+}
+
+// Group sum of normalised limbs: 32 lanes x (2^26 + small) fits 32 bits; 64
+// lanes might not, so G = 64 sums two 32-lane halves, normalises, then adds.
+template <int G>
+__device__ __forceinline__ L5 l5_grp_sum(L5 a, uint32_t lane) {
+    constexpr int H = G < 32 ? G : 32;
+#pragma unroll
+    for (int k = 0; k < 5; k++) a.v[k] = grp_sum<H>(a.v[k], lane);
+    if constexpr (G == 64) {
+        a = l5_norm(a);
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+            a.v[k] += (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane ^ 32u) << 2), (int)a.v[k]);
+    }
+    return a;
+}
+
+// Full reduction mod p of a limb sum (limbs < 2^32), + s mod 2^128 -> tag words.
+__device__ __forceinline__ void poly_finish(L5 h, const uint32_t s[4], uint32_t tag[4]) {
+    uint32_t h0 = h.v[0], h1 = h.v[1], h2 = h.v[2], h3 = h.v[3], h4 = h.v[4];
+    uint32_t c;
+    for (int k = 0; k < 2; k++) {  // two carry rounds: limbs < 2^32 -> < 2^26 (+ tiny)
+        c = h0 >> 26; h0 &= 0x3ffffffu; h1 += c;
+        c = h1 >> 26; h1 &= 0x3ffffffu; h2 += c;
+        c = h2 >> 26; h2 &= 0x3ffffffu; h3 += c;
+        c = h3 >> 26; h3 &= 0x3ffffffu; h4 += c;
+        c = h4 >> 26; h4 &= 0x3ffffffu; h0 += c * 5u;
+    }
+    c = h0 >> 26; h0 &= 0x3ffffffu; h1 += c;
+    uint32_t g0 = h0 + 5u;
+    c = g0 >> 26; g0 &= 0x3ffffffu;
+    uint32_t g1 = h1 + c;
+    c = g1 >> 26; g1 &= 0x3ffffffu;
+    uint32_t g2 = h2 + c;
+    c = g2 >> 26; g2 &= 0x3ffffffu;
+    uint32_t g3 = h3 + c;
+    c = g3 >> 26; g3 &= 0x3ffffffu;
+    const uint32_t g4 = h4 + c - (1u << 26);
+    const uint32_t mask = (g4 >> 31) - 1u;  // all ones when h >= p
+    h0 = (h0 & ~mask) | (g0 & mask);
+    h1 = (h1 & ~mask) | (g1 & mask);
+    h2 = (h2 & ~mask) | (g2 & mask);
+    h3 = (h3 & ~mask) | (g3 & mask);
+    h4 = (h4 & ~mask) | (g4 & mask);
+    const uint64_t f0 = (uint64_t)(uint32_t)(h0 | (h1 << 26)) + s[0];
+    const uint64_t f1 = (uint64_t)(uint32_t)((h1 >> 6) | (h2 << 20)) + s[1] + (f0 >> 32);
+    const uint64_t f2 = (uint64_t)(uint32_t)((h2 >> 12) | (h3 << 14)) + s[2] + (f1 >> 32);
+    const uint64_t f3 = (uint64_t)(uint32_t)((h3 >> 18) | (h4 << 8)) + s[3] + (f2 >> 32);
+    tag[0] = (uint32_t)f0;
+    tag[1] = (uint32_t)f1;
+    tag[2] = (uint32_t)f2;
+    tag[3] = (uint32_t)f3;
+}
+
+// ---------------------------------------------------------------------------
+// Byte movement
+// ---------------------------------------------------------------------------
+static __device__ v4u g_aead_zero16;
+
+__device__ __forceinline__ uint32_t keep_below(uint32_t w, uint32_t m, uint32_t lim) {
+    const int k = (int)lim - 4 * (int)m;  // bytes of dword m below lim
+    return k >= 4 ? w : (k <= 0 ? 0u : (w & ((1u << (8 * k)) - 1u)));
+}
+
+// The 64 bytes at a (of which the first `n` belong to the packet, n may be
+// 0..64; the rest read as zero) as 16 dwords: the aligned 16-B chunks
+// covering them, clamped onto the last one holding a packet byte (so no load
+// leaves the packet's own aligned chunks), funnel-shifted.
+__device__ __forceinline__ void load64(uintptr_t a, uint32_t n, uint32_t W[16]) {
+    const uintptr_t a0 = a & ~(uintptr_t)15;
+    const uintptr_t alast = n ? (a + n - 1) & ~(uintptr_t)15 : a0;
+    const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_aead_zero16);
+    v4u c[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const uintptr_t ca = a0 + 16u * k;
+        c[k] = ld16(n ? (ca > alast ? alast : ca) : zero);
+    }
+    const uint32_t Wd[20] = {c[0][0], c[0][1], c[0][2], c[0][3], c[1][0], c[1][1], c[1][2], c[1][3], c[2][0], c[2][1],
+                             c[2][2], c[2][3], c[3][0], c[3][1], c[3][2], c[3][3], c[4][0], c[4][1], c[4][2], c[4][3]};
+    const uint32_t s = (uint32_t)(a & 15u), q = s >> 2, sh = s & 3u;
+#pragma unroll
+    for (uint32_t m = 0; m < 16; m++) {
+        const uint32_t lo = q == 0 ? Wd[m] : q == 1 ? Wd[m + 1] : q == 2 ? Wd[m + 2] : Wd[m + 3];
+        const uint32_t hi = q == 0 ? Wd[m + 1] : q == 1 ? Wd[m + 2] : q == 2 ? Wd[m + 3] : Wd[m + 4];
+        W[m] = keep_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, n);
+    }
+}
+
+__device__ __forceinline__ void st16(uintptr_t addr, v4u v) {
+    *reinterpret_cast<__attribute__((address_space(1))) v4u *>(addr) = v;
+}
+__device__ __forceinline__ void st8b(uintptr_t addr, uint32_t v) {
+    *reinterpret_cast<__attribute__((address_space(1))) uint8_t *>(addr) = (uint8_t)v;
+}
+
+// Store the first n (0..64) bytes of W at `a` (any alignment): whole 16-B
+// stores for full chunks, bytes for the partial one.
+__device__ __forceinline__ void store_n(uintptr_t a, const uint32_t W[16], uint32_t n) {
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t b0 = 16u * q;
+        if (b0 + 16u <= n) {
+            st16(a + b0, v4u{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]});
+        } else if (b0 < n) {
+            for (uint32_t j = b0; j < n; j++) st8b(a + j, W[j >> 2] >> (8u * (j & 3u)));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The kernel
+// ---------------------------------------------------------------------------
+struct AeadParams {
+    const uint8_t *in;
+    uint8_t *out;
+    int8_t *status;
+    uint64_t total_len;
+    uint64_t n;          // packets (encrypt) / messages (decrypt)
+    uint32_t seg;        // segment_size of the input batch
+    uint32_t receiver;   // encrypt: DataHeader.receiver_index
+    uint64_t counter0;   // encrypt: counter of packet 0
+    AeadKey key;
+};
+
+constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/proto/proto.hpp:36
+
+// kDec = false: encrypt packet i (bytes [i*seg, +len) of `in`) into the data
+// message at out + i*stride, stride = 16 + pad16(seg) + 16.
+// kDec = true: decrypt message i (bytes [i*seg, +len) of `in`) into
+// out + i*(seg - 32); status[i] = 0 / -1.
+template <int G, bool kDec>
+__global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
+    constexpr uint32_t kPer = 64u / G;  // packets per wave
+    const uint32_t lane = lane_id();
+    const uint32_t g = lane & (G - 1u);
+    const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
+    const uint64_t i = wave * kPer + lane / G;
+    const bool live = i < p.n;
+    const uint64_t ii = live ? i : 0;
+    const uint64_t off = ii * p.seg;
+    const uint32_t len = live ? (uint32_t)(p.total_len - off < p.seg ? p.total_len - off : p.seg) : 0u;
+    // payload geometry
+    uint64_t counter;
+    uint32_t plen;  // encrypt: plaintext bytes; decrypt: ciphertext bytes
+    uint32_t pad;   // bytes of the Poly1305 ciphertext region (pad16)
+    uintptr_t src, dst;
+    int8_t st = 0;
+    if constexpr (!kDec) {
+        counter = p.counter0 + ii;
+        plen = len;
+        pad = (len + 15u) & ~15u;
+        src = reinterpret_cast<uintptr_t>(p.in) + off;
+        dst = reinterpret_cast<uintptr_t>(p.out) + ii * (32ull + ((p.seg + 15u) & ~15u));
+        if (counter >= kRejectAfterMessages)  // proto.cpp:560-562: EncryptError::NoSession
+            st = -1;
+    } else {
+        const uintptr_t msg = reinterpret_cast<uintptr_t>(p.in) + off;
+        // DataHeader counter (bytes 8-15), only when the message holds a header
+        const uint32_t hdr_ok = len >= 16u;
+        uint32_t c0 = 0, c1 = 0;
+        if (hdr_ok) {
+            c0 = ld8(msg + 8) | (ld8(msg + 9) << 8) | (ld8(msg + 10) << 16) | (ld8(msg + 11) << 24);
+            c1 = ld8(msg + 12) | (ld8(msg + 13) << 8) | (ld8(msg + 14) << 16) | (ld8(msg + 15) << 24);
+        }
+        counter = ((uint64_t)c1 << 32) | c0;
+        if (len < 16u || counter > kRejectAfterMessages || len < 32u)  // proto.cpp:497-501; clen < ABYTES
+            st = -1;
+        plen = st ? 0u : len - 32u;
+        pad = (plen + 15u) & ~15u;
+        src = msg + 16;
+        dst = reinterpret_cast<uintptr_t>(p.out) + ii * (uint64_t)(p.seg > 32u ? p.seg - 32u : 0u);
+    }
+    const uint32_t n0 = 0, n1 = (uint32_t)counter, n2 = (uint32_t)(counter >> 32);  // nonce: 0^4 || le64(counter)
+    const bool act = live && st == 0;
+
+    // One keystream block per lane for pass 0: counter g — group lane 0's is
+    // block 0, the Poly1305 key; lane g >= 1's is data block g - 1.
+    uint32_t ks[16];
+    chacha20_block(p.key, g, n0, n1, n2, ks);
+    const uint32_t base_lane = lane & ~(G - 1u);
+    uint32_t rw[4], sw[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        rw[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(base_lane << 2), (int)ks[k]);
+        sw[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(base_lane << 2), (int)ks[4 + k]);
+    }
+    // r clamped (RFC 8439 §2.5)
+    rw[0] &= 0x0fffffffu;
+    rw[1] &= 0x0ffffffcu;
+    rw[2] &= 0x0ffffffcu;
+    rw[3] &= 0x0ffffffcu;
+    const L5 r = l5_from_words(rw[0], rw[1], rw[2], rw[3], 0u);
+    const L5 r2 = l5_mul(r, r), r3 = l5_mul(r2, r), r4 = l5_mul(r2, r2);
+
+    // Data blocks: lane g >= 1 takes block g - 1 + 63 * pass (G = 64) or g - 1
+    // (G = 32).  Passes run last to first, F carrying r^(blocks after the pass).
+    const uint32_t nblk = (pad + 63u) / 64u;
+    const uint32_t lanes_per_pass = G - 1u;
+    const uint32_t npass = G == 64 ? (nblk + lanes_per_pass - 1u) / lanes_per_pass : 1u;
+    // wave-uniform pass count (G = 64: one packet per wave)
+    const uint32_t passes = G == 64 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)npass) : 1u;
+    L5 F = l5_one();
+    L5 acc = l5_zero();
+    uint32_t P[16];  // decrypt: the plaintext of pass 0 (processed last)
+    bool tag_ok = true;
+    uint32_t tagw[4] = {0, 0, 0, 0};
+    for (uint32_t pp = passes; pp-- > 0;) {
+        const uint32_t d = g >= 1u ? pp * lanes_per_pass + (g - 1u) : 0xffffffffu;  // data block of this lane
+        const bool has = act && g >= 1u && d < nblk;
+        const uint32_t boff = has ? 64u * d : 0u;
+        const uint32_t nin = has ? (plen - boff < 64u ? plen - boff : 64u) : 0u;  // payload bytes in the block
+        const uint32_t nct = has ? (pad - boff < 64u ? pad - boff : 64u) : 0u;    // Poly1305 bytes in the block
+        uint32_t W[16];
+        load64(src + boff, nin, W);  // plaintext (encrypt) / ciphertext (decrypt), zero past the payload
+        uint32_t kb[16];
+        if (pp == 0) {  // pass 0's blocks were computed with the key block
+#pragma unroll
+            for (int m = 0; m < 16; m++) kb[m] = ks[m];
+        } else {
+            chacha20_block(p.key, d + 1u, n0, n1, n2, kb);
+        }
+        uint32_t C[16];  // ciphertext words, zero past the ciphertext (what Poly1305 sees)
+#pragma unroll
+        for (int m = 0; m < 16; m++) {
+            if constexpr (!kDec) {
+                // padding plaintext bytes are zero (proto.cpp:568-572): their
+                // ciphertext is the keystream itself
+                C[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nct);
+            } else {
+                C[m] = W[m];
+                P[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nin);  // plaintext of pass 0 kept (last processed)
+            }
+        }
+        if (!kDec && has)
+            store_n(dst + 16 + boff, C, nct);
+        // Horner over this lane's 16-B blocks
+        const uint32_t nq = nct / 16u;
+        L5 x = l5_zero();
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            const L5 blk = l5_from_words(C[4 * q], C[4 * q + 1], C[4 * q + 2], C[4 * q + 3], 1u);
+            const L5 t = l5_mul(l5_add(x, blk), r);
+            if (q < nq)
+                x = t;
+        }
+        // Q = r^nq; suffix product over the pass's later lanes
+        L5 Q = nq == 4 ? r4 : nq == 3 ? r3 : nq == 2 ? r2 : nq == 1 ? r : l5_one();
+        L5 S = Q;
+#pragma unroll
+        for (uint32_t o = 1; o < (uint32_t)G; o <<= 1) {
+            const L5 t = l5_down<G>(S, lane, o);
+            if (g + o < (uint32_t)G)
+                S = l5_mul(S, t);
+        }
+        L5 E = l5_down<G>(S, lane, 1u);  // exclusive: product over lanes after this one
+        if (g + 1u >= (uint32_t)G)
+            E = l5_one();
+        // this lane's term: x * r^(blocks after it) * r (the length block) ...
+        const L5 mult = l5_mul(l5_mul(E, F), r);
+        const L5 term = l5_mul(x, mult);
+        if (has)
+            acc = l5_add(acc, term);
+        // F *= product of the whole pass (the group's lane 0 holds S over lanes >= 0)
+        L5 Sall;
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+            Sall.v[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(base_lane << 2), (int)S.v[k]);
+        F = l5_mul(F, Sall);
+    }
+    // the length block: le64(0) || le64(pad / payload length), times r
+    const uint32_t mlen = kDec ? plen : pad;  // AEAD ct length (encrypt: the padded plaintext)
+    const L5 lenblk = l5_from_words(0u, 0u, mlen, 0u, 1u);
+    if (g == 0u && act)
+        acc = l5_add(acc, l5_mul(lenblk, r));
+    // group sum, every lane finishes (lane 0's result is used)
+    const L5 tot = l5_grp_sum<G>(l5_norm(acc), lane);
+    poly_finish(tot, sw, tagw);
+    if constexpr (!kDec) {
+        if (g == 0u && live) {
+            if (act) {
+                st16(dst, v4u{4u, p.receiver, n1, n2});  // DataHeader (proto.cpp:563-566)
+                st16(dst + 16 + pad, v4u{tagw[0], tagw[1], tagw[2], tagw[3]});
+            }
+            if (p.status)
+                p.status[ii] = st;
+        }
+    } else {
+        // tag check (crypto_verify_16), then plaintext or zeros (libsodium
+        // zeroes the message on a bad tag); rejected-before-MAC messages are
+        // left untouched
+        const uintptr_t tsrc = src + plen;
+        uint32_t got[4] = {0, 0, 0, 0};
+        if (act) {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                got[k] = ld8(tsrc + 4 * k) | (ld8(tsrc + 4 * k + 1) << 8) | (ld8(tsrc + 4 * k + 2) << 16) |
+                         (ld8(tsrc + 4 * k + 3) << 24);
+        }
+        const uint32_t diff = (got[0] ^ tagw[0]) | (got[1] ^ tagw[1]) | (got[2] ^ tagw[2]) | (got[3] ^ tagw[3]);
+        tag_ok = diff == 0;
+        // decrypt pass 2: regenerate each block's plaintext and store it
+        for (uint32_t pp = 0; pp < passes; pp++) {
+            const uint32_t d = g >= 1u ? pp * lanes_per_pass + (g - 1u) : 0xffffffffu;
+            const bool has = act && g >= 1u && d < nblk;
+            const uint32_t boff = has ? 64u * d : 0u;
+            const uint32_t nin = has ? (plen - boff < 64u ? plen - boff : 64u) : 0u;
+            uint32_t O[16];
+            if (pp == 0) {
+#pragma unroll
+                for (int m = 0; m < 16; m++) O[m] = P[m];
+            } else {  // G = 64 packets past 4 KiB: regenerate the earlier passes' blocks
+                uint32_t W[16], kb[16];
+                load64(src + boff, nin, W);
+                chacha20_block(p.key, d + 1u, n0, n1, n2, kb);
+#pragma unroll
+                for (int m = 0; m < 16; m++) O[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nin);
+            }
+            if (!tag_ok) {
+#pragma unroll
+                for (int m = 0; m < 16; m++) O[m] = 0u;
+            }
+            if (has)
+                store_n(dst + boff, O, nin);
+        }
+        if (g == 0u && live)
+            p.status[ii] = (int8_t)(st ? st : (tag_ok ? 0 : -1));
+    }
+}
+
+}  // namespace wg
+
+using namespace wg;
+
+static AeadKey key_words(const uint8_t key[32]) {
+    AeadKey k;
+    for (int i = 0; i < 8; i++)
+        k.k[i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
+                 ((uint32_t)key[4 * i + 3] << 24);
+    return k;
+}
+
+template <bool kDec>
+static int launch_aead(AeadParams &p, uint32_t maxpay, hipStream_t st) {
+    // groups of 32 lanes while a packet's blocks (+ the key block) fit
+    const uint32_t nblk = (((maxpay + 15u) & ~15u) + 63u) / 64u;
+    const bool g32 = nblk + 1u <= 32u;
+    const uint64_t per_block = g32 ? 8u : 4u;  // packets per 256-thread block
+    uint64_t blocks = (p.n + per_block - 1) / per_block;
+    if (blocks >= 8)
+        blocks = (blocks + 7) & ~7ull;  // XCD swizzle bijective; surplus waves have no live packet
+    if (blocks > 0x7fffffffull)
+        return WG_ERR_INVALID;
+    if (g32)
+        hipLaunchKernelGGL((aead_kernel<32, kDec>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+    else
+        hipLaunchKernelGGL((aead_kernel<64, kDec>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+    return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+}
+
+extern "C" int wg_aead_encrypt_batch(const uint8_t *dev_in, uint64_t total_len, uint32_t segment_size,
+                                     const uint8_t key[32], uint32_t receiver_index, uint64_t counter0,
+                                     uint8_t *dev_out, int8_t *dev_status, void *stream) {
+    if (!segment_size || segment_size > 65535u || !key)
+        return WG_ERR_INVALID;
+    if (!total_len)
+        return WG_OK;
+    if (!dev_in || !dev_out || (reinterpret_cast<uintptr_t>(dev_out) & 15))
+        return WG_ERR_INVALID;
+    AeadParams p{};
+    p.in = dev_in;
+    p.out = dev_out;
+    p.status = dev_status;
+    p.total_len = total_len;
+    p.n = (total_len + segment_size - 1) / segment_size;
+    p.seg = segment_size;
+    p.receiver = receiver_index;
+    p.counter0 = counter0;
+    p.key = key_words(key);
+    return launch_aead<false>(p, segment_size, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int wg_aead_decrypt_batch(const uint8_t *dev_in, uint64_t total_len, uint32_t segment_size,
+                                     const uint8_t key[32], uint8_t *dev_out, int8_t *dev_status, void *stream) {
+    if (!segment_size || segment_size > 65535u + 32u || !key)
+        return WG_ERR_INVALID;
+    if (!total_len)
+        return WG_OK;
+    if (!dev_in || !dev_out || !dev_status)
+        return WG_ERR_INVALID;
+    AeadParams p{};
+    p.in = dev_in;
+    p.out = dev_out;
+    p.status = dev_status;
+    p.total_len = total_len;
+    p.n = (total_len + segment_size - 1) / segment_size;
+    p.seg = segment_size;
+    p.key = key_words(key);
+    return launch_aead<true>(p, segment_size > 32u ? segment_size - 32u : 0u, static_cast<hipStream_t>(stream));
+}
