@@ -27,6 +27,11 @@ Workloads (--workload; BASELINE.json configs):
   gro                SURVEY §8 f2: GRO finalize (wg_gro_finalize) of
                      4,194,304 coalesced flows per GPU, headers in 64 B slots,
                      mixed v4/v6 x TCP/UDP; metric Mflows/s.
+  aead               SURVEY §8 f4: WireGuard data-message encryption
+                     (wg_aead_encrypt_batch, ChaCha20-Poly1305) of 1,048,576 x
+                     1500 B packets per GPU (the encap worker's PacketBatch),
+                     decrypt of the result in post_checks; metric GiB/s of
+                     plaintext.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2]
   torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -67,7 +72,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="config2",
-                    choices=["config1", "config2", "config3", "config3udp", "config4", "config5", "verify", "gro"])
+                    choices=["config1", "config2", "config3", "config3udp", "config4", "config5", "verify", "gro",
+                             "aead"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-strong", action="store_true", help="skip the config 5 strong-scaling companion")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall seconds of the CPU baseline sample")
@@ -218,6 +224,55 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
         return Workload(launch, n, n * in_len, alg, cfg, "weak", buf,
                         "wg::gso_plan_kernel + wg::gso_split_kernel<4,1,0> + wg::gso_finalize_kernel (one wg_gso_split call)",
                         rank * n, sample=sample, counts=[n] * world, post=post)
+    if name == "aead":
+        # worker/encap.cpp:136-141: Peer::encrypt for every 1500-B segment of a
+        # PacketBatch (config 2's packets), counters encrypt_nonce++ per call
+        n = 1 << 20
+        seed = 0x5EED00F4
+        buf = torch.empty(n * SEG, dtype=torch.uint8, device=dev)
+        wga.synth_fill(buf, seed, counter_base=rank * n * SEG)
+        wga.synth_headers(buf, wga.synth_desc_stride(n, SEG, SEG, 0, seed, rank * n, device=dev), seed, rank * n)
+        key = np.random.default_rng(seed).integers(0, 256, 32, dtype=np.uint8).tobytes()
+        rx, c0 = 0x1A2B3C4D, (rank * n) + 1000
+        mseg = wga.aead_message_stride(SEG)
+        out = torch.empty(n * mseg, dtype=torch.uint8, device=dev)
+        st = torch.empty(n, dtype=torch.int8, device=dev)
+
+        def launch():
+            wga.aead_encrypt_batch(buf, SEG, key, rx, c0, out=out, status=st)
+
+        def post():
+            # decrypt the messages back (worker/decap_ref.cpp:78-86), timed like
+            # the main line; every status 0 and every plaintext equal to its packet
+            pt = torch.empty(n * (mseg - 32), dtype=torch.uint8, device=dev)
+            dst = torch.empty(n, dtype=torch.int8, device=dev)
+            for _ in range(5):
+                wga.aead_decrypt_batch(out, mseg, key, out=pt, status=dst)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(20):
+                wga.aead_decrypt_batch(out, mseg, key, out=pt, status=dst)
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / 20
+            same = bool(torch.equal(pt.view(n, mseg - 32)[:, :SEG], buf.view(n, SEG)))
+            return {"encrypt_status_nonzero": int(torch.count_nonzero(st).item()),
+                    "decrypt": {"kernel_ms": round(ms, 5), "GiB_s": round(n * SEG / (ms * 1e-3) / 2**30, 1),
+                                "status_nonzero": int(torch.count_nonzero(dst).item()),
+                                "plaintext_round_trip_equal": same}}
+
+        def sample(npk):
+            k = min(n, 1 << 16)  # ~98 MB: the scalar C oracle runs ~0.15 GB/s per core
+            return buf[: k * SEG].cpu().numpy(), out[: k * mseg].cpu().numpy(), ("aead", key, rx, c0, SEG)
+
+        cfg = {"workload": "aead (SURVEY §8 f4): WireGuard data-message encryption (ChaCha20-Poly1305, "
+                           "Peer::encrypt per segment) of 1,048,576 x 1500 B packets per GPU",
+               "packets_per_gpu": n, "segment_size": SEG, "message_stride": mseg, "parallelism": f"shard{world}"}
+        return Workload(launch, n, n * SEG, n * SEG + n * mseg + n, cfg, "weak", buf,
+                        "wg::aead_kernel<32,false> (VALU-bound: ChaCha20 + Poly1305)", rank * n, sample=sample,
+                        counts=[n] * world, post=post,
+                        metric="device-resident GiB/s of plaintext, WireGuard data-message encryption (SURVEY f4)")
     if name == "config1":
         # tests/test-checksum.cpp:11-17: checksum(create_packet(n), 0) on random
         # buffers; BASELINE configs[0] at 64 KiB, 16,384 buffers (1 GiB,
@@ -596,6 +651,36 @@ def cpu_baseline(sample_fn, seconds: float):
             gpu_out = None  # the timed in-place runs must reproduce the checked answer
         nbytes = d.size  # flows
         gpu_out = np.concatenate([gpu_out[0].astype(np.int64), gpu_out[1].astype(np.int64)])
+    elif kind[0] == "aead":
+        # Peer::encrypt per segment: the oracle (scalar RFC 8439 restatement,
+        # the bit-exact checker) and, as the stronger CPU comparator of
+        # libsodium's class, the system OpenSSL's EVP_chacha20_poly1305
+        _, key, rx, c0, seg = kind
+        cpu_out = np.zeros(gpu_out.size + 64, np.uint8)
+        oracle.wg_encrypt_batch_mt(key, rx, c0, host, seg, cpu_out, threads)
+        exp, gpu_out = cpu_out[: gpu_out.size], gpu_out
+        sub = host[: host.size // 8 // seg * seg]
+        t0 = time.perf_counter()
+        oracle.wg_encrypt_batch_mt(key, rx, c0, sub, seg, cpu_out, 1)
+        t_1core = (time.perf_counter() - t0) * host.size / sub.size
+        t0 = time.perf_counter()
+        oracle.wg_encrypt_batch_mt(key, rx, c0, host, seg, cpu_out, threads)
+        t_all = time.perf_counter() - t0
+        oss = {}
+        try:
+            t0 = time.perf_counter()
+            oracle.openssl_encrypt_batch(key, rx, c0, sub, seg, cpu_out, 1)
+            oss1 = (time.perf_counter() - t0) * host.size / sub.size
+            t0 = time.perf_counter()
+            oracle.openssl_encrypt_batch(key, rx, c0, host, seg, cpu_out, threads)
+            ossn = time.perf_counter() - t0
+            oss = {"openssl_evp_chacha20_poly1305": {
+                "value": host.size / ossn * 2.0**-30, "value_1core": host.size / oss1 * 2.0**-30, "unit": "GiB/s",
+                "bit_exact_vs_oracle": bool(np.array_equal(cpu_out[: gpu_out.size], exp))}}
+        except Exception as e:  # noqa: BLE001 - a comparator, never the checker
+            oss = {"openssl_evp_chacha20_poly1305": f"unavailable: {e}"}
+        nbytes = host.size
+        npk = host.size // seg
     elif kind[0] == "checksum":
         # checksum(buf, 0) per buffer (BASELINE config 1)
         d = kind[1]
@@ -630,7 +715,9 @@ def cpu_baseline(sample_fn, seconds: float):
     scale, unit = (1e-6, "Mflows/s") if kind[0] == "gro" else (2.0**-30, "GiB/s")
     what = {"verify": "decap verify gates restatement (orc_verify)", "gro": "GRO finalize restatement",
             "gso": "do_tun_gso_split restatement, output bytes compared",
-            "checksum": "checksum(span, 0) restatement"}.get(kind[0], "calc_l4_checksum restatement")
+            "checksum": "checksum(span, 0) restatement",
+            "aead": "Peer::encrypt restatement over RFC 8439 (scalar C), message bytes compared"}.get(
+                kind[0], "calc_l4_checksum restatement")
     nofold = "AVX2 vector nofold (oracle/csum_oracle.c nofold_avx2)" if oracle.have_avx2() else "scalar nofold"
     return {
         "value": nbytes / t_all * scale,
@@ -645,6 +732,7 @@ def cpu_baseline(sample_fn, seconds: float):
                   f"(sched_getaffinity {cores['affinity']}, cgroup quota {cores['cgroup_quota_cpus']}), "
                   f"~{seconds:.1f} s wall; bit-exact vs GPU: {parity}",
         "parity_with_gpu": parity,
+        **(oss if kind[0] == "aead" else {}),
     }
 
 

@@ -13,6 +13,7 @@
  */
 #include "csum_oracle.h"
 
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -274,4 +275,65 @@ void orc_wg_decrypt_batch(const uint8_t key[32], const uint8_t *in, uint64_t tot
         const size_t len = total_len - off < segment_size ? (size_t)(total_len - off) : segment_size;
         status[i] = (int8_t)orc_wg_decrypt(key, in + off, len, out + i * ostride);
     }
+}
+
+/* The two batch drivers over host threads (disjoint packet ranges): the CPU
+ * baseline of bench.py's f4 workload. */
+typedef struct {
+    const uint8_t *key;
+    uint32_t rx;
+    uint64_t c0;
+    const uint8_t *in;
+    uint64_t total_len;
+    uint32_t seg;
+    uint8_t *out;
+    int8_t *status;
+    int dec;
+    uint64_t lo, hi;
+} aead_job;
+
+static void *aead_job_run(void *arg) {
+    aead_job *j = (aead_job *)arg;
+    const size_t stride = 16 + (((size_t)j->seg + 15) & ~(size_t)15) + 16;
+    const size_t ostride = j->seg > 32 ? j->seg - 32 : 0;
+    for (uint64_t i = j->lo; i < j->hi; i++) {
+        const uint64_t off = i * j->seg;
+        const size_t len = j->total_len - off < j->seg ? (size_t)(j->total_len - off) : j->seg;
+        if (j->dec)
+            j->status[i] = (int8_t)orc_wg_decrypt(j->key, j->in + off, len, j->out + i * ostride);
+        else
+            orc_wg_encrypt(j->key, j->rx, j->c0 + i, j->in + off, len, j->out + i * stride);
+    }
+    return NULL;
+}
+
+static void aead_parallel(aead_job proto, uint64_t n, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    if ((uint64_t)threads > n) threads = n ? (int)n : 1;
+    pthread_t tid[256];
+    aead_job jobs[256];
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = proto;
+        jobs[t].lo = n * (uint64_t)t / (uint64_t)threads;
+        jobs[t].hi = n * (uint64_t)(t + 1) / (uint64_t)threads;
+        if (threads == 1)
+            aead_job_run(&jobs[t]);
+        else
+            pthread_create(&tid[t], NULL, aead_job_run, &jobs[t]);
+    }
+    if (threads > 1)
+        for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+}
+
+void orc_wg_encrypt_batch_mt(const uint8_t key[32], uint32_t receiver_index, uint64_t counter0, const uint8_t *in,
+                             uint64_t total_len, uint32_t segment_size, uint8_t *out, int threads) {
+    aead_job j = {key, receiver_index, counter0, in, total_len, segment_size, out, NULL, 0, 0, 0};
+    aead_parallel(j, (total_len + segment_size - 1) / segment_size, threads);
+}
+
+void orc_wg_decrypt_batch_mt(const uint8_t key[32], const uint8_t *in, uint64_t total_len, uint32_t segment_size,
+                             uint8_t *out, int8_t *status, int threads) {
+    aead_job j = {key, 0, 0, in, total_len, segment_size, out, status, 1, 0, 0};
+    aead_parallel(j, (total_len + segment_size - 1) / segment_size, threads);
 }

@@ -200,4 +200,9 @@ void orc_wg_encrypt_batch(const uint8_t key[32], uint32_t receiver_index, uint64
 void orc_wg_decrypt_batch(const uint8_t key[32], const uint8_t *in, uint64_t total_len, uint32_t segment_size,
                           uint8_t *out, int8_t *status);
 
+void orc_wg_encrypt_batch_mt(const uint8_t key[32], uint32_t receiver_index, uint64_t counter0, const uint8_t *in,
+                             uint64_t total_len, uint32_t segment_size, uint8_t *out, int threads);
+void orc_wg_decrypt_batch_mt(const uint8_t key[32], const uint8_t *in, uint64_t total_len, uint32_t segment_size,
+                             uint8_t *out, int8_t *status, int threads);
+
 #endif

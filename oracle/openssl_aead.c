@@ -1,0 +1,87 @@
+/*
+ * openssl_aead.c — the data-message AEAD batch (Peer::encrypt per segment,
+ * reference proto/proto.cpp:544-583, worker/encap.cpp:136-141) over the
+ * system OpenSSL's EVP_chacha20_poly1305: an optimised, independent RFC 8439
+ * implementation of the same class as the reference's libsodium (which is
+ * not installed here).  TEST INFRASTRUCTURE ONLY: bench.py's f4 CPU
+ * comparator and an extra checker in tests/; never part of the product.
+ */
+#include <openssl/evp.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <string.h>
+
+static void st_le32(uint8_t *p, uint32_t v) {
+    p[0] = (uint8_t)v;
+    p[1] = (uint8_t)(v >> 8);
+    p[2] = (uint8_t)(v >> 16);
+    p[3] = (uint8_t)(v >> 24);
+}
+
+typedef struct {
+    const uint8_t *key;
+    uint32_t rx;
+    uint64_t c0;
+    const uint8_t *in;
+    uint64_t total;
+    uint32_t seg;
+    uint8_t *out;
+    uint64_t lo, hi;
+    int rc;
+} job;
+
+static void *run(void *arg) {
+    job *j = (job *)arg;
+    EVP_CIPHER_CTX *ctx = EVP_CIPHER_CTX_new();
+    const size_t stride = 16 + (((size_t)j->seg + 15) & ~(size_t)15) + 16;
+    j->rc = ctx && EVP_EncryptInit_ex(ctx, EVP_chacha20_poly1305(), NULL, j->key, NULL) == 1 ? 0 : -1;
+    for (uint64_t i = j->lo; i < j->hi && !j->rc; i++) {
+        const uint64_t off = i * j->seg;
+        const size_t len = j->total - off < j->seg ? (size_t)(j->total - off) : j->seg;
+        const size_t padded = (len + 15) & ~(size_t)15;
+        const uint64_t counter = j->c0 + i;
+        uint8_t *o = j->out + i * stride;
+        st_le32(o, 4u);
+        st_le32(o + 4, j->rx);
+        st_le32(o + 8, (uint32_t)counter);
+        st_le32(o + 12, (uint32_t)(counter >> 32));
+        uint8_t nonce[12] = {0};
+        memcpy(nonce + 4, o + 8, 8);
+        memcpy(o + 16, j->in + off, len);
+        memset(o + 16 + len, 0, padded - len);
+        int n = 0;
+        if (EVP_EncryptInit_ex(ctx, NULL, NULL, NULL, nonce) != 1 ||
+            (padded && EVP_EncryptUpdate(ctx, o + 16, &n, o + 16, (int)padded) != 1) ||
+            EVP_EncryptFinal_ex(ctx, o + 16 + padded, &n) != 1 ||
+            EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_GET_TAG, 16, o + 16 + padded) != 1)
+            j->rc = -1;
+    }
+    EVP_CIPHER_CTX_free(ctx);
+    return NULL;
+}
+
+/* 0, or -1 if OpenSSL failed; same output layout as orc_wg_encrypt_batch. */
+int oss_wg_encrypt_batch(const uint8_t key[32], uint32_t rx, uint64_t c0, const uint8_t *in, uint64_t total,
+                         uint32_t seg, uint8_t *out, int threads) {
+    const uint64_t n = (total + seg - 1) / seg;
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    if ((uint64_t)threads > n) threads = n ? (int)n : 1;
+    pthread_t tid[256];
+    job jobs[256];
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (job){key, rx, c0, in, total, seg, out, n * (uint64_t)t / (uint64_t)threads,
+                        n * (uint64_t)(t + 1) / (uint64_t)threads, 0};
+        if (threads == 1)
+            run(&jobs[t]);
+        else
+            pthread_create(&tid[t], NULL, run, &jobs[t]);
+    }
+    int rc = 0;
+    for (int t = 0; t < threads; t++) {
+        if (threads > 1)
+            pthread_join(tid[t], NULL);
+        rc |= jobs[t].rc;
+    }
+    return rc;
+}

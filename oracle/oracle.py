@@ -99,6 +99,10 @@ def _load():
     lib.orc_wg_encrypt_batch.argtypes = [vp, u32, u64, vp, u64, u32, vp]
     lib.orc_wg_decrypt_batch.restype = None
     lib.orc_wg_decrypt_batch.argtypes = [vp, vp, u64, u32, vp, vp]
+    lib.orc_wg_encrypt_batch_mt.restype = None
+    lib.orc_wg_encrypt_batch_mt.argtypes = [vp, u32, u64, vp, u64, u32, vp, i32]
+    lib.orc_wg_decrypt_batch_mt.restype = None
+    lib.orc_wg_decrypt_batch_mt.argtypes = [vp, vp, u64, u32, vp, vp, i32]
     lib.orc_time_l4_uniform.restype = ctypes.c_double
     lib.orc_time_l4_uniform.argtypes = [vp, u64, u32, u16, u32, vp, i32, i32]
     return lib
@@ -387,3 +391,43 @@ def wg_decrypt_batch(key: bytes, buf: np.ndarray, segment_size: int):
     st = np.zeros(max(n, 1), np.int8)
     lib.orc_wg_decrypt_batch(k.ctypes.data, a.ctypes.data, a.size, segment_size, out.ctypes.data, st.ctypes.data)
     return out[: n * ostride], st[:n]
+
+
+def wg_encrypt_batch_mt(key: bytes, receiver_index: int, counter0: int, buf: np.ndarray, segment_size: int,
+                        out: np.ndarray, threads: int) -> None:
+    """wg_encrypt_batch into a preallocated `out`, over host threads (the
+    CPU baseline's timed call)."""
+    k, a = _b(key), _u8(buf)
+    lib.orc_wg_encrypt_batch_mt(k.ctypes.data, receiver_index, counter0, a.ctypes.data, a.size, segment_size,
+                                out.ctypes.data, threads)
+
+
+def wg_decrypt_batch_mt(key: bytes, buf: np.ndarray, segment_size: int, out: np.ndarray, status: np.ndarray,
+                        threads: int) -> None:
+    k, a = _b(key), _u8(buf)
+    lib.orc_wg_decrypt_batch_mt(k.ctypes.data, a.ctypes.data, a.size, segment_size, out.ctypes.data,
+                                status.ctypes.data, threads)
+
+
+_OSS = None
+
+
+def openssl_encrypt_batch(key: bytes, receiver_index: int, counter0: int, buf: np.ndarray, segment_size: int,
+                          out: np.ndarray, threads: int) -> None:
+    """The same batch over the system OpenSSL's EVP_chacha20_poly1305
+    (oracle/openssl_aead.c): an optimised RFC 8439 of libsodium's class, the
+    f4 CPU comparator."""
+    global _OSS
+    if _OSS is None:
+        path = HERE / "build" / "libaead_openssl.so"
+        if not path.exists():
+            build()
+        _OSS = ctypes.CDLL(str(path))
+        _OSS.oss_wg_encrypt_batch.restype = ctypes.c_int
+        _OSS.oss_wg_encrypt_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
+                                              ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int]
+    k, a = _b(key), _u8(buf)
+    rc = _OSS.oss_wg_encrypt_batch(k.ctypes.data, receiver_index, counter0, a.ctypes.data, a.size, segment_size,
+                                   out.ctypes.data, threads)
+    if rc != 0:
+        raise RuntimeError("OpenSSL EVP_chacha20_poly1305 failed")

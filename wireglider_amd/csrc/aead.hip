@@ -14,10 +14,11 @@
 // g) for the 64 bytes [64(g-1), 64g) of the padded payload, XORs and stores
 // them.  Poly1305 runs in the lanes too: lane g Horner-evaluates its (up to)
 // four 16-B ciphertext blocks with r, multiplies the result by r^(blocks
-// after it + 1) — a suffix product of r^(n_j) over the later lanes, log2(G)
-// cross-lane steps — and the group sums the products (26-bit limbs, so the
-// sum of 64 products stays below 2^32 per limb) before lane 0 reduces mod
-// 2^130 - 5 and adds s.  ChaCha20 and Poly1305 are integer-VALU work (~1,000
+// after it) — a suffix product of r^(n_j) over the later lanes, log2(G)
+// cross-lane steps — and the group sums the
+// products (normalised 26-bit limbs, so 32 of them fit a dword) before one
+// multiplication by r (the length block comes last), the reduction mod
+// 2^130 - 5 and + s.  ChaCha20 and Poly1305 are integer-VALU work (~1,000
 // and ~700 instructions per 64-B block lane), so this kernel is bound by
 // VALU issue, not HBM.
 #include <hip/hip_runtime.h>
@@ -435,25 +436,29 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
         L5 E = l5_down<G>(S, lane, 1u);  // exclusive: product over lanes after this one
         if (g + 1u >= (uint32_t)G)
             E = l5_one();
-        // this lane's term: x * r^(blocks after it) * r (the length block) ...
-        const L5 mult = l5_mul(l5_mul(E, F), r);
-        const L5 term = l5_mul(x, mult);
+        // this lane's term: x * r^(blocks after it in this pass) * F (the
+        // later passes' blocks); the common factor r (the length block after
+        // everything) is applied once to the group's sum
+        const L5 EF = passes > 1 ? l5_mul(E, F) : E;  // F == 1 with one pass (wave-uniform test)
+        const L5 term = l5_mul(x, EF);
         if (has)
             acc = l5_add(acc, term);
-        // F *= product of the whole pass (the group's lane 0 holds S over lanes >= 0)
-        L5 Sall;
+        if (passes > 1 && pp > 0) {
+            // F *= product of the whole pass (group lane 0 holds S over lanes >= 0)
+            L5 Sall;
 #pragma unroll
-        for (int k = 0; k < 5; k++)
-            Sall.v[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(base_lane << 2), (int)S.v[k]);
-        F = l5_mul(F, Sall);
+            for (int k = 0; k < 5; k++)
+                Sall.v[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(base_lane << 2), (int)S.v[k]);
+            F = l5_mul(F, Sall);
+        }
     }
     // the length block: le64(0) || le64(pad / payload length), times r
     const uint32_t mlen = kDec ? plen : pad;  // AEAD ct length (encrypt: the padded plaintext)
     const L5 lenblk = l5_from_words(0u, 0u, mlen, 0u, 1u);
     if (g == 0u && act)
-        acc = l5_add(acc, l5_mul(lenblk, r));
-    // group sum, every lane finishes (lane 0's result is used)
-    const L5 tot = l5_grp_sum<G>(l5_norm(acc), lane);
+        acc = l5_add(acc, lenblk);
+    // group sum, times r (every term's last factor), every lane finishes
+    const L5 tot = l5_mul(l5_norm(l5_grp_sum<G>(l5_norm(acc), lane)), r);
     poly_finish(tot, sw, tagw);
     if constexpr (!kDec) {
         if (g == 0u && live) {
