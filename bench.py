@@ -299,7 +299,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                            "(tests/test-checksum.cpp:11-17 shape; BASELINE configs[0]), descriptor batch",
                "buffers_per_gpu": n, "buffer_bytes": size, "layout": "descriptor", "parallelism": f"shard{world}"}
         return Workload(launch, n, n * size, n * size + 2 * n + 16 * n, cfg, "weak", buf,
-                        "wg::l4csum_split_kernel<2,nt> (plain checksum, l4_small=5)", rank * n, sample=sample,
+                        "wg::l4csum_coop_kernel<2,nt,4,4> (plain checksum, a 4-wave block per buffer: l4_coop)", rank * n, sample=sample,
                         counts=[n] * world,
                         metric="device-resident GiB/s, checksum(span, 0) over 64 KiB buffers (BASELINE config 1 shape)")
     if name == "verify":

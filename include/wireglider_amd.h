@@ -340,6 +340,9 @@ int wg_device_count(void);
  *   "host_chunk_mb" wg_l4csum_uniform_host chunk size in MiB (1 .. 4096)
  *   "l4_unroll"  descriptor batches: 16-B loads in flight per lane while
  *                streaming a packet's bytes past its first 2 KiB (4, 8)
+ *   "l4_coop"    descriptor batches of n <= l4_coop descriptors: a block of
+ *                l4_coop_waves waves per packet (few, long packets; 0 never)
+ *   "l4_coop_waves" waves sharing one packet in that mode (2, 4, 8, 16)
  *   "gso_ablate" GSO A/B variants: 1 = non-temporal payload stores, 32 = no
  *                XCD swizzle (both correct); 0 = the default kernel.
  * Thread-safe: each launch reads one consistent snapshot of the knobs. */

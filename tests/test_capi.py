@@ -142,7 +142,8 @@ def test_tune_knobs_validate_and_round_trip():
         wga.tune_set(k, v)
         assert wga.tune_get(k) == v
     for k, bad in (("l4_ppw", 3), ("l4_occ", 6), ("gso_groups", 0), ("gso_groups", 65), ("verify_hdr", 2),
-                   ("gso_waves", 16), ("gso_ablate", 7), ("gso_ablate", 2)):
+                   ("gso_waves", 16), ("gso_ablate", 7), ("gso_ablate", 2), ("l4_coop_waves", 3),
+                   ("l4_coop_waves", 32)):
         v = wga.tune_get(k)
         with pytest.raises(Exception):
             wga.tune_set(k, bad)

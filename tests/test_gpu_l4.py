@@ -115,7 +115,9 @@ def test_uniform_geometry_sweep(gpu, seg, occ):
 DESC_VARIANTS = [{"l4_occ": 0}, {"l4_occ": 7}, {"l4_occ": 8}, {"l4_descv": 1}, {"l4_descv": 2, "l4_iters": 2},
                  {"l4_descv": 2, "l4_iters": 3, "l4_occ": 0}, {"l4_descv": 2, "l4_iters": 8, "l4_ppw": 2},
                  {"l4_small": 0}, {"l4_small": 1}, {"l4_small": 2}, {"l4_small": 3}, {"l4_small": 4},
-                 {"l4_small": 1, "l4_nt": 0}, {"l4_small": 5}, {"l4_small": 5, "l4_nt": 0}]
+                 {"l4_small": 1, "l4_nt": 0}, {"l4_small": 5}, {"l4_small": 5, "l4_nt": 0},
+                 {"l4_coop": 1 << 20, "l4_coop_waves": 2}, {"l4_coop": 1 << 20, "l4_coop_waves": 4, "l4_unroll": 4},
+                 {"l4_coop": 1 << 20, "l4_coop_waves": 8, "l4_nt": 0}, {"l4_coop": 1 << 20, "l4_coop_waves": 16}]
 
 
 @pytest.mark.parametrize("knobs", DESC_VARIANTS, ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()))
@@ -127,7 +129,7 @@ def test_desc_random(gpu, knobs):
 
     wga = _wga()
     saved = {k: wga.tune_get(k) for k in ("l4_occ", "l4_descv", "l4_iters", "l4_ppw", "l4_blocks", "l4_small",
-                                          "l4_nt")}
+                                          "l4_nt", "l4_coop", "l4_coop_waves", "l4_unroll")}
     for k, v in knobs.items():
         wga.tune_set(k, v)
     rng = np.random.default_rng(1234)
@@ -335,13 +337,19 @@ def test_results_deterministic_across_launches(gpu):
     assert torch.equal(a, b)
 
 
-def test_long_packets(gpu):
+@pytest.mark.parametrize("coop", [0, 2, 4, 8, 16])
+def test_long_packets(gpu, coop):
     """Packets past the issue phase's 2 KiB (the finish phase's long-packet
     loop), up to the 64 KiB maximum IP packet, at odd offsets, through the
-    descriptor, verify and uniform entry points."""
+    descriptor, verify and uniform entry points; coop > 0: the
+    block-per-descriptor kernel with that many waves per packet."""
     import torch
 
     wga = _wga()
+    saved = {k: wga.tune_get(k) for k in ("l4_coop", "l4_coop_waves")}
+    wga.tune_set("l4_coop", 1 << 20 if coop else 0)
+    if coop:
+        wga.tune_set("l4_coop_waves", coop)
     rng = np.random.default_rng(65535)
     n = 600
     lens = rng.integers(2000, 65536, n)
@@ -353,9 +361,16 @@ def test_long_packets(gpu):
     d["csum_start"] = rng.choice([20, 21, 40, 41, 1000], n)
     d["flags"] = rng.integers(0, 4, n)
     back, view = to_dev(buf, gpu, 3)
-    out = wga.calc_l4_checksum_desc(view, desc_dev(d, gpu))
+    dd = desc_dev(d, gpu)
+    out = wga.calc_l4_checksum_desc(view, dd)
+    plain = wga.checksum_desc(view, dd)
     torch.cuda.synchronize()
+    for k, v in saved.items():
+        wga.tune_set(k, v)
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.l4_desc(buf, d))
+    np.testing.assert_array_equal(plain.cpu().numpy(), oracle.checksum_desc(buf, d))
+    if coop:
+        return
     seg = 65535
     total = seg * 5 - 777
     u = rng.integers(0, 256, total, dtype=np.uint8)

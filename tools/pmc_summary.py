@@ -32,7 +32,7 @@ def main():
     if "--workload" in args:
         workload = args[args.index("--workload") + 1]
     res = {"workload": workload, "bench_args": args}
-    for kern in ("l4csum_kernel", "l4csum_split_kernel", "gso_split_kernel", "verify_kernel", "gro_finalize",
+    for kern in ("l4csum_kernel", "l4csum_split_kernel", "l4csum_coop_kernel", "gso_split_kernel", "verify_kernel", "gro_finalize",
                  "aead_kernel"):
         f = per_dispatch(str(out / "pmc_FETCH_SIZE" / "**" / "*counter_collection.csv"), kern)
         w = per_dispatch(str(out / "pmc_WRITE_SIZE" / "**" / "*counter_collection.csv"), kern)
@@ -49,7 +49,7 @@ def main():
             "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024,
         }
     main_k = {"config3": "gso_split_kernel", "config3udp": "gso_split_kernel", "verify": "verify_kernel",
-              "gro": "gro_finalize", "config1": "l4csum_split_kernel", "config4": "l4csum_split_kernel",
+              "gro": "gro_finalize", "config1": "l4csum_coop_kernel", "config4": "l4csum_split_kernel",
               "config5": "l4csum_split_kernel", "aead": "aead_kernel"}.get(workload, "l4csum_kernel")
     if main_k in res:
         res["hbm_bytes_per_launch"] = res[main_k]["hbm_bytes_per_launch"]

@@ -7,18 +7,21 @@
 //          (worker/encap.cpp:136-141; counter = encrypt_nonce++ per call);
 //   decap: every message of a UDP GRO batch (worker/decap_ref.cpp:78-86).
 //
-// Layout: a group of G lanes (G = 32: two packets per wave; G = 64: one,
-// in passes of 63 blocks for packets past 4 KiB) per packet.  Group lane 0
-// computes ChaCha20 block 0 (the Poly1305 key), writes the DataHeader and
-// handles the length block; lane g >= 1 computes keystream block g (counter
-// g) for the 64 bytes [64(g-1), 64g) of the padded payload, XORs and stores
-// them.  Poly1305 runs in the lanes too: lane g Horner-evaluates its (up to)
-// four 16-B ciphertext blocks with r, multiplies the result by r^(blocks
-// after it) — a suffix product of r^(n_j) over the later lanes, log2(G)
-// cross-lane steps — and the group sums the
-// products (normalised 26-bit limbs, so 32 of them fit a dword) before one
-// multiplication by r (the length block comes last), the reduction mod
-// 2^130 - 5 and + s.  ChaCha20 and Poly1305 are integer-VALU work (~1,000
+// Layout: a group of G lanes per packet (the smallest power of two that holds
+// its blocks; G = 64 in passes for packets past 64 K blocks), K consecutive
+// ChaCha20 blocks per lane (knob aead_k, default 4): block counter c is lane
+// c / K's.  Counter 0 (group lane 0's first block) is the Poly1305 key; the
+// lane writing it also writes the DataHeader and handles the length block;
+// counter c >= 1 is the keystream for the 64 bytes [64(c-1), 64c) of the
+// padded payload, XORed and stored.  Poly1305 runs in the lanes too: each
+// lane Horner-evaluates its (up to) 4K 16-B ciphertext blocks with r,
+// multiplies the result by r^(blocks after it) — a suffix product of
+// r^(n_j) over the later lanes, log2(G) cross-lane steps — and the group sums
+// the products (normalised 26-bit limbs, so 32 of them fit a dword) before
+// one multiplication by r (the length block comes last), the reduction mod
+// 2^130 - 5 and + s.  The per-lane fixed costs (powers of r, the scan, the
+// term) are paid once per K blocks, so larger K means fewer multiplications
+// per byte: K = 4 puts a 1,500-B packet in 8 lanes (8 per wave).  ChaCha20 and Poly1305 are integer-VALU work (~1,000
 // and ~700 instructions per 64-B block lane), so this kernel is bound by
 // VALU issue, not HBM.
 #include <hip/hip_runtime.h>
@@ -309,9 +312,13 @@ constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/prot
 // message at out + i*stride, stride = 16 + pad16(seg) + 16.
 // kDec = true: decrypt message i (bytes [i*seg, +len) of `in`) into
 // out + i*(seg - 32); status[i] = 0 / -1.
-template <int G, bool kDec>
+// G lanes per packet, K consecutive ChaCha20 blocks per lane: a pass covers
+// counters [pass*G*K, +G*K), lane g the K from pass*G*K + g*K; counter 0 is
+// the Poly1305 key block, counter c >= 1 the payload's 64-B block c - 1.
+template <int G, int K, bool kDec>
 __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     constexpr uint32_t kPer = 64u / G;  // packets per wave
+    constexpr uint32_t kPass = (uint32_t)(G * K);  // counters per pass
     const uint32_t lane = lane_id();
     const uint32_t g = lane & (G - 1u);
     const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
@@ -354,10 +361,10 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     const uint32_t n0 = 0, n1 = (uint32_t)counter, n2 = (uint32_t)(counter >> 32);  // nonce: 0^4 || le64(counter)
     const bool act = live && st == 0;
 
-    // One keystream block per lane for pass 0: counter g — group lane 0's is
-    // block 0, the Poly1305 key; lane g >= 1's is data block g - 1.
+    // Each lane's first block of pass 0 (counter g*K) up front: group lane
+    // 0's is block 0, the Poly1305 key (r, s), which every lane needs first.
     uint32_t ks[16];
-    chacha20_block(p.key, g, n0, n1, n2, ks);
+    chacha20_block(p.key, g * (uint32_t)K, n0, n1, n2, ks);
     const uint32_t base_lane = lane & ~(G - 1u);
     uint32_t rw[4], sw[4];
 #pragma unroll
@@ -372,61 +379,79 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     rw[3] &= 0x0ffffffcu;
     const L5 r = l5_from_words(rw[0], rw[1], rw[2], rw[3], 0u);
     const L5 r2 = l5_mul(r, r), r3 = l5_mul(r2, r), r4 = l5_mul(r2, r2);
+    // r^(4a), a = 1..K, for a lane's weight r^(its 16-B blocks)
+    L5 r4a[K];
+    r4a[0] = r4;
+    if constexpr (K >= 2)
+        r4a[1] = l5_mul(r4, r4);
+    if constexpr (K == 4) {
+        r4a[2] = l5_mul(r4a[1], r4);
+        r4a[3] = l5_mul(r4a[1], r4a[1]);
+    }
 
-    // Data blocks: lane g >= 1 takes block g - 1 + 63 * pass (G = 64) or g - 1
-    // (G = 32).  Passes run last to first, F carrying r^(blocks after the pass).
-    const uint32_t nblk = (pad + 63u) / 64u;
-    const uint32_t lanes_per_pass = G - 1u;
-    const uint32_t npass = G == 64 ? (nblk + lanes_per_pass - 1u) / lanes_per_pass : 1u;
-    // wave-uniform pass count (G = 64: one packet per wave)
+    const uint32_t nblk = (pad + 63u) / 64u;  // payload blocks: counters 1 .. nblk
+    const uint32_t npass = G == 64 ? (nblk + kPass) / kPass : 1u;  // (nblk + 1) counters
+    // wave-uniform pass count (G = 64: one packet per wave); passes run last
+    // to first, F carrying r^(16-B blocks after the pass)
     const uint32_t passes = G == 64 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)npass) : 1u;
     L5 F = l5_one();
     L5 acc = l5_zero();
-    uint32_t P[16];  // decrypt: the plaintext of pass 0 (processed last)
-    bool tag_ok = true;
-    uint32_t tagw[4] = {0, 0, 0, 0};
     for (uint32_t pp = passes; pp-- > 0;) {
-        const uint32_t d = g >= 1u ? pp * lanes_per_pass + (g - 1u) : 0xffffffffu;  // data block of this lane
-        const bool has = act && g >= 1u && d < nblk;
-        const uint32_t boff = has ? 64u * d : 0u;
-        const uint32_t nin = has ? (plen - boff < 64u ? plen - boff : 64u) : 0u;  // payload bytes in the block
-        const uint32_t nct = has ? (pad - boff < 64u ? pad - boff : 64u) : 0u;    // Poly1305 bytes in the block
-        uint32_t W[16];
-        load64(src + boff, nin, W);  // plaintext (encrypt) / ciphertext (decrypt), zero past the payload
-        uint32_t kb[16];
-        if (pp == 0) {  // pass 0's blocks were computed with the key block
-#pragma unroll
-            for (int m = 0; m < 16; m++) kb[m] = ks[m];
-        } else {
-            chacha20_block(p.key, d + 1u, n0, n1, n2, kb);
-        }
-        uint32_t C[16];  // ciphertext words, zero past the ciphertext (what Poly1305 sees)
-#pragma unroll
-        for (int m = 0; m < 16; m++) {
-            if constexpr (!kDec) {
-                // padding plaintext bytes are zero (proto.cpp:568-572): their
-                // ciphertext is the keystream itself
-                C[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nct);
-            } else {
-                C[m] = W[m];
-                P[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nin);  // plaintext of pass 0 kept (last processed)
-            }
-        }
-        if (!kDec && has)
-            store_n(dst + 16 + boff, C, nct);
-        // Horner over this lane's 16-B blocks
-        const uint32_t nq = nct / 16u;
         L5 x = l5_zero();
+        uint32_t nq = 0;  // 16-B blocks absorbed by this lane in this pass
+#pragma unroll 1
+        for (uint32_t j = 0; j < (uint32_t)K; j++) {
+            const uint32_t c = pp * kPass + g * (uint32_t)K + j;  // block counter
+            const uint32_t d = c - 1u;                              // payload block
+            const bool has = act && c >= 1u && d < nblk;
+            const uint32_t boff = has ? 64u * d : 0u;
+            const uint32_t nin = has ? (plen - boff < 64u ? plen - boff : 64u) : 0u;  // payload bytes in the block
+            const uint32_t nct = has ? (pad - boff < 64u ? pad - boff : 64u) : 0u;    // Poly1305 bytes in the block
+            uint32_t W[16];
+            load64(src + boff, nin, W);  // plaintext (encrypt) / ciphertext (decrypt), zero past the payload
+            uint32_t kb[16];
+            if (pp == 0 && j == 0) {
 #pragma unroll
-        for (uint32_t q = 0; q < 4; q++) {
-            const L5 blk = l5_from_words(C[4 * q], C[4 * q + 1], C[4 * q + 2], C[4 * q + 3], 1u);
-            const L5 t = l5_mul(l5_add(x, blk), r);
-            if (q < nq)
-                x = t;
+                for (int m = 0; m < 16; m++) kb[m] = ks[m];
+            } else {
+                chacha20_block(p.key, c, n0, n1, n2, kb);
+            }
+            uint32_t C[16];  // ciphertext words, zero past the ciphertext (what Poly1305 sees)
+#pragma unroll
+            for (int m = 0; m < 16; m++) {
+                if constexpr (!kDec) {
+                    // padding plaintext bytes are zero (proto.cpp:568-572):
+                    // their ciphertext is the keystream itself
+                    C[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nct);
+                } else {
+                    C[m] = W[m];
+                    kb[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nin);  // plaintext
+                }
+            }
+            // decrypt stores the plaintext now; a bad tag zeroes it below
+            // (the final bytes are libsodium's either way)
+            if (has)
+                store_n(kDec ? dst + boff : dst + 16 + boff, kDec ? kb : C, kDec ? nin : nct);
+            // Horner over the block's 16-B blocks, continuing the lane's chain
+            const uint32_t nqj = nct / 16u;
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                const L5 blk = l5_from_words(C[4 * q], C[4 * q + 1], C[4 * q + 2], C[4 * q + 3], 1u);
+                const L5 t = l5_mul(l5_add(x, blk), r);
+                if (q < nqj)
+                    x = t;
+            }
+            nq += nqj;
         }
-        // Q = r^nq; suffix product over the pass's later lanes
-        L5 Q = nq == 4 ? r4 : nq == 3 ? r3 : nq == 2 ? r2 : nq == 1 ? r : l5_one();
-        L5 S = Q;
+        // Q = r^nq = r^(4a) * r^b; suffix product over the pass's later lanes
+        const uint32_t a4 = nq >> 2, b = nq & 3u;
+        L5 QA = l5_one();
+#pragma unroll
+        for (int k = 0; k < K; k++)
+            if (a4 == (uint32_t)k + 1u)
+                QA = r4a[k];
+        const L5 QB = b == 3u ? r3 : b == 2u ? r2 : b == 1u ? r : l5_one();
+        L5 S = b == 0u ? QA : (a4 == 0u ? QB : l5_mul(QA, QB));
 #pragma unroll
         for (uint32_t o = 1; o < (uint32_t)G; o <<= 1) {
             const L5 t = l5_down<G>(S, lane, o);
@@ -441,7 +466,7 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
         // everything) is applied once to the group's sum
         const L5 EF = passes > 1 ? l5_mul(E, F) : E;  // F == 1 with one pass (wave-uniform test)
         const L5 term = l5_mul(x, EF);
-        if (has)
+        if (nq)
             acc = l5_add(acc, term);
         if (passes > 1 && pp > 0) {
             // F *= product of the whole pass (group lane 0 holds S over lanes >= 0)
@@ -459,6 +484,7 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
         acc = l5_add(acc, lenblk);
     // group sum, times r (every term's last factor), every lane finishes
     const L5 tot = l5_mul(l5_norm(l5_grp_sum<G>(l5_norm(acc), lane)), r);
+    uint32_t tagw[4];
     poly_finish(tot, sw, tagw);
     if constexpr (!kDec) {
         if (g == 0u && live) {
@@ -470,9 +496,9 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                 p.status[ii] = st;
         }
     } else {
-        // tag check (crypto_verify_16), then plaintext or zeros (libsodium
-        // zeroes the message on a bad tag); rejected-before-MAC messages are
-        // left untouched
+        // tag check (crypto_verify_16); on a mismatch libsodium zeroes the
+        // message: overwrite this lane's plaintext blocks.  Messages rejected
+        // before the MAC wrote nothing and stay untouched.
         const uintptr_t tsrc = src + plen;
         uint32_t got[4] = {0, 0, 0, 0};
         if (act) {
@@ -482,30 +508,19 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                          (ld8(tsrc + 4 * k + 3) << 24);
         }
         const uint32_t diff = (got[0] ^ tagw[0]) | (got[1] ^ tagw[1]) | (got[2] ^ tagw[2]) | (got[3] ^ tagw[3]);
-        tag_ok = diff == 0;
-        // decrypt pass 2: regenerate each block's plaintext and store it
-        for (uint32_t pp = 0; pp < passes; pp++) {
-            const uint32_t d = g >= 1u ? pp * lanes_per_pass + (g - 1u) : 0xffffffffu;
-            const bool has = act && g >= 1u && d < nblk;
-            const uint32_t boff = has ? 64u * d : 0u;
-            const uint32_t nin = has ? (plen - boff < 64u ? plen - boff : 64u) : 0u;
-            uint32_t O[16];
-            if (pp == 0) {
-#pragma unroll
-                for (int m = 0; m < 16; m++) O[m] = P[m];
-            } else {  // G = 64 packets past 4 KiB: regenerate the earlier passes' blocks
-                uint32_t W[16], kb[16];
-                load64(src + boff, nin, W);
-                chacha20_block(p.key, d + 1u, n0, n1, n2, kb);
-#pragma unroll
-                for (int m = 0; m < 16; m++) O[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nin);
+        const bool tag_ok = diff == 0;
+        if (act && !tag_ok) {
+            const uint32_t Z[16] = {};
+            for (uint32_t pp = 0; pp < passes; pp++) {
+                for (uint32_t j = 0; j < (uint32_t)K; j++) {
+                    const uint32_t c = pp * kPass + g * (uint32_t)K + j;
+                    const uint32_t d = c - 1u;
+                    if (c >= 1u && d < nblk) {
+                        const uint32_t boff = 64u * d;
+                        store_n(dst + boff, Z, plen - boff < 64u ? plen - boff : 64u);
+                    }
+                }
             }
-            if (!tag_ok) {
-#pragma unroll
-                for (int m = 0; m < 16; m++) O[m] = 0u;
-            }
-            if (has)
-                store_n(dst + boff, O, nin);
         }
         if (g == 0u && live)
             p.status[ii] = (int8_t)(st ? st : (tag_ok ? 0 : -1));
@@ -524,21 +539,46 @@ static AeadKey key_words(const uint8_t key[32]) {
     return k;
 }
 
+template <int G, int K, bool kDec>
+static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
+    hipLaunchKernelGGL((aead_kernel<G, K, kDec>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+}
+
+template <int K, bool kDec>
+static void launch_k(const AeadParams &p, uint32_t G, uint64_t blocks, hipStream_t st) {
+    switch (G) {
+    case 1: launch_gk<1, K, kDec>(p, blocks, st); break;
+    case 2: launch_gk<2, K, kDec>(p, blocks, st); break;
+    case 4: launch_gk<4, K, kDec>(p, blocks, st); break;
+    case 8: launch_gk<8, K, kDec>(p, blocks, st); break;
+    case 16: launch_gk<16, K, kDec>(p, blocks, st); break;
+    case 32: launch_gk<32, K, kDec>(p, blocks, st); break;
+    default: launch_gk<64, K, kDec>(p, blocks, st); break;
+    }
+}
+
 template <bool kDec>
 static int launch_aead(AeadParams &p, uint32_t maxpay, hipStream_t st) {
-    // groups of 32 lanes while a packet's blocks (+ the key block) fit
+    // counters per packet: the key block + the padded payload's 64-B blocks;
+    // K (knob aead_k) consecutive blocks per lane, the smallest power-of-two
+    // group holding them (G = 64 and several passes past 64 K blocks)
     const uint32_t nblk = (((maxpay + 15u) & ~15u) + 63u) / 64u;
-    const bool g32 = nblk + 1u <= 32u;
-    const uint64_t per_block = g32 ? 8u : 4u;  // packets per 256-thread block
+    const uint32_t K = tune().aead_k;
+    const uint32_t lanes = (nblk + 1u + K - 1u) / K;
+    uint32_t G = 1;
+    while (G < lanes && G < 64u) G <<= 1;
+    const uint64_t per_block = 4u * (64u / G);  // packets per 256-thread block
     uint64_t blocks = (p.n + per_block - 1) / per_block;
     if (blocks >= 8)
         blocks = (blocks + 7) & ~7ull;  // XCD swizzle bijective; surplus waves have no live packet
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
-    if (g32)
-        hipLaunchKernelGGL((aead_kernel<32, kDec>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+    if (K == 1)
+        launch_k<1, kDec>(p, G, blocks, st);
+    else if (K == 2)
+        launch_k<2, kDec>(p, G, blocks, st);
     else
-        hipLaunchKernelGGL((aead_kernel<64, kDec>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+        launch_k<4, kDec>(p, G, blocks, st);
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }
 

@@ -30,7 +30,7 @@ struct Knob {
 
 static const uint64_t kPpw[] = {1, 2, 4, 8}, kOcc[] = {0, 7, 8}, kVOcc[] = {0, 6, 8}, kDm[] = {0, 2},
                       kWaves[] = {1, 2, 4, 8}, kAbl[] = {0, 1, 32},
-                      kUnroll[] = {4, 8};
+                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {1, 2, 4};
 #define WG_N(a) (sizeof(a) / sizeof(a[0]))
 static const Knob kKnobs[] = {
     {"l4_blocks", &Tune::l4_blocks, nullptr, 1, 1u << 20, nullptr, 0},
@@ -56,6 +56,9 @@ static const Knob kKnobs[] = {
     {"gso_ablate", nullptr, &Tune::gso_ablate, 0, 0, kAbl, WG_N(kAbl)},
     {"host_chunk_mb", nullptr, &Tune::host_chunk_mb, 1, 4096, nullptr, 0},
     {"l4_unroll", nullptr, &Tune::l4_unroll, 0, 0, kUnroll, WG_N(kUnroll)},
+    {"l4_coop", &Tune::l4_coop, nullptr, 0, 1u << 20, nullptr, 0},
+    {"l4_coop_waves", nullptr, &Tune::l4_coop_waves, 0, 0, kCoopW, WG_N(kCoopW)},
+    {"aead_k", nullptr, &Tune::aead_k, 0, 0, kAeadK, WG_N(kAeadK)},
 };
 #undef WG_N
 
@@ -136,6 +139,15 @@ static Tune &tune_storage() {
         // buffers) -26 %, config 5 (no long packets) unchanged
         // (profiles/r02_unroll_ab.json)
         x.l4_unroll = 8;
+        // descriptor batches of <= 16,384 packets: a 4-wave block per packet.
+        // The split kernel's grid is sized by descriptor count (n / 16
+        // waves), so few long packets starve the HBM pipe: 16,384 x 64 KiB
+        // 0.178 -> 0.159 ms, 1,024 x 64 KiB 0.146 -> 0.014 ms; at 16,384
+        // packets of 64 / 1,500 / 9,000 B within +1.3 us, past 16 K packets
+        // of 1,500 B the split kernel wins 2x (profiles/r02_coop_probe.json)
+        x.l4_coop = 16384;
+        x.l4_coop_waves = 4;
+        x.aead_k = 4;
         // environment overrides: WG_<KNOB> (upper case), same accepted values
         // as wg_tune_set; anything else is ignored
         for (const Knob &k : kKnobs) {

@@ -32,6 +32,9 @@ struct Tune {
     uint32_t gro_chunks;  // 16-B chunks staged per flow by the LDS variant (4, 5)
     uint32_t host_chunk_mb;  // host-memory pipeline chunk size, MiB
     uint32_t l4_unroll;   // split kernel: loads in flight per lane on a long packet's rest (4, 8)
+    uint64_t l4_coop;     // descriptor batches of n <= l4_coop: a block of l4_coop_waves waves per packet (0: never)
+    uint32_t l4_coop_waves;  // waves per packet in that mode (2, 4, 8, 16)
+    uint32_t aead_k;      // AEAD: consecutive ChaCha20 blocks per lane (1, 2, 4)
     uint32_t gso_ablate;  // GSO A/B variants (1 non-temporal stores, 32 no XCD swizzle; both correct)
 };
 
