@@ -9,7 +9,7 @@
 //
 // Layout: a group of G lanes per packet (the smallest power of two that holds
 // its blocks; G = 64 in passes for packets past 64 K blocks), K consecutive
-// ChaCha20 blocks per lane (knob aead_k, default 4): block counter c is lane
+// ChaCha20 blocks per lane (knob aead_k, default 2): block counter c is lane
 // c / K's.  Counter 0 (group lane 0's first block) is the Poly1305 key; the
 // lane writing it also writes the DataHeader and handles the length block;
 // counter c >= 1 is the keystream for the 64 bytes [64(c-1), 64c) of the
@@ -21,7 +21,8 @@
 // one multiplication by r (the length block comes last), the reduction mod
 // 2^130 - 5 and + s.  The per-lane fixed costs (powers of r, the scan, the
 // term) are paid once per K blocks, so larger K means fewer multiplications
-// per byte: K = 4 puts a 1,500-B packet in 8 lanes (8 per wave).  ChaCha20 and Poly1305 are integer-VALU work (~1,000
+// per byte, against registers: K = 2 puts a 1,500-B packet in 16 lanes
+// (4 per wave); K = 4 (8 lanes) needs 99 VGPRs and measured 4 % slower.  ChaCha20 and Poly1305 are integer-VALU work (~1,000
 // and ~700 instructions per 64-B block lane), so this kernel is bound by
 // VALU issue, not HBM.
 #include <hip/hip_runtime.h>
@@ -102,6 +103,13 @@ __device__ __forceinline__ L5 l5_from_words(uint32_t w0, uint32_t w1, uint32_t w
     a.v[3] = ((w2 >> 14) | (w3 << 18)) & 0x3ffffffu;
     a.v[4] = (w3 >> 8) | (hibit << 24);
     return a;
+}
+
+__device__ __forceinline__ L5 l5_sel(bool c, const L5 &a, const L5 &b) {
+    L5 o;
+#pragma unroll
+    for (int i = 0; i < 5; i++) o.v[i] = c ? a.v[i] : b.v[i];
+    return o;
 }
 
 __device__ __forceinline__ L5 l5_add(const L5 &a, const L5 &b) {
@@ -241,8 +249,10 @@ __device__ __forceinline__ void poly_finish(L5 h, const uint32_t s[4], uint32_t 
 static __device__ v4u g_aead_zero16;
 
 __device__ __forceinline__ uint32_t keep_below(uint32_t w, uint32_t m, uint32_t lim) {
-    const int k = (int)lim - 4 * (int)m;  // bytes of dword m below lim
-    return k >= 4 ? w : (k <= 0 ? 0u : (w & ((1u << (8 * k)) - 1u)));
+    // bytes of dword m below lim, clamped to 0..4; the mask by a 64-bit
+    // shift so 4 bytes need no special case (branch-free)
+    const uint32_t k = lim > 4u * m ? (lim - 4u * m < 4u ? lim - 4u * m : 4u) : 0u;
+    return w & (uint32_t)((1ull << (8u * k)) - 1ull);
 }
 
 // The 64 bytes at a (of which the first `n` belong to the packet, n may be
@@ -253,21 +263,52 @@ __device__ __forceinline__ void load64(uintptr_t a, uint32_t n, uint32_t W[16]) 
     const uintptr_t a0 = a & ~(uintptr_t)15;
     const uintptr_t alast = n ? (a + n - 1) & ~(uintptr_t)15 : a0;
     const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_aead_zero16);
-    v4u c[5];
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-        const uintptr_t ca = a0 + 16u * k;
-        c[k] = ld16(n ? (ca > alast ? alast : ca) : zero);
-    }
-    const uint32_t Wd[20] = {c[0][0], c[0][1], c[0][2], c[0][3], c[1][0], c[1][1], c[1][2], c[1][3], c[2][0], c[2][1],
-                             c[2][2], c[2][3], c[3][0], c[3][1], c[3][2], c[3][3], c[4][0], c[4][1], c[4][2], c[4][3]};
-    const uint32_t s = (uint32_t)(a & 15u), q = s >> 2, sh = s & 3u;
-#pragma unroll
-    for (uint32_t m = 0; m < 16; m++) {
-        const uint32_t lo = q == 0 ? Wd[m] : q == 1 ? Wd[m + 1] : q == 2 ? Wd[m + 2] : Wd[m + 3];
-        const uint32_t hi = q == 0 ? Wd[m + 1] : q == 1 ? Wd[m + 2] : q == 2 ? Wd[m + 3] : Wd[m + 4];
-        W[m] = keep_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, n);
-    }
+    const v4u c0 = ld16(n ? (a0 + 0u > alast ? alast : a0 + 0u) : zero);
+    const v4u c1 = ld16(n ? (a0 + 16u > alast ? alast : a0 + 16u) : zero);
+    const v4u c2 = ld16(n ? (a0 + 32u > alast ? alast : a0 + 32u) : zero);
+    const v4u c3 = ld16(n ? (a0 + 48u > alast ? alast : a0 + 48u) : zero);
+    const v4u c4 = ld16(n ? (a0 + 64u > alast ? alast : a0 + 64u) : zero);
+    // dword m of the result funnels dwords m + q and m + q + 1 of the chunks,
+    // q = (a / 4) mod 4 per lane: chosen by q's two bits over NAMED values
+    // (selects between elements of an array became a scratch array indexed
+    // at run time; a select chain on q became exec-mask branches per dword)
+    const uint32_t sh = (uint32_t)a & 3u;
+    const bool q1 = a & 4u, q2 = a & 8u;
+    const uint32_t t0 = q1 ? c0[1] : c0[0];
+    const uint32_t t1 = q1 ? c0[2] : c0[1];
+    const uint32_t t2 = q1 ? c0[3] : c0[2];
+    const uint32_t t3 = q1 ? c1[0] : c0[3];
+    const uint32_t t4 = q1 ? c1[1] : c1[0];
+    const uint32_t t5 = q1 ? c1[2] : c1[1];
+    const uint32_t t6 = q1 ? c1[3] : c1[2];
+    const uint32_t t7 = q1 ? c2[0] : c1[3];
+    const uint32_t t8 = q1 ? c2[1] : c2[0];
+    const uint32_t t9 = q1 ? c2[2] : c2[1];
+    const uint32_t t10 = q1 ? c2[3] : c2[2];
+    const uint32_t t11 = q1 ? c3[0] : c2[3];
+    const uint32_t t12 = q1 ? c3[1] : c3[0];
+    const uint32_t t13 = q1 ? c3[2] : c3[1];
+    const uint32_t t14 = q1 ? c3[3] : c3[2];
+    const uint32_t t15 = q1 ? c4[0] : c3[3];
+    const uint32_t t16 = q1 ? c4[1] : c4[0];
+    const uint32_t t17 = q1 ? c4[2] : c4[1];
+    const uint32_t t18 = q1 ? c4[3] : c4[2];
+    W[0] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t3 : t1, q2 ? t2 : t0, sh), 0u, n);
+    W[1] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t4 : t2, q2 ? t3 : t1, sh), 1u, n);
+    W[2] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t5 : t3, q2 ? t4 : t2, sh), 2u, n);
+    W[3] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t6 : t4, q2 ? t5 : t3, sh), 3u, n);
+    W[4] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t7 : t5, q2 ? t6 : t4, sh), 4u, n);
+    W[5] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t8 : t6, q2 ? t7 : t5, sh), 5u, n);
+    W[6] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t9 : t7, q2 ? t8 : t6, sh), 6u, n);
+    W[7] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t10 : t8, q2 ? t9 : t7, sh), 7u, n);
+    W[8] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t11 : t9, q2 ? t10 : t8, sh), 8u, n);
+    W[9] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t12 : t10, q2 ? t11 : t9, sh), 9u, n);
+    W[10] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t13 : t11, q2 ? t12 : t10, sh), 10u, n);
+    W[11] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t14 : t12, q2 ? t13 : t11, sh), 11u, n);
+    W[12] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t15 : t13, q2 ? t14 : t12, sh), 12u, n);
+    W[13] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t16 : t14, q2 ? t15 : t13, sh), 13u, n);
+    W[14] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t17 : t15, q2 ? t16 : t14, sh), 14u, n);
+    W[15] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t18 : t16, q2 ? t17 : t15, sh), 15u, n);
 }
 
 __device__ __forceinline__ void st16(uintptr_t addr, v4u v) {
@@ -286,7 +327,12 @@ __device__ __forceinline__ void store_n(uintptr_t a, const uint32_t W[16], uint3
         if (b0 + 16u <= n) {
             st16(a + b0, v4u{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]});
         } else if (b0 < n) {
-            for (uint32_t j = b0; j < n; j++) st8b(a + j, W[j >> 2] >> (8u * (j & 3u)));
+            // the partial chunk byte by byte, static register indices (a
+            // run-time index would put W in scratch)
+#pragma unroll
+            for (uint32_t j = 0; j < 15; j++)
+                if (b0 + j < n)
+                    st8b(a + b0 + j, W[4 * q + (j >> 2)] >> (8u * (j & 3u)));
         }
     }
 }
@@ -378,16 +424,6 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     rw[2] &= 0x0ffffffcu;
     rw[3] &= 0x0ffffffcu;
     const L5 r = l5_from_words(rw[0], rw[1], rw[2], rw[3], 0u);
-    const L5 r2 = l5_mul(r, r), r3 = l5_mul(r2, r), r4 = l5_mul(r2, r2);
-    // r^(4a), a = 1..K, for a lane's weight r^(its 16-B blocks)
-    L5 r4a[K];
-    r4a[0] = r4;
-    if constexpr (K >= 2)
-        r4a[1] = l5_mul(r4, r4);
-    if constexpr (K == 4) {
-        r4a[2] = l5_mul(r4a[1], r4);
-        r4a[3] = l5_mul(r4a[1], r4a[1]);
-    }
 
     const uint32_t nblk = (pad + 63u) / 64u;  // payload blocks: counters 1 .. nblk
     const uint32_t npass = G == 64 ? (nblk + kPass) / kPass : 1u;  // (nblk + 1) counters
@@ -397,77 +433,49 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     L5 F = l5_one();
     L5 acc = l5_zero();
     for (uint32_t pp = passes; pp-- > 0;) {
-        L5 x = l5_zero();
-        uint32_t nq = 0;  // 16-B blocks absorbed by this lane in this pass
-#pragma unroll 1
-        for (uint32_t j = 0; j < (uint32_t)K; j++) {
-            const uint32_t c = pp * kPass + g * (uint32_t)K + j;  // block counter
-            const uint32_t d = c - 1u;                              // payload block
-            const bool has = act && c >= 1u && d < nblk;
-            const uint32_t boff = has ? 64u * d : 0u;
-            const uint32_t nin = has ? (plen - boff < 64u ? plen - boff : 64u) : 0u;  // payload bytes in the block
-            const uint32_t nct = has ? (pad - boff < 64u ? pad - boff : 64u) : 0u;    // Poly1305 bytes in the block
-            uint32_t W[16];
-            load64(src + boff, nin, W);  // plaintext (encrypt) / ciphertext (decrypt), zero past the payload
-            uint32_t kb[16];
-            if (pp == 0 && j == 0) {
-#pragma unroll
-                for (int m = 0; m < 16; m++) kb[m] = ks[m];
-            } else {
-                chacha20_block(p.key, c, n0, n1, n2, kb);
-            }
-            uint32_t C[16];  // ciphertext words, zero past the ciphertext (what Poly1305 sees)
-#pragma unroll
-            for (int m = 0; m < 16; m++) {
-                if constexpr (!kDec) {
-                    // padding plaintext bytes are zero (proto.cpp:568-572):
-                    // their ciphertext is the keystream itself
-                    C[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nct);
-                } else {
-                    C[m] = W[m];
-                    kb[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nin);  // plaintext
+        const uint32_t cf = pp * kPass + g * (uint32_t)K;  // this lane's first counter
+        // This lane's 16-B Poly1305 blocks in the pass follow from the
+        // geometry alone: payload blocks [lo, hi) (counter c is block c - 1)
+        // cut at pad.  So its weight r^nq and the suffix product over the
+        // later lanes are computed here, before the block loop, and the
+        // powers of r are dead by the time the keystream needs registers.
+        uint32_t nq = 0;
+        if (act) {
+            const uint32_t lo = cf ? cf - 1u : 0u;
+            const uint32_t hi = cf + K - 1u < nblk ? cf + K - 1u : nblk;
+            nq = hi > lo ? ((64u * hi < pad ? 64u * hi : pad) - 64u * lo) / 16u : 0u;
+        }
+        L5 S;
+        {
+            // r^nq = r^(4a) r^b from r, r^2 and r^4, r^8 (K >= 2), r^12, r^16
+            // (K = 4); limb-wise selects (a select between whole L5 values
+            // became a scratch array indexed at run time)
+            const L5 r2 = l5_mul(r, r);
+            const uint32_t a4 = nq >> 2, b = nq & 3u;
+            const L5 r4 = l5_mul(r2, r2);
+            L5 QA = l5_sel(a4 == 1u, r4, l5_one());
+            if constexpr (K >= 2) {
+                const L5 r8 = l5_mul(r4, r4);
+                QA = l5_sel(a4 == 2u, r8, QA);
+                if constexpr (K == 4) {
+                    const L5 r12 = l5_mul(r8, r4), r16 = l5_mul(r8, r8);
+                    QA = l5_sel(a4 == 3u, r12, l5_sel(a4 == 4u, r16, QA));
                 }
             }
-            // decrypt stores the plaintext now; a bad tag zeroes it below
-            // (the final bytes are libsodium's either way)
-            if (has)
-                store_n(kDec ? dst + boff : dst + 16 + boff, kDec ? kb : C, kDec ? nin : nct);
-            // Horner over the block's 16-B blocks, continuing the lane's chain
-            const uint32_t nqj = nct / 16u;
-#pragma unroll
-            for (uint32_t q = 0; q < 4; q++) {
-                const L5 blk = l5_from_words(C[4 * q], C[4 * q + 1], C[4 * q + 2], C[4 * q + 3], 1u);
-                const L5 t = l5_mul(l5_add(x, blk), r);
-                if (q < nqj)
-                    x = t;
-            }
-            nq += nqj;
+            const L5 rb = l5_sel(b >= 2u, r2, l5_sel(b == 1u, r, l5_one()));
+            const L5 QB = l5_sel(b == 3u, l5_mul(rb, r), rb);  // r^3 = r^2 r
+            S = l5_sel(b == 0u, QA, l5_sel(a4 == 0u, QB, l5_mul(QA, QB)));
         }
-        // Q = r^nq = r^(4a) * r^b; suffix product over the pass's later lanes
-        const uint32_t a4 = nq >> 2, b = nq & 3u;
-        L5 QA = l5_one();
-#pragma unroll
-        for (int k = 0; k < K; k++)
-            if (a4 == (uint32_t)k + 1u)
-                QA = r4a[k];
-        const L5 QB = b == 3u ? r3 : b == 2u ? r2 : b == 1u ? r : l5_one();
-        L5 S = b == 0u ? QA : (a4 == 0u ? QB : l5_mul(QA, QB));
 #pragma unroll
         for (uint32_t o = 1; o < (uint32_t)G; o <<= 1) {
             const L5 t = l5_down<G>(S, lane, o);
             if (g + o < (uint32_t)G)
                 S = l5_mul(S, t);
         }
-        L5 E = l5_down<G>(S, lane, 1u);  // exclusive: product over lanes after this one
-        if (g + 1u >= (uint32_t)G)
-            E = l5_one();
-        // this lane's term: x * r^(blocks after it in this pass) * F (the
-        // later passes' blocks); the common factor r (the length block after
-        // everything) is applied once to the group's sum
-        const L5 EF = passes > 1 ? l5_mul(E, F) : E;  // F == 1 with one pass (wave-uniform test)
-        const L5 term = l5_mul(x, EF);
-        if (nq)
-            acc = l5_add(acc, term);
+        // exclusive: product over lanes after this one
+        const L5 E = l5_sel(g + 1u >= (uint32_t)G, l5_one(), l5_down<G>(S, lane, 1u));
+        // the later passes' blocks (F == 1 with one pass: wave-uniform test)
+        const L5 EF = passes > 1 ? l5_mul(E, F) : E;
         if (passes > 1 && pp > 0) {
             // F *= product of the whole pass (group lane 0 holds S over lanes >= 0)
             L5 Sall;
@@ -476,6 +484,56 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                 Sall.v[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(base_lane << 2), (int)S.v[k]);
             F = l5_mul(F, Sall);
         }
+
+        // the lane's K blocks: keystream, XOR, store, Horner with r
+        L5 x = l5_zero();
+        auto block = [&](uint32_t c, uint32_t kb[16]) {
+            const uint32_t d = c - 1u;  // payload block
+            const bool has = act && c >= 1u && d < nblk;
+            const uint32_t boff = has ? 64u * d : 0u;
+            const uint32_t nin = has ? (plen - boff < 64u ? plen - boff : 64u) : 0u;  // payload bytes in the block
+            const uint32_t nct = has ? (pad - boff < 64u ? pad - boff : 64u) : 0u;    // Poly1305 bytes in the block
+            uint32_t W[16];
+            load64(src + boff, nin, W);  // plaintext (encrypt) / ciphertext (decrypt), zero past the payload
+#pragma unroll
+            for (int m = 0; m < 16; m++) {
+                if constexpr (!kDec) {
+                    // padding plaintext bytes are zero (proto.cpp:568-572):
+                    // their ciphertext is the keystream itself
+                    W[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nct);  // ciphertext, what Poly1305 sees
+                } else {
+                    kb[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nin);  // plaintext
+                }
+            }
+            // decrypt stores the plaintext now; a bad tag zeroes it below
+            // (the final bytes are libsodium's either way)
+            if (has)
+                store_n(kDec ? dst + boff : dst + 16 + boff, kDec ? kb : W, kDec ? nin : nct);
+            const uint32_t nqj = nct / 16u;
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                const L5 blk = l5_from_words(W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3], 1u);
+                const L5 t = l5_mul(l5_add(x, blk), r);
+                if (q < nqj)
+                    x = t;
+            }
+        };
+        uint32_t j0 = 0;
+        if (pp == 0) {  // pass 0 starts with the block computed up front
+            block(cf, ks);
+            j0 = 1;
+        }
+#pragma unroll 1
+        for (uint32_t j = j0; j < (uint32_t)K; j++) {
+            uint32_t kb[16];
+            chacha20_block(p.key, cf + j, n0, n1, n2, kb);
+            block(cf + j, kb);
+        }
+        // this lane's term: x * r^(blocks after it in this pass) * F; the
+        // common factor r (the length block after everything) is applied
+        // once to the group's sum
+        if (nq)
+            acc = l5_add(acc, l5_mul(x, EF));
     }
     // the length block: le64(0) || le64(pad / payload length), times r
     const uint32_t mlen = kDec ? plen : pad;  // AEAD ct length (encrypt: the padded plaintext)

@@ -147,7 +147,10 @@ static Tune &tune_storage() {
         // of 1,500 B the split kernel wins 2x (profiles/r02_coop_probe.json)
         x.l4_coop = 16384;
         x.l4_coop_waves = 4;
-        x.aead_k = 4;
+        // AEAD: 2 consecutive ChaCha20 blocks per lane (1,500-B packets: 16-lane
+        // groups, 4 per wave): 1.605 ms per 1 M packets vs 1.965 (K = 1) and
+        // 1.673 (K = 4, 99 VGPRs: 5 waves/SIMD) (profiles/r02_aead_k_ab.json)
+        x.aead_k = 2;
         // environment overrides: WG_<KNOB> (upper case), same accepted values
         // as wg_tune_set; anything else is ignored
         for (const Knob &k : kKnobs) {
