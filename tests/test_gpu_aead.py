@@ -4,8 +4,9 @@ vectors in tests/test_oracle_aead.py), through the C ABI.
 
 Encrypt: Peer::encrypt for every segment of a PacketBatch (proto/proto.cpp:
 544-583, worker/encap.cpp:136-141) — byte-identical messages, at every
-segment size class the kernel distinguishes (32-lane groups up to 1,984 B,
-64-lane groups, multi-pass packets up to 64 KiB), short last segments, empty
+segment size class the kernel distinguishes (every power-of-two group size,
+64-lane groups in several passes up to 64 KiB, under each aead_k blocking),
+short last segments, empty
 segments (keepalives), counters across 2^32 and RejectAfterMessages.
 Decrypt: Peer::decrypt for every message of a GRO batch (proto.cpp:496-523) —
 plaintexts, statuses, zeroed output on a bad tag, untouched output on the
@@ -37,11 +38,25 @@ def _dev(a, gpu):
 
 ENC_CASES = [(1460, 1460 * 40 + 777), (1460, 1460 * 3), (64, 64 * 300 + 1), (1, 17), (15, 15 * 9 + 4), (16, 16 * 33),
              (17, 17 * 20 + 16), (1984, 1984 * 10 + 5), (1985, 1985 * 9 + 1984), (4032, 4032 * 4 + 63),
-             (4033, 4033 * 3 + 1), (9000, 9000 * 5 + 8999), (65535, 65535 * 2 + 100), (1500, 1500 * 64)]
+             (4033, 4033 * 3 + 1), (9000, 9000 * 5 + 8999), (65535, 65535 * 2 + 100), (1500, 1500 * 64),
+             # one-pass limits of the 64-lane group at K = 2 / 4 (127 / 255 payload blocks) and past them
+             (8128, 8128 * 3 + 1), (8129, 8129 * 2 + 8128), (16320, 16320 * 2 + 5), (16321, 16321 * 2 + 16000),
+             (32768, 32768 * 2 + 1)]
+
+
+@pytest.fixture(params=[1, 2, 4], ids=lambda k: f"aead_k={k}")
+def aead_k(request):
+    """Every lane-blocking variant (consecutive ChaCha20 blocks per lane: a
+    speed knob that must not change any byte)."""
+    wga = _wga()
+    saved = wga.tune_get("aead_k")
+    wga.tune_set("aead_k", request.param)
+    yield request.param
+    wga.tune_set("aead_k", saved)
 
 
 @pytest.mark.parametrize("seg,total", ENC_CASES)
-def test_encrypt_batch_matches_oracle(gpu, seg, total):
+def test_encrypt_batch_matches_oracle(gpu, aead_k, seg, total):
     import torch
 
     wga = _wga()
@@ -104,14 +119,16 @@ def _messages(rng, key, seg_pt, n, counter0=1):
     return oracle.wg_encrypt_batch(key, 3, counter0, buf, seg_pt), buf
 
 
-@pytest.mark.parametrize("seg_pt", [1, 16, 63, 1440, 1460, 1984, 2000, 4032, 4100, 9000])
-def test_decrypt_batch_matches_oracle(gpu, seg_pt):
+@pytest.mark.parametrize("seg_pt", [1, 16, 63, 1440, 1460, 1984, 2000, 4032, 4100, 9000, 16320, 40000])
+def test_decrypt_batch_matches_oracle(gpu, aead_k, seg_pt):
     import torch
 
     wga = _wga()
     rng = np.random.default_rng(seg_pt)
     key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
     n = 40 if seg_pt < 5000 else 12
+    if seg_pt > 10000:
+        n = 10
     msgs, _ = _messages(rng, key, seg_pt, n)
     mseg = wga.aead_message_stride(seg_pt)
     msgs = msgs.copy()
@@ -131,7 +148,7 @@ def test_decrypt_batch_matches_oracle(gpu, seg_pt):
         assert exp_st[2] == exp_st[5] == exp_st[7] == exp_st[9] == -1 and exp_st[0] == 0
 
 
-def test_keepalive_and_rejections(gpu):
+def test_keepalive_and_rejections(gpu, aead_k):
     """32-byte keepalives (encrypt of an empty payload, worker/encap.cpp:156)
     decrypt to nothing; 15- and 31-byte messages are rejected untouched."""
     import torch
@@ -151,7 +168,7 @@ def test_keepalive_and_rejections(gpu):
         assert (pt.cpu().numpy() == 0xEE).all()  # rejected before the MAC: untouched
 
 
-def test_round_trip_on_device(gpu):
+def test_round_trip_on_device(gpu, aead_k):
     """GPU encrypt -> GPU decrypt of a config-3-shaped batch (45 segments of
     1460 B and a 1295-B last one, the GSO output the encap worker encrypts)."""
     import torch
