@@ -553,24 +553,34 @@ def measured_read_peak(torch, wga, buf, iters: int = 30, run_bytes: int = 0) -> 
     and, for batches of <= 2 KiB packets (run_bytes), the L4 kernel's own
     issue structure (4 packets per wave, two 16-B loads per lane each).  The
     best of them is the ceiling."""
+    # The WHOLE buffer, in <= 4 GiB slices: a 25 GB buffer's rate depends on
+    # its physical pages (profiles/r02_config5_placement.json), so the
+    # ceiling must read the same pages the kernel reads.
     acc = torch.zeros(1, dtype=torch.int64, device=buf.device)
-    n = min(buf.numel(), 4 << 30) // 16 * 16
-    view = buf[:n]
     variants = [(f"contiguous_{k}KiB", k, 0) for k in (2, 4, 8)]
     if 0 < run_bytes <= 2048:
         variants.append((f"runs_{run_bytes}B_x4_per_wave", 1, run_bytes))
+    iters = iters if buf.numel() <= 4 << 30 else max(3, iters * (4 << 30) // buf.numel())
     rates = {}
     for name, kib, run in variants:
-        nb = n if not run else n // run * run
-        settle(torch, lambda: wga.probe_read(view, acc, kib, run_bytes=run), 0.05)
+        step = (4 << 30) // (16 * run) * 16 * run if run else 4 << 30  # slices stay 16-B aligned
+        views = [buf[o: o + min(step, buf.numel() - o) // 16 * 16] for o in range(0, buf.numel(), step)]
+        views = [v for v in views if v.numel() >= max(run, 16)]
+        nb = sum(v.numel() // run * run if run else v.numel() for v in views)
+
+        def once():
+            for v in views:
+                wga.probe_read(v, acc, kib, run_bytes=run)
+
+        settle(torch, once, 0.05)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(iters):
-            wga.probe_read(view, acc, kib, run_bytes=run)
+            once()
         e1.record()
         torch.cuda.synchronize()
         rates[name] = round(nb * iters / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
-    return {"best": max(rates.values()), "variants": rates}
+    return {"best": max(rates.values()), "variants": rates, "bytes": int(buf.numel())}
 
 
 def cpu_baseline(sample_fn, seconds: float):
