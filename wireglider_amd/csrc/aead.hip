@@ -24,7 +24,7 @@
 // per byte, against registers: K = 2 puts a 1,500-B packet in 16 lanes
 // (4 per wave); K = 4 (8 lanes) needs 99 VGPRs and measured 4 % slower.  ChaCha20 and Poly1305 are integer-VALU work (~1,000
 // and ~700 instructions per 64-B block lane), so this kernel is bound by
-// VALU issue, not HBM (DESIGN.md §9 f4).
+// VALU issue, not HBM (DESIGN.md §6.5).
 #include <hip/hip_runtime.h>
 
 #include "wg_device.hpp"
