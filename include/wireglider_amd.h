@@ -344,6 +344,8 @@ int wg_device_count(void);
  *                l4_coop_waves waves per packet (few, long packets; 0 never)
  *   "l4_coop_waves" waves sharing one packet in that mode (2, 4, 8, 16)
  *   "aead_k"     AEAD kernels: consecutive ChaCha20 blocks per lane (1, 2, 4)
+ *   "aead_pair"  aead_k = 2: the lane's two blocks computed together (1) or
+ *                one after the other (0)
  *   "gso_ablate" GSO A/B variants: 1 = non-temporal payload stores, 32 = no
  *                XCD swizzle (both correct); 0 = the default kernel.
  * Thread-safe: each launch reads one consistent snapshot of the knobs. */

@@ -82,6 +82,44 @@ __device__ __forceinline__ void chacha20_block(const AeadKey &key, uint32_t ctr,
     out[14] = x14 + n1;
     out[15] = x15 + n2;
 }
+// Two consecutive blocks (counters ctr, ctr + 1) with their quarter rounds
+// interleaved: 8 independent columns per step instead of 4, for a lane's
+// first two blocks (aead_k = 2), so a wave has twice the independent VALU
+// work between dependent instructions.
+__device__ __forceinline__ void chacha20_block2(const AeadKey &key, uint32_t ctr, uint32_t n0, uint32_t n1,
+                                                uint32_t n2, uint32_t o0[16], uint32_t o1[16]) {
+    uint32_t x[16], y[16];
+    const uint32_t init[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key.k[0], key.k[1], key.k[2],
+                               key.k[3],    key.k[4],    key.k[5],    key.k[6],    key.k[7], ctr,      n0,
+                               n1,          n2};
+#pragma unroll
+    for (int m = 0; m < 16; m++) x[m] = y[m] = init[m];
+    y[12] = ctr + 1u;
+#pragma unroll 2
+    for (int i = 0; i < 10; i++) {
+        WG_QR(x[0], x[4], x[8], x[12]);
+        WG_QR(y[0], y[4], y[8], y[12]);
+        WG_QR(x[1], x[5], x[9], x[13]);
+        WG_QR(y[1], y[5], y[9], y[13]);
+        WG_QR(x[2], x[6], x[10], x[14]);
+        WG_QR(y[2], y[6], y[10], y[14]);
+        WG_QR(x[3], x[7], x[11], x[15]);
+        WG_QR(y[3], y[7], y[11], y[15]);
+        WG_QR(x[0], x[5], x[10], x[15]);
+        WG_QR(y[0], y[5], y[10], y[15]);
+        WG_QR(x[1], x[6], x[11], x[12]);
+        WG_QR(y[1], y[6], y[11], y[12]);
+        WG_QR(x[2], x[7], x[8], x[13]);
+        WG_QR(y[2], y[7], y[8], y[13]);
+        WG_QR(x[3], x[4], x[9], x[14]);
+        WG_QR(y[3], y[4], y[9], y[14]);
+    }
+#pragma unroll
+    for (int m = 0; m < 16; m++) {
+        o0[m] = x[m] + init[m];
+        o1[m] = y[m] + (m == 12 ? ctr + 1u : init[m]);
+    }
+}
 #undef WG_QR
 
 // ---------------------------------------------------------------------------
@@ -361,7 +399,7 @@ constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/prot
 // G lanes per packet, K consecutive ChaCha20 blocks per lane: a pass covers
 // counters [pass*G*K, +G*K), lane g the K from pass*G*K + g*K; counter 0 is
 // the Poly1305 key block, counter c >= 1 the payload's 64-B block c - 1.
-template <int G, int K, bool kDec>
+template <int G, int K, bool kDec, bool kP = false>
 __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     constexpr uint32_t kPer = 64u / G;  // packets per wave
     constexpr uint32_t kPass = (uint32_t)(G * K);  // counters per pass
@@ -409,8 +447,14 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
 
     // Each lane's first block of pass 0 (counter g*K) up front: group lane
     // 0's is block 0, the Poly1305 key (r, s), which every lane needs first.
-    uint32_t ks[16];
-    chacha20_block(p.key, g * (uint32_t)K, n0, n1, n2, ks);
+    // kPair (K = 2, one pass): the lane's second block comes up front too,
+    // interleaved with the first (chacha20_block2)
+    constexpr bool kPair = kP && K == 2 && G < 64;
+    uint32_t ks[16], ks1[16];
+    if constexpr (kPair)
+        chacha20_block2(p.key, g * (uint32_t)K, n0, n1, n2, ks, ks1);
+    else
+        chacha20_block(p.key, g * (uint32_t)K, n0, n1, n2, ks);
     const uint32_t base_lane = lane & ~(G - 1u);
     uint32_t rw[4], sw[4];
 #pragma unroll
@@ -519,9 +563,13 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             }
         };
         uint32_t j0 = 0;
-        if (pp == 0) {  // pass 0 starts with the block computed up front
+        if (pp == 0) {  // pass 0 starts with the block(s) computed up front
             block(cf, ks);
             j0 = 1;
+            if constexpr (kPair) {
+                block(cf + 1u, ks1);
+                j0 = 2;
+            }
         }
 #pragma unroll 1
         for (uint32_t j = j0; j < (uint32_t)K; j++) {
@@ -599,6 +647,12 @@ static AeadKey key_words(const uint8_t key[32]) {
 
 template <int G, int K, bool kDec>
 static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
+    if constexpr (K == 2 && G < 64) {
+        if (tune().aead_pair) {
+            hipLaunchKernelGGL((aead_kernel<G, K, kDec, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+            return;
+        }
+    }
     hipLaunchKernelGGL((aead_kernel<G, K, kDec>), dim3((unsigned)blocks), dim3(256), 0, st, p);
 }
 

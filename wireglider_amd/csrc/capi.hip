@@ -59,6 +59,7 @@ static const Knob kKnobs[] = {
     {"l4_coop", &Tune::l4_coop, nullptr, 0, 1u << 20, nullptr, 0},
     {"l4_coop_waves", nullptr, &Tune::l4_coop_waves, 0, 0, kCoopW, WG_N(kCoopW)},
     {"aead_k", nullptr, &Tune::aead_k, 0, 0, kAeadK, WG_N(kAeadK)},
+    {"aead_pair", nullptr, &Tune::aead_pair, 0, 1, nullptr, 0},
 };
 #undef WG_N
 
@@ -151,6 +152,11 @@ static Tune &tune_storage() {
         // groups, 4 per wave): 1.605 ms per 1 M packets vs 1.965 (K = 1) and
         // 1.673 (K = 4, 99 VGPRs: 5 waves/SIMD) (profiles/r02_aead_k_ab.json)
         x.aead_k = 2;
+        // ... with its two blocks computed together, quarter rounds
+        // interleaved (8 independent columns): 1.695 -> 1.557 ms although
+        // 115 VGPRs leave 4 waves/SIMD (the kernel waits on dependent VALU
+        // issue, not memory: profiles/r02_aead_pair_ab.json)
+        x.aead_pair = 1;
         // environment overrides: WG_<KNOB> (upper case), same accepted values
         // as wg_tune_set; anything else is ignored
         for (const Knob &k : kKnobs) {
