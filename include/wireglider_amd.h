@@ -343,6 +343,8 @@ int wg_device_count(void);
  *   "l4_coop"    descriptor batches of n <= l4_coop descriptors: a block of
  *                l4_coop_waves waves per packet (few, long packets; 0 never)
  *   "l4_coop_waves" waves sharing one packet in that mode (2, 4, 8, 16)
+ *   "l4_split_waves" split-role descriptor kernel: waves per block, 4 (16
+ *                descriptors per wave) or 8 (8 per wave)
  *   "aead_k"     AEAD kernels: consecutive ChaCha20 blocks per lane (1, 2, 4)
  *   "aead_pair"  aead_k = 2: the lane's two blocks computed together (1) or
  *                one after the other (0)

@@ -117,7 +117,8 @@ DESC_VARIANTS = [{"l4_occ": 0}, {"l4_occ": 7}, {"l4_occ": 8}, {"l4_descv": 1}, {
                  {"l4_small": 0}, {"l4_small": 1}, {"l4_small": 2}, {"l4_small": 3}, {"l4_small": 4},
                  {"l4_small": 1, "l4_nt": 0}, {"l4_small": 5}, {"l4_small": 5, "l4_nt": 0},
                  {"l4_coop": 1 << 20, "l4_coop_waves": 2}, {"l4_coop": 1 << 20, "l4_coop_waves": 4, "l4_unroll": 4},
-                 {"l4_coop": 1 << 20, "l4_coop_waves": 8, "l4_nt": 0}, {"l4_coop": 1 << 20, "l4_coop_waves": 16}]
+                 {"l4_coop": 1 << 20, "l4_coop_waves": 8, "l4_nt": 0}, {"l4_coop": 1 << 20, "l4_coop_waves": 16},
+                 {"l4_small": 5, "l4_split_waves": 8}, {"l4_small": 5, "l4_split_waves": 8, "l4_unroll": 4}]
 
 
 @pytest.mark.parametrize("knobs", DESC_VARIANTS, ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()))
@@ -129,7 +130,7 @@ def test_desc_random(gpu, knobs):
 
     wga = _wga()
     saved = {k: wga.tune_get(k) for k in ("l4_occ", "l4_descv", "l4_iters", "l4_ppw", "l4_blocks", "l4_small",
-                                          "l4_nt", "l4_coop", "l4_coop_waves", "l4_unroll")}
+                                          "l4_nt", "l4_coop", "l4_coop_waves", "l4_unroll", "l4_split_waves")}
     for k, v in knobs.items():
         wga.tune_set(k, v)
     rng = np.random.default_rng(1234)
@@ -187,7 +188,7 @@ def test_uniform_small_segments(gpu, seg, knob):
         wga.tune_set("l4_small_uniform", saved)
 
 
-@pytest.mark.parametrize("small", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("small", [0, 1, 2, 3, 4, 5, 58])
 @pytest.mark.parametrize("seed", [5, 6])
 def test_desc_small_packets(gpu, small, seed):
     """Batches of mostly small packets (0-130 B, every alignment, csum_start
@@ -198,8 +199,9 @@ def test_desc_small_packets(gpu, small, seed):
     import torch
 
     wga = _wga()
-    saved = wga.tune_get("l4_small")
-    wga.tune_set("l4_small", small)
+    saved = {k: wga.tune_get(k) for k in ("l4_small", "l4_split_waves")}
+    wga.tune_set("l4_small", 5 if small == 58 else small)  # 58: the split kernel with 8-wave blocks
+    wga.tune_set("l4_split_waves", 8 if small == 58 else 4)
     rng = np.random.default_rng(seed)
     n = 30001
     lens = rng.integers(0, 131, n)
@@ -224,7 +226,8 @@ def test_desc_small_packets(gpu, small, seed):
     out = wga.calc_l4_checksum_desc(view, dd)
     plain = wga.checksum_desc(view, dd)
     torch.cuda.synchronize()
-    wga.tune_set("l4_small", saved)
+    for k, v in saved.items():
+        wga.tune_set(k, v)
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.l4_desc(buf, d))
     np.testing.assert_array_equal(plain.cpu().numpy(), oracle.checksum_desc(buf, d))
 

@@ -30,7 +30,7 @@ struct Knob {
 
 static const uint64_t kPpw[] = {1, 2, 4, 8}, kOcc[] = {0, 7, 8}, kVOcc[] = {0, 6, 8}, kDm[] = {0, 2},
                       kWaves[] = {1, 2, 4, 8}, kAbl[] = {0, 1, 32},
-                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {1, 2, 4};
+                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {1, 2, 4}, kSplitW[] = {4, 8};
 #define WG_N(a) (sizeof(a) / sizeof(a[0]))
 static const Knob kKnobs[] = {
     {"l4_blocks", &Tune::l4_blocks, nullptr, 1, 1u << 20, nullptr, 0},
@@ -58,6 +58,7 @@ static const Knob kKnobs[] = {
     {"l4_unroll", nullptr, &Tune::l4_unroll, 0, 0, kUnroll, WG_N(kUnroll)},
     {"l4_coop", &Tune::l4_coop, nullptr, 0, 1u << 20, nullptr, 0},
     {"l4_coop_waves", nullptr, &Tune::l4_coop_waves, 0, 0, kCoopW, WG_N(kCoopW)},
+    {"l4_split_waves", nullptr, &Tune::l4_split_waves, 0, 0, kSplitW, WG_N(kSplitW)},
     {"aead_k", nullptr, &Tune::aead_k, 0, 0, kAeadK, WG_N(kAeadK)},
     {"aead_pair", nullptr, &Tune::aead_pair, 0, 1, nullptr, 0},
 };
@@ -151,6 +152,9 @@ static Tune &tune_storage() {
         // AEAD: 2 consecutive ChaCha20 blocks per lane (1,500-B packets: 16-lane
         // groups, 4 per wave): 1.605 ms per 1 M packets vs 1.965 (K = 1) and
         // 1.673 (K = 4, 99 VGPRs: 5 waves/SIMD) (profiles/r02_aead_k_ab.json)
+        // split kernel: 4-wave blocks (16 descriptors per wave); 8-wave blocks
+        // (8 per wave) config 4 -1.5 %, config 5 +13 % (profiles/r02_split_waves_ab.json)
+        x.l4_split_waves = 4;
         x.aead_k = 2;
         // ... with its two blocks computed together, quarter rounds
         // interleaved (8 independent columns): 1.695 -> 1.557 ms although

@@ -462,18 +462,21 @@ __global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
 // batch keeps a lane per packet (waves 1-3 leave after one descriptor load),
 // an all-long one keeps the short 16-packet waves with every descriptor in
 // one vector load.  One launch, no host knowledge of the mix.
-template <int kKind, bool kNT, int U = 4>  // U: loads in flight per lane on a long packet's rest
-__global__ __launch_bounds__(256) void l4csum_split_kernel(L4Params p) {
+// kW = 8: 512-thread blocks, wave k owning group (k mod 4) of quarters
+// 2 (k / 4) and 2 (k / 4) + 1 — 8 descriptors per wave, shorter-lived waves.
+template <int kKind, bool kNT, int U = 4, int kW = 4>  // U: loads in flight per lane on a long packet's rest
+__global__ __launch_bounds__(64 * kW) void l4csum_split_kernel(L4Params p) {
     constexpr bool kL4 = kKind != kDescPlain;
+    constexpr uint32_t kQpw = 16u / kW;  // quarters per wave in the wave role (4 or 2)
     const uint32_t lane = lane_id();
     const uint32_t wib = wave_in_block();
     const uint64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
     const uint64_t Q = p.quarter;
     // lane -> (quarter, offset in the block's 16 of that quarter)
-    const uint32_t qq = wib == 0 ? lane >> 4 : (lane >> 2) & 3u;
-    const uint32_t oo = wib == 0 ? lane & 15u : 4u * wib + (lane & 3u);
+    const uint32_t qq = wib == 0 ? lane >> 4 : kQpw * (wib >> 2) + ((lane >> 2) & (kQpw - 1u));
+    const uint32_t oo = wib == 0 ? lane & 15u : 4u * (wib & 3u) + (lane & 3u);
     const uint64_t i = (uint64_t)qq * Q + 16u * blk + oo;
-    const bool live = (wib == 0 || lane < 16u) && 16u * blk < Q && i < p.n;
+    const bool live = (wib == 0 || lane < 4u * kQpw) && 16u * blk < Q && i < p.n;
     const v4u d = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : p.n - 1));
     const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
     const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + (live ? off : 0u);
@@ -484,7 +487,7 @@ __global__ __launch_bounds__(256) void l4csum_split_kernel(L4Params p) {
     const uint64_t gl = __ballot(live && len > kSmallMax);
     const bool grp_long = ((gl >> (lane & ~3u)) & 0xfu) != 0;
     // ---- wave role: this wave's groups that hold a long packet
-    const bool own = wib == 0 ? (lane & 15u) < 4u : true;
+    const bool own = wib == 0 ? (lane & 15u) < 4u && (lane >> 4) < kQpw : true;
     const bool mine = live && own && grp_long;
     uint32_t res = 0;
     wave_long<kL4, kNT, 4, U>(__ballot(mine), a, len, cs, fl, p.base, lane, res);
@@ -624,7 +627,13 @@ static int launch_small(const L4Params &p, uint32_t mode, hipStream_t st) {
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
     const dim3 grid((unsigned)blocks), blk(256);
-    if (mode == 5 && tune().l4_unroll == 8)
+    const Tune t = tune();
+    if (mode == 5 && t.l4_split_waves == 8) {
+        if (t.l4_unroll == 8)
+            hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 8, 8>), grid, dim3(512), 0, st, q);
+        else
+            hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 4, 8>), grid, dim3(512), 0, st, q);
+    } else if (mode == 5 && t.l4_unroll == 8)
         hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 8>), grid, blk, 0, st, q);
     else if (mode == 5)
         hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT>), grid, blk, 0, st, q);
