@@ -761,6 +761,25 @@ def load_traffic(workload: str):
         return None
 
 
+# Peak VALU issue: one wave64 VALU instruction per 2 cycles per SIMD
+# (MI355X_MICROARCH.md cycle constants, v_fma_f32 wave64 on SIMD-32), 1,024
+# SIMDs at 2.4 GHz.
+VALU_PEAK_WINST = 1024 * 2.4e9 / 2
+
+
+def load_valu(workload: str):
+    """VALU wave-instructions per launch of a VALU-bound workload's kernel
+    from its committed rocprofv3 summary (profiles/valu_<workload>.json,
+    SQ_INSTS_VALU), or None."""
+    p = ROOT / "profiles" / f"valu_{workload}.json"
+    if not p.exists():
+        return None
+    try:
+        return json.loads(p.read_text())
+    except Exception:
+        return None
+
+
 def post_checks(torch, wga, wl: Workload, world: int, dev):
     """Outside the timed region: verify pass, result hash, RCCL gather."""
     from wireglider_amd import dist as wdist
@@ -986,6 +1005,17 @@ def main():
         },
         "post_checks": post,
     }
+    valu = load_valu(args.workload)
+    if valu and valu.get("valu_winst_per_launch"):
+        # the issue roofline of a VALU-bound kernel (f4): every VALU
+        # instruction priced at full rate, so 64-bit multiplies make the true
+        # bound tighter than this fraction suggests
+        ach = valu["valu_winst_per_launch"] / (kern_ms * 1e-3)
+        line["roofline"]["valu_issue"] = {
+            "bound": "valu", "achieved": round(ach / 1e12, 4), "peak": round(VALU_PEAK_WINST / 1e12, 4),
+            "unit": "T wave64-instructions/s", "frac": round(ach / VALU_PEAK_WINST, 4),
+            "instructions_per_launch": valu["valu_winst_per_launch"],
+            "source": f"profiles/valu_{args.workload}.json (rocprofv3 SQ_INSTS_VALU, {valu.get('kernel')})"}
     if strong is not None:
         line["strong_scaling"] = strong
     if rank == 0:

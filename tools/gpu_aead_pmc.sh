@@ -25,3 +25,10 @@ print(json.dumps(out, indent=1))
 json.dump(out, open("/root/repo/gpurun_out/aead_pmc/pmc.json", "w"), indent=1)
 PY
 find $OUT/prof -name "*kernel_stats.csv" -exec head -4 {} \;
+python3 - <<'PY'
+import json
+d = json.load(open("/root/repo/gpurun_out/aead_pmc/pmc.json"))
+k = next(k for k in d if "aead_kernel" in k and "false" in k)
+json.dump({"kernel": k, "valu_winst_per_launch": d[k]["SQ_INSTS_VALU"], "salu_winst_per_launch": d[k]["SQ_INSTS_SALU"],
+           "waves": d[k]["SQ_WAVES"], "workload": "aead"}, open("/root/repo/gpurun_out/aead_pmc/valu_aead.json", "w"), indent=1)
+PY
