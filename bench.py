@@ -983,7 +983,11 @@ def main():
         "data": "synthetic (device-generated, seeded; BASELINE config shapes)",
         "config": meta["config"],
         "distributed": {"backend": backend if world > 1 else None, "world_size": got,
-                        "kernel_ms_per_rank": t["kern_ms_per_rank"], "wall_s_per_rank": t["wall_s_per_rank"]},
+                        "kernel_ms_per_rank": t["kern_ms_per_rank"], "wall_s_per_rank": t["wall_s_per_rank"],
+                        # the whole job against R x HBM peak (algorithmic
+                        # bytes of every rank / the slowest rank's kernel time)
+                        "frac_of_world_hbm_peak": round(meta["alg_bytes"] * got / (t["kern_ms_max"] * 1e-3)
+                                                        / 1e9 / (HBM_PEAK_GBS * got), 4)},
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved, 2),

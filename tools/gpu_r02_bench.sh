@@ -12,7 +12,7 @@ shift || true
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-python3 -c "import sys; sys.path.insert(0, 'oracle'); import oracle, json; print(json.dumps(oracle.host_cores()))" > "$OUT/host_cores.json"
+python3 -c "import os, json; print(json.dumps({'affinity': len(os.sched_getaffinity(0)), 'cpu_count': os.cpu_count()}))" > "$OUT/host_cores.json"  # bench.py's cpu_baseline reports the granted cores
 cat /sys/fs/cgroup/cpu.max >> "$OUT/host_cores.json" 2>/dev/null || true
 nproc >> "$OUT/host_cores.json"
 echo "== pytest -m gpu"
