@@ -346,8 +346,8 @@ int wg_device_count(void);
  *   "l4_split_waves" split-role descriptor kernel: waves per block, 4 (16
  *                descriptors per wave) or 8 (8 per wave)
  *   "aead_k"     AEAD kernels: consecutive ChaCha20 blocks per lane (1, 2, 4)
- *   "aead_pair"  aead_k = 2: the lane's two blocks computed together (1) or
- *                one after the other (0)
+ *   "aead_pair"  aead_k = 2, 4: a lane's blocks computed two at a time,
+ *                interleaved (1), or one after the other (0)
  *   "gso_ablate" GSO A/B variants: 1 = non-temporal payload stores, 32 = no
  *                XCD swizzle (both correct); 0 = the default kernel.
  * Thread-safe: each launch reads one consistent snapshot of the knobs. */

@@ -44,7 +44,7 @@ ENC_CASES = [(1460, 1460 * 40 + 777), (1460, 1460 * 3), (64, 64 * 300 + 1), (1, 
              (32768, 32768 * 2 + 1)]
 
 
-@pytest.fixture(params=[(1, 0), (2, 0), (2, 1), (4, 0)], ids=lambda kp: f"aead_k={kp[0]},pair={kp[1]}")
+@pytest.fixture(params=[(1, 0), (2, 0), (2, 1), (4, 0), (4, 1)], ids=lambda kp: f"aead_k={kp[0]},pair={kp[1]}")
 def aead_k(request):
     """Every lane-blocking variant (consecutive ChaCha20 blocks per lane, the
     two-block interleave: speed knobs that must not change any byte)."""

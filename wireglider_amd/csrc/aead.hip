@@ -447,9 +447,9 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
 
     // Each lane's first block of pass 0 (counter g*K) up front: group lane
     // 0's is block 0, the Poly1305 key (r, s), which every lane needs first.
-    // kPair (K = 2, one pass): the lane's second block comes up front too,
-    // interleaved with the first (chacha20_block2)
-    constexpr bool kPair = kP && K == 2 && G < 64;
+    // kPair (K = 2 or 4, one pass): the lane's blocks two at a time, each
+    // pair interleaved (chacha20_block2); the first pair up front
+    constexpr bool kPair = kP && (K == 2 || K == 4) && G < 64;
     uint32_t ks[16], ks1[16];
     if constexpr (kPair)
         chacha20_block2(p.key, g * (uint32_t)K, n0, n1, n2, ks, ks1);
@@ -571,11 +571,21 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                 j0 = 2;
             }
         }
+        if constexpr (kPair) {
 #pragma unroll 1
-        for (uint32_t j = j0; j < (uint32_t)K; j++) {
-            uint32_t kb[16];
-            chacha20_block(p.key, cf + j, n0, n1, n2, kb);
-            block(cf + j, kb);
+            for (uint32_t j = j0; j < (uint32_t)K; j += 2) {
+                uint32_t kb[16], kb1[16];
+                chacha20_block2(p.key, cf + j, n0, n1, n2, kb, kb1);
+                block(cf + j, kb);
+                block(cf + j + 1u, kb1);
+            }
+        } else {
+#pragma unroll 1
+            for (uint32_t j = j0; j < (uint32_t)K; j++) {
+                uint32_t kb[16];
+                chacha20_block(p.key, cf + j, n0, n1, n2, kb);
+                block(cf + j, kb);
+            }
         }
         // this lane's term: x * r^(blocks after it in this pass) * F; the
         // common factor r (the length block after everything) is applied
@@ -647,7 +657,7 @@ static AeadKey key_words(const uint8_t key[32]) {
 
 template <int G, int K, bool kDec>
 static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
-    if constexpr (K == 2 && G < 64) {
+    if constexpr ((K == 2 || K == 4) && G < 64) {
         if (tune().aead_pair) {
             hipLaunchKernelGGL((aead_kernel<G, K, kDec, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
             return;

@@ -36,7 +36,7 @@ struct Tune {
     uint32_t l4_coop_waves;  // waves per packet in that mode (2, 4, 8, 16)
     uint32_t l4_split_waves;  // split kernel: waves per block, 4 (16 descriptors per wave) or 8 (8 per wave)
     uint32_t aead_k;      // AEAD: consecutive ChaCha20 blocks per lane (1, 2, 4)
-    uint32_t aead_pair;   // AEAD, aead_k = 2: the lane's two blocks computed together, interleaved (1)
+    uint32_t aead_pair;   // AEAD, aead_k = 2, 4: a lane's blocks two at a time, interleaved (1)
     uint32_t gso_ablate;  // GSO A/B variants (1 non-temporal stores, 32 no XCD swizzle; both correct)
 };
 
