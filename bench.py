@@ -270,7 +270,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                            "Peer::encrypt per segment) of 1,048,576 x 1500 B packets per GPU",
                "packets_per_gpu": n, "segment_size": SEG, "message_stride": mseg, "parallelism": f"shard{world}"}
         return Workload(launch, n, n * SEG, n * SEG + n * mseg + n, cfg, "weak", buf,
-                        "wg::aead_kernel<16,2,false,true> (VALU-bound: ChaCha20 + Poly1305)", rank * n, sample=sample,
+                        "wg::aead_kernel<0,3,false,true> (9-lane groups, VALU-bound: ChaCha20 + Poly1305)", rank * n, sample=sample,
                         counts=[n] * world, post=post,
                         metric="device-resident GiB/s of plaintext, WireGuard data-message encryption (SURVEY f4)")
     if name == "config1":

@@ -345,9 +345,12 @@ int wg_device_count(void);
  *   "l4_coop_waves" waves sharing one packet in that mode (2, 4, 8, 16)
  *   "l4_split_waves" split-role descriptor kernel: waves per block, 4 (16
  *                descriptors per wave) or 8 (8 per wave)
- *   "aead_k"     AEAD kernels: consecutive ChaCha20 blocks per lane (1, 2, 4)
- *   "aead_pair"  aead_k = 2, 4: a lane's blocks computed two at a time,
- *                interleaved (1), or one after the other (0)
+ *   "aead_k"     AEAD kernels: consecutive ChaCha20 blocks per lane (1-4; 0
+ *                = 2 or 3, whichever fills a wave better for the batch)
+ *   "aead_pair"  a lane's blocks computed two at a time, interleaved (1),
+ *                or one after the other (0)
+ *   "aead_flex"  groups of exactly the lanes a packet needs (1, up to 32)
+ *                or the next power of two (0)
  *   "gso_ablate" GSO A/B variants: 1 = non-temporal payload stores, 32 = no
  *                XCD swizzle (both correct); 0 = the default kernel.
  * Thread-safe: each launch reads one consistent snapshot of the knobs. */

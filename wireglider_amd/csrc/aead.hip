@@ -9,7 +9,8 @@
 //
 // Layout: a group of G lanes per packet (the smallest power of two that holds
 // its blocks; G = 64 in passes for packets past 64 K blocks), K consecutive
-// ChaCha20 blocks per lane (knob aead_k, default 2): block counter c is lane
+// ChaCha20 blocks per lane (knob aead_k; by default 2 or 3 per batch, see
+// launch_aead): block counter c is lane
 // c / K's.  Counter 0 (group lane 0's first block) is the Poly1305 key; the
 // lane writing it also writes the DataHeader and handles the length block;
 // counter c >= 1 is the keystream for the 64 bytes [64(c-1), 64c) of the
@@ -212,6 +213,19 @@ __device__ __forceinline__ uint32_t grp_sum(uint32_t v, uint32_t lane) {
     return v;
 }
 
+// The same for a group size known only at run time (gs lanes from base, any
+// gs <= 32): `g` is the lane's index in its group.
+__device__ __forceinline__ uint32_t grp_down_rt(uint32_t v, uint32_t lane, uint32_t g, uint32_t gs, uint32_t off) {
+    const uint32_t src = g + off < gs ? lane + off : lane;
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((src & 63u) << 2), (int)v);
+}
+__device__ __forceinline__ L5 l5_down_rt(const L5 &a, uint32_t lane, uint32_t g, uint32_t gs, uint32_t off) {
+    L5 b;
+#pragma unroll
+    for (int i = 0; i < 5; i++) b.v[i] = grp_down_rt(a.v[i], lane, g, gs, off);
+    return b;
+}
+
 // Carry-normalise (value unchanged mod p): every limb < 2^26 but limb 1,
 // which may exceed it by a few units.  Limbs in must be < 2^32 - 2^29.
 __device__ __forceinline__ L5 l5_norm(L5 h) {
@@ -388,6 +402,7 @@ struct AeadParams {
     uint32_t receiver;   // encrypt: DataHeader.receiver_index
     uint64_t counter0;   // encrypt: counter of packet 0
     AeadKey key;
+    uint32_t grp;        // aead_kernel<0, ...>: lanes per packet (1..32)
 };
 
 constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/proto/proto.hpp:36
@@ -399,15 +414,21 @@ constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/prot
 // G lanes per packet, K consecutive ChaCha20 blocks per lane: a pass covers
 // counters [pass*G*K, +G*K), lane g the K from pass*G*K + g*K; counter 0 is
 // the Poly1305 key block, counter c >= 1 the payload's 64-B block c - 1.
+// G = 0: the group size is p.grp (any 1..32, set at launch as the lanes a
+// packet needs: a 1,500-B packet's 25 blocks at K = 3 take 9 lanes, 7
+// packets fill 63 of a wave's 64 lanes), one pass.
 template <int G, int K, bool kDec, bool kP = false>
 __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
-    constexpr uint32_t kPer = 64u / G;  // packets per wave
-    constexpr uint32_t kPass = (uint32_t)(G * K);  // counters per pass
+    constexpr bool kFlex = G == 0;
+    const uint32_t GG = kFlex ? p.grp : (uint32_t)G;  // lanes per packet
+    const uint32_t kPer = kFlex ? 64u / GG : 64u / (uint32_t)(G ? G : 1);  // packets per wave
+    const uint32_t kPass = GG * (uint32_t)K;  // counters per pass
     const uint32_t lane = lane_id();
-    const uint32_t g = lane & (G - 1u);
+    const uint32_t slot = kFlex ? lane / GG : lane / (uint32_t)(G ? G : 1);  // packet of the wave
+    const uint32_t g = kFlex ? lane - slot * GG : lane & (uint32_t)(G - 1);
     const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
-    const uint64_t i = wave * kPer + lane / G;
-    const bool live = i < p.n;
+    const uint64_t i = wave * kPer + slot;
+    const bool live = slot < kPer && i < p.n;
     const uint64_t ii = live ? i : 0;
     const uint64_t off = ii * p.seg;
     const uint32_t len = live ? (uint32_t)(p.total_len - off < p.seg ? p.total_len - off : p.seg) : 0u;
@@ -449,13 +470,13 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     // 0's is block 0, the Poly1305 key (r, s), which every lane needs first.
     // kPair (K = 2 or 4, one pass): the lane's blocks two at a time, each
     // pair interleaved (chacha20_block2); the first pair up front
-    constexpr bool kPair = kP && (K == 2 || K == 4) && G < 64;
+    constexpr bool kPair = kP && K >= 2 && G < 64;
     uint32_t ks[16], ks1[16];
     if constexpr (kPair)
         chacha20_block2(p.key, g * (uint32_t)K, n0, n1, n2, ks, ks1);
     else
         chacha20_block(p.key, g * (uint32_t)K, n0, n1, n2, ks);
-    const uint32_t base_lane = lane & ~(G - 1u);
+    const uint32_t base_lane = kFlex ? slot * GG : lane & ~(uint32_t)(G - 1);
     uint32_t rw[4], sw[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -501,23 +522,35 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             if constexpr (K >= 2) {
                 const L5 r8 = l5_mul(r4, r4);
                 QA = l5_sel(a4 == 2u, r8, QA);
-                if constexpr (K == 4) {
-                    const L5 r12 = l5_mul(r8, r4), r16 = l5_mul(r8, r8);
-                    QA = l5_sel(a4 == 3u, r12, l5_sel(a4 == 4u, r16, QA));
+                if constexpr (K >= 3) {
+                    const L5 r12 = l5_mul(r8, r4);
+                    QA = l5_sel(a4 == 3u, r12, QA);
+                    if constexpr (K == 4)
+                        QA = l5_sel(a4 == 4u, l5_mul(r8, r8), QA);
                 }
             }
             const L5 rb = l5_sel(b >= 2u, r2, l5_sel(b == 1u, r, l5_one()));
             const L5 QB = l5_sel(b == 3u, l5_mul(rb, r), rb);  // r^3 = r^2 r
             S = l5_sel(b == 0u, QA, l5_sel(a4 == 0u, QB, l5_mul(QA, QB)));
         }
+        L5 E;
+        if constexpr (kFlex) {
+            for (uint32_t o = 1; o < GG; o <<= 1) {  // wave-uniform trip count
+                const L5 t = l5_down_rt(S, lane, g, GG, o);
+                if (g + o < GG)
+                    S = l5_mul(S, t);
+            }
+            E = l5_sel(g + 1u >= GG, l5_one(), l5_down_rt(S, lane, g, GG, 1u));
+        } else {
 #pragma unroll
-        for (uint32_t o = 1; o < (uint32_t)G; o <<= 1) {
-            const L5 t = l5_down<G>(S, lane, o);
-            if (g + o < (uint32_t)G)
-                S = l5_mul(S, t);
+            for (uint32_t o = 1; o < (uint32_t)G; o <<= 1) {
+                const L5 t = l5_down<G ? G : 1>(S, lane, o);
+                if (g + o < (uint32_t)G)
+                    S = l5_mul(S, t);
+            }
+            // exclusive: product over lanes after this one
+            E = l5_sel(g + 1u >= (uint32_t)G, l5_one(), l5_down<G ? G : 1>(S, lane, 1u));
         }
-        // exclusive: product over lanes after this one
-        const L5 E = l5_sel(g + 1u >= (uint32_t)G, l5_one(), l5_down<G>(S, lane, 1u));
         // the later passes' blocks (F == 1 with one pass: wave-uniform test)
         const L5 EF = passes > 1 ? l5_mul(E, F) : E;
         if (passes > 1 && pp > 0) {
@@ -572,12 +605,18 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             }
         }
         if constexpr (kPair) {
+            uint32_t j = j0;
 #pragma unroll 1
-            for (uint32_t j = j0; j < (uint32_t)K; j += 2) {
+            for (; j + 1u < (uint32_t)K; j += 2) {
                 uint32_t kb[16], kb1[16];
                 chacha20_block2(p.key, cf + j, n0, n1, n2, kb, kb1);
                 block(cf + j, kb);
                 block(cf + j + 1u, kb1);
+            }
+            if (j < (uint32_t)K) {  // K odd: the last block alone
+                uint32_t kb[16];
+                chacha20_block(p.key, cf + j, n0, n1, n2, kb);
+                block(cf + j, kb);
             }
         } else {
 #pragma unroll 1
@@ -599,7 +638,23 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     if (g == 0u && act)
         acc = l5_add(acc, lenblk);
     // group sum, times r (every term's last factor), every lane finishes
-    const L5 tot = l5_mul(l5_norm(l5_grp_sum<G>(l5_norm(acc), lane)), r);
+    L5 tot;
+    if constexpr (kFlex) {
+        // reduction tree by down-shifts (lane g sums [g, g + 2^k)), then the
+        // group's first lane broadcasts: any group size
+        L5 a = l5_norm(acc);
+        for (uint32_t o = 1; o < GG; o <<= 1) {
+            const L5 t = l5_down_rt(a, lane, g, GG, o);
+            if (g + o < GG)
+                a = l5_add(a, t);
+        }
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+            a.v[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(base_lane << 2), (int)a.v[k]);
+        tot = l5_mul(l5_norm(a), r);
+    } else {
+        tot = l5_mul(l5_norm(l5_grp_sum<G ? G : 1>(l5_norm(acc), lane)), r);
+    }
     uint32_t tagw[4];
     poly_finish(tot, sw, tagw);
     if constexpr (!kDec) {
@@ -657,7 +712,7 @@ static AeadKey key_words(const uint8_t key[32]) {
 
 template <int G, int K, bool kDec>
 static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
-    if constexpr ((K == 2 || K == 4) && G < 64) {
+    if constexpr (K >= 2 && G < 64) {
         if (tune().aead_pair) {
             hipLaunchKernelGGL((aead_kernel<G, K, kDec, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
             return;
@@ -669,6 +724,7 @@ static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
 template <int K, bool kDec>
 static void launch_k(const AeadParams &p, uint32_t G, uint64_t blocks, hipStream_t st) {
     switch (G) {
+    case 0: launch_gk<0, K, kDec>(p, blocks, st); break;
     case 1: launch_gk<1, K, kDec>(p, blocks, st); break;
     case 2: launch_gk<2, K, kDec>(p, blocks, st); break;
     case 4: launch_gk<4, K, kDec>(p, blocks, st); break;
@@ -682,25 +738,44 @@ static void launch_k(const AeadParams &p, uint32_t G, uint64_t blocks, hipStream
 template <bool kDec>
 static int launch_aead(AeadParams &p, uint32_t maxpay, hipStream_t st) {
     // counters per packet: the key block + the padded payload's 64-B blocks;
-    // K (knob aead_k) consecutive blocks per lane, the smallest power-of-two
-    // group holding them (G = 64 and several passes past 64 K blocks)
+    // K (knob aead_k) consecutive blocks per lane; a group of exactly the
+    // lanes needed (aead_flex, up to 32: 64 / lanes packets per wave), else
+    // the smallest power-of-two group (64 lanes and several passes past 64 K
+    // blocks)
     const uint32_t nblk = (((maxpay + 15u) & ~15u) + 63u) / 64u;
-    const uint32_t K = tune().aead_k;
+    const Tune t = tune();
+    uint32_t K = t.aead_k;
+    if (K == 0) {
+        // auto: K = 2 or 3, whichever moves more packets per unit of lane
+        // work with exact-size groups (64 / lanes packets per wave, K blocks
+        // each lane): 1,500 B (25 blocks) -> K = 3, 9 lanes, 7 packets per
+        // wave (63 of 64 lanes); 64 B (2 blocks) -> K = 2, 64 per wave
+        const uint32_t c = nblk + 1u;
+        const uint32_t l2 = (c + 1u) / 2u, l3 = (c + 2u) / 3u;
+        const uint32_t w2 = l2 <= 32u ? 64u / l2 : 0u, w3 = l3 <= 32u ? 64u / l3 : 0u;
+        K = 2u * w3 > 3u * w2 ? 3u : 2u;  // w3 / 3 > w2 / 2
+    }
     const uint32_t lanes = (nblk + 1u + K - 1u) / K;
     uint32_t G = 1;
     while (G < lanes && G < 64u) G <<= 1;
-    const uint64_t per_block = 4u * (64u / G);  // packets per 256-thread block
+    uint32_t per_wave = 64u / G;
+    if (t.aead_flex && lanes <= 32u && lanes != G) {
+        p.grp = lanes;
+        per_wave = 64u / lanes;
+        G = 0;
+    }
+    const uint64_t per_block = 4u * per_wave;  // packets per 256-thread block
     uint64_t blocks = (p.n + per_block - 1) / per_block;
     if (blocks >= 8)
         blocks = (blocks + 7) & ~7ull;  // XCD swizzle bijective; surplus waves have no live packet
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
-    if (K == 1)
-        launch_k<1, kDec>(p, G, blocks, st);
-    else if (K == 2)
-        launch_k<2, kDec>(p, G, blocks, st);
-    else
-        launch_k<4, kDec>(p, G, blocks, st);
+    switch (K) {
+    case 1: launch_k<1, kDec>(p, G, blocks, st); break;
+    case 2: launch_k<2, kDec>(p, G, blocks, st); break;
+    case 3: launch_k<3, kDec>(p, G, blocks, st); break;
+    default: launch_k<4, kDec>(p, G, blocks, st); break;
+    }
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }
 

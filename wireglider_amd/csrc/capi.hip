@@ -30,7 +30,7 @@ struct Knob {
 
 static const uint64_t kPpw[] = {1, 2, 4, 8}, kOcc[] = {0, 7, 8}, kVOcc[] = {0, 6, 8}, kDm[] = {0, 2},
                       kWaves[] = {1, 2, 4, 8}, kAbl[] = {0, 1, 32},
-                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {1, 2, 4}, kSplitW[] = {4, 8};
+                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {0, 1, 2, 3, 4}, kSplitW[] = {4, 8};
 #define WG_N(a) (sizeof(a) / sizeof(a[0]))
 static const Knob kKnobs[] = {
     {"l4_blocks", &Tune::l4_blocks, nullptr, 1, 1u << 20, nullptr, 0},
@@ -61,6 +61,7 @@ static const Knob kKnobs[] = {
     {"l4_split_waves", nullptr, &Tune::l4_split_waves, 0, 0, kSplitW, WG_N(kSplitW)},
     {"aead_k", nullptr, &Tune::aead_k, 0, 0, kAeadK, WG_N(kAeadK)},
     {"aead_pair", nullptr, &Tune::aead_pair, 0, 1, nullptr, 0},
+    {"aead_flex", nullptr, &Tune::aead_flex, 0, 1, nullptr, 0},
 };
 #undef WG_N
 
@@ -149,18 +150,19 @@ static Tune &tune_storage() {
         // of 1,500 B the split kernel wins 2x (profiles/r02_coop_probe.json)
         x.l4_coop = 16384;
         x.l4_coop_waves = 4;
-        // AEAD: 2 consecutive ChaCha20 blocks per lane (1,500-B packets: 16-lane
-        // groups, 4 per wave): 1.605 ms per 1 M packets vs 1.965 (K = 1) and
-        // 1.673 (K = 4, 99 VGPRs: 5 waves/SIMD) (profiles/r02_aead_k_ab.json)
         // split kernel: 4-wave blocks (16 descriptors per wave); 8-wave blocks
         // (8 per wave) config 4 -1.5 %, config 5 +13 % (profiles/r02_split_waves_ab.json)
         x.l4_split_waves = 4;
-        x.aead_k = 2;
-        // ... with its two blocks computed together, quarter rounds
-        // interleaved (8 independent columns): 1.695 -> 1.557 ms although
-        // 115 VGPRs leave 4 waves/SIMD (the kernel waits on dependent VALU
-        // issue, not memory: profiles/r02_aead_pair_ab.json)
+        // AEAD: K consecutive ChaCha20 blocks per lane, chosen per batch (0:
+        // 2 or 3, whichever fills the wave better), each lane's blocks two at
+        // a time with interleaved quarter rounds (the kernel waits on
+        // dependent VALU issue, not memory), groups of exactly the lanes a
+        // packet needs.  1 M x 1500 B: K = 3 in 9-lane groups 1.401 ms vs
+        // K = 2 in 16-lane groups 1.506 (profiles/r02_aead_flex_ab.json), the
+        // interleave -8 % (profiles/r02_aead_pair_ab.json)
+        x.aead_k = 0;
         x.aead_pair = 1;
+        x.aead_flex = 1;
         // environment overrides: WG_<KNOB> (upper case), same accepted values
         // as wg_tune_set; anything else is ignored
         for (const Knob &k : kKnobs) {

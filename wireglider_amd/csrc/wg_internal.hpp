@@ -35,7 +35,8 @@ struct Tune {
     uint64_t l4_coop;     // descriptor batches of n <= l4_coop: a block of l4_coop_waves waves per packet (0: never)
     uint32_t l4_coop_waves;  // waves per packet in that mode (2, 4, 8, 16)
     uint32_t l4_split_waves;  // split kernel: waves per block, 4 (16 descriptors per wave) or 8 (8 per wave)
-    uint32_t aead_k;      // AEAD: consecutive ChaCha20 blocks per lane (1, 2, 4)
+    uint32_t aead_k;      // AEAD: consecutive ChaCha20 blocks per lane (1, 2, 3, 4)
+    uint32_t aead_flex;   // AEAD: groups of exactly the lanes a packet needs (<= 32), not a power of two
     uint32_t aead_pair;   // AEAD, aead_k = 2, 4: a lane's blocks two at a time, interleaved (1)
     uint32_t gso_ablate;  // GSO A/B variants (1 non-temporal stores, 32 no XCD swizzle; both correct)
 };
