@@ -257,10 +257,59 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / 20
             same = bool(torch.equal(pt.view(n, mseg - 32)[:, :SEG], buf.view(n, SEG)))
-            return {"encrypt_status_nonzero": int(torch.count_nonzero(st).item()),
-                    "decrypt": {"kernel_ms": round(ms, 5), "GiB_s": round(n * SEG / (ms * 1e-3) / 2**30, 1),
-                                "status_nonzero": int(torch.count_nonzero(dst).item()),
-                                "plaintext_round_trip_equal": same}}
+            res = {"encrypt_status_nonzero": int(torch.count_nonzero(st).item()),
+                   "decrypt": {"kernel_ms": round(ms, 5), "GiB_s": round(n * SEG / (ms * 1e-3) / 2**30, 1),
+                               "status_nonzero": int(torch.count_nonzero(dst).item()),
+                               "plaintext_round_trip_equal": same}}
+            del pt, dst
+            res["decap_fused"] = decap_fused()
+            return res
+
+        def timed(fn, reps=20):
+            for _ in range(3):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / reps
+
+        def decap_fused():
+            """The decap worker's decrypt + evaluate_packet (worker/decap_ref.cpp:
+            81-86) on 1 M valid 1,504-B packets (a multiple of 16, so the padded
+            plaintext is the IP packet and every gate runs): decrypt then
+            wg_verify_desc over the plaintexts, against the fused
+            wg_aead_decrypt_verify_batch (one pass, the plaintext never re-read);
+            verdicts and L4 results identical."""
+            s2 = 1504
+            m2 = wga.aead_message_stride(s2)
+            pk = torch.empty(n * s2, dtype=torch.uint8, device=dev)
+            wga.synth_fill(pk, seed + 1, counter_base=rank * n * s2)
+            d2 = wga.synth_desc_stride(n, s2, s2, 1, seed + 1, rank * n, device=dev)
+            wga.synth_headers(pk, d2, seed + 1, rank * n)
+            wga.store_l4csum(pk, d2, wga.calc_l4_checksum_desc(pk, d2))
+            msgs = torch.empty(n * m2, dtype=torch.uint8, device=dev)
+            wga.aead_encrypt_batch(pk, s2, key, rx, c0, out=msgs)
+            del pk
+            pt = torch.empty(n * (m2 - 32), dtype=torch.uint8, device=dev)
+            dst = torch.empty(n, dtype=torch.int8, device=dev)
+            vd = torch.empty(n, dtype=torch.uint8, device=dev)
+            l4a = torch.empty(n, dtype=torch.uint16, device=dev)
+            vf = torch.empty(n, dtype=torch.uint8, device=dev)
+            l4f = torch.empty(n, dtype=torch.uint16, device=dev)
+            t_dec = timed(lambda: wga.aead_decrypt_batch(msgs, m2, key, out=pt, status=dst))
+            t_ver = timed(lambda: wga.verify_desc(pt, d2, verdict=vd, l4=l4a))  # plaintext i at i * 1504: d2
+            t_fused = timed(lambda: wga.aead_decrypt_verify_batch(msgs, m2, key, out=pt, status=dst, verdict=vf,
+                                                                  l4=l4f))
+            equal = bool(torch.equal(vd, vf) and torch.equal(l4a, l4f))
+            passing = int(torch.count_nonzero((vf & 3) == 3).item())
+            return {"packets": n, "packet_bytes": s2, "decrypt_ms": round(t_dec, 5), "verify_ms": round(t_ver, 5),
+                    "decrypt_plus_verify_ms": round(t_dec + t_ver, 5), "fused_ms": round(t_fused, 5),
+                    "fused_GiB_s": round(n * s2 / (t_fused * 1e-3) / 2**30, 1),
+                    "verdicts_equal_to_separate": equal, "packets_passing_both_gates": passing}
 
         def sample(npk):
             k = min(n, 1 << 16)  # ~98 MB: the scalar C oracle runs ~0.15 GB/s per core

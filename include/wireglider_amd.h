@@ -238,6 +238,18 @@ int wg_aead_encrypt_batch(const uint8_t *dev_in, uint64_t total_len, uint32_t se
 int wg_aead_decrypt_batch(const uint8_t *dev_in, uint64_t total_len, uint32_t segment_size, const uint8_t key[32],
                           uint8_t *dev_out, int8_t *dev_status, void *stream);
 
+/* wg_aead_decrypt_verify_batch: wg_aead_decrypt_batch, and in the same pass
+ * the decap verify gates of wg_verify_desc over every plaintext as it is
+ * produced (Peer::decrypt then evaluate_packet, worker/decap_ref.cpp:81-86,
+ * include/worker/evaluator.hpp:112-149), over the plaintext's libsodium
+ * length (the padded one, as the reference evaluates it): dev_verdict[i] =
+ * WG_VERDICT_* bits and dev_l4[i] = the L4 checksum result, exactly
+ * wg_verify_desc's on the plaintext; 0 / 0 for messages with status -1.
+ * The plaintext is read from HBM zero times more than decryption needs. */
+int wg_aead_decrypt_verify_batch(const uint8_t *dev_in, uint64_t total_len, uint32_t segment_size,
+                                 const uint8_t key[32], uint8_t *dev_out, int8_t *dev_status, uint8_t *dev_verdict,
+                                 uint16_t *dev_l4, void *stream);
+
 /* ------------------------------------------------------------------------
  * Host-memory path: the batch starts and ends in host memory
  * (tun read buffers, worker/encap.cpp:74-97; UDP GRO recvmsg buffers,

@@ -192,3 +192,52 @@ def test_round_trip_on_device(gpu, aead_k):
     for i in range(45):
         ln = 1460 if i < 44 else 1295
         assert np.array_equal(p[i * (mseg - 32): i * (mseg - 32) + ln], pts[i * 1460: i * 1460 + ln])
+
+
+@pytest.mark.parametrize("seg_pt", [1504, 1500, 9008, 64, 48, 20])
+def test_decrypt_verify_matches_oracle(gpu, aead_k, seg_pt):
+    """Decrypt + the decap verify gates in one pass (wg_aead_decrypt_verify_batch)
+    == the oracle's decrypt, then the oracle's evaluate_packet gates over each
+    plaintext at its libsodium (padded) length, as worker/decap_ref.cpp:81-86
+    hands it to push_packet: a 1,504-B packet (a multiple of 16) passes the IP
+    gates, a 1,500-B one cannot (its padded length is not its ip_len).  Mixed
+    v4/v6 x TCP/UDP with valid checksums, one corrupted payload byte, one
+    corrupted header byte, one bad tag, one rejected counter."""
+    import torch
+
+    wga = _wga()
+    rng = np.random.default_rng(seg_pt + 17)
+    key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    n = 120
+    buf = torch.empty(n * seg_pt, dtype=torch.uint8, device=gpu)
+    wga.synth_fill(buf, seg_pt)
+    desc = wga.synth_desc_stride(n, seg_pt, seg_pt, 1, seg_pt, 0, device=gpu)
+    wga.synth_headers(buf, desc, seg_pt, 0)
+    if seg_pt >= 48:
+        wga.store_l4csum(buf, desc, wga.calc_l4_checksum_desc(buf, desc))
+    torch.cuda.synchronize()
+    pts = buf.cpu().numpy().copy()
+    pts[3 * seg_pt + seg_pt - 1] ^= 0x20  # payload byte: L4 checksum fails
+    pts[5 * seg_pt + 13] ^= 0x01  # a v4 source-address byte (IP checksum) / v6 address byte (L4 checksum)
+    msgs = oracle.wg_encrypt_batch(key, 3, 77, pts, seg_pt).copy()
+    mseg = wga.aead_message_stride(seg_pt)
+    msgs[7 * mseg + mseg - 2] ^= 0x04  # tag
+    msgs[9 * mseg + 8: 9 * mseg + 16] = np.frombuffer((oracle.REJECT_AFTER_MESSAGES + 1).to_bytes(8, "little"), np.uint8)
+    exp_pt, exp_st = oracle.wg_decrypt_batch(key, msgs, mseg)
+    out, st, ver, l4 = wga.aead_decrypt_verify_batch(_dev(msgs, gpu), mseg, key)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(st.cpu().numpy()[:n], exp_st)
+    plen = mseg - 32
+    got_pt = out.cpu().numpy()[: n * plen]
+    ok = exp_st == 0
+    for i in np.nonzero(ok)[0]:
+        assert np.array_equal(got_pt[i * plen:(i + 1) * plen], exp_pt[i * plen:(i + 1) * plen]), i
+    d = np.zeros(n, dtype=oracle.PKT_DESC)
+    d["offset"] = np.arange(n, dtype=np.uint64) * plen
+    d["len"] = plen
+    ev, el4 = oracle.verify_desc(exp_pt, d)
+    ev[~ok], el4[~ok] = 0, 0
+    np.testing.assert_array_equal(ver.cpu().numpy()[:n], ev)
+    np.testing.assert_array_equal(l4.cpu().numpy()[:n], el4)
+    if seg_pt == 1504:  # the gates really ran: most packets pass both, the corrupted ones do not
+        assert np.count_nonzero(ev & 0x03 == 0x03) >= n - 4 and ev[3] & 0x02 == 0

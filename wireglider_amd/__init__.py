@@ -42,6 +42,7 @@ EXPORTED_SYMBOLS = (
     "wg_gro_finalize",
     "wg_aead_encrypt_batch",
     "wg_aead_decrypt_batch",
+    "wg_aead_decrypt_verify_batch",
     "wg_l4csum_uniform_host",
     "wg_host_release",
     "wg_host_alloc",
@@ -114,6 +115,7 @@ def _load() -> ctypes.CDLL:
         "wg_gro_finalize": (i32, [u8p, vp, u64, vp]),
         "wg_aead_encrypt_batch": (i32, [u8p, u64, u32, ctypes.c_char_p, u32, u64, u8p, vp, vp]),
         "wg_aead_decrypt_batch": (i32, [u8p, u64, u32, ctypes.c_char_p, u8p, vp, vp]),
+        "wg_aead_decrypt_verify_batch": (i32, [u8p, u64, u32, ctypes.c_char_p, u8p, vp, vp, vp, vp]),
         "wg_l4csum_uniform_host": (i32, [u8p, u64, u32, u16, u32, vp]),
         "wg_host_release": (i32, []),
         "wg_host_alloc": (i32, [ctypes.POINTER(ctypes.c_void_p), u64]),
@@ -358,6 +360,39 @@ def aead_decrypt_batch(msgs, segment_size: int, key: bytes, out=None, status=Non
                                        status.data_ptr(), _stream_ptr(stream, msgs))
     _check(rc, "wg_aead_decrypt_batch")
     return out, status
+
+
+def aead_decrypt_verify_batch(msgs, segment_size: int, key: bytes, out=None, status=None, verdict=None, l4=None,
+                              stream=None):
+    """aead_decrypt_batch and, in the same pass, the decap verify gates
+    (wg_verify_desc, evaluate_packet: include/worker/evaluator.hpp:112-149)
+    over every plaintext at its libsodium (padded) length, as
+    worker/decap_ref.cpp:81-86 evaluates it.  Returns (out, status, verdict,
+    l4)."""
+    torch = _torch()
+    _require_cuda(msgs, "msgs")
+    if len(key) != 32:
+        raise WireGliderError("key must be 32 bytes")
+    n = nr_segments(msgs.numel(), segment_size)
+    need = n * max(segment_size - 32, 0)
+    if out is None:
+        out = torch.empty(max(need, 1), dtype=torch.uint8, device=msgs.device)
+    _check_out(out, need, torch.uint8, msgs, "out")
+    if status is None:
+        status = torch.empty(max(n, 1), dtype=torch.int8, device=msgs.device)
+    _check_out(status, n, torch.int8, msgs, "status")
+    if verdict is None:
+        verdict = torch.empty(max(n, 1), dtype=torch.uint8, device=msgs.device)
+    _check_out(verdict, n, torch.uint8, msgs, "verdict")
+    if l4 is None:
+        l4 = torch.empty(max(n, 1), dtype=torch.uint16, device=msgs.device)
+    _check_out(l4, n, torch.uint16, msgs, "l4")
+    with _on(msgs):
+        rc = lib.wg_aead_decrypt_verify_batch(msgs.data_ptr(), msgs.numel(), segment_size, bytes(key),
+                                              out.data_ptr(), status.data_ptr(), verdict.data_ptr(), l4.data_ptr(),
+                                              _stream_ptr(stream, msgs))
+    _check(rc, "wg_aead_decrypt_verify_batch")
+    return out, status, verdict, l4
 
 
 def calc_l4_checksum_host(buf: bytes | bytearray | memoryview, segment_size: int, isv6: bool,

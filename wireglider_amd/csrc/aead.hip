@@ -403,7 +403,62 @@ struct AeadParams {
     uint64_t counter0;   // encrypt: counter of packet 0
     AeadKey key;
     uint32_t grp;        // aead_kernel<0, ...>: lanes per packet (1..32)
+    uint8_t *verdict;    // decrypt + verify: WG_VERDICT_* per message (kVer)
+    uint16_t *l4;        // decrypt + verify: the L4 checksum result per message (kVer)
 };
+
+// The decap verify gates (wg_verify_desc, SURVEY §8 f1: evaluate_packet,
+// include/worker/evaluator.hpp:112-149, worker/evaluator.cpp:14-58) decided
+// from a packet's first 64 bytes R[16] (zero past len): the verdict bits,
+// the protocol, the header length, whether the L4 checksum is computed, and
+// the sums the L4 checksum needs besides the packet's own word sum: the
+// header words [0, ihs) (subtracted) and the pseudo-header addresses.
+struct HdrGate {
+    uint32_t v, proto, ihs, hsum, asum;
+    bool l4;
+};
+
+__device__ __forceinline__ uint32_t hsum32(uint32_t w) { return (w & 0xffffu) + (w >> 16); }
+
+__device__ __forceinline__ HdrGate hdr_gate(const uint32_t R[16], uint32_t len) {
+    HdrGate h{0u, 0u, 20u, 0u, 0u, false};
+    if (len < 1u)
+        return h;
+    const uint32_t b0 = R[0] & 0xffu;
+    const bool v6 = (b0 >> 4) == 6;
+    h.v = v6 ? WG_VERDICT_V6 : 0u;
+    h.ihs = v6 ? 40u : 20u;
+    bool ip_ok = false;
+    if (len >= h.ihs && len <= 65535u) {  // evaluator.hpp:118-121
+        if (!v6) {
+            const uint32_t hs = hsum32(R[0]) + hsum32(R[1]) + hsum32(R[2]) + hsum32(R[3]) + hsum32(R[4]);
+            ip_ok = (b0 & 0xfu) == 5u &&                      // ip_hl, evaluator.cpp:19
+                    len == bswap16(R[0] >> 16) &&              // ip_len, :21
+                    (bswap16(R[1] >> 16) & ~0x4000u) == 0 &&  // ip_off & ~IP_DF, :24
+                    fold16_32(hs) == 0xffffu;                 // header checksum == 0, :27
+            h.proto = (R[2] >> 8) & 0xffu;
+        } else {
+            ip_ok = len - 40u == bswap16(R[1] & 0xffffu);  // ip6_plen, :47
+            h.proto = (R[1] >> 16) & 0xffu;
+        }
+    }
+    if (ip_ok) {
+        h.v |= WG_VERDICT_IP_OK;
+        if (h.proto == 6u) {
+            h.v |= WG_VERDICT_TCP;
+            h.l4 = len - h.ihs > 20u;  // evaluator.hpp:61
+        } else if (h.proto == 17u) {
+            h.v |= WG_VERDICT_UDP;
+            h.l4 = len - h.ihs > 8u;  // evaluator.hpp:91
+        }
+    }
+#pragma unroll
+    for (uint32_t m = 0; m < 10; m++) {
+        h.hsum += 4u * m < h.ihs ? hsum32(R[m]) : 0u;
+        h.asum += (v6 ? (m >= 2u && m < 10u) : (m == 3u || m == 4u)) ? hsum32(R[m]) : 0u;  // v6 8-39, v4 12-19
+    }
+    return h;
+}
 
 constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/proto/proto.hpp:36
 
@@ -417,7 +472,16 @@ constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/prot
 // G = 0: the group size is p.grp (any 1..32, set at launch as the lanes a
 // packet needs: a 1,500-B packet's 25 blocks at K = 3 take 9 lanes, 7
 // packets fill 63 of a wave's 64 lanes), one pass.
-template <int G, int K, bool kDec, bool kP = false>
+// kVer (decrypt only): the decap verify gates over each plaintext as it is
+// produced (decrypt + evaluate_packet in one pass: no second read of the
+// plaintext from HBM).  Every lane sums its plaintext's 16-bit words (blocks
+// start at even offsets: packet-relative pairing); the lane holding payload
+// block 0 decides the header gates from its 16 dwords (hdr_gate); the L4
+// sum is the group's total minus the header words [0, ihs) plus the
+// pseudo-header — exact, because subtracting x mod 0xFFFF is adding
+// 0xFFFF - x and the total is never zero (the protocol word), so its fold
+// only depends on the sum mod 0xFFFF.
+template <int G, int K, bool kDec, bool kP = false, bool kVer = false>
 __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     constexpr bool kFlex = G == 0;
     const uint32_t GG = kFlex ? p.grp : (uint32_t)G;  // lanes per packet
@@ -497,6 +561,8 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     const uint32_t passes = G == 64 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)npass) : 1u;
     L5 F = l5_one();
     L5 acc = l5_zero();
+    uint32_t vsum = 0;                          // kVer: this lane's plaintext word sum
+    HdrGate gate{0u, 0u, 20u, 0u, 0u, false};   // kVer: set in the lane holding payload block 0
     for (uint32_t pp = passes; pp-- > 0;) {
         const uint32_t cf = pp * kPass + g * (uint32_t)K;  // this lane's first counter
         // This lane's 16-B Poly1305 blocks in the pass follow from the
@@ -581,6 +647,13 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                 } else {
                     kb[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nin);  // plaintext
                 }
+            }
+            if constexpr (kVer) {
+                // the plaintext's words; the first 64 bytes decide the gates
+#pragma unroll
+                for (int m = 0; m < 16; m++) vsum += hsum32(kb[m]);
+                if (has && d == 0u)
+                    gate = hdr_gate(kb, plen);
             }
             // decrypt stores the plaintext now; a bad tag zeroes it below
             // (the final bytes are libsodium's either way)
@@ -695,6 +768,33 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
         }
         if (g == 0u && live)
             p.status[ii] = (int8_t)(st ? st : (tag_ok ? 0 : -1));
+        if constexpr (kVer) {
+            // the group's word sum (< 2^32: at most 32,768 words), to every lane
+            uint32_t tsum = vsum;
+            if constexpr (kFlex) {
+                for (uint32_t o = 1; o < GG; o <<= 1) {
+                    const uint32_t t = grp_down_rt(tsum, lane, g, GG, o);
+                    if (g + o < GG)
+                        tsum += t;
+                }
+                tsum = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(base_lane << 2), (int)tsum);
+            } else {
+                tsum = grp_sum<G ? G : 1>(tsum, lane);
+            }
+            // the lane holding payload block 0 (counter 1) writes the verdict
+            const uint32_t h0 = 1u / (uint32_t)K < GG ? 1u / (uint32_t)K : 0u;  // (an empty plaintext: a 1-lane group)
+            if (g == h0 && live) {
+                const bool ok = act && tag_ok;  // rejected / failed messages: no packet
+                uint32_t c = 0;
+                if (ok && gate.l4) {
+                    const uint32_t T = fold16_32(tsum) + (0xffffu - fold16_32(gate.hsum)) + fold16_32(gate.asum) +
+                                       (gate.proto << 8) + bswap16((plen - gate.ihs) & 0xffffu);
+                    c = ~fold16_32(T) & 0xffffu;
+                }
+                p.verdict[ii] = (uint8_t)(ok ? (gate.v | (gate.l4 && c == 0u ? WG_VERDICT_L4_OK : 0u)) : 0u);
+                p.l4[ii] = (uint16_t)c;
+            }
+        }
     }
 }
 
@@ -712,6 +812,13 @@ static AeadKey key_words(const uint8_t key[32]) {
 
 template <int G, int K, bool kDec>
 static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
+    if constexpr (kDec) {
+        if (p.verdict) {  // decrypt + verify (always with the pair interleave where it applies)
+            constexpr bool kPv = K >= 2 && G < 64;
+            hipLaunchKernelGGL((aead_kernel<G, K, true, kPv, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+            return;
+        }
+    }
     if constexpr (K >= 2 && G < 64) {
         if (tune().aead_pair) {
             hipLaunchKernelGGL((aead_kernel<G, K, kDec, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
@@ -813,6 +920,29 @@ extern "C" int wg_aead_decrypt_batch(const uint8_t *dev_in, uint64_t total_len, 
     p.in = dev_in;
     p.out = dev_out;
     p.status = dev_status;
+    p.total_len = total_len;
+    p.n = (total_len + segment_size - 1) / segment_size;
+    p.seg = segment_size;
+    p.key = key_words(key);
+    return launch_aead<true>(p, segment_size > 32u ? segment_size - 32u : 0u, static_cast<hipStream_t>(stream));
+}
+
+
+extern "C" int wg_aead_decrypt_verify_batch(const uint8_t *dev_in, uint64_t total_len, uint32_t segment_size,
+                                            const uint8_t key[32], uint8_t *dev_out, int8_t *dev_status,
+                                            uint8_t *dev_verdict, uint16_t *dev_l4, void *stream) {
+    if (!segment_size || segment_size > 65535u + 32u || !key)
+        return WG_ERR_INVALID;
+    if (!total_len)
+        return WG_OK;
+    if (!dev_in || !dev_out || !dev_status || !dev_verdict || !dev_l4)
+        return WG_ERR_INVALID;
+    AeadParams p{};
+    p.in = dev_in;
+    p.out = dev_out;
+    p.status = dev_status;
+    p.verdict = dev_verdict;
+    p.l4 = dev_l4;
     p.total_len = total_len;
     p.n = (total_len + segment_size - 1) / segment_size;
     p.seg = segment_size;
