@@ -65,6 +65,17 @@ def test_invalid_args_rejected_without_gpu():
     # the kernel-shaped read probe takes segments of at most 2 KiB
     assert wga.lib.wg_probe_read(16, 1 << 20, 16, 1, 4096, None) == -1
     assert wga.lib.wg_probe_read(16, 100, 16, 1, 1500, None) == -1
+    # AEAD batches: segment size 0 / past 64 KiB, no key, misaligned or missing outputs
+    key = bytes(32)
+    assert wga.lib.wg_aead_encrypt_batch(16, 100, 0, key, 1, 0, 16, None, None) == -1
+    assert wga.lib.wg_aead_encrypt_batch(16, 100, 65536, key, 1, 0, 16, None, None) == -1
+    assert wga.lib.wg_aead_encrypt_batch(16, 100, 50, None, 1, 0, 16, None, None) == -1
+    assert wga.lib.wg_aead_encrypt_batch(16, 100, 50, key, 1, 0, 17, None, None) == -1  # out not 16-B aligned
+    assert wga.lib.wg_aead_decrypt_batch(16, 100, 64, key, 16, None, None) == -1  # status required
+    assert wga.lib.wg_aead_decrypt_verify_batch(16, 100, 64, key, 16, 16, None, 16, None) == -1  # verdict required
+    assert wga.lib.wg_aead_decrypt_verify_batch(16, 100, 64, key, 16, 16, 16, None, None) == -1  # l4 required
+    assert wga.lib.wg_aead_decrypt_verify_batch(16, 100, 65536 + 33, key, 16, 16, 16, 16, None) == -1
+    assert wga.lib.wg_aead_decrypt_verify_batch(16, 0, 64, key, 16, 16, 16, 16, None) == 0  # empty batch: no-op
 
 
 DROPIN_TEST = r"""
