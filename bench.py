@@ -72,7 +72,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="config2",
-                    choices=["config1", "config2", "config3", "config3udp", "config4", "config5", "verify", "gro",
+                    choices=["config1", "config2", "config3", "config3udp", "config4", "config5", "verify", "gro", "encap",
                              "aead"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-strong", action="store_true", help="skip the config 5 strong-scaling companion")
@@ -155,6 +155,8 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                   for r in range(world)]
         return Workload(launch, n, n * SEG, n * SEG + 2 * n + 16 * n, cfg, "strong", buf,
                         "wg::l4csum_split_kernel<1,nt> (l4_small=5)", lo, out, desc, sample, counts, probe_run=SEG)
+    if name == "encap":
+        return build_encap(wga, torch, rank, world, dev)
     if name in ("config3", "config3udp"):
         udp = name == "config3udp"
         n, in_stride, out_stride = 1 << 18, 65536, 73216  # outbuf stride of worker/encap.cpp:26
@@ -582,6 +584,84 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                     rank * n, out, desc, sample, [n] * world, post=post)
 
 
+def build_encap(wga, torch, rank: int, world: int, dev) -> Workload:
+    """The encap worker's data path on the device (worker/encap.cpp:107-160):
+    config 3's 262,144 x 64 KiB tun super-buffers -> do_tun_gso_split
+    (wg_gso_split) -> Peer::encrypt for every segment in order with
+    encrypt_nonce++ (wg_encap_encrypt), one peer; per step both calls, no
+    host round trip.  value = GiB/s of tun input."""
+    import numpy as np
+
+    n, in_stride, out_stride, in_len = 1 << 18, 65536, 73216, 65535
+    hdr, gso, seed = 40, 1460, 0x5EED00E5
+    seg = hdr + gso
+    nseg = (in_len - hdr + gso - 1) // gso
+    out_len = in_len - hdr + nseg * hdr
+    mstride = wga.aead_message_stride(seg)
+    last = out_len - (nseg - 1) * seg
+    mbytes = (nseg - 1) * mstride + wga.aead_message_stride(last)
+    buf = torch.empty(n * in_stride, dtype=torch.uint8, device=dev)
+    wga.synth_fill(buf, seed, counter_base=rank * n * in_stride)
+    pd = np.zeros(n, dtype=wga.PKT_DESC_DTYPE)
+    pd["offset"] = np.arange(n, dtype=np.uint64) * in_stride
+    pd["len"], pd["csum_start"], pd["flags"] = in_len, 20, 2
+    wga.synth_headers(buf, torch.from_numpy(pd.view(np.uint8).copy()).to(dev), seed, rank * n)
+    gd = np.zeros(n, dtype=wga.GSO_DESC_DTYPE)
+    gd["in_offset"] = pd["offset"]
+    gd["out_offset"] = np.arange(n, dtype=np.uint64) * out_stride
+    gd["in_len"], gd["out_cap"] = in_len, out_stride
+    gd["vnet"]["flags"], gd["vnet"]["gso_type"], gd["vnet"]["gso_size"] = 1, 1, gso
+    gd["vnet"]["csum_start"], gd["vnet"]["csum_offset"] = 20, 16
+    d_desc = torch.from_numpy(gd.view(np.uint8).copy()).to(dev)
+    outb = torch.empty(n * out_stride, dtype=torch.uint8, device=dev)
+    res = torch.empty(n * wga.GSO_RESULT_BYTES, dtype=torch.uint8, device=dev)
+    mcap = nseg * mstride
+    msg_off_np = np.arange(n, dtype=np.int64) * mcap
+    msg_off = torch.from_numpy(msg_off_np).to(dev)
+    msgs = torch.empty(n * mcap, dtype=torch.uint8, device=dev)
+    eres = torch.zeros(n * wga.ENCAP_RESULT_BYTES, dtype=torch.uint8, device=dev)
+    work = torch.empty(n + 1024, dtype=torch.int32, device=dev)
+    tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    key = np.random.default_rng(seed).integers(0, 256, 32, dtype=np.uint8).tobytes()
+    rx, c0 = 0x0E0CA9, 1 + rank * n * nseg
+
+    def launch():
+        wga.gso_split(buf, d_desc, outb, results=res)
+        wga.encap_encrypt(buf, outb, d_desc, res, key, rx, c0, msg_off, mcap, nseg, seg, msgs, results=eres,
+                          work=work, total=tot)
+
+    def post():
+        # every super-buffer: 45 messages at consecutive counters, and a
+        # sample of them decrypted back to their GSO segments on the device
+        e = eres.cpu().numpy().view(wga.ENCAP_RESULT_DTYPE)
+        ok = bool(np.all(e["nmsg"] == nseg) and np.all(e["msg_bytes"] == mbytes)
+                  and np.array_equal(e["counter0"], c0 + np.arange(n, dtype=np.uint64) * nseg))
+        k = 256
+        full = torch.cat([msgs[int(msg_off_np[i]): int(msg_off_np[i]) + (nseg - 1) * mstride] for i in range(k)])
+        pt, st = wga.aead_decrypt_batch(full, mstride, key)
+        segs = torch.cat([outb[i * out_stride: i * out_stride + (nseg - 1) * seg] for i in range(k)])
+        torch.cuda.synchronize()
+        same = bool(torch.equal(pt.view(-1, mstride - 32)[:, :seg].reshape(-1), segs))
+        return {"results_ok": ok, "messages_total": int(tot.cpu()[0]), "sample_super_buffers_decrypted": k,
+                "sample_plaintexts_equal_segments": same, "sample_status_nonzero": int(torch.count_nonzero(st).item())}
+
+    def sample(_npk):
+        k = min(n, 1024)
+        return (buf[: k * in_stride].cpu().numpy(), msgs[: k * mcap].cpu().numpy(),
+                ("encap", gd[:k].copy(), k * out_stride, key, rx, c0, seg, nseg, mcap, mbytes))
+
+    cfg = {"workload": "encap: config 3's 262,144 x 64 KiB IPv4/TCP tun super-buffers -> do_tun_gso_split (45 x "
+                       "1460 B segments) -> Peer::encrypt per segment, one peer, consecutive counters (the encap "
+                       "worker, worker/encap.cpp:107-160)", "super_buffers_per_gpu": n, "segments_per_buffer": nseg,
+           "message_stride": mstride, "parallelism": f"shard{world}"}
+    alg = (n * in_len + n * out_len + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES)  # the split
+           + n * out_len + n * mbytes + n * (wga.ENCAP_RESULT_BYTES + 8))           # the encryption
+    return Workload(launch, n, n * in_len, alg, cfg, "weak", buf,
+                    "wg_gso_split (3 kernels) + wg_encap_encrypt (2 scan kernels + wg::aead_kernel<0,3,false,true,false,true>)",
+                    rank * n, sample=sample, counts=[n] * world, post=post,
+                    metric="device-resident GiB/s of tun input, GSO split + data-message encryption (encap worker)")
+
+
 def settle(torch, fn, seconds: float) -> int:
     """Run `fn` back to back until `seconds` of wall time have passed, so the
     timed region starts at the sustained clock/memory state rather than the
@@ -632,6 +712,11 @@ def measured_read_peak(torch, wga, buf, iters: int = 30, run_bytes: int = 0) -> 
             torch.cuda.synchronize()
             rates[name] = max(rates.get(name, 0.0), round(nb * iters / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1))
     return {"best": max(rates.values()), "variants": rates, "bytes": int(buf.numel())}
+
+
+def wga_stride(seg: int) -> int:
+    """Peer::expected_encrypt_size (include/proto/proto.hpp:266-269)."""
+    return 16 + (seg + 15) // 16 * 16 + 16
 
 
 def cpu_baseline(sample_fn, seconds: float):
@@ -742,6 +827,43 @@ def cpu_baseline(sample_fn, seconds: float):
             oss = {"openssl_evp_chacha20_poly1305": f"unavailable: {e}"}
         nbytes = host.size
         npk = host.size // seg
+    elif kind[0] == "encap":
+        # do_tun_gso_split restatement (pthreads) then Peer::encrypt per
+        # segment: exact messages for the parity check from the oracle per
+        # super-buffer; timed: the split + OpenSSL's EVP ChaCha20-Poly1305
+        # over the same segments as one batch (each super-buffer's shorter
+        # last segment at full size: +0.3 % work)
+        _, gk, out_bytes, key, rx, c0, seg, nseg, mcap, mbytes = kind
+        seg_out = np.zeros(out_bytes, np.uint8)
+        st = oracle.gso_split_desc(host, gk, seg_out, threads)
+        exp = np.zeros(gk.size * mcap, np.uint8)
+        ostride = out_bytes // gk.size
+        for i in range(gk.size):
+            ol = int(gk["in_len"][i]) - 40 + nseg * 40
+            m = oracle.wg_encrypt_batch(key, rx, c0 + i * nseg, seg_out[i * ostride: i * ostride + ol], seg)
+            exp[i * mcap: i * mcap + m.size] = m
+            gpu_out[i * mcap + m.size: (i + 1) * mcap] = 0  # only the messages are compared
+        segs = np.ascontiguousarray(seg_out.reshape(gk.size, ostride)[:, : nseg * seg]).reshape(-1)
+        enc_out = np.zeros(gk.size * nseg * wga_stride(seg) + 64, np.uint8)
+        sub = gk[: max(1, gk.size // 8)]
+        t0 = time.perf_counter()
+        oracle.gso_split_desc(host, sub, seg_out, 1)
+        t_g1 = (time.perf_counter() - t0) * gk.size / sub.size
+        t0 = time.perf_counter()
+        oracle.gso_split_desc(host, gk, seg_out, threads)
+        t_gn = time.perf_counter() - t0
+        ssub = segs[: segs.size // 8 // seg * seg]
+        t0 = time.perf_counter()
+        oracle.openssl_encrypt_batch(key, rx, c0, ssub, seg, enc_out, 1)
+        t_e1 = (time.perf_counter() - t0) * segs.size / ssub.size
+        t0 = time.perf_counter()
+        oracle.openssl_encrypt_batch(key, rx, c0, segs, seg, enc_out, threads)
+        t_en = time.perf_counter() - t0
+        t_1core, t_all = t_g1 + t_e1, t_gn + t_en
+        nbytes = int(gk["in_len"].astype(np.int64).sum())
+        npk = gk.size
+        if np.any(st != 0):
+            gpu_out = None
     elif kind[0] == "checksum":
         # checksum(buf, 0) per buffer (BASELINE config 1)
         d = kind[1]
@@ -777,7 +899,9 @@ def cpu_baseline(sample_fn, seconds: float):
     what = {"verify": "decap verify gates restatement (orc_verify)", "gro": "GRO finalize restatement",
             "gso": "do_tun_gso_split restatement, output bytes compared",
             "checksum": "checksum(span, 0) restatement",
-            "aead": "Peer::encrypt restatement over RFC 8439 (scalar C), message bytes compared"}.get(
+            "aead": "Peer::encrypt restatement over RFC 8439 (scalar C), message bytes compared",
+            "encap": "do_tun_gso_split restatement + OpenSSL EVP ChaCha20-Poly1305 timed; messages compared with "
+                     "the RFC 8439 restatement"}.get(
                 kind[0], "calc_l4_checksum restatement")
     nofold = "AVX2 vector nofold (oracle/csum_oracle.c nofold_avx2)" if oracle.have_avx2() else "scalar nofold"
     return {

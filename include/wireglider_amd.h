@@ -250,6 +250,37 @@ int wg_aead_decrypt_verify_batch(const uint8_t *dev_in, uint64_t total_len, uint
                                  const uint8_t key[32], uint8_t *dev_out, int8_t *dev_status, uint8_t *dev_verdict,
                                  uint16_t *dev_l4, void *stream);
 
+/* Encap: every segment of wg_gso_split's PacketBatches encrypted for ONE peer,
+ * super-buffer by super-buffer and segment by segment, with the counters the
+ * reference's encap worker would use (worker/encap.cpp:136-141: Peer::encrypt
+ * per segment, encrypt_nonce++): counter0 for super-buffer 0's first
+ * segment, then consecutive over every message.  No host round trip: the
+ * segment counts come from dev_gso_res on the device.
+ *   dev_in / dev_seg / dev_desc / dev_gso_res: wg_gso_split's dev_in, dev_out,
+ *     dev_desc and dev_res (passthrough batches are read from dev_in);
+ *   dev_msg_offset[i]: where super-buffer i's messages go in dev_msgs
+ *     (16-B aligned), msg_cap bytes available there; its messages follow each
+ *     other at stride 32 + pad16(segment_size), the last one shorter — the
+ *     reference's outbuf layout (worker/encap.cpp:131-141,161-168);
+ *   max_segments / max_segment_size: bounds over the batch (super-buffers
+ *     past them, or whose messages exceed msg_cap, get nmsg 0);
+ *   dev_res[i]: counter0, nmsg (0 for GSO errors), msg_bytes;
+ *   dev_work: 4 * (n + 1024) bytes of scratch; dev_total (nullable): messages
+ *     in all, i.e. counter0 + *dev_total is the peer's next encrypt_nonce.
+ * n <= 2^20 super-buffers per call.  A message whose counter reaches
+ * RejectAfterMessages is not written (the reference's encrypt refuses it). */
+typedef struct wg_encap_result {
+    uint64_t counter0;
+    uint32_t nmsg;
+    uint32_t msg_bytes;
+} wg_encap_result; /* 16 bytes */
+
+int wg_encap_encrypt(const uint8_t *dev_in, const uint8_t *dev_seg, const wg_gso_desc *dev_desc,
+                     const wg_gso_result *dev_gso_res, uint64_t n, const uint8_t key[32], uint32_t receiver_index,
+                     uint64_t counter0, const uint64_t *dev_msg_offset, uint32_t msg_cap, uint32_t max_segments,
+                     uint32_t max_segment_size, uint8_t *dev_msgs, wg_encap_result *dev_res, uint32_t *dev_work,
+                     uint64_t *dev_total, void *stream);
+
 /* ------------------------------------------------------------------------
  * Host-memory path: the batch starts and ends in host memory
  * (tun read buffers, worker/encap.cpp:74-97; UDP GRO recvmsg buffers,

@@ -1,0 +1,98 @@
+"""The encap worker's step on the device (wg_encap_encrypt, SURVEY §8 f4 on
+A6's output): every segment of wg_gso_split's PacketBatches encrypted for one
+peer with consecutive counters in super-buffer / segment order, as
+worker/encap.cpp:136-141 runs Peer::encrypt per segment with
+encrypt_nonce++ — compared message for message with the oracle's
+wg_encrypt_batch over each PacketBatch (the GSO output itself is pinned in
+tests/test_gpu_gso.py).  Random super-buffers of every GSO type: splits,
+passthrough (GSO_NONE, unknown types), errors (no messages), batches past
+the segment / size / capacity bounds (no messages)."""
+import numpy as np
+import pytest
+
+import oracle
+from test_gpu_gso import random_case
+
+pytestmark = pytest.mark.gpu
+
+
+def _wga():
+    import wireglider_amd as wga
+
+    return wga
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+@pytest.mark.parametrize("knobs", [{}, {"aead_k": 2, "aead_flex": 0}, {"aead_k": 1}],
+                         ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()) or "default")
+def test_encap_matches_oracle(gpu, seed, knobs):
+    import torch
+
+    wga = _wga()
+    saved = {k: wga.tune_get(k) for k in knobs}
+    for k, v in knobs.items():
+        wga.tune_set(k, v)
+    rng = np.random.default_rng(seed)
+    cases = [random_case(rng) for _ in range(250)]
+    n = len(cases)
+    desc = np.zeros(n, dtype=wga.GSO_DESC_DTYPE)
+    in_off = out_off = 0
+    for k, (pkt, vnet, cap) in enumerate(cases):
+        in_off += int(rng.integers(0, 17))
+        out_off += int(rng.integers(0, 17))
+        if cap is None:
+            cap = len(pkt) + (len(pkt) // max(1, vnet.get("gso_size", 1)) + 2) * 200
+        desc[k]["in_offset"], desc[k]["out_offset"] = in_off, out_off
+        desc[k]["in_len"], desc[k]["out_cap"] = len(pkt), cap
+        for f in ("flags", "gso_type", "hdr_len", "gso_size", "csum_start", "csum_offset"):
+            desc[k]["vnet"][f] = vnet.get(f, 0)
+        in_off += len(pkt)
+        out_off += cap
+    inbuf = np.zeros(in_off + 64, np.uint8)
+    for k, (pkt, _, _) in enumerate(cases):
+        o = int(desc[k]["in_offset"])
+        inbuf[o:o + len(pkt)] = np.frombuffer(pkt, np.uint8)
+    d_in = torch.from_numpy(inbuf).to(gpu)
+    d_out = torch.zeros(out_off + 64, dtype=torch.uint8, device=gpu)
+    d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(gpu)
+    d_res = wga.gso_split(d_in, d_desc, d_out)
+    max_seg, max_size, cap = 48, 9100, 48 * (32 + 9104)
+    cap_small = 7000  # some super-buffers' messages will not fit: nmsg 0
+    msg_off = np.arange(n, dtype=np.int64) * cap
+    msgs = torch.full((n * cap + 64,), 0xEE, dtype=torch.uint8, device=gpu)
+    key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    c0 = int(rng.choice([1, (1 << 32) - 40]))
+    m_cap = cap_small if seed == 12 else cap
+    eres, total = wga.encap_encrypt(d_in, d_out, d_desc, d_res, key, 0xBEEF, c0, torch.from_numpy(msg_off).to(gpu),
+                                    m_cap, max_seg, max_size, msgs)
+    torch.cuda.synchronize()
+    for k, v in saved.items():
+        wga.tune_set(k, v)
+    g_in, g_out = d_in.cpu().numpy(), d_out.cpu().numpy()
+    r = d_res.cpu().numpy().view(wga.GSO_RESULT_DTYPE)
+    e = eres.cpu().numpy().view(wga.ENCAP_RESULT_DTYPE)
+    got = msgs.cpu().numpy()
+    ctr, n_msgs = c0, 0
+    for i in range(n):
+        S, ol = int(r[i]["segment_size"]), int(r[i]["out_len"])
+        ns = nb = 0
+        if int(r[i]["status"]) == 0 and S and ol:
+            ns = (ol + S - 1) // S
+            last = ol - (ns - 1) * S
+            nb = (ns - 1) * (32 + (S + 15) // 16 * 16) + 32 + (last + 15) // 16 * 16
+            if ns > max_seg or S > max_size or nb > m_cap:
+                ns = nb = 0
+        assert (int(e[i]["nmsg"]), int(e[i]["msg_bytes"])) == (ns, nb), i
+        if ns:
+            assert int(e[i]["counter0"]) == ctr, i
+            src = (g_in[int(desc[i]["in_offset"]):] if int(r[i]["passthrough"]) else g_out[int(desc[i]["out_offset"]):])
+            exp = oracle.wg_encrypt_batch(key, 0xBEEF, ctr, src[:ol], S)
+            o = int(msg_off[i])
+            assert exp.size == nb
+            np.testing.assert_array_equal(got[o:o + nb], exp, err_msg=f"super-buffer {i}")
+            assert np.all(got[o + nb:o + min(m_cap, cap)] == 0xEE), i  # nothing past its messages
+        else:
+            assert np.all(got[int(msg_off[i]):int(msg_off[i]) + 64] == 0xEE), i
+        ctr += ns
+        n_msgs += ns
+    assert int(total.cpu()[0]) == n_msgs and n_msgs > 50

@@ -43,6 +43,7 @@ EXPORTED_SYMBOLS = (
     "wg_aead_encrypt_batch",
     "wg_aead_decrypt_batch",
     "wg_aead_decrypt_verify_batch",
+    "wg_encap_encrypt",
     "wg_l4csum_uniform_host",
     "wg_host_release",
     "wg_host_alloc",
@@ -116,6 +117,8 @@ def _load() -> ctypes.CDLL:
         "wg_aead_encrypt_batch": (i32, [u8p, u64, u32, ctypes.c_char_p, u32, u64, u8p, vp, vp]),
         "wg_aead_decrypt_batch": (i32, [u8p, u64, u32, ctypes.c_char_p, u8p, vp, vp]),
         "wg_aead_decrypt_verify_batch": (i32, [u8p, u64, u32, ctypes.c_char_p, u8p, vp, vp, vp, vp]),
+        "wg_encap_encrypt": (i32, [u8p, u8p, vp, vp, u64, ctypes.c_char_p, u32, u64, vp, u32, u32, u32, u8p, vp, vp,
+                                   vp, vp]),
         "wg_l4csum_uniform_host": (i32, [u8p, u64, u32, u16, u32, vp]),
         "wg_host_release": (i32, []),
         "wg_host_alloc": (i32, [ctypes.POINTER(ctypes.c_void_p), u64]),
@@ -393,6 +396,55 @@ def aead_decrypt_verify_batch(msgs, segment_size: int, key: bytes, out=None, sta
                                               _stream_ptr(stream, msgs))
     _check(rc, "wg_aead_decrypt_verify_batch")
     return out, status, verdict, l4
+
+
+ENCAP_RESULT_BYTES = 16
+
+
+def _encap_dtype():
+    import numpy as np
+
+    d = np.dtype([("counter0", "<u8"), ("nmsg", "<u4"), ("msg_bytes", "<u4")])
+    assert d.itemsize == ENCAP_RESULT_BYTES
+    return d
+
+
+ENCAP_RESULT_DTYPE = _encap_dtype()
+
+
+def encap_encrypt(inbuf, seg_out, gso_desc, gso_results, key: bytes, receiver_index: int, counter0: int, msg_offset,
+                  msg_cap: int, max_segments: int, max_segment_size: int, msgs, results=None, work=None, total=None,
+                  stream=None):
+    """Encap worker step (worker/encap.cpp:136-141) after gso_split: every
+    segment of every super-buffer's PacketBatch encrypted for one peer, with
+    consecutive counters from counter0 in super-buffer / segment order,
+    messages of super-buffer i at msg_offset[i] (uint64 device tensor).
+    Returns (results uint8 tensor of wg_encap_result, total uint64 tensor)."""
+    torch = _torch()
+    _require_cuda(inbuf, "inbuf")
+    if len(key) != 32:
+        raise WireGliderError("key must be 32 bytes")
+    n = gso_desc.numel() * gso_desc.element_size() // GSO_DESC_BYTES
+    _check_out(gso_results, n * GSO_RESULT_BYTES, torch.uint8, inbuf, "gso_results")
+    _check_out(msg_offset, n, torch.int64, inbuf, "msg_offset")
+    if results is None:
+        results = torch.zeros(max(n, 1) * ENCAP_RESULT_BYTES, dtype=torch.uint8, device=inbuf.device)
+    _check_out(results, n * ENCAP_RESULT_BYTES, torch.uint8, inbuf, "results")
+    if work is None:
+        work = torch.empty(n + 1024, dtype=torch.int32, device=inbuf.device)
+    _check_out(work, n + 1024, torch.int32, inbuf, "work")
+    if total is None:
+        total = torch.zeros(1, dtype=torch.int64, device=inbuf.device)
+    _check_out(total, 1, torch.int64, inbuf, "total")
+    for t, nm in ((seg_out, "seg_out"), (msgs, "msgs"), (gso_desc, "gso_desc")):
+        _require_cuda(t, nm)
+    with _on(inbuf):
+        rc = lib.wg_encap_encrypt(inbuf.data_ptr(), seg_out.data_ptr(), gso_desc.data_ptr(), gso_results.data_ptr(), n,
+                                  bytes(key), receiver_index, counter0 & (2**64 - 1), msg_offset.data_ptr(), msg_cap,
+                                  max_segments, max_segment_size, msgs.data_ptr(), results.data_ptr(),
+                                  work.data_ptr(), total.data_ptr(), _stream_ptr(stream, inbuf))
+    _check(rc, "wg_encap_encrypt")
+    return results, total
 
 
 def calc_l4_checksum_host(buf: bytes | bytearray | memoryview, segment_size: int, isv6: bool,

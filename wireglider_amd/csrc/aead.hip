@@ -405,6 +405,14 @@ struct AeadParams {
     uint32_t grp;        // aead_kernel<0, ...>: lanes per packet (1..32)
     uint8_t *verdict;    // decrypt + verify: WG_VERDICT_* per message (kVer)
     uint16_t *l4;        // decrypt + verify: the L4 checksum result per message (kVer)
+    // encap (kGso): packet pi is segment pi % gm of super-buffer pi / gm
+    const uint8_t *gin;          // wg_gso_split's input (passthrough batches)
+    const wg_gso_desc *gdesc;
+    const wg_gso_result *gres;
+    const uint64_t *msg_off;     // where super-buffer i's messages go
+    const uint32_t *work;        // [n] local exclusive prefixes of nmsg, [n + b] block prefixes
+    wg_encap_result *eres;
+    uint32_t gm;                 // max segments per super-buffer
 };
 
 // The decap verify gates (wg_verify_desc, SURVEY §8 f1: evaluate_packet,
@@ -481,7 +489,11 @@ constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/prot
 // pseudo-header — exact, because subtracting x mod 0xFFFF is adding
 // 0xFFFF - x and the total is never zero (the protocol word), so its fold
 // only depends on the sum mod 0xFFFF.
-template <int G, int K, bool kDec, bool kP = false, bool kVer = false>
+// kGso (encrypt only): the packets are the segments of wg_gso_split's
+// PacketBatches, super-buffer by super-buffer (worker/encap.cpp:136-141 for
+// each tun read's batch), counters in order over all of them (the scan of
+// encap_scan_*), messages at the caller's per-super-buffer offsets.
+template <int G, int K, bool kDec, bool kP = false, bool kVer = false, bool kGso = false>
 __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     constexpr bool kFlex = G == 0;
     const uint32_t GG = kFlex ? p.grp : (uint32_t)G;  // lanes per packet
@@ -492,10 +504,31 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     const uint32_t g = kFlex ? lane - slot * GG : lane & (uint32_t)(G - 1);
     const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
     const uint64_t i = wave * kPer + slot;
-    const bool live = slot < kPer && i < p.n;
+    bool live = slot < kPer && i < p.n;
     const uint64_t ii = live ? i : 0;
-    const uint64_t off = ii * p.seg;
-    const uint32_t len = live ? (uint32_t)(p.total_len - off < p.seg ? p.total_len - off : p.seg) : 0u;
+    uint64_t off = ii * p.seg;
+    uint32_t len = live ? (uint32_t)(p.total_len - off < p.seg ? p.total_len - off : p.seg) : 0u;
+    // kGso: segment s of super-buffer sb
+    uint64_t sb = 0;
+    uint32_t gs = 0, gstride = 0;
+    uintptr_t gsrc = 0, gdst = 0;
+    uint64_t gctr = 0;
+    if constexpr (kGso) {
+        sb = ii / p.gm;
+        gs = (uint32_t)(ii - sb * p.gm);
+        const wg_encap_result er = p.eres[sb];  // nmsg from encap_scan_local
+        const wg_gso_result gr = p.gres[sb];
+        const wg_gso_desc gd = p.gdesc[sb];
+        live = live && gs < er.nmsg;
+        const uint32_t S = gr.segment_size;
+        const uint64_t so = (uint64_t)gs * S;
+        len = live ? (uint32_t)(gr.out_len - so < S ? gr.out_len - so : S) : 0u;
+        gsrc = (gr.passthrough ? reinterpret_cast<uintptr_t>(p.gin) + gd.in_offset
+                               : reinterpret_cast<uintptr_t>(p.in) + gd.out_offset) + so;
+        gstride = 32u + ((S + 15u) & ~15u);
+        gdst = reinterpret_cast<uintptr_t>(p.out) + p.msg_off[sb] + (uint64_t)gs * gstride;
+        gctr = p.counter0 + p.work[p.n / p.gm + sb / 1024u] + p.work[sb] + gs;
+    }
     // payload geometry
     uint64_t counter;
     uint32_t plen;  // encrypt: plaintext bytes; decrypt: ciphertext bytes
@@ -503,11 +536,11 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     uintptr_t src, dst;
     int8_t st = 0;
     if constexpr (!kDec) {
-        counter = p.counter0 + ii;
+        counter = kGso ? gctr : p.counter0 + ii;
         plen = len;
         pad = (len + 15u) & ~15u;
-        src = reinterpret_cast<uintptr_t>(p.in) + off;
-        dst = reinterpret_cast<uintptr_t>(p.out) + ii * (32ull + ((p.seg + 15u) & ~15u));
+        src = kGso ? gsrc : reinterpret_cast<uintptr_t>(p.in) + off;
+        dst = kGso ? gdst : reinterpret_cast<uintptr_t>(p.out) + ii * (32ull + ((p.seg + 15u) & ~15u));
         if (counter >= kRejectAfterMessages)  // proto.cpp:560-562: EncryptError::NoSession
             st = -1;
     } else {
@@ -736,8 +769,12 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                 st16(dst, v4u{4u, p.receiver, n1, n2});  // DataHeader (proto.cpp:563-566)
                 st16(dst + 16 + pad, v4u{tagw[0], tagw[1], tagw[2], tagw[3]});
             }
-            if (p.status)
+            if constexpr (kGso) {
+                if (gs == 0u)
+                    p.eres[sb].counter0 = counter;
+            } else if (p.status) {
                 p.status[ii] = st;
+            }
         }
     } else {
         // tag check (crypto_verify_16); on a mismatch libsodium zeroes the
@@ -798,6 +835,78 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Encap counter scan: each super-buffer's message count (its PacketBatch's
+// segments, 0 on a GSO error or a bound exceeded), exclusive prefix over the
+// batch — block-local (encap_scan_local) then over the block totals
+// (encap_scan_blocks) — so the AEAD kernel gives segment s of super-buffer i
+// the counter counter0 + prefix(i) + s, as the reference's serial
+// encrypt_nonce++ would.
+// ---------------------------------------------------------------------------
+struct EncapScan {
+    const wg_gso_result *gres;
+    wg_encap_result *eres;
+    uint32_t *work;
+    uint64_t *total;
+    uint64_t n;
+    uint32_t msg_cap, max_segments, max_segment_size;
+};
+
+__device__ __forceinline__ uint32_t block_excl_scan_1024(uint32_t v, uint32_t *lds, uint32_t t, uint32_t &tot) {
+    // Hillis-Steele inclusive scan over 1,024 threads in LDS
+    lds[t] = v;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024u; o <<= 1) {
+        const uint32_t a = t >= o ? lds[t - o] : 0u;
+        __syncthreads();
+        lds[t] += a;
+        __syncthreads();
+    }
+    tot = lds[1023];
+    return lds[t] - v;
+}
+
+__global__ __launch_bounds__(1024) void encap_scan_local(EncapScan q) {
+    __shared__ uint32_t lds[1024];
+    const uint32_t t = threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * 1024u + t;
+    uint32_t nm = 0, bytes = 0;
+    if (i < q.n) {
+        const wg_gso_result r = q.gres[i];
+        const uint32_t S = r.segment_size;
+        if (r.status == 0 && S && r.out_len) {
+            const uint64_t ns = (r.out_len + S - 1) / S;
+            const uint64_t last = r.out_len - (ns - 1) * S;
+            const uint64_t b = (ns - 1) * (32ull + ((S + 15u) & ~15u)) + 32ull + ((last + 15u) & ~15ull);
+            if (ns <= q.max_segments && S <= q.max_segment_size && b <= q.msg_cap) {
+                nm = (uint32_t)ns;
+                bytes = (uint32_t)b;
+            }
+        }
+        q.eres[i].nmsg = nm;
+        q.eres[i].msg_bytes = bytes;
+        q.eres[i].counter0 = 0;
+    }
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan_1024(nm, lds, t, tot);
+    if (i < q.n)
+        q.work[i] = ex;
+    if (t == 0)
+        q.work[q.n + blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(1024) void encap_scan_blocks(EncapScan q, uint32_t nb) {
+    __shared__ uint32_t lds[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t v = t < nb ? q.work[q.n + t] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan_1024(v, lds, t, tot);
+    if (t < nb)
+        q.work[q.n + t] = ex;
+    if (t == 0 && q.total)
+        q.total[0] = tot;
+}
+
 }  // namespace wg
 
 using namespace wg;
@@ -812,6 +921,14 @@ static AeadKey key_words(const uint8_t key[32]) {
 
 template <int G, int K, bool kDec>
 static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
+    if constexpr (!kDec) {
+        if (p.eres) {  // encap: GSO segments (with the pair interleave where it applies)
+            constexpr bool kPg = K >= 2 && G < 64;
+            hipLaunchKernelGGL((aead_kernel<G, K, false, kPg, false, true>), dim3((unsigned)blocks), dim3(256), 0, st,
+                               p);
+            return;
+        }
+    }
     if constexpr (kDec) {
         if (p.verdict) {  // decrypt + verify (always with the pair interleave where it applies)
             constexpr bool kPv = K >= 2 && G < 64;
@@ -948,4 +1065,47 @@ extern "C" int wg_aead_decrypt_verify_batch(const uint8_t *dev_in, uint64_t tota
     p.seg = segment_size;
     p.key = key_words(key);
     return launch_aead<true>(p, segment_size > 32u ? segment_size - 32u : 0u, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int wg_encap_encrypt(const uint8_t *dev_in, const uint8_t *dev_seg, const wg_gso_desc *dev_desc,
+                                const wg_gso_result *dev_gso_res, uint64_t n, const uint8_t key[32],
+                                uint32_t receiver_index, uint64_t counter0, const uint64_t *dev_msg_offset,
+                                uint32_t msg_cap, uint32_t max_segments, uint32_t max_segment_size, uint8_t *dev_msgs,
+                                wg_encap_result *dev_res, uint32_t *dev_work, uint64_t *dev_total, void *stream) {
+    if (!key || !max_segments || !max_segment_size || max_segment_size > 65535u || n > (1ull << 20))
+        return WG_ERR_INVALID;
+    if (!n)
+        return WG_OK;
+    if (!dev_in || !dev_seg || !dev_desc || !dev_gso_res || !dev_msg_offset || !dev_msgs || !dev_res || !dev_work ||
+        (reinterpret_cast<uintptr_t>(dev_msgs) & 15) || (reinterpret_cast<uintptr_t>(dev_gso_res) & 7) ||
+        (reinterpret_cast<uintptr_t>(dev_desc) & 7) || (reinterpret_cast<uintptr_t>(dev_res) & 7) ||
+        (reinterpret_cast<uintptr_t>(dev_msg_offset) & 7) || (reinterpret_cast<uintptr_t>(dev_work) & 3))
+        return WG_ERR_INVALID;
+    if ((uint64_t)max_segments * n > (1ull << 40))
+        return WG_ERR_INVALID;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    EncapScan q{dev_gso_res, dev_res, dev_work, dev_total, n, msg_cap, max_segments, max_segment_size};
+    const uint32_t nb = (uint32_t)((n + 1023) / 1024);
+    hipLaunchKernelGGL(encap_scan_local, dim3(nb), dim3(1024), 0, st, q);
+    hipLaunchKernelGGL(encap_scan_blocks, dim3(1), dim3(1024), 0, st, q, nb);
+    if (hipGetLastError() != hipSuccess)
+        return WG_ERR_LAUNCH;
+    AeadParams p{};
+    p.in = dev_seg;
+    p.out = dev_msgs;
+    p.status = nullptr;
+    p.n = n * max_segments;  // packet pi = segment pi % max_segments of super-buffer pi / max_segments
+    p.seg = max_segment_size;
+    p.total_len = p.n * (uint64_t)max_segment_size;  // unused by the kGso geometry
+    p.receiver = receiver_index;
+    p.counter0 = counter0;
+    p.key = key_words(key);
+    p.gin = dev_in;
+    p.gdesc = dev_desc;
+    p.gres = dev_gso_res;
+    p.msg_off = dev_msg_offset;
+    p.work = dev_work;
+    p.eres = dev_res;
+    p.gm = max_segments;
+    return launch_aead<false>(p, max_segment_size, st);
 }
