@@ -76,6 +76,15 @@ def test_invalid_args_rejected_without_gpu():
     assert wga.lib.wg_aead_decrypt_verify_batch(16, 100, 64, key, 16, 16, 16, None, None) == -1  # l4 required
     assert wga.lib.wg_aead_decrypt_verify_batch(16, 100, 65536 + 33, key, 16, 16, 16, 16, None) == -1
     assert wga.lib.wg_aead_decrypt_verify_batch(16, 0, 64, key, 16, 16, 16, 16, None) == 0  # empty batch: no-op
+    # encap: bounds, too many super-buffers, misaligned message buffer, no-op on n = 0
+    assert wga.lib.wg_encap_encrypt(16, 16, 16, 16, 1, key, 1, 0, 16, 1 << 16, 0, 1500, 16, 16, 16, None, None) == -1
+    assert wga.lib.wg_encap_encrypt(16, 16, 16, 16, 1, key, 1, 0, 16, 1 << 16, 45, 0, 16, 16, 16, None, None) == -1
+    assert wga.lib.wg_encap_encrypt(16, 16, 16, 16, 1, key, 1, 0, 16, 1 << 16, 45, 70000, 16, 16, 16, None, None) == -1
+    assert wga.lib.wg_encap_encrypt(16, 16, 16, 16, (1 << 20) + 1, key, 1, 0, 16, 1 << 16, 45, 1500, 16, 16, 16, None,
+                                    None) == -1
+    assert wga.lib.wg_encap_encrypt(16, 16, 16, 16, 1, key, 1, 0, 16, 1 << 16, 45, 1500, 8, 16, 16, None, None) == -1
+    assert wga.lib.wg_encap_encrypt(16, 16, 16, 16, 1, None, 1, 0, 16, 1 << 16, 45, 1500, 16, 16, 16, None, None) == -1
+    assert wga.lib.wg_encap_encrypt(16, 16, 16, 16, 0, key, 1, 0, 16, 1 << 16, 45, 1500, 16, 16, 16, None, None) == 0
 
 
 DROPIN_TEST = r"""
