@@ -22,10 +22,13 @@
 // one multiplication by r (the length block comes last), the reduction mod
 // 2^130 - 5 and + s.  The per-lane fixed costs (powers of r, the scan, the
 // term) are paid once per K blocks, so larger K means fewer multiplications
-// per byte, against registers: K = 2 puts a 1,500-B packet in 16 lanes
-// (4 per wave); K = 4 (8 lanes) needs 99 VGPRs and measured 4 % slower.  ChaCha20 and Poly1305 are integer-VALU work (~1,000
-// and ~700 instructions per 64-B block lane), so this kernel is bound by
-// VALU issue, not HBM.
+// per byte, against registers.  Groups are exactly the lanes a packet needs
+// (aead_flex; the scan and sums then run by down-shift trees), and a lane's
+// blocks are computed two at a time with their quarter rounds interleaved
+// (aead_pair): a 1,500-B packet takes K = 3 in 9 lanes, 7 packets per wave.
+// ChaCha20 and Poly1305 are integer-VALU work (~1,000 and ~200
+// instructions per 64-B block lane), so this kernel is bound by VALU issue,
+// not HBM.
 #include <hip/hip_runtime.h>
 
 #include "wg_device.hpp"
