@@ -73,7 +73,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="config2",
                     choices=["config1", "config2", "config3", "config3udp", "config4", "config5", "verify", "gro", "encap",
-                             "aead"])
+                             "encap_2call", "aead"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-strong", action="store_true", help="skip the config 5 strong-scaling companion")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall seconds of the CPU baseline sample")
@@ -155,8 +155,8 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                   for r in range(world)]
         return Workload(launch, n, n * SEG, n * SEG + 2 * n + 16 * n, cfg, "strong", buf,
                         "wg::l4csum_split_kernel<1,nt> (l4_small=5)", lo, out, desc, sample, counts, probe_run=SEG)
-    if name == "encap":
-        return build_encap(wga, torch, rank, world, dev)
+    if name in ("encap", "encap_2call"):
+        return build_encap(wga, torch, rank, world, dev, fused=name == "encap")
     if name in ("config3", "config3udp"):
         udp = name == "config3udp"
         n, in_stride, out_stride = 1 << 18, 65536, 73216  # outbuf stride of worker/encap.cpp:26
@@ -584,12 +584,13 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                     rank * n, out, desc, sample, [n] * world, post=post)
 
 
-def build_encap(wga, torch, rank: int, world: int, dev) -> Workload:
+def build_encap(wga, torch, rank: int, world: int, dev, fused: bool = True) -> Workload:
     """The encap worker's data path on the device (worker/encap.cpp:107-160):
-    config 3's 262,144 x 64 KiB tun super-buffers -> do_tun_gso_split
-    (wg_gso_split) -> Peer::encrypt for every segment in order with
-    encrypt_nonce++ (wg_encap_encrypt), one peer; per step both calls, no
-    host round trip.  value = GiB/s of tun input."""
+    config 3's 262,144 x 64 KiB tun super-buffers -> do_tun_gso_split ->
+    Peer::encrypt for every segment in order with encrypt_nonce++, one peer,
+    no host round trip.  fused: one wg_encap_batch per step (headers-only
+    split, payload encrypted from the input); else wg_gso_split +
+    wg_encap_encrypt (workload encap_2call).  value = GiB/s of tun input."""
     import numpy as np
 
     n, in_stride, out_stride, in_len = 1 << 18, 65536, 73216, 65535
@@ -626,9 +627,13 @@ def build_encap(wga, torch, rank: int, world: int, dev) -> Workload:
     rx, c0 = 0x0E0CA9, 1 + rank * n * nseg
 
     def launch():
-        wga.gso_split(buf, d_desc, outb, results=res)
-        wga.encap_encrypt(buf, outb, d_desc, res, key, rx, c0, msg_off, mcap, nseg, seg, msgs, results=eres,
-                          work=work, total=tot)
+        if fused:
+            wga.encap_batch(buf, d_desc, outb, res, key, rx, c0, msg_off, mcap, nseg, seg, msgs, results=eres,
+                            work=work, total=tot)
+        else:
+            wga.gso_split(buf, d_desc, outb, results=res)
+            wga.encap_encrypt(buf, outb, d_desc, res, key, rx, c0, msg_off, mcap, nseg, seg, msgs, results=eres,
+                              work=work, total=tot)
 
     def post():
         # every super-buffer: 45 messages at consecutive counters, and a
@@ -639,7 +644,11 @@ def build_encap(wga, torch, rank: int, world: int, dev) -> Workload:
         k = 256
         full = torch.cat([msgs[int(msg_off_np[i]): int(msg_off_np[i]) + (nseg - 1) * mstride] for i in range(k)])
         pt, st = wga.aead_decrypt_batch(full, mstride, key)
-        segs = torch.cat([outb[i * out_stride: i * out_stride + (nseg - 1) * seg] for i in range(k)])
+        # the reference segments: a full split of the sample (the fused call
+        # leaves only the headers in outb; splitting again is idempotent)
+        ref = torch.empty(k * out_stride, dtype=torch.uint8, device=dev)
+        wga.gso_split(buf[: k * in_stride], d_desc[: k * wga.GSO_DESC_BYTES], ref)
+        segs = torch.cat([ref[i * out_stride: i * out_stride + (nseg - 1) * seg] for i in range(k)])
         torch.cuda.synchronize()
         same = bool(torch.equal(pt.view(-1, mstride - 32)[:, :seg].reshape(-1), segs))
         return {"results_ok": ok, "messages_total": int(tot.cpu()[0]), "sample_super_buffers_decrypted": k,
@@ -653,11 +662,18 @@ def build_encap(wga, torch, rank: int, world: int, dev) -> Workload:
     cfg = {"workload": "encap: config 3's 262,144 x 64 KiB IPv4/TCP tun super-buffers -> do_tun_gso_split (45 x "
                        "1460 B segments) -> Peer::encrypt per segment, one peer, consecutive counters (the encap "
                        "worker, worker/encap.cpp:107-160)", "super_buffers_per_gpu": n, "segments_per_buffer": nseg,
-           "message_stride": mstride, "parallelism": f"shard{world}"}
-    alg = (n * in_len + n * out_len + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES)  # the split
-           + n * out_len + n * mbytes + n * (wga.ENCAP_RESULT_BYTES + 8))           # the encryption
+           "message_stride": mstride, "parallelism": f"shard{world}",
+           "entry": "wg_encap_batch" if fused else "wg_gso_split + wg_encap_encrypt"}
+    # the split reads the input and writes the segments (fused: only each
+    # segment's header block, pad64(hdr) bytes); the AEAD reads every
+    # segment's plaintext once and writes the messages
+    split_w = n * nseg * ((hdr + 63) // 64 * 64) if fused else n * out_len
+    alg = (n * in_len + split_w + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES)
+           + n * out_len + n * mbytes + n * (wga.ENCAP_RESULT_BYTES + 8))
+    aead_k = "wg::aead_kernel<0,3,false,true,false,%d>" % (2 if fused else 1)
     return Workload(launch, n, n * in_len, alg, cfg, "weak", buf,
-                    "wg_gso_split (3 kernels) + wg_encap_encrypt (2 scan kernels + wg::aead_kernel<0,3,false,true,false,true>)",
+                    ("wg_encap_batch (3 split kernels, headers only, + 2 scan kernels + %s)" if fused else
+                     "wg_gso_split (3 kernels) + wg_encap_encrypt (2 scan kernels + %s)") % aead_k,
                     rank * n, sample=sample, counts=[n] * world, post=post,
                     metric="device-resident GiB/s of tun input, GSO split + data-message encryption (encap worker)")
 

@@ -281,6 +281,22 @@ int wg_encap_encrypt(const uint8_t *dev_in, const uint8_t *dev_seg, const wg_gso
                      uint32_t max_segment_size, uint8_t *dev_msgs, wg_encap_result *dev_res, uint32_t *dev_work,
                      uint64_t *dev_total, void *stream);
 
+/* The whole encap step in one call: wg_gso_split(dev_in, dev_desc, n,
+ * dev_out, dev_gso_res) then wg_encap_encrypt over its output, except that
+ * the split writes only each segment's HEADER into dev_out (bytes
+ * [0, hdr_len) of every segment slot, checksums as always) and the AEAD reads
+ * each segment's payload straight from dev_in — the segment payload copy is
+ * never materialised.  On return dev_gso_res, dev_res, dev_msgs, dev_total
+ * and dev_in's zeroed prefix fields are exactly what the two calls give;
+ * dev_out holds the segment headers only.  dev_out must be sized as for
+ * wg_gso_split (the headers sit at the segments' offsets).  Arguments and
+ * bounds as for the two calls. */
+int wg_encap_batch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
+                   wg_gso_result *dev_gso_res, const uint8_t key[32], uint32_t receiver_index, uint64_t counter0,
+                   const uint64_t *dev_msg_offset, uint32_t msg_cap, uint32_t max_segments, uint32_t max_segment_size,
+                   uint8_t *dev_msgs, wg_encap_result *dev_res, uint32_t *dev_work, uint64_t *dev_total,
+                   void *stream);
+
 /* ------------------------------------------------------------------------
  * Host-memory path: the batch starts and ends in host memory
  * (tun read buffers, worker/encap.cpp:74-97; UDP GRO recvmsg buffers,

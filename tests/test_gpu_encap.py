@@ -6,7 +6,12 @@ encrypt_nonce++ — compared message for message with the oracle's
 wg_encrypt_batch over each PacketBatch (the GSO output itself is pinned in
 tests/test_gpu_gso.py).  Random super-buffers of every GSO type: splits,
 passthrough (GSO_NONE, unknown types), errors (no messages), batches past
-the segment / size / capacity bounds (no messages)."""
+the segment / size / capacity bounds (no messages).
+
+fused=True runs the same step through wg_encap_batch (the headers-only split
++ the AEAD reading payload from the input): its messages, counters, result
+records, GSO results and input prefix zeroing must equal the two-call path's,
+and the segment headers it leaves in `out` the split's."""
 import numpy as np
 import pytest
 
@@ -22,10 +27,11 @@ def _wga():
     return wga
 
 
+@pytest.mark.parametrize("fused", [False, True], ids=["split+encrypt", "encap_batch"])
 @pytest.mark.parametrize("seed", [11, 12])
 @pytest.mark.parametrize("knobs", [{}, {"aead_k": 2, "aead_flex": 0}, {"aead_k": 1}],
                          ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()) or "default")
-def test_encap_matches_oracle(gpu, seed, knobs):
+def test_encap_matches_oracle(gpu, seed, knobs, fused):
     import torch
 
     wga = _wga()
@@ -55,6 +61,7 @@ def test_encap_matches_oracle(gpu, seed, knobs):
     d_in = torch.from_numpy(inbuf).to(gpu)
     d_out = torch.zeros(out_off + 64, dtype=torch.uint8, device=gpu)
     d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(gpu)
+    d_in_f = d_in.clone()  # the fused call's own copy (the split zeroes prefix fields in place)
     d_res = wga.gso_split(d_in, d_desc, d_out)
     max_seg, max_size, cap = 48, 9100, 48 * (32 + 9104)
     cap_small = 7000  # some super-buffers' messages will not fit: nmsg 0
@@ -63,8 +70,15 @@ def test_encap_matches_oracle(gpu, seed, knobs):
     key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
     c0 = int(rng.choice([1, (1 << 32) - 40]))
     m_cap = cap_small if seed == 12 else cap
-    eres, total = wga.encap_encrypt(d_in, d_out, d_desc, d_res, key, 0xBEEF, c0, torch.from_numpy(msg_off).to(gpu),
-                                    m_cap, max_seg, max_size, msgs)
+    d_msg_off = torch.from_numpy(msg_off).to(gpu)
+    if fused:
+        d_hdr = torch.full_like(d_out, 0x5A)
+        d_res_f = torch.zeros_like(d_res)
+        eres, total = wga.encap_batch(d_in_f, d_desc, d_hdr, d_res_f, key, 0xBEEF, c0, d_msg_off, m_cap, max_seg,
+                                      max_size, msgs)
+    else:
+        eres, total = wga.encap_encrypt(d_in, d_out, d_desc, d_res, key, 0xBEEF, c0, d_msg_off, m_cap, max_seg,
+                                        max_size, msgs)
     torch.cuda.synchronize()
     for k, v in saved.items():
         wga.tune_set(k, v)
@@ -72,6 +86,18 @@ def test_encap_matches_oracle(gpu, seed, knobs):
     r = d_res.cpu().numpy().view(wga.GSO_RESULT_DTYPE)
     e = eres.cpu().numpy().view(wga.ENCAP_RESULT_DTYPE)
     got = msgs.cpu().numpy()
+    if fused:
+        assert torch.equal(d_res_f, d_res)
+        assert torch.equal(d_in_f, d_in)
+        g_hdr = d_hdr.cpu().numpy()
+        for i in range(n):
+            if int(r[i]["status"]) or int(r[i]["passthrough"]):
+                continue
+            S, ol, hl = int(r[i]["segment_size"]), int(r[i]["out_len"]), int(r[i]["hdr_len"])
+            o = int(desc[i]["out_offset"])
+            for so in range(0, ol, S):
+                np.testing.assert_array_equal(g_hdr[o + so:o + so + hl], g_out[o + so:o + so + hl],
+                                              err_msg=f"super-buffer {i} segment header at {so}")
     ctr, n_msgs = c0, 0
     for i in range(n):
         S, ol = int(r[i]["segment_size"]), int(r[i]["out_len"])

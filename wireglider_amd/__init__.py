@@ -44,6 +44,7 @@ EXPORTED_SYMBOLS = (
     "wg_aead_decrypt_batch",
     "wg_aead_decrypt_verify_batch",
     "wg_encap_encrypt",
+    "wg_encap_batch",
     "wg_l4csum_uniform_host",
     "wg_host_release",
     "wg_host_alloc",
@@ -119,6 +120,8 @@ def _load() -> ctypes.CDLL:
         "wg_aead_decrypt_verify_batch": (i32, [u8p, u64, u32, ctypes.c_char_p, u8p, vp, vp, vp, vp]),
         "wg_encap_encrypt": (i32, [u8p, u8p, vp, vp, u64, ctypes.c_char_p, u32, u64, vp, u32, u32, u32, u8p, vp, vp,
                                    vp, vp]),
+        "wg_encap_batch": (i32, [u8p, vp, u64, u8p, vp, ctypes.c_char_p, u32, u64, vp, u32, u32, u32, u8p, vp, vp, vp,
+                                 vp]),
         "wg_l4csum_uniform_host": (i32, [u8p, u64, u32, u16, u32, vp]),
         "wg_host_release": (i32, []),
         "wg_host_alloc": (i32, [ctypes.POINTER(ctypes.c_void_p), u64]),
@@ -412,14 +415,8 @@ def _encap_dtype():
 ENCAP_RESULT_DTYPE = _encap_dtype()
 
 
-def encap_encrypt(inbuf, seg_out, gso_desc, gso_results, key: bytes, receiver_index: int, counter0: int, msg_offset,
-                  msg_cap: int, max_segments: int, max_segment_size: int, msgs, results=None, work=None, total=None,
-                  stream=None):
-    """Encap worker step (worker/encap.cpp:136-141) after gso_split: every
-    segment of every super-buffer's PacketBatch encrypted for one peer, with
-    consecutive counters from counter0 in super-buffer / segment order,
-    messages of super-buffer i at msg_offset[i] (uint64 device tensor).
-    Returns (results uint8 tensor of wg_encap_result, total uint64 tensor)."""
+def _encap_outputs(inbuf, gso_desc, gso_results, key, msg_offset, results, work, total):
+    """Shared argument checks / default outputs of encap_encrypt and encap_batch."""
     torch = _torch()
     _require_cuda(inbuf, "inbuf")
     if len(key) != 32:
@@ -436,6 +433,18 @@ def encap_encrypt(inbuf, seg_out, gso_desc, gso_results, key: bytes, receiver_in
     if total is None:
         total = torch.zeros(1, dtype=torch.int64, device=inbuf.device)
     _check_out(total, 1, torch.int64, inbuf, "total")
+    return n, results, work, total
+
+
+def encap_encrypt(inbuf, seg_out, gso_desc, gso_results, key: bytes, receiver_index: int, counter0: int, msg_offset,
+                  msg_cap: int, max_segments: int, max_segment_size: int, msgs, results=None, work=None, total=None,
+                  stream=None):
+    """Encap worker step (worker/encap.cpp:136-141) after gso_split: every
+    segment of every super-buffer's PacketBatch encrypted for one peer, with
+    consecutive counters from counter0 in super-buffer / segment order,
+    messages of super-buffer i at msg_offset[i] (uint64 device tensor).
+    Returns (results uint8 tensor of wg_encap_result, total uint64 tensor)."""
+    n, results, work, total = _encap_outputs(inbuf, gso_desc, gso_results, key, msg_offset, results, work, total)
     for t, nm in ((seg_out, "seg_out"), (msgs, "msgs"), (gso_desc, "gso_desc")):
         _require_cuda(t, nm)
     with _on(inbuf):
@@ -444,6 +453,26 @@ def encap_encrypt(inbuf, seg_out, gso_desc, gso_results, key: bytes, receiver_in
                                   max_segments, max_segment_size, msgs.data_ptr(), results.data_ptr(),
                                   work.data_ptr(), total.data_ptr(), _stream_ptr(stream, inbuf))
     _check(rc, "wg_encap_encrypt")
+    return results, total
+
+
+def encap_batch(inbuf, gso_desc, out, gso_results, key: bytes, receiver_index: int, counter0: int, msg_offset,
+                msg_cap: int, max_segments: int, max_segment_size: int, msgs, results=None, work=None, total=None,
+                stream=None):
+    """The whole encap step (worker/encap.cpp:107-168: do_tun_gso_split, then
+    Peer::encrypt per segment) in one call: gso_split writing only the
+    segments' headers into `out`, then encap_encrypt reading every segment's
+    payload from `inbuf`.  Same results / messages / total as gso_split +
+    encap_encrypt; `out` holds the segment headers only."""
+    n, results, work, total = _encap_outputs(inbuf, gso_desc, gso_results, key, msg_offset, results, work, total)
+    for t, nm in ((out, "out"), (msgs, "msgs"), (gso_desc, "gso_desc")):
+        _require_cuda(t, nm)
+    with _on(inbuf):
+        rc = lib.wg_encap_batch(inbuf.data_ptr(), gso_desc.data_ptr(), n, out.data_ptr(), gso_results.data_ptr(),
+                                bytes(key), receiver_index, counter0 & (2**64 - 1), msg_offset.data_ptr(), msg_cap,
+                                max_segments, max_segment_size, msgs.data_ptr(), results.data_ptr(), work.data_ptr(),
+                                total.data_ptr(), _stream_ptr(stream, inbuf))
+    _check(rc, "wg_encap_batch")
     return results, total
 
 

@@ -416,6 +416,8 @@ struct AeadParams {
     const uint32_t *work;        // [n] local exclusive prefixes of nmsg, [n + b] block prefixes
     wg_encap_result *eres;
     uint32_t gm;                 // max segments per super-buffer
+    uint32_t gmode;              // kGso: 1 segments from `in` (wg_encap_encrypt), 2 headers from `in`,
+                                 // payload from `gin` (wg_encap_batch)
 };
 
 // The decap verify gates (wg_verify_desc, SURVEY §8 f1: evaluate_packet,
@@ -496,7 +498,12 @@ constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/prot
 // PacketBatches, super-buffer by super-buffer (worker/encap.cpp:136-141 for
 // each tun read's batch), counters in order over all of them (the scan of
 // encap_scan_*), messages at the caller's per-super-buffer offsets.
-template <int G, int K, bool kDec, bool kP = false, bool kVer = false, bool kGso = false>
+// kGso = 1: segment s of a split super-buffer is read whole from the split
+// output; kGso = 2: only its first 64-B blocks up to the end of the header
+// are (the headers-only split writes exactly those bytes), every later
+// block from the input itself, where plaintext byte q >= hdr_len of segment
+// s is input byte s * gso + q — one source per block, no merge.
+template <int G, int K, bool kDec, bool kP = false, bool kVer = false, int kGso = 0>
 __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     constexpr bool kFlex = G == 0;
     const uint32_t GG = kFlex ? p.grp : (uint32_t)G;  // lanes per packet
@@ -515,6 +522,8 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     uint64_t sb = 0;
     uint32_t gs = 0, gstride = 0;
     uintptr_t gsrc = 0, gdst = 0;
+    uintptr_t hsrc = 0;  // kGso == 2: the segment slot, holding plaintext [0, hl)
+    uint32_t hl = 0;     // kGso == 2: hdr_len rounded up to whole 64-B blocks (0: passthrough)
     uint64_t gctr = 0;
     if constexpr (kGso) {
         sb = ii / p.gm;
@@ -526,8 +535,15 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
         const uint32_t S = gr.segment_size;
         const uint64_t so = (uint64_t)gs * S;
         len = live ? (uint32_t)(gr.out_len - so < S ? gr.out_len - so : S) : 0u;
-        gsrc = (gr.passthrough ? reinterpret_cast<uintptr_t>(p.gin) + gd.in_offset
-                               : reinterpret_cast<uintptr_t>(p.in) + gd.out_offset) + so;
+        if constexpr (kGso == 2) {
+            hl = gr.passthrough ? 0u : ((uint32_t)gr.hdr_len + 63u) & ~63u;
+            hsrc = reinterpret_cast<uintptr_t>(p.in) + gd.out_offset + so;
+            gsrc = reinterpret_cast<uintptr_t>(p.gin) + gd.in_offset +
+                   (gr.passthrough ? so : (uint64_t)gs * (S - gr.hdr_len));
+        } else {
+            gsrc = (gr.passthrough ? reinterpret_cast<uintptr_t>(p.gin) + gd.in_offset
+                                   : reinterpret_cast<uintptr_t>(p.in) + gd.out_offset) + so;
+        }
         gstride = 32u + ((S + 15u) & ~15u);
         gdst = reinterpret_cast<uintptr_t>(p.out) + p.msg_off[sb] + (uint64_t)gs * gstride;
         gctr = p.counter0 + p.work[p.n / p.gm + sb / 1024u] + p.work[sb] + gs;
@@ -673,7 +689,10 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             const uint32_t nin = has ? (plen - boff < 64u ? plen - boff : 64u) : 0u;  // payload bytes in the block
             const uint32_t nct = has ? (pad - boff < 64u ? pad - boff : 64u) : 0u;    // Poly1305 bytes in the block
             uint32_t W[16];
-            load64(src + boff, nin, W);  // plaintext (encrypt) / ciphertext (decrypt), zero past the payload
+            // plaintext (encrypt) / ciphertext (decrypt), zero past the
+            // payload; kGso == 2: blocks below hl from the segment slot
+            const uintptr_t bsrc = kGso == 2 && boff < hl ? hsrc : src;
+            load64(bsrc + boff, nin, W);
 #pragma unroll
             for (int m = 0; m < 16; m++) {
                 if constexpr (!kDec) {
@@ -927,8 +946,12 @@ static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
     if constexpr (!kDec) {
         if (p.eres) {  // encap: GSO segments (with the pair interleave where it applies)
             constexpr bool kPg = K >= 2 && G < 64;
-            hipLaunchKernelGGL((aead_kernel<G, K, false, kPg, false, true>), dim3((unsigned)blocks), dim3(256), 0, st,
-                               p);
+            if (p.gmode == 2)
+                hipLaunchKernelGGL((aead_kernel<G, K, false, kPg, false, 2>), dim3((unsigned)blocks), dim3(256), 0,
+                                   st, p);
+            else
+                hipLaunchKernelGGL((aead_kernel<G, K, false, kPg, false, 1>), dim3((unsigned)blocks), dim3(256), 0,
+                                   st, p);
             return;
         }
     }
@@ -1070,23 +1093,13 @@ extern "C" int wg_aead_decrypt_verify_batch(const uint8_t *dev_in, uint64_t tota
     return launch_aead<true>(p, segment_size > 32u ? segment_size - 32u : 0u, static_cast<hipStream_t>(stream));
 }
 
-extern "C" int wg_encap_encrypt(const uint8_t *dev_in, const uint8_t *dev_seg, const wg_gso_desc *dev_desc,
-                                const wg_gso_result *dev_gso_res, uint64_t n, const uint8_t key[32],
-                                uint32_t receiver_index, uint64_t counter0, const uint64_t *dev_msg_offset,
-                                uint32_t msg_cap, uint32_t max_segments, uint32_t max_segment_size, uint8_t *dev_msgs,
-                                wg_encap_result *dev_res, uint32_t *dev_work, uint64_t *dev_total, void *stream) {
-    if (!key || !max_segments || !max_segment_size || max_segment_size > 65535u || n > (1ull << 20))
-        return WG_ERR_INVALID;
-    if (!n)
-        return WG_OK;
-    if (!dev_in || !dev_seg || !dev_desc || !dev_gso_res || !dev_msg_offset || !dev_msgs || !dev_res || !dev_work ||
-        (reinterpret_cast<uintptr_t>(dev_msgs) & 15) || (reinterpret_cast<uintptr_t>(dev_gso_res) & 7) ||
-        (reinterpret_cast<uintptr_t>(dev_desc) & 7) || (reinterpret_cast<uintptr_t>(dev_res) & 7) ||
-        (reinterpret_cast<uintptr_t>(dev_msg_offset) & 7) || (reinterpret_cast<uintptr_t>(dev_work) & 3))
-        return WG_ERR_INVALID;
-    if ((uint64_t)max_segments * n > (1ull << 40))
-        return WG_ERR_INVALID;
-    hipStream_t st = static_cast<hipStream_t>(stream);
+// the encap scans + the AEAD over GSO output (gmode 1: whole segments in
+// dev_seg; 2: headers in dev_seg, payload in dev_in)
+static int encap_launch(const uint8_t *dev_in, const uint8_t *dev_seg, const wg_gso_desc *dev_desc,
+                        const wg_gso_result *dev_gso_res, uint64_t n, const uint8_t key[32], uint32_t receiver_index,
+                        uint64_t counter0, const uint64_t *dev_msg_offset, uint32_t msg_cap, uint32_t max_segments,
+                        uint32_t max_segment_size, uint8_t *dev_msgs, wg_encap_result *dev_res, uint32_t *dev_work,
+                        uint64_t *dev_total, uint32_t gmode, hipStream_t st) {
     EncapScan q{dev_gso_res, dev_res, dev_work, dev_total, n, msg_cap, max_segments, max_segment_size};
     const uint32_t nb = (uint32_t)((n + 1023) / 1024);
     hipLaunchKernelGGL(encap_scan_local, dim3(nb), dim3(1024), 0, st, q);
@@ -1110,5 +1123,56 @@ extern "C" int wg_encap_encrypt(const uint8_t *dev_in, const uint8_t *dev_seg, c
     p.work = dev_work;
     p.eres = dev_res;
     p.gm = max_segments;
+    p.gmode = gmode;
     return launch_aead<false>(p, max_segment_size, st);
+}
+
+// the arguments both encap entry points share
+static bool encap_args_ok(const uint8_t *key, uint64_t n, const void *dev_in, const void *dev_seg,
+                          const wg_gso_desc *dev_desc, const wg_gso_result *dev_gso_res,
+                          const uint64_t *dev_msg_offset, uint32_t max_segments, uint32_t max_segment_size,
+                          const uint8_t *dev_msgs, const wg_encap_result *dev_res, const uint32_t *dev_work) {
+    if (!key || !max_segments || !max_segment_size || max_segment_size > 65535u || n > (1ull << 20))
+        return false;
+    if (!n)
+        return true;
+    if (!dev_in || !dev_seg || !dev_desc || !dev_gso_res || !dev_msg_offset || !dev_msgs || !dev_res || !dev_work ||
+        (reinterpret_cast<uintptr_t>(dev_msgs) & 15) || (reinterpret_cast<uintptr_t>(dev_gso_res) & 7) ||
+        (reinterpret_cast<uintptr_t>(dev_desc) & 7) || (reinterpret_cast<uintptr_t>(dev_res) & 7) ||
+        (reinterpret_cast<uintptr_t>(dev_msg_offset) & 7) || (reinterpret_cast<uintptr_t>(dev_work) & 3))
+        return false;
+    return (uint64_t)max_segments * n <= (1ull << 40);
+}
+
+extern "C" int wg_encap_encrypt(const uint8_t *dev_in, const uint8_t *dev_seg, const wg_gso_desc *dev_desc,
+                                const wg_gso_result *dev_gso_res, uint64_t n, const uint8_t key[32],
+                                uint32_t receiver_index, uint64_t counter0, const uint64_t *dev_msg_offset,
+                                uint32_t msg_cap, uint32_t max_segments, uint32_t max_segment_size, uint8_t *dev_msgs,
+                                wg_encap_result *dev_res, uint32_t *dev_work, uint64_t *dev_total, void *stream) {
+    if (!encap_args_ok(key, n, dev_in, dev_seg, dev_desc, dev_gso_res, dev_msg_offset, max_segments, max_segment_size,
+                       dev_msgs, dev_res, dev_work))
+        return WG_ERR_INVALID;
+    if (!n)
+        return WG_OK;
+    return encap_launch(dev_in, dev_seg, dev_desc, dev_gso_res, n, key, receiver_index, counter0, dev_msg_offset,
+                        msg_cap, max_segments, max_segment_size, dev_msgs, dev_res, dev_work, dev_total, 1u,
+                        static_cast<hipStream_t>(stream));
+}
+
+extern "C" int wg_encap_batch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
+                              wg_gso_result *dev_gso_res, const uint8_t key[32], uint32_t receiver_index,
+                              uint64_t counter0, const uint64_t *dev_msg_offset, uint32_t msg_cap,
+                              uint32_t max_segments, uint32_t max_segment_size, uint8_t *dev_msgs,
+                              wg_encap_result *dev_res, uint32_t *dev_work, uint64_t *dev_total, void *stream) {
+    if (!encap_args_ok(key, n, dev_in, dev_out, dev_desc, dev_gso_res, dev_msg_offset, max_segments, max_segment_size,
+                       dev_msgs, dev_res, dev_work))
+        return WG_ERR_INVALID;
+    if (!n)
+        return WG_OK;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int rc = gso_split_launch(dev_in, dev_desc, n, dev_out, dev_gso_res, true, st);
+    if (rc != WG_OK)
+        return rc;
+    return encap_launch(dev_in, dev_out, dev_desc, dev_gso_res, n, key, receiver_index, counter0, dev_msg_offset,
+                        msg_cap, max_segments, max_segment_size, dev_msgs, dev_res, dev_work, dev_total, 2u, st);
 }

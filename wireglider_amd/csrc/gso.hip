@@ -44,7 +44,11 @@ __device__ __forceinline__ void st16_nt(uintptr_t addr, v4u v) {
 // blocks -> super-buffers in launch order instead of XCD-swizzled (the
 // swizzle keeps consecutive super-buffers on one XCD).  Timing-only
 // ablations with wrong output live in tools/exp, never in this library.
-enum : int { kAblNtStore = 1, kAblNoSwizzle = 32 };
+// 64 is not an ablation but the headers-only mode of wg_encap_batch: every
+// segment's header and the payload up to the header's 64-B block boundary
+// are written (checksums over the whole loaded payload as always), the rest
+// of the payload is not — the AEAD reads it from the input instead.
+enum : int { kAblNtStore = 1, kAblNoSwizzle = 32, kHdrOnly = 64 };
 
 template <int A>
 __device__ __forceinline__ void st16x(uintptr_t addr, v4u v) {
@@ -160,24 +164,33 @@ __device__ __forceinline__ void seg_finish(const Ctx &c, uintptr_t out_base, con
     const uint32_t i = f.i, pktlen = g.pktlen;
     Acc acc;
     // payload: store and sum (destination-aligned chunks: absolute pairing)
+    // headers-only: the payload bytes in the header's last 64-B block (the
+    // AEAD reads whole blocks below that bound from the segment slot); every
+    // such chunk is among the first 64
+    constexpr bool kPay = !(Abl & kHdrOnly);
+    const uintptr_t hlim = g.seg + ((c.hdr_len + 63u) & ~63u);
     if (lane < g.nint) {
-        st16x<Abl>(g.c0 + 16u * lane, f.lo0);
+        if (kPay || g.c0 + 16u * lane < hlim)
+            st16x<Abl>(g.c0 + 16u * lane, f.lo0);
         acc.add4(f.lo0);
     }
     if (lane + 64 < g.nint) {
-        st16x<Abl>(g.c0 + 16u * (lane + 64), f.lo1);
+        if constexpr (kPay)
+            st16x<Abl>(g.c0 + 16u * (lane + 64), f.lo1);
         acc.add4(f.lo1);
     }
     if (g.nint > 128) {  // long segments (gso > ~2 KiB)
         for (uint32_t k = lane + 128; k < g.nint; k += 64) {
             const v4u v = ld16(g.base + 16u * k);
-            st16x<Abl>(g.c0 + 16u * k, v);
+            if constexpr (kPay)
+                st16x<Abl>(g.c0 + 16u * k, v);
             acc.add4(v);
         }
     }
     const uint32_t eo = edge_off(g, lane);
     if (eo != kNoEdge) {
-        st8(g.oa + eo, f.pb);
+        if (kPay || g.oa + eo < hlim)
+            st8(g.oa + eo, f.pb);
         acc.add(f.pb << (8u * (((uint32_t)g.oa + eo) & 1u)));
     }
 
@@ -512,16 +525,13 @@ static void launch_split(const GsoParams &p, dim3 g, uint32_t waves, hipStream_t
     }
 }
 
-extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
-                            wg_gso_result *dev_res, void *stream) {
-    if (!n)
-        return WG_OK;
-    if (!dev_in || !dev_desc || !dev_out || !dev_res || (reinterpret_cast<uintptr_t>(dev_desc) & 7) ||
-        (reinterpret_cast<uintptr_t>(dev_res) & 7))
-        return WG_ERR_INVALID;
+namespace wg {
+// plan -> split -> finalize for n super-buffers (wg_gso_split; hdr_only:
+// wg_encap_batch's headers-only split)
+int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
+                     wg_gso_result *dev_res, bool hdr_only, hipStream_t st) {
     const Tune t = tune();
     GsoParams p{dev_in, dev_desc, n, dev_out, dev_res, t.gso_groups};
-    hipStream_t st = static_cast<hipStream_t>(stream);
     // 1. plans (into dev_res), thread per super-buffer
     const uint64_t pb = (n + kPlanBlock - 1) / kPlanBlock;
     if (pb > 0x7fffffffull)
@@ -535,14 +545,22 @@ extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64
     if (blocks >= 8)
         blocks &= ~7ull;  // the XCD swizzle wants a multiple of 8 (the grid-stride loop covers the rest)
     const dim3 g((unsigned)blocks, t.gso_split);
-    switch (t.gso_ablate) {  // correct A/B variants
-    case 1: launch_split<0, 1>(p, g, 4, st); break;
-    case 32: launch_split<0, 32>(p, g, 4, st); break;
-    default:
+    if (hdr_only) {
         switch (t.gso_spw) {
-        case 1: launch_split<1, 0>(p, g, t.gso_waves, st); break;
-        case 2: launch_split<2, 0>(p, g, t.gso_waves, st); break;
-        default: launch_split<0, 0>(p, g, t.gso_waves, st); break;
+        case 1: launch_split<1, kHdrOnly>(p, g, t.gso_waves, st); break;
+        case 2: launch_split<2, kHdrOnly>(p, g, t.gso_waves, st); break;
+        default: launch_split<0, kHdrOnly>(p, g, t.gso_waves, st); break;
+        }
+    } else {
+        switch (t.gso_ablate) {  // correct A/B variants
+        case 1: launch_split<0, 1>(p, g, 4, st); break;
+        case 32: launch_split<0, 32>(p, g, 4, st); break;
+        default:
+            switch (t.gso_spw) {
+            case 1: launch_split<1, 0>(p, g, t.gso_waves, st); break;
+            case 2: launch_split<2, 0>(p, g, t.gso_waves, st); break;
+            default: launch_split<0, 0>(p, g, t.gso_waves, st); break;
+            }
         }
     }
     if (hipGetLastError() != hipSuccess || !debug_sync(st, "gso_split_kernel"))
@@ -552,4 +570,15 @@ extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64
     if (!debug_sync(st, "gso_finalize_kernel"))
         return WG_ERR_LAUNCH;
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+}
+}  // namespace wg
+
+extern "C" int wg_gso_split(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
+                            wg_gso_result *dev_res, void *stream) {
+    if (!n)
+        return WG_OK;
+    if (!dev_in || !dev_desc || !dev_out || !dev_res || (reinterpret_cast<uintptr_t>(dev_desc) & 7) ||
+        (reinterpret_cast<uintptr_t>(dev_res) & 7))
+        return WG_ERR_INVALID;
+    return gso_split_launch(dev_in, dev_desc, n, dev_out, dev_res, false, static_cast<hipStream_t>(stream));
 }

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "wireglider_amd.h"
+
 namespace wg {
 
 // Launch geometry, read once from the environment (WG_L4_BLOCKS, ...; the
@@ -49,5 +51,10 @@ Tune tune();
 // stream after a launch and report a failing kernel by name on stderr.
 // Returns false when the kernel failed.
 bool debug_sync(hipStream_t st, const char *kernel);
+
+// wg_gso_split's three launches (gso.hip); hdr_only = wg_encap_batch's
+// headers-only split (segment headers written, payload left in the input).
+int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
+                     wg_gso_result *dev_res, bool hdr_only, hipStream_t st);
 
 }  // namespace wg
