@@ -224,7 +224,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                "segments_per_buffer": nseg, "parallelism": f"shard{world}"}
         alg = n * in_len + n * out_len + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES)
         return Workload(launch, n, n * in_len, alg, cfg, "weak", buf,
-                        "wg::gso_plan_kernel + wg::gso_split_kernel<4,1,0> + wg::gso_finalize_kernel (one wg_gso_split call)",
+                        "wg::gso_plan_kernel + wg::gso_split_kernel<4,4,0> + wg::gso_finalize_kernel (one wg_gso_split call)",
                         rank * n, sample=sample, counts=[n] * world, post=post)
     if name == "aead":
         # worker/encap.cpp:136-141: Peer::encrypt for every 1500-B segment of a

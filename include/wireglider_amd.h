@@ -383,7 +383,7 @@ int wg_device_count(void);
  *   "gso_groups" blocks per super-buffer, consecutive in the flat grid (1 .. 64)
  *   "gso_waves"  waves per GSO block (1, 2, 4, 8)
  *   "gso_split"  further blocks per super-buffer in grid y (1 .. 64)
- *   "gso_spw"    segments per wave step: 0 serial, 1 ping-pong, 2 pairs
+ *   "gso_spw"    segments per wave step: 0 serial, 1 ping-pong, 2-4 issued together (4)
  *   "verify_dm"  verify descriptor mode: 0 one-shot waves, 2 prefetch
  *   "verify_occ" verify waves/SIMD target (0 = compiler, 6, 8)
  *   "verify_hdr" verify header bytes from the L4 byte gather (1) or a

@@ -45,7 +45,7 @@ static const Knob kKnobs[] = {
     {"gso_waves", nullptr, &Tune::gso_waves, 0, 0, kWaves, WG_N(kWaves)},
     {"gso_split", nullptr, &Tune::gso_split, 1, 64, nullptr, 0},
     {"gso_groups", nullptr, &Tune::gso_groups, 1, 64, nullptr, 0},
-    {"gso_spw", nullptr, &Tune::gso_spw, 0, 2, nullptr, 0},
+    {"gso_spw", nullptr, &Tune::gso_spw, 0, 4, nullptr, 0},
     {"verify_dm", nullptr, &Tune::verify_dm, 0, 0, kDm, WG_N(kDm)},
     {"verify_occ", nullptr, &Tune::verify_occ, 0, 0, kVOcc, WG_N(kVOcc)},
     {"verify_hdr", nullptr, &Tune::verify_hdr, 0, 1, nullptr, 0},
@@ -117,14 +117,16 @@ static Tune &tune_storage() {
         x.l4_small_uniform = 2;  // lane per segment: 64-B PacketBatch 0.342 -> 0.043 ms (quad 0.074)
         x.l4_iters = 4;
         x.gso_blocks = 1u << 23;
-        // GSO: three 4-wave blocks per super-buffer, each wave a ping-pong
-        // pipeline (next segment's loads in flight while this one finishes;
-        // 3 groups -2.5 % vs 1 on two boxes once the per-wave setup is one
-        // scalar round trip); the verify kernel at 8 waves/SIMD (64 VGPRs,
-        // no spill) (tools/ab.py, profiles/r01_ab_*.json).
+        // GSO: three 4-wave blocks per super-buffer (3 groups -2.5 % vs 1 on
+        // two boxes once the per-wave setup is one scalar round trip), each
+        // wave issuing the loads of 4 segments before finishing them (93
+        // VGPRs, 5 waves/SIMD: config 3 -1.7 %, the fused encap -1.4 % vs
+        // the ping-pong pipeline, profiles/r02_gso_spw_ab.json); the verify
+        // kernel at 8 waves/SIMD (64 VGPRs, no spill) (tools/ab.py,
+        // profiles/r01_ab_*.json).
         x.gso_waves = 4;
         x.gso_split = 1;
-        x.gso_spw = 1;
+        x.gso_spw = 4;
         x.gso_groups = 3;
         x.verify_occ = 8;
         x.verify_dm = 0;

@@ -258,7 +258,9 @@ __device__ __forceinline__ void seg_finish(const Ctx &c, uintptr_t out_base, con
 // template bytes, field codes) again: G = 3 x W = 4 measured best.
 // S = segments per wave step: 0 one at a time (occupancy hides latency),
 // 1 ping-pong pipeline (the next segment's loads in flight while this one
-// finishes), 2 two issued then both finished.
+// finishes), 2-4 that many issued then all finished (4, the default: with 3
+// groups of 4 waves a 45-segment super-buffer's wave sends all its ~4
+// segments' loads out at once).
 template <int W, int S, int Abl>
 __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
     constexpr uint32_t kStep = S ? S : 1;
@@ -549,6 +551,8 @@ int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, u
         switch (t.gso_spw) {
         case 1: launch_split<1, kHdrOnly>(p, g, t.gso_waves, st); break;
         case 2: launch_split<2, kHdrOnly>(p, g, t.gso_waves, st); break;
+        case 3: launch_split<3, kHdrOnly>(p, g, t.gso_waves, st); break;
+        case 4: launch_split<4, kHdrOnly>(p, g, t.gso_waves, st); break;
         default: launch_split<0, kHdrOnly>(p, g, t.gso_waves, st); break;
         }
     } else {
@@ -559,6 +563,8 @@ int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, u
             switch (t.gso_spw) {
             case 1: launch_split<1, 0>(p, g, t.gso_waves, st); break;
             case 2: launch_split<2, 0>(p, g, t.gso_waves, st); break;
+            case 3: launch_split<3, 0>(p, g, t.gso_waves, st); break;
+            case 4: launch_split<4, 0>(p, g, t.gso_waves, st); break;
             default: launch_split<0, 0>(p, g, t.gso_waves, st); break;
             }
         }
