@@ -95,7 +95,7 @@ __device__ __forceinline__ T sload(const T *p) {
 #endif
 }
 
-// One output segment by one wave, in two phases so a wave may have several
+// One output segment of the full split by one wave, in two phases so a wave may have several
 // segments' loads in flight: seg_issue() issues every load of the segment
 // (branch-free: clamped offsets, masked use); seg_finish() stores, sums and
 // writes the header.  Only the loaded data and the segment index cross the
@@ -164,33 +164,24 @@ __device__ __forceinline__ void seg_finish(const Ctx &c, uintptr_t out_base, con
     const uint32_t i = f.i, pktlen = g.pktlen;
     Acc acc;
     // payload: store and sum (destination-aligned chunks: absolute pairing)
-    // headers-only: the payload bytes in the header's last 64-B block (the
-    // AEAD reads whole blocks below that bound from the segment slot); every
-    // such chunk is among the first 64
-    constexpr bool kPay = !(Abl & kHdrOnly);
-    const uintptr_t hlim = g.seg + ((c.hdr_len + 63u) & ~63u);
     if (lane < g.nint) {
-        if (kPay || g.c0 + 16u * lane < hlim)
-            st16x<Abl>(g.c0 + 16u * lane, f.lo0);
+        st16x<Abl>(g.c0 + 16u * lane, f.lo0);
         acc.add4(f.lo0);
     }
     if (lane + 64 < g.nint) {
-        if constexpr (kPay)
-            st16x<Abl>(g.c0 + 16u * (lane + 64), f.lo1);
+        st16x<Abl>(g.c0 + 16u * (lane + 64), f.lo1);
         acc.add4(f.lo1);
     }
     if (g.nint > 128) {  // long segments (gso > ~2 KiB)
         for (uint32_t k = lane + 128; k < g.nint; k += 64) {
             const v4u v = ld16(g.base + 16u * k);
-            if constexpr (kPay)
-                st16x<Abl>(g.c0 + 16u * k, v);
+            st16x<Abl>(g.c0 + 16u * k, v);
             acc.add4(v);
         }
     }
     const uint32_t eo = edge_off(g, lane);
     if (eo != kNoEdge) {
-        if (kPay || g.oa + eo < hlim)
-            st8(g.oa + eo, f.pb);
+        st8(g.oa + eo, f.pb);
         acc.add(f.pb << (8u * (((uint32_t)g.oa + eo) & 1u)));
     }
 
@@ -247,6 +238,144 @@ __device__ __forceinline__ void seg_finish(const Ctx &c, uintptr_t out_base, con
                 st8(g.seg + j, hdr_byte_slow(hv, hdr_code(c, j), ld8(c.in + j)));
         }
     }
+}
+
+// The headers-only split (wg_encap_batch) on raw buffer ops.  Most of its
+// lanes have nothing to store (only the header's 64-B block of payload is
+// written), so every access is a buffer op at a 32-bit offset from the
+// super-buffer's input / output base and an idle lane gets the offset kOob:
+// the range check drops its store and returns 0 for its load (adding
+// nothing to the sum) — no EXEC save / restore per conditional access and no
+// 64-bit address arithmetic per lane.  3-4 % faster than seg_issue /
+// seg_finish on the encap step; 1 % slower than them on the full split
+// (config 3), which therefore stays on global_* ops.
+struct HSegGeom {
+    uint32_t seg, oa, sa;  // segment start, payload destination (from c.out), payload source (from c.in)
+    uint32_t c0, src0;     // first destination-aligned interior chunk, and its (unaligned) source
+    uint32_t datalen, pktlen, nint, he, ts;
+    bool last;
+};
+
+__device__ __forceinline__ HSegGeom hseg_geom(const Ctx &c, uint32_t i) {
+    HSegGeom g;
+    g.seg = i * (c.hdr_len + c.gso);
+    const uint32_t off = i * c.gso;
+    g.datalen = c.rest - off < c.gso ? c.rest - off : c.gso;
+    g.pktlen = c.hdr_len + g.datalen;
+    g.last = i + 1 == c.nseg;
+    g.oa = g.seg + c.hdr_len;
+    g.sa = c.hdr_len + off;
+    // destination-aligned interior chunks [A0, A1) in "absolute low bits"
+    // terms (offset + omis), head [oa, A0) and tail [A1, ob) <= 15 bytes each
+    const uint32_t x0 = g.oa + c.omis, xb = x0 + g.datalen;
+    const uint32_t A0 = (x0 + 15u) & ~15u, A1 = xb & ~15u;
+    g.nint = A1 > A0 ? (A1 - A0) >> 4 : 0u;
+    g.c0 = A0 - c.omis;
+    g.he = (A0 < xb ? A0 : xb) - x0;
+    g.ts = (A1 > A0 ? A1 : A0) - x0;
+    g.src0 = g.c0 + (g.sa - g.oa);  // mod 2^32: src0 + 16k is the true, small offset
+    return g;
+}
+
+__device__ __forceinline__ uint32_t hedge_off(const HSegGeom &g, uint32_t lane) {
+    const uint32_t xt = g.ts + lane - 16u;
+    const bool h = lane < 16 && lane < g.he;
+    const bool t = lane >= 16 && lane < 32 && xt < g.datalen;
+    return h ? lane : (t ? xt : kNoEdge);
+}
+
+__device__ __forceinline__ void hseg_issue(const Ctx &c, uint32_t i, uint32_t lane, SegFront &f) {
+    const HSegGeom g = hseg_geom(c, i);
+    f.i = i;
+    f.lo0 = bld16(c.rin, lane < g.nint ? g.src0 + 16u * lane : kOob);
+    f.lo1 = bld16(c.rin, lane + 64 < g.nint ? g.src0 + 16u * lane + 1024u : kOob);
+    const uint32_t eo = hedge_off(g, lane);
+    f.pb = bld8(c.rin, eo != kNoEdge ? g.sa + eo : kOob);
+}
+
+__device__ __forceinline__ void hseg_finish(const Ctx &c, const SegFront &f, uint32_t lane) {
+    const HSegGeom g = hseg_geom(c, f.i);
+    const uint32_t i = f.i, pktlen = g.pktlen;
+    Acc acc;
+    // every payload byte is summed; only those in the header's last 64-B
+    // block are stored (every such chunk is among the first 64)
+    const uint32_t hlim = g.seg + ((c.hdr_len + 63u) & ~63u);
+    const uint32_t d0 = g.c0 + 16u * lane;
+    bst16(c.rout, (lane < g.nint && d0 < hlim) ? d0 : kOob, f.lo0);
+    acc.add4(f.lo0);
+    acc.add4(f.lo1);
+    for (uint32_t k0 = 128; k0 < g.nint; k0 += 64) {  // long segments (gso > ~2 KiB)
+        const uint32_t k = k0 + lane;
+        acc.add4(bld16(c.rin, k < g.nint ? g.src0 + 16u * k : kOob));
+    }
+    const uint32_t eo = hedge_off(g, lane);
+    const uint32_t eoff = g.oa + eo;
+    bst8(c.rout, (eo != kNoEdge && eoff < hlim) ? eoff : kOob, f.pb);
+    acc.add(f.pb << (8u * ((eoff + c.omis) & 1u)));  // pb = 0 on lanes without an edge byte
+
+    uint32_t ipcs = 0;
+    if (!c.v6)
+        ipcs = ~fold16_32(c.ip_base + bswap16(pktlen & 0xffffu) + bswap16((c.id0 + i) & 0xffffu)) & 0xffffu;
+    const uint32_t seq = c.seq0 + c.gso * i;
+    const uint32_t flags = g.last ? c.flags13 : (c.flags13 & ~0x09u);
+    uint32_t l4h = c.l4h_base;
+    if (c.tcp)
+        l4h += bswap16(seq >> 16) + bswap16(seq & 0xffffu) + (flags << 8);
+    else
+        l4h += bswap16((pktlen - c.cs) & 0xffffu);
+    uint32_t lp = fold16(acc.value());
+    if ((g.seg + c.cs + c.omis) & 1u)
+        lp = bswap16(lp);
+    uint32_t T = wave_sum_u32(lp) + l4h + c.ps_sum;
+    T += ((c.tcp ? 6u : 17u) << 8) + bswap16((pktlen - c.cs) & 0xffffu);
+    const uint32_t l4cs = ~fold16_32(T) & 0xffffu;
+    // the header prefix, as in seg_finish
+    uint32_t tbl = 0;
+    tbl = (uint32_t)wg_writelane_i32((int)pktlen, kFldPkt, (int)tbl);
+    tbl = (uint32_t)wg_writelane_i32((int)(c.id0 + i), kFldId, (int)tbl);
+    tbl = (uint32_t)wg_writelane_i32((int)ipcs, kFldIpcs, (int)tbl);
+    tbl = (uint32_t)wg_writelane_i32((int)l4cs, kFldL4cs, (int)tbl);
+    tbl = (uint32_t)wg_writelane_i32((int)seq, kFldSeq, (int)tbl);
+    tbl = (uint32_t)wg_writelane_i32((int)(pktlen - c.cs), kFldUlen, (int)tbl);
+    tbl = (uint32_t)wg_writelane_i32((int)flags, kFldFlags, (int)tbl);
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((c.hc0 & 7u) << 2), (int)tbl);
+    const uint32_t b0 = (c.hc0 & 7u) ? (r0 >> (c.hc0 >> 8)) & 0xffu : c.hb0;
+    bst8(c.rout, lane < c.hdr_len ? g.seg + lane : kOob, b0);
+    if (c.hdr_len > 64) {
+        const uint32_t r1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((c.hc1 & 7u) << 2), (int)tbl);
+        const uint32_t b1 = (c.hc1 & 7u) ? (r1 >> (c.hc1 >> 8)) & 0xffu : c.hb1;
+        bst8(c.rout, lane + 64 < c.hdr_len ? g.seg + lane + 64u : kOob, b1);
+        if (c.hdr_len > 128) {
+            HdrVals hv;
+            hv.v[0] = 0;
+            hv.v[kFldPkt] = pktlen;
+            hv.v[kFldId] = c.id0 + i;
+            hv.v[kFldIpcs] = ipcs;
+            hv.v[kFldL4cs] = l4cs;
+            hv.v[kFldSeq] = seq;
+            hv.v[kFldUlen] = pktlen - c.cs;
+            hv.v[kFldFlags] = flags;
+            for (uint32_t j = lane + 128; j < c.hdr_len; j += 64)
+                st8(c.out + g.seg + j, hdr_byte_slow(hv, hdr_code(c, j), ld8(c.in + j)));
+        }
+    }
+}
+
+// One segment's loads / completion: the headers-only split on buffer ops,
+// everything else on global_* ops.
+template <int Abl>
+__device__ __forceinline__ void seg_go(const Ctx &c, uintptr_t out_base, uint32_t i, uint32_t lane, SegFront &f) {
+    if constexpr (Abl & kHdrOnly)
+        hseg_issue(c, i, lane, f);
+    else
+        seg_issue<Abl>(c, out_base, i, lane, f);
+}
+template <int Abl>
+__device__ __forceinline__ void seg_done(const Ctx &c, uintptr_t out_base, const SegFront &f, uint32_t lane) {
+    if constexpr (Abl & kHdrOnly)
+        hseg_finish(c, f, lane);
+    else
+        seg_finish<Abl>(c, out_base, f, lane);
 }
 
 // Main kernel.  The flat grid walks (super-buffer, group) units: unit u is
@@ -309,36 +438,42 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
         c.hb0 = ld8(c.in + (lane < c.hdr_len ? lane : 0u));
         c.hb1 = ld8(c.in + (lane + 64 < c.hdr_len ? lane + 64 : 0u));
         const uintptr_t out_base = reinterpret_cast<uintptr_t>(p.out) + out_off;
+        if constexpr (Abl & kHdrOnly) {
+            c.out = out_base;
+            c.omis = (uint32_t)out_base & 15u;
+            c.rin = make_rsrc(c.in);
+            c.rout = make_rsrc(out_base);
+        }
         if constexpr (S == 0) {
             c.hc0 = hdr_code(c, lane);
             c.hc1 = hdr_code(c, lane + 64);
             for (uint32_t i = gw; i < c.nseg; i += gstride) {
                 SegFront A;
-                seg_issue<Abl>(c, out_base, i, lane, A);
-                seg_finish<Abl>(c, out_base, A, lane);
+                seg_go<Abl>(c, out_base, i, lane, A);
+                seg_done<Abl>(c, out_base, A, lane);
             }
         } else if constexpr (S == 1) {
             const uint32_t last = c.nseg - 1;
             uint32_t i = gw;
             SegFront A, B;
-            seg_issue<Abl>(c, out_base, i, lane, A);
+            seg_go<Abl>(c, out_base, i, lane, A);
             // the header field codes are needed only when the first header is
             // written: computed while the first segment's loads are in flight
             c.hc0 = hdr_code(c, lane);
             c.hc1 = hdr_code(c, lane + 64);
             if (i + gstride > last) {  // the slot's only segment: no second slot to fill
-                seg_finish<Abl>(c, out_base, A, lane);
+                seg_done<Abl>(c, out_base, A, lane);
                 continue;
             }
             for (;;) {
                 const uint32_t i1 = i + gstride;
-                seg_issue<Abl>(c, out_base, i1 < last ? i1 : last, lane, B);
-                seg_finish<Abl>(c, out_base, A, lane);
+                seg_go<Abl>(c, out_base, i1 < last ? i1 : last, lane, B);
+                seg_done<Abl>(c, out_base, A, lane);
                 if (i1 > last)
                     break;
                 const uint32_t i2 = i1 + gstride;
-                seg_issue<Abl>(c, out_base, i2 < last ? i2 : last, lane, A);
-                seg_finish<Abl>(c, out_base, B, lane);
+                seg_go<Abl>(c, out_base, i2 < last ? i2 : last, lane, A);
+                seg_done<Abl>(c, out_base, B, lane);
                 if (i2 > last)
                     break;
                 i = i2;
@@ -350,11 +485,11 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
                 SegFront f[S];
 #pragma unroll
                 for (int k = 0; k < S; k++)
-                    seg_issue<Abl>(c, out_base, i0 + k < c.nseg ? i0 + k : c.nseg - 1, lane, f[k]);
+                    seg_go<Abl>(c, out_base, i0 + k < c.nseg ? i0 + k : c.nseg - 1, lane, f[k]);
 #pragma unroll
                 for (int k = 0; k < S; k++)
                     if (i0 + k < c.nseg)
-                        seg_finish<Abl>(c, out_base, f[k], lane);
+                        seg_done<Abl>(c, out_base, f[k], lane);
             }
         }
     }

@@ -137,6 +137,32 @@ __device__ __forceinline__ uint32_t ld8(uintptr_t addr) {
     return *reinterpret_cast<g_u8 *>(addr);
 }
 
+// Raw buffer access (buffer_load / buffer_store through a 128-bit resource
+// built from a wave-uniform base): a 32-bit per-lane byte offset instead of
+// a 64-bit address, and the hardware range check as a free lane mask — a
+// lane whose offset is kOob (past kRsrcRecords) loads 0 and stores nothing,
+// with no EXEC manipulation.  Callers keep every real offset below
+// kRsrcRecords (a super-buffer's bytes: < 2^17).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr uint32_t kOob = 0x80000000u;
+constexpr int kRsrcRecords = 0x40000000;
+
+__device__ __forceinline__ rsrc_t make_rsrc(uintptr_t base) {
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, kRsrcRecords, 0x00020000);
+}
+__device__ __forceinline__ v4u bld16(rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+__device__ __forceinline__ uint32_t bld8(rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+}
+__device__ __forceinline__ void bst16(rsrc_t r, uint32_t off, v4u v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+__device__ __forceinline__ void bst8(rsrc_t r, uint32_t off, uint32_t b) {
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)b, r, off, 0, 0);
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;

@@ -45,6 +45,12 @@ struct Ctx {
     uint32_t flags13;   // TCP flags byte of the prefix
     uint32_t hb0, hb1;  // split kernel: this lane's prefix bytes lane, lane + 64
     uint32_t hc0, hc1;  // per-segment field code of prefix bytes lane, lane + 64 (hdr_code)
+    // split kernel: the super-buffer's output base, its low 4 address bits
+    // (destination chunks are 16-B aligned in absolute terms), and buffer
+    // resources over the input super-buffer and its output area
+    uintptr_t out;
+    uint32_t omis;
+    rsrc_t rin, rout;
 };
 
 // Is prefix byte j one of the per-segment L4 header fields?
