@@ -1,0 +1,186 @@
+// Experiment (not built into the library): do the byte stores cost the GSO
+// split its last ~10 % to a plain copy?  Copy-only, config 3 layout
+// (262,144 x 65,535 B in at stride 65,536 -> 45 segments of 1,500 B out at
+// stride 73,216), one-shot waves, one segment each, global order:
+//   C  header bytes and the <= 15-B payload head / tail by byte stores,
+//      interior payload chunks by 16-B stores (the production split's
+//      store pattern; tools/exp/gso_order.hip variant C)
+//   D  every output byte by ONE aligned 16-B store: the wave of segment i
+//      owns the aligned chunks that START in [seg_i, seg_i+1); a chunk mixing
+//      header and payload bytes (segment i's header / payload head, or
+//      segment i's payload tail + segment i+1's first header bytes) is
+//      composed in registers from a payload-aligned and a header-aligned
+//      16-B load with a per-byte select; only the super-buffer's last chunk
+//      (past its output) uses byte stores.
+// Both verified against a host copy of the same layout.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) v4u g_v4u;
+typedef __attribute__((address_space(1))) unsigned char g_u8;
+
+constexpr unsigned N = 1u << 18, IN_STRIDE = 65536, OUT_STRIDE = 73216, IN_LEN = 65535, H = 40, G = 1460;
+constexpr unsigned NSEG = (IN_LEN - H + G - 1) / G, S = H + G;
+constexpr unsigned SLACK = 64;  // readable bytes before / after the input (header / payload over-reads in D)
+
+__device__ __forceinline__ unsigned lane_id() { return threadIdx.x & 63u; }
+__device__ __forceinline__ unsigned wave_in_block() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+__device__ __forceinline__ unsigned seg_dl(unsigned i) {
+    const unsigned rest = IN_LEN - H - i * G;
+    return rest < G ? rest : G;
+}
+
+// C: production store pattern
+__global__ __launch_bounds__(256) void kC(const unsigned char *in, unsigned char *out) {
+    const unsigned nb = gridDim.x, bx = blockIdx.x;
+    const unsigned vb = (bx & 7u) * (nb >> 3) + (bx >> 3);
+    const unsigned g = vb * 4u + wave_in_block();
+    if (g >= N * NSEG) return;
+    const unsigned b = g / NSEG, i = g % NSEG, lane = lane_id();
+    const unsigned char *hdr = in + (size_t)b * IN_STRIDE;
+    const unsigned char *src = hdr + H + (size_t)i * G;
+    unsigned char *dst = out + (size_t)b * OUT_STRIDE + (size_t)i * S;
+    const unsigned dl = seg_dl(i);
+    const uintptr_t oa = (uintptr_t)dst + H, ob = oa + dl;
+    const uintptr_t c0 = (oa + 15) & ~(uintptr_t)15, c1 = ob & ~(uintptr_t)15;
+    const unsigned nint = c1 > c0 ? (unsigned)((c1 - c0) >> 4) : 0u;
+    const uintptr_t base = (uintptr_t)src + (c0 - oa);
+    const unsigned last = nint ? nint - 1 : 0u;
+    const v4u a = *(const g_v4u *)(base + 16u * (lane < last ? lane : last));
+    const v4u c = *(const g_v4u *)(base + 16u * (lane + 64 < last ? lane + 64 : last));
+    const unsigned hb = *(const g_u8 *)((uintptr_t)hdr + (lane < H ? lane : 0u));
+    const unsigned he = (unsigned)(c0 - oa), ts = (unsigned)(c1 - oa);
+    const unsigned off = lane < 16 ? lane : ts + lane - 16;
+    const bool ok = lane < 16 ? lane < he : (lane < 32 && off < dl);
+    const unsigned eb = *(const g_u8 *)((uintptr_t)src + (ok ? off : 0u));
+    if (lane < nint) *(g_v4u *)(c0 + 16u * lane) = a;
+    if (lane + 64 < nint) *(g_v4u *)(c0 + 16u * (lane + 64)) = c;
+    if (lane < H) *(g_u8 *)((uintptr_t)dst + lane) = (unsigned char)hb;
+    if (ok) *(g_u8 *)(oa + off) = (unsigned char)eb;
+}
+
+// select bytes of h where the byte's bit in m (16 bits) is set, else p
+__device__ __forceinline__ v4u sel_bytes(v4u p, v4u h, unsigned m) {
+    auto dm = [](unsigned m4) {  // 4 mask bits -> byte mask
+        return ((m4 & 1u) ? 0xffu : 0u) | ((m4 & 2u) ? 0xff00u : 0u) | ((m4 & 4u) ? 0xff0000u : 0u) |
+               ((m4 & 8u) ? 0xff000000u : 0u);
+    };
+    const unsigned m0 = dm(m & 15u), m1 = dm((m >> 4) & 15u), m2 = dm((m >> 8) & 15u), m3 = dm(m >> 12);
+    return v4u{(p.x & ~m0) | (h.x & m0), (p.y & ~m1) | (h.y & m1), (p.z & ~m2) | (h.z & m2), (p.w & ~m3) | (h.w & m3)};
+}
+
+// D: every byte by one aligned 16-B store (segment starts are 4-B aligned here:
+// S = 1,500 and the super-buffer stride are multiples of 4; the chunk
+// composition itself works at any byte offset)
+__device__ __forceinline__ void d_chunk(const unsigned char *hdr, const unsigned char *src, uintptr_t sd,
+                                        unsigned dl, bool lastseg, unsigned k, uintptr_t c0) {
+    // chunk k of the segment's ownership range: start cA = c0 + 16k, c0 the first aligned address >= sd
+    const uintptr_t cA = c0 + 16u * k;
+    const unsigned rel = (unsigned)(cA - sd);          // offset of the chunk start in segment i (>= 0)
+    const v4u P = *(const g_v4u *)((uintptr_t)src + rel - H);  // payload-aligned (bytes rel..rel+15 of segment i as payload)
+    // header bytes: of segment i when rel < H, else of segment i+1 (at offset rel - S, may be negative)
+    // (chunks without header bytes read the template's first chunk: in bounds)
+    const int hrel = rel < H ? (int)rel : (rel + 16u > S ? (int)rel - (int)S : 0);
+    const v4u Hd = *(const g_v4u *)((intptr_t)hdr + hrel);
+    // header byte positions: the first H - rel (segment i's header), the last
+    // rel + 16 - S (segment i+1's), as a 16-bit mask
+    const unsigned nlo = rel < H ? (H - rel < 16u ? H - rel : 16u) : 0u;
+    const unsigned nhi = (!lastseg && rel + 16u > S) ? rel + 16u - S : 0u;
+    const unsigned m = ((1u << nlo) - 1u) | (0xffffu & ~((1u << (16u - nhi)) - 1u));
+    const v4u v = sel_bytes(P, Hd, m);
+    const unsigned end = H + dl;  // bytes of segment i
+    if (!lastseg || rel + 16u <= end) {
+        *(g_v4u *)cA = v;
+    } else {  // the super-buffer's last, partial chunk
+        const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (unsigned q = 0; q < 16; q++)
+            if (rel + q < end) *(g_u8 *)(cA + q) = (unsigned char)(w[q >> 2] >> (8u * (q & 3u)));
+    }
+}
+
+__global__ __launch_bounds__(256) void kD(const unsigned char *in, unsigned char *out) {
+    const unsigned nb = gridDim.x, bx = blockIdx.x;
+    const unsigned vb = (bx & 7u) * (nb >> 3) + (bx >> 3);
+    const unsigned g = vb * 4u + wave_in_block();
+    if (g >= N * NSEG) return;
+    const unsigned b = g / NSEG, i = g % NSEG, lane = lane_id();
+    const unsigned char *hdr = in + (size_t)b * IN_STRIDE;
+    const unsigned char *src = hdr + H + (size_t)i * G;
+    const uintptr_t sd = (uintptr_t)out + (size_t)b * OUT_STRIDE + (size_t)i * S;
+    const unsigned dl = seg_dl(i);
+    const bool lastseg = i + 1 == NSEG;
+    const uintptr_t c0 = (sd + 15) & ~(uintptr_t)15;                  // first chunk starting in the segment
+    const uintptr_t cend = lastseg ? sd + H + dl : sd + S;             // ownership ends (exclusive)
+    const unsigned nch = (unsigned)((cend - c0 + 15) >> 4);
+    // segment 0 of a super-buffer starts aligned here (OUT_STRIDE % 16 == 0), so no chunk before c0 is ours
+    if (lane < nch) d_chunk(hdr, src, sd, dl, lastseg, lane, c0);
+    if (lane + 64 < nch) d_chunk(hdr, src, sd, dl, lastseg, lane + 64, c0);
+}
+
+int main(int argc, char **argv) {
+    const bool verify = argc > 1 && atoi(argv[1]);
+    unsigned char *inb, *out;
+    const size_t in_bytes = (size_t)N * IN_STRIDE, out_bytes = (size_t)N * OUT_STRIDE;
+    hipMalloc(&inb, in_bytes + 2 * SLACK);
+    hipMalloc(&out, out_bytes);
+    unsigned char *in = inb + SLACK;
+    {
+        std::vector<unsigned char> h(in_bytes);
+        unsigned x = 12345;
+        for (size_t k = 0; k < in_bytes; k++) { x = x * 1664525u + 1013904223u; h[k] = (unsigned char)(x >> 24); }
+        hipMemcpy(in, h.data(), in_bytes, hipMemcpyHostToDevice);
+    }
+    const double bytes = (double)N * IN_LEN + (double)N * (IN_LEN - H + NSEG * H);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    const unsigned nbk = ((N * NSEG + 3) / 4 + 7) & ~7u;
+    auto check = [&](const char *name) {
+        if (!verify) return;
+        std::vector<unsigned char> hi(in_bytes), ho(out_bytes);
+        hipMemcpy(hi.data(), in, in_bytes, hipMemcpyDeviceToHost);
+        hipMemcpy(ho.data(), out, out_bytes, hipMemcpyDeviceToHost);
+        size_t bad = 0;
+        for (unsigned b = 0; b < N; b += 97)
+            for (unsigned i = 0; i < NSEG; i++) {
+                const unsigned char *hh = &hi[(size_t)b * IN_STRIDE];
+                const unsigned char *o = &ho[(size_t)b * OUT_STRIDE + (size_t)i * S];
+                const unsigned dl = IN_LEN - H - i * G < G ? IN_LEN - H - i * G : G;
+                bad += memcmp(o, hh, H) != 0;
+                bad += memcmp(o + H, hh + H + (size_t)i * G, dl) != 0;
+            }
+        printf("{\"verify\": \"%s\", \"bad_segments\": %zu}\n", name, bad);
+    };
+    auto run = [&](const char *name, auto launch) {
+        hipMemset(out, 0, out_bytes);
+        for (int w = 0; w < 3; w++) launch();
+        check(name);
+        float best = 1e9, sum = 0;
+        for (int r = 0; r < 10; r++) {
+            hipEventRecord(e0);
+            launch();
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms;
+            hipEventElapsedTime(&ms, e0, e1);
+            best = ms < best ? ms : best;
+            sum += ms;
+        }
+        printf("{\"variant\": \"%s\", \"ms_avg\": %.4f, \"ms_best\": %.4f, \"TBps_avg\": %.3f}\n", name, sum / 10, best,
+               bytes / (sum / 10 * 1e-3) / 1e12);
+        fflush(stdout);
+    };
+    for (int rep = 0; rep < 3; rep++) {
+        run("C byte stores for header + edges", [&] { hipLaunchKernelGGL(kC, dim3(nbk), dim3(256), 0, 0, in, out); });
+        run("D aligned 16-B stores only", [&] { hipLaunchKernelGGL(kD, dim3(nbk), dim3(256), 0, 0, in, out); });
+    }
+    printf("err=%s\n", hipGetErrorString(hipGetLastError()));
+    return 0;
+}
