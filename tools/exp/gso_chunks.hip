@@ -12,7 +12,14 @@
 //      composed in registers from a payload-aligned and a header-aligned
 //      16-B load with a per-byte select; only the super-buffer's last chunk
 //      (past its output) uses byte stores.
-// Both verified against a host copy of the same layout.
+// Both verified against a host copy of the same layout.  Then, to locate the
+// segment-shaped copy's distance to the plain copy probe (same bytes):
+//   Cn  C with non-temporal loads and stores
+//   Ca  C with each segment's source moved to the destination's 16-B phase
+//       (timing only: reads the same number of bytes, aligned alike)
+//   Dn  D with non-temporal loads and stores
+//   P   plain copy, 4 KiB per one-shot wave, default policy / Pn non-temporal
+//       (the bench copy probe's structure), in -> out contiguous
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -36,33 +43,75 @@ __device__ __forceinline__ unsigned seg_dl(unsigned i) {
     return rest < G ? rest : G;
 }
 
-// C: production store pattern
-__global__ __launch_bounds__(256) void kC(const unsigned char *in, unsigned char *out) {
+// C: production store pattern (NT: non-temporal loads / stores; AL: source
+// moved to the destination's 16-B phase, timing only)
+template <bool NT, bool AL>
+__global__ __launch_bounds__(256) void kCt(const unsigned char *in, unsigned char *out) {
     const unsigned nb = gridDim.x, bx = blockIdx.x;
     const unsigned vb = (bx & 7u) * (nb >> 3) + (bx >> 3);
     const unsigned g = vb * 4u + wave_in_block();
     if (g >= N * NSEG) return;
     const unsigned b = g / NSEG, i = g % NSEG, lane = lane_id();
     const unsigned char *hdr = in + (size_t)b * IN_STRIDE;
-    const unsigned char *src = hdr + H + (size_t)i * G;
     unsigned char *dst = out + (size_t)b * OUT_STRIDE + (size_t)i * S;
+    const unsigned char *src = hdr + H + (size_t)i * G;
+    if constexpr (AL)
+        src = hdr + (((size_t)i * G) & ~(size_t)15) + (((uintptr_t)dst + H) & 15u);
     const unsigned dl = seg_dl(i);
     const uintptr_t oa = (uintptr_t)dst + H, ob = oa + dl;
     const uintptr_t c0 = (oa + 15) & ~(uintptr_t)15, c1 = ob & ~(uintptr_t)15;
     const unsigned nint = c1 > c0 ? (unsigned)((c1 - c0) >> 4) : 0u;
     const uintptr_t base = (uintptr_t)src + (c0 - oa);
     const unsigned last = nint ? nint - 1 : 0u;
-    const v4u a = *(const g_v4u *)(base + 16u * (lane < last ? lane : last));
-    const v4u c = *(const g_v4u *)(base + 16u * (lane + 64 < last ? lane + 64 : last));
+    v4u a, c;
+    if constexpr (NT) {
+        a = __builtin_nontemporal_load((const g_v4u *)(base + 16u * (lane < last ? lane : last)));
+        c = __builtin_nontemporal_load((const g_v4u *)(base + 16u * (lane + 64 < last ? lane + 64 : last)));
+    } else {
+        a = *(const g_v4u *)(base + 16u * (lane < last ? lane : last));
+        c = *(const g_v4u *)(base + 16u * (lane + 64 < last ? lane + 64 : last));
+    }
     const unsigned hb = *(const g_u8 *)((uintptr_t)hdr + (lane < H ? lane : 0u));
     const unsigned he = (unsigned)(c0 - oa), ts = (unsigned)(c1 - oa);
     const unsigned off = lane < 16 ? lane : ts + lane - 16;
     const bool ok = lane < 16 ? lane < he : (lane < 32 && off < dl);
     const unsigned eb = *(const g_u8 *)((uintptr_t)src + (ok ? off : 0u));
-    if (lane < nint) *(g_v4u *)(c0 + 16u * lane) = a;
-    if (lane + 64 < nint) *(g_v4u *)(c0 + 16u * (lane + 64)) = c;
+    if constexpr (NT) {
+        if (lane < nint) __builtin_nontemporal_store(a, (g_v4u *)(c0 + 16u * lane));
+        if (lane + 64 < nint) __builtin_nontemporal_store(c, (g_v4u *)(c0 + 16u * (lane + 64)));
+    } else {
+        if (lane < nint) *(g_v4u *)(c0 + 16u * lane) = a;
+        if (lane + 64 < nint) *(g_v4u *)(c0 + 16u * (lane + 64)) = c;
+    }
     if (lane < H) *(g_u8 *)((uintptr_t)dst + lane) = (unsigned char)hb;
     if (ok) *(g_u8 *)(oa + off) = (unsigned char)eb;
+}
+
+// P: plain copy of nbytes (multiple of 16), 4 KiB per one-shot wave
+template <bool NT>
+__global__ __launch_bounds__(256) void kP(const unsigned char *in, unsigned char *out, size_t nch) {
+    const unsigned nb = gridDim.x, bx = blockIdx.x;
+    const size_t vb = (size_t)(bx & 7u) * (nb >> 3) + (bx >> 3);
+    const size_t c0 = (vb * 4u + wave_in_block()) * 256u;
+    const unsigned lane = lane_id();
+    v4u v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const size_t c = c0 + 64u * u + lane;
+        const g_v4u *q = (const g_v4u *)(in + 16u * (c < nch ? c : nch - 1));
+        v[u] = NT ? __builtin_nontemporal_load(q) : *q;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const size_t c = c0 + 64u * u + lane;
+        if (c < nch) {
+            g_v4u *q = (g_v4u *)(out + 16u * c);
+            if (NT)
+                __builtin_nontemporal_store(v[u], q);
+            else
+                *q = v[u];
+        }
+    }
 }
 
 // select bytes of h where the byte's bit in m (16 bits) is set, else p
@@ -78,12 +127,14 @@ __device__ __forceinline__ v4u sel_bytes(v4u p, v4u h, unsigned m) {
 // D: every byte by one aligned 16-B store (segment starts are 4-B aligned here:
 // S = 1,500 and the super-buffer stride are multiples of 4; the chunk
 // composition itself works at any byte offset)
+template <bool NT>
 __device__ __forceinline__ void d_chunk(const unsigned char *hdr, const unsigned char *src, uintptr_t sd,
                                         unsigned dl, bool lastseg, unsigned k, uintptr_t c0) {
     // chunk k of the segment's ownership range: start cA = c0 + 16k, c0 the first aligned address >= sd
     const uintptr_t cA = c0 + 16u * k;
     const unsigned rel = (unsigned)(cA - sd);          // offset of the chunk start in segment i (>= 0)
-    const v4u P = *(const g_v4u *)((uintptr_t)src + rel - H);  // payload-aligned (bytes rel..rel+15 of segment i as payload)
+    const g_v4u *pq = (const g_v4u *)((uintptr_t)src + rel - H);  // payload-aligned (bytes rel..rel+15 of segment i as payload)
+    const v4u P = NT ? __builtin_nontemporal_load(pq) : *pq;
     // header bytes: of segment i when rel < H, else of segment i+1 (at offset rel - S, may be negative)
     // (chunks without header bytes read the template's first chunk: in bounds)
     const int hrel = rel < H ? (int)rel : (rel + 16u > S ? (int)rel - (int)S : 0);
@@ -96,7 +147,10 @@ __device__ __forceinline__ void d_chunk(const unsigned char *hdr, const unsigned
     const v4u v = sel_bytes(P, Hd, m);
     const unsigned end = H + dl;  // bytes of segment i
     if (!lastseg || rel + 16u <= end) {
-        *(g_v4u *)cA = v;
+        if (NT)
+            __builtin_nontemporal_store(v, (g_v4u *)cA);
+        else
+            *(g_v4u *)cA = v;
     } else {  // the super-buffer's last, partial chunk
         const unsigned w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -105,6 +159,7 @@ __device__ __forceinline__ void d_chunk(const unsigned char *hdr, const unsigned
     }
 }
 
+template <bool NT>
 __global__ __launch_bounds__(256) void kD(const unsigned char *in, unsigned char *out) {
     const unsigned nb = gridDim.x, bx = blockIdx.x;
     const unsigned vb = (bx & 7u) * (nb >> 3) + (bx >> 3);
@@ -120,8 +175,8 @@ __global__ __launch_bounds__(256) void kD(const unsigned char *in, unsigned char
     const uintptr_t cend = lastseg ? sd + H + dl : sd + S;             // ownership ends (exclusive)
     const unsigned nch = (unsigned)((cend - c0 + 15) >> 4);
     // segment 0 of a super-buffer starts aligned here (OUT_STRIDE % 16 == 0), so no chunk before c0 is ours
-    if (lane < nch) d_chunk(hdr, src, sd, dl, lastseg, lane, c0);
-    if (lane + 64 < nch) d_chunk(hdr, src, sd, dl, lastseg, lane + 64, c0);
+    if (lane < nch) d_chunk<NT>(hdr, src, sd, dl, lastseg, lane, c0);
+    if (lane + 64 < nch) d_chunk<NT>(hdr, src, sd, dl, lastseg, lane + 64, c0);
 }
 
 int main(int argc, char **argv) {
@@ -158,7 +213,8 @@ int main(int argc, char **argv) {
             }
         printf("{\"verify\": \"%s\", \"bad_segments\": %zu}\n", name, bad);
     };
-    auto run = [&](const char *name, auto launch) {
+    auto run = [&](const char *name, auto launch, double nbytes = 0) {
+        if (nbytes == 0) nbytes = bytes;
         hipMemset(out, 0, out_bytes);
         for (int w = 0; w < 3; w++) launch();
         check(name);
@@ -174,12 +230,24 @@ int main(int argc, char **argv) {
             sum += ms;
         }
         printf("{\"variant\": \"%s\", \"ms_avg\": %.4f, \"ms_best\": %.4f, \"TBps_avg\": %.3f}\n", name, sum / 10, best,
-               bytes / (sum / 10 * 1e-3) / 1e12);
+               nbytes / (sum / 10 * 1e-3) / 1e12);
         fflush(stdout);
     };
     for (int rep = 0; rep < 3; rep++) {
-        run("C byte stores for header + edges", [&] { hipLaunchKernelGGL(kC, dim3(nbk), dim3(256), 0, 0, in, out); });
-        run("D aligned 16-B stores only", [&] { hipLaunchKernelGGL(kD, dim3(nbk), dim3(256), 0, 0, in, out); });
+        run("C byte stores for header + edges", [&] { hipLaunchKernelGGL((kCt<false, false>), dim3(nbk), dim3(256), 0, 0, in, out); });
+        run("D aligned 16-B stores only", [&] { hipLaunchKernelGGL(kD<false>, dim3(nbk), dim3(256), 0, 0, in, out); });
+        run("Dn D non-temporal", [&] { hipLaunchKernelGGL(kD<true>, dim3(nbk), dim3(256), 0, 0, in, out); });
+        if (!verify) {
+            run("Cn C non-temporal", [&] { hipLaunchKernelGGL((kCt<true, false>), dim3(nbk), dim3(256), 0, 0, in, out); });
+            run("Ca C source in the destination's 16-B phase", [&] { hipLaunchKernelGGL((kCt<false, true>), dim3(nbk), dim3(256), 0, 0, in, out); });
+            // the whole input copied (2 x 17.18 GB moved; C moves 34.84 GB)
+            const size_t nch = in_bytes / 16;
+            const unsigned pbk = (unsigned)(((nch + 1023) / 1024 + 7) & ~(size_t)7);
+            run("P plain copy 4 KiB/wave", [&] { hipLaunchKernelGGL(kP<false>, dim3(pbk), dim3(256), 0, 0, in, out, nch); },
+                2.0 * in_bytes);
+            run("Pn plain copy 4 KiB/wave non-temporal", [&] { hipLaunchKernelGGL(kP<true>, dim3(pbk), dim3(256), 0, 0, in, out, nch); },
+                2.0 * in_bytes);
+        }
     }
     printf("err=%s\n", hipGetErrorString(hipGetLastError()));
     return 0;
