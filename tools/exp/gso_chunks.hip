@@ -18,6 +18,7 @@
 //   Ca  C with each segment's source moved to the destination's 16-B phase
 //       (timing only: reads the same number of bytes, aligned alike)
 //   Dn  D with non-temporal loads and stores
+//   R   region-owning waves with per-segment sums (kR), Rn non-temporal
 //   P   plain copy, 4 KiB per one-shot wave, default policy / Pn non-temporal
 //       (the bench copy probe's structure), in -> out contiguous
 #include <hip/hip_runtime.h>
@@ -179,12 +180,70 @@ __global__ __launch_bounds__(256) void kD(const unsigned char *in, unsigned char
     if (lane + 64 < nch) d_chunk<NT>(hdr, src, sd, dl, lastseg, lane + 64, c0);
 }
 
+
+// R: region-owning waves (the next-step design): wave = one 4-KiB region of a
+// super-buffer's output, every byte by an aligned 16-B store (composed as in
+// D); the wave that holds a segment's start also loads that segment's whole
+// payload and sums it (bytes the neighbouring region's wave loads too: L2),
+// the sum stored per segment.
+constexpr unsigned RB = 4096, OUT_LEN = (NSEG - 1) * S + H + (IN_LEN - H - (NSEG - 1) * G);
+constexpr unsigned NREG = (OUT_LEN + RB - 1) / RB;
+
+__device__ __forceinline__ unsigned wsum64(unsigned v) {
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+template <bool NT>
+__global__ __launch_bounds__(256) void kR(const unsigned char *in, unsigned char *out, unsigned *sums) {
+    const unsigned nb = gridDim.x, bx = blockIdx.x;
+    const unsigned vb = (bx & 7u) * (nb >> 3) + (bx >> 3);
+    const unsigned g = vb * 4u + wave_in_block();
+    if (g >= N * NREG) return;
+    const unsigned b = g / NREG, r = g % NREG, lane = lane_id();
+    const unsigned char *hdr = in + (size_t)b * IN_STRIDE;
+    const uintptr_t ob = (uintptr_t)out + (size_t)b * OUT_STRIDE;
+    const unsigned R0 = r * RB, R1 = R0 + RB < OUT_LEN ? R0 + RB : OUT_LEN;
+#pragma unroll
+    for (unsigned u = 0; u < 4; u++) {
+        const unsigned off = R0 + 16u * (lane + 64u * u);
+        if (off < R1) {
+            const unsigned j = off / S, rel = off - j * S;
+            const unsigned char *src = hdr + H + (size_t)j * G;
+            d_chunk<NT>(hdr, src, ob + (size_t)j * S, seg_dl(j), j + 1 == NSEG, 0, ob + off);
+            (void)rel;
+        }
+    }
+    // sums of the segments starting in [R0, R1)
+    const unsigned j0 = (R0 + S - 1) / S, j1 = (R1 + S - 1) / S;
+    for (unsigned j = j0; j < j1 && j < NSEG; j++) {
+        const unsigned char *src = hdr + H + (size_t)j * G;
+        const unsigned dl = seg_dl(j), nc = (dl + 15u) / 16u;
+        unsigned acc = 0;
+        for (unsigned k = lane; k < nc; k += 64) {
+            const v4u v = NT ? __builtin_nontemporal_load((const g_v4u *)(src + 16u * k)) : *(const g_v4u *)(src + 16u * k);
+            const unsigned nbytes = dl - 16u * k < 16u ? dl - 16u * k : 16u;
+            const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (unsigned q = 0; q < 4; q++) {
+                const unsigned kb = nbytes > 4u * q ? (nbytes - 4u * q < 4u ? nbytes - 4u * q : 4u) : 0u;
+                const unsigned x = w[q] & (unsigned)((1ull << (8u * kb)) - 1ull);
+                acc += (x & 0xffffu) + (x >> 16);
+            }
+        }
+        acc = wsum64(acc);
+        if (lane == 0) sums[(size_t)b * NSEG + j] = acc;
+    }
+}
+
 int main(int argc, char **argv) {
     const bool verify = argc > 1 && atoi(argv[1]);
     unsigned char *inb, *out;
     const size_t in_bytes = (size_t)N * IN_STRIDE, out_bytes = (size_t)N * OUT_STRIDE;
     hipMalloc(&inb, in_bytes + 2 * SLACK);
     hipMalloc(&out, out_bytes);
+    unsigned *sums;
+    hipMalloc(&sums, sizeof(unsigned) * N * NSEG);
     unsigned char *in = inb + SLACK;
     {
         std::vector<unsigned char> h(in_bytes);
@@ -237,6 +296,9 @@ int main(int argc, char **argv) {
         run("C byte stores for header + edges", [&] { hipLaunchKernelGGL((kCt<false, false>), dim3(nbk), dim3(256), 0, 0, in, out); });
         run("D aligned 16-B stores only", [&] { hipLaunchKernelGGL(kD<false>, dim3(nbk), dim3(256), 0, 0, in, out); });
         run("Dn D non-temporal", [&] { hipLaunchKernelGGL(kD<true>, dim3(nbk), dim3(256), 0, 0, in, out); });
+        const unsigned rbk = ((N * NREG + 3) / 4 + 7) & ~7u;
+        run("R region waves + segment sums", [&] { hipLaunchKernelGGL(kR<false>, dim3(rbk), dim3(256), 0, 0, in, out, sums); });
+        run("Rn R non-temporal", [&] { hipLaunchKernelGGL(kR<true>, dim3(rbk), dim3(256), 0, 0, in, out, sums); });
         if (!verify) {
             run("Cn C non-temporal", [&] { hipLaunchKernelGGL((kCt<true, false>), dim3(nbk), dim3(256), 0, 0, in, out); });
             run("Ca C source in the destination's 16-B phase", [&] { hipLaunchKernelGGL((kCt<false, true>), dim3(nbk), dim3(256), 0, 0, in, out); });
