@@ -142,10 +142,11 @@ __device__ __forceinline__ uint32_t ld8(uintptr_t addr) {
 // a 64-bit address, and the hardware range check as a free lane mask — a
 // lane whose offset is kOob (past kRsrcRecords) loads 0 and stores nothing,
 // with no EXEC manipulation.  Callers keep every real offset below
-// kRsrcRecords (a super-buffer's bytes: < 2^17).
+// kRsrcRecords (a super-buffer's input < 2^16 bytes; its split output at
+// most ~2^30: 32,767 one-byte segments behind a 32,768-byte header).
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr uint32_t kOob = 0x80000000u;
-constexpr int kRsrcRecords = 0x40000000;
+constexpr int kRsrcRecords = 0x7fffffff;
 
 __device__ __forceinline__ rsrc_t make_rsrc(uintptr_t base) {
     return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, kRsrcRecords, 0x00020000);
