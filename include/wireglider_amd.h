@@ -264,11 +264,16 @@ int wg_aead_decrypt_verify_batch(const uint8_t *dev_in, uint64_t total_len, uint
  *     reference's outbuf layout (worker/encap.cpp:131-141,161-168);
  *   max_segments / max_segment_size: bounds over the batch (super-buffers
  *     past them, or whose messages exceed msg_cap, get nmsg 0);
- *   dev_res[i]: counter0, nmsg (0 for GSO errors), msg_bytes;
+ *   dev_res[i]: counter0, nmsg (0 for GSO errors), msg_bytes = the bytes of
+ *     the messages written, i.e. up to the first refused counter (the
+ *     reference's outbuf advances over accepted messages only,
+ *     worker/encap.cpp:138-140, while encrypt_nonce counts every segment);
  *   dev_work: 4 * (n + 1024) bytes of scratch; dev_total (nullable): messages
  *     in all, i.e. counter0 + *dev_total is the peer's next encrypt_nonce.
- * n <= 2^20 super-buffers per call.  A message whose counter reaches
- * RejectAfterMessages is not written (the reference's encrypt refuses it). */
+ * n <= 2^20 super-buffers per call and max_segments * n < 2^32 (the counter
+ * scan indexes messages in 32 bits; larger calls are WG_ERR_INVALID, never a
+ * repeated nonce).  A message whose counter reaches RejectAfterMessages is
+ * not written (the reference's encrypt refuses it). */
 typedef struct wg_encap_result {
     uint64_t counter0;
     uint32_t nmsg;
@@ -302,19 +307,59 @@ int wg_encap_batch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uin
  * (tun read buffers, worker/encap.cpp:74-97; UDP GRO recvmsg buffers,
  * worker/decap.cpp:16-28,90-156).  Synchronous.  The batch is cut into
  * chunks of whole segments (~host_chunk_mb MiB) that flow through a per-thread pipeline of
- * three device slots on two streams: chunk k+1's hipMemcpyAsync H2D runs
- * under chunk k's kernel and result copy; results gather in a pinned buffer
- * and reach host_out once at the end.  host_base may be pageable (the HIP
- * runtime stages it) or pinned (wg_host_alloc: DMA straight from it).  The
+ * three device slots on three streams (H2D, kernels, D2H): chunk k+1's
+ * hipMemcpyAsync H2D runs under chunk k's kernel and chunk k-1's result copy;
+ * results gather in a pinned buffer and reach host_out once at the end.
+ * host_base may be pageable (the HIP runtime stages it) or pinned
+ * (wg_host_alloc: DMA straight from it).  The
  * workspace (streams, events, device slots, pinned results) is per calling
- * thread, reused across calls, and freed at thread exit or by
- * wg_host_release().  Rate: PCIe-bound, never the metric.
+ * thread and per its current device, reused across calls, and freed at thread
+ * exit or by wg_host_release().  An error after the first copy was queued
+ * drains the streams before returning: no DMA touches the caller's buffers
+ * after any host-path call returns.  Rate: PCIe-bound,
+ * never the metric.
  * ---------------------------------------------------------------------- */
 int wg_l4csum_uniform_host(const uint8_t *host_base, uint64_t total_len, uint32_t segment_size,
                            uint16_t csum_start, uint32_t flags, uint16_t *host_out);
 
+/* The decap worker's step from a UDP GRO batch in host memory
+ * (worker/decap.cpp:90-156 recvmsg -> worker/decap_ref.cpp:53-89 decrypt +
+ * evaluate_packet): every message of the batch (equal-size data messages at
+ * stride segment_size, the last may be short) decrypted, and — when
+ * host_verdict / host_l4 are given (both or neither) — run through the f1
+ * verify gates in the same pass, exactly as wg_aead_decrypt_verify_batch
+ * (wg_aead_decrypt_batch without them).  Plaintext i lands at host_plain +
+ * i * (segment_size - 32) (n * (segment_size - 32) bytes); host_status[i],
+ * host_verdict[i], host_l4[i] per message.  Bytes of host_plain outside an
+ * accepted message's plaintext (rejected messages, the tail of a short last
+ * message's slot) are unspecified.  Pipelined like wg_l4csum_uniform_host
+ * (chunks of ~host_chunk_mb MiB of messages, H2D / kernel / D2H on three
+ * streams); synchronous; pinned buffers (wg_host_alloc) keep the copies
+ * asynchronous. */
+int wg_decap_host(const uint8_t *host_msgs, uint64_t total_len, uint32_t segment_size, const uint8_t key[32],
+                  uint8_t *host_plain, int8_t *host_status, uint8_t *host_verdict, uint16_t *host_l4);
+
+/* The encap worker's step from tun reads in host memory (worker/encap.cpp:
+ * 22-170: do_tun_recv -> do_tun_gso_split -> Peer::encrypt per segment):
+ * host_desc[i] (wg_gso_desc) describes tun read i at host_in +
+ * in_offset (reads in input order, not overlapping; out_cap = the split's
+ * output capacity as the reference's outbuf, out_offset ignored: the segment
+ * headers stay on the device).  Exactly wg_encap_batch over the whole batch,
+ * with the counters running on across chunks on the device: super-buffer i's
+ * messages at host_msgs + i * msg_cap (msg_cap a multiple of 16; bytes of
+ * host_msgs past msg_bytes are unspecified), host_res[i] its wg_encap_result,
+ * host_gso_res[i] (nullable) its wg_gso_result, *next_counter (nullable) =
+ * counter0 + every segment's message = the peer's next encrypt_nonce.
+ * Chunks of whole super-buffers, ~host_chunk_mb MiB of input each; input
+ * prefixes are zeroed on the device copy only. */
+int wg_encap_host(const uint8_t *host_in, const wg_gso_desc *host_desc, uint64_t n, const uint8_t key[32],
+                  uint32_t receiver_index, uint64_t counter0, uint32_t max_segments, uint32_t max_segment_size,
+                  uint32_t msg_cap, uint8_t *host_msgs, wg_encap_result *host_res, wg_gso_result *host_gso_res,
+                  uint64_t *next_counter);
+
 /* Free the calling thread's host-path workspace now (it is rebuilt on the
- * next wg_l4csum_uniform_host call).  Always WG_OK. */
+ * next host-path call).  The caller's current device is left as it was.
+ * Always WG_OK. */
 int wg_host_release(void);
 
 /* Pinned (page-locked) host memory for packet I/O buffers — the reference's

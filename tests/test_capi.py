@@ -85,6 +85,12 @@ def test_invalid_args_rejected_without_gpu():
     assert wga.lib.wg_encap_encrypt(16, 16, 16, 16, 1, key, 1, 0, 16, 1 << 16, 45, 1500, 8, 16, 16, None, None) == -1
     assert wga.lib.wg_encap_encrypt(16, 16, 16, 16, 1, None, 1, 0, 16, 1 << 16, 45, 1500, 16, 16, 16, None, None) == -1
     assert wga.lib.wg_encap_encrypt(16, 16, 16, 16, 0, key, 1, 0, 16, 1 << 16, 45, 1500, 16, 16, 16, None, None) == 0
+    # 2^32 messages or more in one call: the 32-bit counter scan would wrap
+    # (repeated nonces), so it is refused on the host
+    assert wga.lib.wg_encap_encrypt(16, 16, 16, 16, 1 << 20, key, 1, 0, 16, 1 << 16, 4096, 1500, 16, 16, 16, None,
+                                    None) == -1
+    assert wga.lib.wg_encap_batch(16, 16, 1 << 20, 16, 16, key, 1, 0, 16, 1 << 16, 4096, 1500, 16, 16, 16, None,
+                                  None) == -1
     # the fused encap step: the same bounds, out (the header slots) required
     assert wga.lib.wg_encap_batch(16, 16, 1, 16, 16, key, 1, 0, 16, 1 << 16, 0, 1500, 16, 16, 16, None, None) == -1
     assert wga.lib.wg_encap_batch(16, 16, 1, 16, 16, key, 1, 0, 16, 1 << 16, 45, 70000, 16, 16, 16, None, None) == -1

@@ -122,3 +122,57 @@ def test_encap_matches_oracle(gpu, seed, knobs, fused):
         ctr += ns
         n_msgs += ns
     assert int(total.cpu()[0]) == n_msgs and n_msgs > 50
+
+
+@pytest.mark.parametrize("fused", [False, True], ids=["split+encrypt", "encap_batch"])
+def test_encap_reject_after_messages(gpu, fused):
+    """Counters crossing RejectAfterMessages inside a super-buffer: the
+    reference's encrypt refuses every counter >= it (proto.cpp:560-562) but
+    still advances encrypt_nonce, and the encap worker advances its outbuf
+    over accepted messages only (worker/encap.cpp:138-140): super-buffer 0 is
+    all accepted, super-buffer 1 keeps its first 2 messages, super-buffer 2
+    none; nmsg / counter0 / the total count every segment."""
+    import torch
+
+    import pktbuild
+
+    wga = _wga()
+    n, gso, pay = 3, 100, 500  # 5 segments each
+    pkts = [pktbuild.make_tcp(False, "192.0.2.1", 1, "192.0.2.2", 1, 0x18, pay, 1000 + k) for k in range(n)]
+    cap = 8192
+    desc = np.zeros(n, dtype=wga.GSO_DESC_DTYPE)
+    desc["in_offset"] = np.arange(n) * 1024
+    desc["out_offset"] = np.arange(n) * cap
+    desc["in_len"], desc["out_cap"] = [len(p) for p in pkts], cap
+    for f, v in (("flags", 1), ("gso_type", 1), ("hdr_len", 40), ("gso_size", gso), ("csum_start", 20),
+                 ("csum_offset", 16)):
+        desc["vnet"][f] = v
+    inbuf = np.zeros(n * 1024, np.uint8)
+    for k, p in enumerate(pkts):
+        inbuf[k * 1024:k * 1024 + len(p)] = np.frombuffer(p, np.uint8)
+    d_in = torch.from_numpy(inbuf).to(gpu)
+    d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(gpu)
+    d_out = torch.zeros(n * cap, dtype=torch.uint8, device=gpu)
+    key = bytes(range(32))
+    c0 = oracle.REJECT_AFTER_MESSAGES - 7  # super-buffer 1's segments 2-4 are refused
+    msg_off = torch.from_numpy(np.arange(n, dtype=np.int64) * cap).to(gpu)
+    msgs = torch.full((n * cap,), 0xEE, dtype=torch.uint8, device=gpu)
+    d_res = wga.gso_split(d_in.clone(), d_desc, d_out)
+    if fused:
+        eres, total = wga.encap_batch(d_in.clone(), d_desc, torch.zeros_like(d_out), torch.zeros_like(d_res), key, 7,
+                                      c0, msg_off, cap, 8, 200, msgs)
+    else:
+        eres, total = wga.encap_encrypt(d_in, d_out, d_desc, d_res, key, 7, c0, msg_off, cap, 8, 200, msgs)
+    torch.cuda.synchronize()
+    e = eres.cpu().numpy().view(wga.ENCAP_RESULT_DTYPE)
+    got, segs = msgs.cpu().numpy(), d_out.cpu().numpy()
+    stride = 32 + (140 + 15) // 16 * 16
+    assert int(total.cpu()[0]) == 5 * n
+    assert list(e["nmsg"]) == [5, 5, 5]
+    assert list(e["counter0"]) == [c0, c0 + 5, c0 + 10]
+    assert list(e["msg_bytes"]) == [5 * stride, 2 * stride, 0]
+    for i, keep in enumerate((5, 2, 0)):
+        ol = 5 * 140
+        exp = oracle.wg_encrypt_batch(key, 7, c0 + 5 * i, segs[i * cap:i * cap + ol], 140)
+        np.testing.assert_array_equal(got[i * cap:i * cap + keep * stride], exp[:keep * stride])
+        assert np.all(got[i * cap + keep * stride:(i + 1) * cap] == 0xEE), i  # refused messages: nothing written

@@ -46,6 +46,8 @@ EXPORTED_SYMBOLS = (
     "wg_encap_encrypt",
     "wg_encap_batch",
     "wg_l4csum_uniform_host",
+    "wg_decap_host",
+    "wg_encap_host",
     "wg_host_release",
     "wg_host_alloc",
     "wg_host_free",
@@ -123,6 +125,9 @@ def _load() -> ctypes.CDLL:
         "wg_encap_batch": (i32, [u8p, vp, u64, u8p, vp, ctypes.c_char_p, u32, u64, vp, u32, u32, u32, u8p, vp, vp, vp,
                                  vp]),
         "wg_l4csum_uniform_host": (i32, [u8p, u64, u32, u16, u32, vp]),
+        "wg_decap_host": (i32, [u8p, u64, u32, ctypes.c_char_p, vp, vp, vp, vp]),
+        "wg_encap_host": (i32, [u8p, vp, u64, ctypes.c_char_p, u32, u64, u32, u32, u32, vp, vp, vp,
+                                ctypes.POINTER(u64)]),
         "wg_host_release": (i32, []),
         "wg_host_alloc": (i32, [ctypes.POINTER(ctypes.c_void_p), u64]),
         "wg_host_free": (i32, [vp]),
@@ -489,6 +494,74 @@ def calc_l4_checksum_host(buf: bytes | bytearray | memoryview, segment_size: int
                                     out.ctypes.data)
     _check(rc, "wg_l4csum_uniform_host")
     return out
+
+
+def _host_u8(a, name):
+    import numpy as np
+
+    if not isinstance(a, np.ndarray) or a.dtype != np.uint8 or not a.flags.c_contiguous:
+        raise WireGliderError(f"{name} must be a contiguous numpy uint8 array (host memory)")
+    return a
+
+
+def decap_host(msgs, segment_size: int, key: bytes, verify: bool = True, plain=None):
+    """The decap worker's step on a UDP GRO batch in host memory
+    (worker/decap_ref.cpp:53-89: Peer::decrypt, then evaluate_packet): msgs
+    (numpy uint8, e.g. a PinnedBuffer's array) holds equal-size messages at
+    stride segment_size.  Returns (plaintext uint8 array, status int8, verdict
+    uint8 or None, l4 uint16 or None), as aead_decrypt_verify_batch would."""
+    import numpy as np
+
+    if len(key) != 32:
+        raise WireGliderError("key must be 32 bytes")
+    m = _host_u8(msgs, "msgs")
+    n = nr_segments(m.size, segment_size)
+    need = n * max(segment_size - 32, 0)
+    if plain is None:
+        plain = np.empty(max(need, 1), np.uint8)
+    _host_u8(plain, "plain")
+    if plain.size < need:
+        raise WireGliderError(f"plain: {plain.size} bytes, the batch needs {need}")
+    status = np.empty(max(n, 1), np.int8)
+    verdict = np.empty(max(n, 1), np.uint8) if verify else None
+    l4 = np.empty(max(n, 1), np.uint16) if verify else None
+    rc = lib.wg_decap_host(m.ctypes.data, m.size, segment_size, bytes(key), plain.ctypes.data, status.ctypes.data,
+                           verdict.ctypes.data if verify else None, l4.ctypes.data if verify else None)
+    _check(rc, "wg_decap_host")
+    return plain[:need], status[:n], (verdict[:n] if verify else None), (l4[:n] if verify else None)
+
+
+def encap_host(inbuf, gso_desc, key: bytes, receiver_index: int, counter0: int, max_segments: int,
+               max_segment_size: int, msg_cap: int, msgs=None):
+    """The encap worker's step on tun reads in host memory (worker/encap.cpp:
+    22-170): inbuf (numpy uint8) holds the super-buffers gso_desc (numpy
+    GSO_DESC_DTYPE array) describes, in input order; super-buffer i's
+    messages at msgs[i * msg_cap:].  Returns (msgs, results ENCAP_RESULT_DTYPE,
+    gso results GSO_RESULT_DTYPE, next counter)."""
+    import numpy as np
+
+    if len(key) != 32:
+        raise WireGliderError("key must be 32 bytes")
+    a = _host_u8(inbuf, "inbuf")
+    d = np.ascontiguousarray(gso_desc)
+    if d.dtype != GSO_DESC_DTYPE:
+        raise WireGliderError("gso_desc must be a GSO_DESC_DTYPE array")
+    n = d.size
+    if n and int((d["in_offset"] + d["in_len"]).max()) > a.size:
+        raise WireGliderError("gso_desc reaches past inbuf")
+    if msgs is None:
+        msgs = np.empty(max(n * msg_cap, 1), np.uint8)
+    _host_u8(msgs, "msgs")
+    if msgs.size < n * msg_cap:
+        raise WireGliderError(f"msgs: {msgs.size} bytes, the batch needs {n * msg_cap}")
+    res = np.zeros(max(n, 1), ENCAP_RESULT_DTYPE)
+    gres = np.zeros(max(n, 1), GSO_RESULT_DTYPE)
+    nxt = ctypes.c_uint64(0)
+    rc = lib.wg_encap_host(a.ctypes.data, d.ctypes.data, n, bytes(key), receiver_index, counter0 & (2**64 - 1),
+                           max_segments, max_segment_size, msg_cap, msgs.ctypes.data, res.ctypes.data,
+                           gres.ctypes.data, ctypes.byref(nxt))
+    _check(rc, "wg_encap_host")
+    return msgs, res[:n], gres[:n], int(nxt.value)
 
 
 def host_release() -> None:

@@ -21,7 +21,7 @@ OBJDIR = LIBDIR / "obj"
 LIBNAME = "libwireglider_amd.so"
 ARCH = os.environ.get("WG_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["l4csum.hip", "gso.hip", "gro.hip", "aead.hip", "synth.hip", "capi.hip", "checksum.cpp"]
+SOURCES = ["l4csum.hip", "gso.hip", "gro.hip", "aead.hip", "synth.hip", "capi.hip", "hostpath.hip", "checksum.cpp"]
 
 
 def _hipcc() -> str:

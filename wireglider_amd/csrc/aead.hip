@@ -418,6 +418,8 @@ struct AeadParams {
     uint32_t gm;                 // max segments per super-buffer
     uint32_t gmode;              // kGso: 1 segments from `in` (wg_encap_encrypt), 2 headers from `in`,
                                  // payload from `gin` (wg_encap_batch)
+    const uint64_t *ctr_base;    // kGso, nullable: messages of earlier chunks, added to counter0
+                                 // (the host path's chained chunks)
 };
 
 // The decap verify gates (wg_verify_desc, SURVEY §8 f1: evaluate_packet,
@@ -546,7 +548,7 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
         }
         gstride = 32u + ((S + 15u) & ~15u);
         gdst = reinterpret_cast<uintptr_t>(p.out) + p.msg_off[sb] + (uint64_t)gs * gstride;
-        gctr = p.counter0 + p.work[p.n / p.gm + sb / 1024u] + p.work[sb] + gs;
+        gctr = p.counter0 + (p.ctr_base ? *p.ctr_base : 0ull) + p.work[p.n / p.gm + sb / 1024u] + p.work[sb] + gs;
     }
     // payload geometry
     uint64_t counter;
@@ -794,6 +796,14 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             if constexpr (kGso) {
                 if (gs == 0u)
                     p.eres[sb].counter0 = counter;
+                // the first refused message ends the batch's output: the
+                // reference advances its outbuf only over accepted messages
+                // (worker/encap.cpp:138-140) while encrypt_nonce still counts
+                // the refused ones (proto.cpp:556-562), and counters only
+                // grow, so the accepted messages are a prefix of full-stride
+                // ones
+                if (st != 0 && (gs == 0u || counter - 1u < kRejectAfterMessages))
+                    p.eres[sb].msg_bytes = gs * gstride;
             } else if (p.status) {
                 p.status[ii] = st;
             }
@@ -872,6 +882,7 @@ struct EncapScan {
     uint64_t *total;
     uint64_t n;
     uint32_t msg_cap, max_segments, max_segment_size;
+    const uint64_t *base;  // nullable: added to *total (chained chunks of the host path)
 };
 
 __device__ __forceinline__ uint32_t block_excl_scan_1024(uint32_t v, uint32_t *lds, uint32_t t, uint32_t &tot) {
@@ -926,7 +937,7 @@ __global__ __launch_bounds__(1024) void encap_scan_blocks(EncapScan q, uint32_t 
     if (t < nb)
         q.work[q.n + t] = ex;
     if (t == 0 && q.total)
-        q.total[0] = tot;
+        q.total[0] = (q.base ? q.base[0] : 0ull) + tot;
 }
 
 }  // namespace wg
@@ -1099,8 +1110,8 @@ static int encap_launch(const uint8_t *dev_in, const uint8_t *dev_seg, const wg_
                         const wg_gso_result *dev_gso_res, uint64_t n, const uint8_t key[32], uint32_t receiver_index,
                         uint64_t counter0, const uint64_t *dev_msg_offset, uint32_t msg_cap, uint32_t max_segments,
                         uint32_t max_segment_size, uint8_t *dev_msgs, wg_encap_result *dev_res, uint32_t *dev_work,
-                        uint64_t *dev_total, uint32_t gmode, hipStream_t st) {
-    EncapScan q{dev_gso_res, dev_res, dev_work, dev_total, n, msg_cap, max_segments, max_segment_size};
+                        uint64_t *dev_total, uint32_t gmode, const uint64_t *dev_base, hipStream_t st) {
+    EncapScan q{dev_gso_res, dev_res, dev_work, dev_total, n, msg_cap, max_segments, max_segment_size, dev_base};
     const uint32_t nb = (uint32_t)((n + 1023) / 1024);
     hipLaunchKernelGGL(encap_scan_local, dim3(nb), dim3(1024), 0, st, q);
     hipLaunchKernelGGL(encap_scan_blocks, dim3(1), dim3(1024), 0, st, q, nb);
@@ -1124,6 +1135,7 @@ static int encap_launch(const uint8_t *dev_in, const uint8_t *dev_seg, const wg_
     p.eres = dev_res;
     p.gm = max_segments;
     p.gmode = gmode;
+    p.ctr_base = dev_base;
     return launch_aead<false>(p, max_segment_size, st);
 }
 
@@ -1141,7 +1153,10 @@ static bool encap_args_ok(const uint8_t *key, uint64_t n, const void *dev_in, co
         (reinterpret_cast<uintptr_t>(dev_desc) & 7) || (reinterpret_cast<uintptr_t>(dev_res) & 7) ||
         (reinterpret_cast<uintptr_t>(dev_msg_offset) & 7) || (reinterpret_cast<uintptr_t>(dev_work) & 3))
         return false;
-    return (uint64_t)max_segments * n <= (1ull << 40);
+    // the counter scan keeps per-super-buffer prefixes and block totals in
+    // 32 bits: every message of the call must have a distinct 32-bit index,
+    // or two segments would share a nonce
+    return (uint64_t)max_segments * n < (1ull << 32);
 }
 
 extern "C" int wg_encap_encrypt(const uint8_t *dev_in, const uint8_t *dev_seg, const wg_gso_desc *dev_desc,
@@ -1156,23 +1171,37 @@ extern "C" int wg_encap_encrypt(const uint8_t *dev_in, const uint8_t *dev_seg, c
         return WG_OK;
     return encap_launch(dev_in, dev_seg, dev_desc, dev_gso_res, n, key, receiver_index, counter0, dev_msg_offset,
                         msg_cap, max_segments, max_segment_size, dev_msgs, dev_res, dev_work, dev_total, 1u,
-                        static_cast<hipStream_t>(stream));
+                        nullptr, static_cast<hipStream_t>(stream));
 }
+
+namespace wg {
+
+int encap_batch_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
+                       wg_gso_result *dev_gso_res, const uint8_t key[32], uint32_t receiver_index, uint64_t counter0,
+                       const uint64_t *dev_msg_offset, uint32_t msg_cap, uint32_t max_segments,
+                       uint32_t max_segment_size, uint8_t *dev_msgs, wg_encap_result *dev_res, uint32_t *dev_work,
+                       uint64_t *dev_total, const uint64_t *dev_base, hipStream_t st) {
+    if (!encap_args_ok(key, n, dev_in, dev_out, dev_desc, dev_gso_res, dev_msg_offset, max_segments, max_segment_size,
+                       dev_msgs, dev_res, dev_work))
+        return WG_ERR_INVALID;
+    if (!n)
+        return WG_OK;
+    const int rc = gso_split_launch(dev_in, dev_desc, n, dev_out, dev_gso_res, true, st);
+    if (rc != WG_OK)
+        return rc;
+    return encap_launch(dev_in, dev_out, dev_desc, dev_gso_res, n, key, receiver_index, counter0, dev_msg_offset,
+                        msg_cap, max_segments, max_segment_size, dev_msgs, dev_res, dev_work, dev_total, 2u, dev_base,
+                        st);
+}
+
+}  // namespace wg
 
 extern "C" int wg_encap_batch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
                               wg_gso_result *dev_gso_res, const uint8_t key[32], uint32_t receiver_index,
                               uint64_t counter0, const uint64_t *dev_msg_offset, uint32_t msg_cap,
                               uint32_t max_segments, uint32_t max_segment_size, uint8_t *dev_msgs,
                               wg_encap_result *dev_res, uint32_t *dev_work, uint64_t *dev_total, void *stream) {
-    if (!encap_args_ok(key, n, dev_in, dev_out, dev_desc, dev_gso_res, dev_msg_offset, max_segments, max_segment_size,
-                       dev_msgs, dev_res, dev_work))
-        return WG_ERR_INVALID;
-    if (!n)
-        return WG_OK;
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    const int rc = gso_split_launch(dev_in, dev_desc, n, dev_out, dev_gso_res, true, st);
-    if (rc != WG_OK)
-        return rc;
-    return encap_launch(dev_in, dev_out, dev_desc, dev_gso_res, n, key, receiver_index, counter0, dev_msg_offset,
-                        msg_cap, max_segments, max_segment_size, dev_msgs, dev_res, dev_work, dev_total, 2u, st);
+    return encap_batch_launch(dev_in, dev_desc, n, dev_out, dev_gso_res, key, receiver_index, counter0,
+                              dev_msg_offset, msg_cap, max_segments, max_segment_size, dev_msgs, dev_res, dev_work,
+                              dev_total, nullptr, static_cast<hipStream_t>(stream));
 }

@@ -1,12 +1,11 @@
-// capi.hip — misc C ABI (version, errors, device count), launch tuning, and
-// the host-memory path (tun / UDP buffers live in host memory).
+// capi.hip — misc C ABI (version, errors, device count), launch tuning and
+// the roofline probes.  The host-memory path is hostpath.hip.
 #include <hip/hip_runtime.h>
 
 #include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <atomic>
 #include <mutex>
 #include <string>
 
@@ -49,7 +48,7 @@ static const Knob kKnobs[] = {
     {"verify_dm", nullptr, &Tune::verify_dm, 0, 0, kDm, WG_N(kDm)},
     {"verify_occ", nullptr, &Tune::verify_occ, 0, 0, kVOcc, WG_N(kVOcc)},
     {"verify_hdr", nullptr, &Tune::verify_hdr, 0, 1, nullptr, 0},
-    {"verify_small", nullptr, &Tune::verify_small, 0, 3, nullptr, 0},
+    {"verify_small", nullptr, &Tune::verify_small, 0, 5, nullptr, 0},
     {"gro_lds", nullptr, &Tune::gro_lds, 0, 1, nullptr, 0},
     {"gro_wide", nullptr, &Tune::gro_wide, 0, 1, nullptr, 0},
     {"gro_chunks", nullptr, &Tune::gro_chunks, 4, 5, nullptr, 0},
@@ -202,114 +201,6 @@ bool debug_sync(hipStream_t st, const char *kernel) {
         return true;
     std::fprintf(stderr, "wireglider_amd: %s failed: %s\n", kernel, hipGetErrorString(e));
     return false;
-}
-
-// Host-memory path: per host thread, a pipeline of kSlots
-// device chunk buffers on two streams.  Chunk k's H2D copy (stream h2d)
-// waits only for the kernel that last used its slot; its kernel and the D2H
-// of its results (stream exec) wait for its copy — so chunk k+1's copy runs
-// under chunk k's kernel and result copy.  Results land in a pinned buffer
-// and are copied to the caller's array once at the end (2 B per packet), so
-// no D2H targets pageable memory mid-pipeline (a pageable D2H synchronises).
-// Device memory is reused across calls and grows only with the chunk size.
-struct HostPipe {
-    static constexpr int kSlots = 3;
-    int device = -1;
-    hipStream_t h2d = nullptr, exec = nullptr;
-    hipEvent_t copied[kSlots] = {}, done[kSlots] = {};
-    uint8_t *dbuf[kSlots] = {};
-    uint16_t *dres[kSlots] = {};
-    size_t slot_bytes = 0, slot_res = 0;
-    uint16_t *hres = nullptr;  // pinned
-    size_t hres_cap = 0;
-    void release();
-    ~HostPipe();
-};
-
-// Set by an atexit handler (registered when the first pipeline is built):
-// thread-exit destructors that run after it must not call into a HIP runtime
-// that may already be torn down — the process is ending and the driver
-// reclaims the memory anyway.
-static std::atomic<bool> g_exiting{false};
-
-void HostPipe::release() {
-    if (device < 0)
-        return;
-    hipSetDevice(device);
-    for (int k = 0; k < kSlots; k++) {
-        if (dbuf[k]) hipFree(dbuf[k]);
-        if (dres[k]) hipFree(dres[k]);
-        if (copied[k]) hipEventDestroy(copied[k]);
-        if (done[k]) hipEventDestroy(done[k]);
-        dbuf[k] = nullptr;
-        dres[k] = nullptr;
-        copied[k] = done[k] = nullptr;
-    }
-    if (hres) hipHostFree(hres);
-    if (h2d) hipStreamDestroy(h2d);
-    if (exec) hipStreamDestroy(exec);
-    hres = nullptr;
-    h2d = exec = nullptr;
-    hres_cap = slot_bytes = slot_res = 0;
-    device = -1;
-}
-
-HostPipe::~HostPipe() {
-    if (!g_exiting.load())
-        release();
-}
-
-static thread_local HostPipe g_pipe;
-
-static int pipe_init(HostPipe &c) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess)
-        return WG_ERR_NODEV;
-    if (c.device == dev)
-        return WG_OK;
-    c.release();  // first use on this thread, or the thread switched devices
-    static std::once_flag once;
-    std::call_once(once, [] { std::atexit([] { g_exiting.store(true); }); });
-    c.device = dev;
-    if (hipStreamCreateWithFlags(&c.h2d, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c.exec, hipStreamNonBlocking) != hipSuccess)
-        return WG_ERR_RUNTIME;
-    for (int k = 0; k < HostPipe::kSlots; k++)
-        if (hipEventCreateWithFlags(&c.copied[k], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c.done[k], hipEventDisableTiming) != hipSuccess)
-            return WG_ERR_RUNTIME;
-    return WG_OK;
-}
-
-static int pipe_reserve(HostPipe &c, size_t slot_bytes, size_t slot_res, size_t total_res) {
-    if (slot_bytes > c.slot_bytes || slot_res > c.slot_res) {
-        if (hipStreamSynchronize(c.exec) != hipSuccess || hipStreamSynchronize(c.h2d) != hipSuccess)
-            return WG_ERR_RUNTIME;
-        const size_t nb = slot_bytes > c.slot_bytes ? slot_bytes : c.slot_bytes;
-        const size_t nr = slot_res > c.slot_res ? slot_res : c.slot_res;
-        for (int k = 0; k < HostPipe::kSlots; k++) {
-            if (c.dbuf[k]) hipFree(c.dbuf[k]);
-            if (c.dres[k]) hipFree(c.dres[k]);
-            c.dbuf[k] = nullptr;
-            c.dres[k] = nullptr;
-        }
-        c.slot_bytes = c.slot_res = 0;
-        for (int k = 0; k < HostPipe::kSlots; k++)
-            if (hipMalloc(&c.dbuf[k], nb) != hipSuccess || hipMalloc(&c.dres[k], nr * sizeof(uint16_t)) != hipSuccess)
-                return WG_ERR_RUNTIME;
-        c.slot_bytes = nb;
-        c.slot_res = nr;
-    }
-    if (total_res > c.hres_cap) {
-        if (c.hres) hipHostFree(c.hres);
-        c.hres = nullptr;
-        c.hres_cap = 0;
-        const size_t cap = total_res < 4096 ? 4096 : total_res;
-        if (hipHostMalloc(reinterpret_cast<void **>(&c.hres), cap * sizeof(uint16_t), hipHostMallocDefault) != hipSuccess)
-            return WG_ERR_RUNTIME;
-        c.hres_cap = cap;
-    }
-    return WG_OK;
 }
 
 // Read-roofline probe: the checksum kernels' access structure with nothing
@@ -479,77 +370,4 @@ extern "C" int wg_device_count(void) {
     if (hipGetDeviceCount(&n) != hipSuccess)
         return 0;
     return n;
-}
-
-
-extern "C" int wg_l4csum_uniform_host(const uint8_t *host_base, uint64_t total_len, uint32_t segment_size,
-                                      uint16_t csum_start, uint32_t flags, uint16_t *host_out) {
-    if (!segment_size || (total_len && (!host_base || !host_out)))
-        return WG_ERR_INVALID;
-    if (!total_len)
-        return WG_OK;
-    if (wg_device_count() <= 0)
-        return WG_ERR_NODEV;
-    HostPipe &c = g_pipe;
-    int rc = pipe_init(c);
-    if (rc != WG_OK)
-        return rc;
-    const uint64_t nseg_total = (total_len + segment_size - 1) / segment_size;
-    // whole segments per chunk, ~host_chunk_mb MiB (knob)
-    uint64_t per = ((uint64_t)tune().host_chunk_mb << 20) / segment_size;
-    if (per == 0)
-        per = 1;
-    const uint64_t chunk = per * segment_size;
-    const uint64_t slot_bytes = chunk < total_len ? chunk : total_len;
-    rc = pipe_reserve(c, (size_t)slot_bytes, (size_t)(per < nseg_total ? per : nseg_total), (size_t)nseg_total);
-    if (rc != WG_OK)
-        return rc;
-    for (uint64_t off = 0, k = 0; off < total_len; off += chunk, k++) {
-        const int slot = (int)(k % HostPipe::kSlots);
-        const uint64_t len = total_len - off < chunk ? total_len - off : chunk;
-        const uint64_t first = off / segment_size, nseg = (len + segment_size - 1) / segment_size;
-        // the slot's previous kernel must have read its bytes
-        if (k >= (uint64_t)HostPipe::kSlots && hipStreamWaitEvent(c.h2d, c.done[slot], 0) != hipSuccess)
-            return WG_ERR_RUNTIME;
-        if (hipMemcpyAsync(c.dbuf[slot], host_base + off, len, hipMemcpyHostToDevice, c.h2d) != hipSuccess ||
-            hipEventRecord(c.copied[slot], c.h2d) != hipSuccess ||
-            hipStreamWaitEvent(c.exec, c.copied[slot], 0) != hipSuccess)
-            return WG_ERR_RUNTIME;
-        rc = wg_l4csum_uniform(c.dbuf[slot], len, segment_size, csum_start, flags, c.dres[slot], c.exec);
-        if (rc != WG_OK)
-            return rc;
-        if (hipMemcpyAsync(c.hres + first, c.dres[slot], nseg * sizeof(uint16_t), hipMemcpyDeviceToHost, c.exec) !=
-                hipSuccess ||
-            hipEventRecord(c.done[slot], c.exec) != hipSuccess)
-            return WG_ERR_RUNTIME;
-    }
-    if (hipStreamSynchronize(c.exec) != hipSuccess)
-        return WG_ERR_RUNTIME;
-    std::memcpy(host_out, c.hres, nseg_total * sizeof(uint16_t));
-    return WG_OK;
-}
-
-extern "C" int wg_host_release(void) {
-    if (g_pipe.device >= 0) {
-        hipSetDevice(g_pipe.device);
-        hipStreamSynchronize(g_pipe.exec);
-        hipStreamSynchronize(g_pipe.h2d);
-    }
-    g_pipe.release();
-    return WG_OK;
-}
-
-extern "C" int wg_host_alloc(void **ptr, uint64_t bytes) {
-    if (!ptr || !bytes)
-        return WG_ERR_INVALID;
-    *ptr = nullptr;
-    if (wg_device_count() <= 0)
-        return WG_ERR_NODEV;
-    return hipHostMalloc(ptr, bytes, hipHostMallocDefault) == hipSuccess ? WG_OK : WG_ERR_RUNTIME;
-}
-
-extern "C" int wg_host_free(void *ptr) {
-    if (!ptr)
-        return WG_OK;
-    return hipHostFree(ptr) == hipSuccess ? WG_OK : WG_ERR_RUNTIME;
 }

@@ -1061,6 +1061,90 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Two-role verify (knob verify_small 4 and 5).  The wave-per-packet kernel is
+// fastest on long packets as one-shot 4-packet waves at 8 waves/SIMD, and the
+// lane decode is fastest on small ones at 64 descriptors per wave; any layout
+// that puts both roles in one wave costs the long packets occupancy or
+// one-shot waves (verify_small 1-3).  Here the roles get separate waves:
+//  - LANE role: a lane per descriptor; packets of <= kSmallMax bytes are
+//    decoded in their lane (verify_lane), longer ones left alone;
+//  - WAVE role: one-shot waves of 4 consecutive descriptors through
+//    verify_group (the default kernel's body), taking only the packets longer
+//    than kSmallMax; a wave whose 4 packets are all small exits after its
+//    descriptor load.
+// Every descriptor's result is stored by exactly one role.  verify_small = 4
+// runs the roles as two launches, 5 as the two block ranges of one launch.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void verify_lane_role(const VerifyParams &p, uint64_t i) {
+    const bool live = i < p.n;
+    const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0));
+    const uint32_t len = live ? dv.z : 0u;
+    const bool small = live && len <= kSmallMax;
+    if (!__ballot(small))  // wave-uniform: nothing small here
+        return;
+    uint32_t rv = 0, rc = 0;
+    verify_lane(reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)dv.y << 32) | dv.x), small ? len : 0u, small, rv,
+                rc);
+    if (small) {
+        p.verdict[i] = (uint8_t)rv;
+        if (p.l4)
+            p.l4[i] = (uint16_t)rc;
+    }
+}
+
+__device__ __forceinline__ void verify_wave_role(const VerifyParams &p, uint64_t i0, uint32_t lane) {
+    constexpr int P = 4;
+    uint64_t doff[P];
+    uint32_t len[P], tgt[P];
+    uint32_t keep = 0;
+#pragma unroll
+    for (int j = 0; j < P; j++) {
+        const wg_pkt_desc d = p.desc[i0 + j < p.n ? i0 + j : p.n - 1];
+        const uint32_t L = i0 + j < p.n ? d.len : 0u;
+        const bool lg = L > kSmallMax;
+        keep |= (uint32_t)lg << j;
+        doff[j] = d.offset;
+        len[j] = lg ? L : 0u;  // the lane role's packets: nothing issued
+        tgt[j] = (uint32_t)j;
+    }
+    if (!keep)
+        return;
+    uint32_t rv = 0, rc = 0;
+    verify_group<P, true>(p.base, doff, len, tgt, lane, rv, rc, [] {});
+    if (lane < (uint32_t)P && ((keep >> lane) & 1u)) {
+        p.verdict[i0 + lane] = (uint8_t)rv;
+        if (p.l4)
+            p.l4[i0 + lane] = (uint16_t)rc;
+    }
+}
+
+__global__ __launch_bounds__(256) void verify_lane_kernel(VerifyParams p) {
+    verify_lane_role(p, (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 256u + threadIdx.x);
+}
+
+template <int O = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_long_kernel(
+    VerifyParams p) {
+    const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
+    if (wave * 4u < p.n)
+        verify_wave_role(p, wave * 4u, lane_id());
+}
+
+// One launch: blocks [0, nl) lane role (256 descriptors each), the rest wave
+// role (16 descriptors each); both ranges multiples of 8 blocks (XCD swizzle).
+template <int O = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_roles_kernel(
+    VerifyParams p, uint32_t nl) {
+    if (blockIdx.x < nl) {
+        verify_lane_role(p, (uint64_t)xcd_swizzle(blockIdx.x, nl) * 256u + threadIdx.x);
+        return;
+    }
+    const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x - nl, gridDim.x - nl) * 4u + wave_in_block();
+    if (wave * 4u < p.n)
+        verify_wave_role(p, wave * 4u, lane_id());
+}
+
 }  // namespace wg
 
 extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_desc, uint64_t n,
@@ -1071,6 +1155,26 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
         return WG_ERR_INVALID;
     VerifyParams p{dev_base, dev_desc, dev_verdict, dev_l4, n};
     const Tune t = tune();
+    if (t.verify_small == 4 || t.verify_small == 5) {
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        uint64_t nl = (n + 255) / 256, nw = (n + 15) / 16;  // lane-role / wave-role blocks
+        if (nl >= 8) nl = (nl + 7) & ~7ull;
+        if (nw >= 8) nw = (nw + 7) & ~7ull;
+        if (nl + nw > 0x7fffffffull)
+            return WG_ERR_INVALID;
+        if (t.verify_small == 4) {
+            hipLaunchKernelGGL(verify_lane_kernel, dim3((unsigned)nl), dim3(256), 0, st, p);
+            if (t.verify_occ == 8)
+                hipLaunchKernelGGL(verify_long_kernel<8>, dim3((unsigned)nw), dim3(256), 0, st, p);
+            else
+                hipLaunchKernelGGL(verify_long_kernel<0>, dim3((unsigned)nw), dim3(256), 0, st, p);
+        } else if (t.verify_occ == 8) {
+            hipLaunchKernelGGL(verify_roles_kernel<8>, dim3((unsigned)(nl + nw)), dim3(256), 0, st, p, (uint32_t)nl);
+        } else {
+            hipLaunchKernelGGL(verify_roles_kernel<0>, dim3((unsigned)(nl + nw)), dim3(256), 0, st, p, (uint32_t)nl);
+        }
+        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+    }
     if (t.verify_small == 3) {
         const uint64_t Q = ((n + 3) / 4 + 15) & ~15ull;  // as l4csum_split_kernel's quarters
         uint64_t sb = Q / 16;

@@ -57,4 +57,13 @@ bool debug_sync(hipStream_t st, const char *kernel);
 int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
                      wg_gso_result *dev_res, bool hdr_only, hipStream_t st);
 
+// wg_encap_batch with a device-resident counter base (aead.hip): counters
+// start at counter0 + *dev_base (nullable: 0) and *dev_total gets *dev_base +
+// this call's messages, so the host path chains its chunks on the device.
+int encap_batch_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
+                       wg_gso_result *dev_gso_res, const uint8_t key[32], uint32_t receiver_index, uint64_t counter0,
+                       const uint64_t *dev_msg_offset, uint32_t msg_cap, uint32_t max_segments,
+                       uint32_t max_segment_size, uint8_t *dev_msgs, wg_encap_result *dev_res, uint32_t *dev_work,
+                       uint64_t *dev_total, const uint64_t *dev_base, hipStream_t st);
+
 }  // namespace wg
