@@ -72,11 +72,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="config2",
-                    choices=["config1", "config2", "config3", "config3udp", "config4", "config5", "verify", "gro", "encap",
-                             "encap_2call", "aead"])
+                    choices=["config1", "config2", "config3", "config3udp", "config4", "config4strong", "config5",
+                             "verify", "gro", "encap", "encap_2call", "aead", "encap_host", "decap_host"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-strong", action="store_true", help="skip the config 5 strong-scaling companion")
-    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall seconds of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=2.0,
+                    help="wall seconds of each CPU baseline repetition (5 on all cores, 3 on one)")
     ap.add_argument("--settle-seconds", type=float, default=0.3,
                     help="untimed back-to-back launches before the warmup (clock/memory settle)")
     return ap.parse_args()
@@ -102,6 +103,7 @@ class Workload:
     value_scale: float = 2.0**-30     # metric value = payload units/s x value_scale
     post: Optional[Callable] = None   # workload-specific post-check
     probe_run: int = 0                # packet size for the kernel-shaped read probe (0: contiguous only)
+    pcie: Optional[dict] = None       # host-memory workloads: PCIe bytes per step {"h2d": B, "d2h": B}
 
 
 def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workload:
@@ -481,6 +483,12 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                         "wg::gro_finalize_lds_kernel<true>", rank * n, sample=sample, counts=[n] * world,
                         metric="device-resident Mflows/s, GRO finalize (SURVEY f2)", unit="Mflows/s",
                         value_scale=1e-6, post=post)
+    if name == "config4strong":
+        return build_config4_strong(wga, torch, rank, world, dev)
+    if name == "encap_host":
+        return build_encap_host(wga, torch, rank, world, dev)
+    if name == "decap_host":
+        return build_decap_host(wga, torch, rank, world, dev)
     # config4 bimodal
     n = 1 << 22
     seed = 0x5EED0004 + rank
@@ -582,6 +590,224 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
            "packets_per_gpu": n, "layout": "descriptor", "parallelism": f"shard{world}"}
     return Workload(launch, n, total, total + 2 * n + 16 * n, cfg, "weak", buf, "wg::l4csum_split_kernel<1,nt> (l4_small=5)",
                     rank * n, out, desc, sample, [n] * world, post=post)
+
+
+def config4_lengths():
+    """BASELINE config 4's packet lengths: 4,194,304 packets, 64 B or 9000 B
+    50/50 by a seeded draw (0x5EED0004), packed back to back."""
+    import numpy as np
+
+    n = 1 << 22
+    rng = np.random.default_rng(0x5EED0004)
+    lens = np.where(rng.random(n) < 0.5, 64, 9000).astype(np.int64)
+    return lens, np.concatenate([[0], np.cumsum(lens[:-1])])
+
+
+def build_config4_strong(wga, torch, rank: int, world: int, dev) -> Workload:
+    """Config 4's ONE 4 M-packet bimodal batch split across the ranks by BYTES
+    (dist.shard_bounds_by_bytes): rank r holds the packets of
+    its byte-balanced range, generated from the global byte counter and packet
+    index, so its shard equals the same slice of the N = 1 batch and the
+    all-reduced result hash is the same at every N."""
+    import numpy as np
+
+    from wireglider_amd import dist as wdist
+
+    seed = 0x5EED0004
+    lens, offs = config4_lengths()
+    bounds = wdist.shard_bounds_by_bytes(lens, world)
+    lo, hi = bounds[rank]
+    n = hi - lo
+    g0 = int(offs[lo]) if n else 0
+    base = g0 & ~15  # synth_fill's counter base is 16-B aligned: start the shard buffer there
+    end = int(offs[hi - 1] + lens[hi - 1]) if n else base
+    raw = np.zeros((max(n, 1), 2), dtype=np.int64)
+    raw[:n, 0] = offs[lo:hi] - base
+    raw[:n, 1] = lens[lo:hi] | (20 << 32)  # v4/UDP, csum_start 20
+    desc = torch.from_numpy(raw[:n].copy()).to(dev)
+    buf = torch.empty(end - base + 16, dtype=torch.uint8, device=dev)
+    wga.synth_fill(buf, seed, counter_base=base)
+    wga.synth_headers(buf, desc, seed, lo)
+    out = torch.empty(max(n, 1), dtype=torch.uint16, device=dev)[:n]
+
+    def launch():
+        wga.calc_l4_checksum_desc(buf, desc, out=out)
+
+    payload = int(lens[lo:hi].sum())
+    counts = [b - a for a, b in bounds]
+    cfg = {"workload": "config4 strong: ONE 4,194,304-packet 64 B / 9000 B IPv4/UDP batch split across the GPUs "
+                       "by bytes (shard_bounds_by_bytes)", "packets_total": int(lens.size), "packets_per_gpu": n,
+           "layout": "descriptor", "parallelism": f"shard{world} (byte-balanced contiguous ranges)"}
+    return Workload(launch, n, payload, payload + 18 * n, cfg, "strong", buf,
+                    "wg::l4csum_split_kernel<1,nt> (l4_small=5)", lo, out, desc, None, counts)
+
+
+def _pinned_copy(wga, t):
+    """A device tensor's bytes in a wg_host_alloc (pinned) buffer."""
+    import numpy as np
+
+    pb = wga.PinnedBuffer(t.numel())
+    pb.array[:] = t.cpu().numpy().reshape(-1)
+    return pb
+
+
+def pcie_ceiling(torch, h2d_bytes: int, d2h_bytes: int, reps: int = 5) -> dict:
+    """Raw PCIe copy rates on this box with pinned host memory: hipMemcpyAsync
+    H2D alone, D2H alone, and both at once on two streams (PCIe is full
+    duplex) — the ceiling of a host-memory pipeline moving these bytes."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    hin = torch.empty(h2d_bytes, dtype=torch.uint8).pin_memory()
+    hout = torch.empty(d2h_bytes, dtype=torch.uint8).pin_memory()
+    din = torch.empty(h2d_bytes, dtype=torch.uint8, device=dev)
+    dout = torch.empty(d2h_bytes, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def run(up, down):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            if up:
+                with torch.cuda.stream(s1):
+                    din.copy_(hin, non_blocking=True)
+            if down:
+                with torch.cuda.stream(s2):
+                    hout.copy_(dout, non_blocking=True)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps
+
+    run(True, True)
+    t_up, t_down, t_both = run(True, False), run(False, True), run(True, True)
+    res = {"h2d_GBps": round(h2d_bytes / t_up / 1e9, 2), "d2h_GBps": round(d2h_bytes / t_down / 1e9, 2),
+           "both_GBps": round((h2d_bytes + d2h_bytes) / t_both / 1e9, 2),
+           "both_ms": round(t_both * 1e3, 3), "bytes": {"h2d": h2d_bytes, "d2h": d2h_bytes}}
+    del hin, hout, din, dout
+    return res
+
+
+def build_encap_host(wga, torch, rank: int, world: int, dev) -> Workload:
+    """The encap worker's step from host memory (SURVEY §8 f3 with A6 + f4,
+    worker/encap.cpp:22-170): 32,768 tun reads of config 3's shape (64 KiB
+    IPv4/TCP super-buffers, 1,460-B segments) in a pinned buffer ->
+    wg_encap_host (chunked H2D, the headers-only GSO split + encryption of
+    every segment on the device, messages D2H into a pinned send buffer).
+    value = GiB/s of tun input, host memory to host memory."""
+    import numpy as np
+
+    n, in_stride, in_len, hdr, gso, seed = 1 << 15, 65536, 65535, 40, 1460, 0x5EED00E6
+    seg = hdr + gso
+    nseg = (in_len - hdr + gso - 1) // gso
+    out_len = in_len - hdr + nseg * hdr
+    mstride = wga.aead_message_stride(seg)
+    mbytes = (nseg - 1) * mstride + wga.aead_message_stride(out_len - (nseg - 1) * seg)
+    mcap = nseg * mstride
+    d_in = torch.empty(n * in_stride, dtype=torch.uint8, device=dev)
+    wga.synth_fill(d_in, seed, counter_base=rank * n * in_stride)
+    pd = np.zeros(n, dtype=wga.PKT_DESC_DTYPE)
+    pd["offset"] = np.arange(n, dtype=np.uint64) * in_stride
+    pd["len"], pd["csum_start"], pd["flags"] = in_len, 20, 2
+    wga.synth_headers(d_in, torch.from_numpy(pd.view(np.uint8).copy()).to(dev), seed, rank * n)
+    gd = np.zeros(n, dtype=wga.GSO_DESC_DTYPE)
+    gd["in_offset"] = pd["offset"]
+    gd["in_len"], gd["out_cap"] = in_len, 73216  # the reference's per-worker outbuf (worker/encap.cpp:26)
+    gd["vnet"]["flags"], gd["vnet"]["gso_type"], gd["vnet"]["gso_size"] = 1, 1, gso
+    gd["vnet"]["csum_start"], gd["vnet"]["csum_offset"] = 20, 16
+    pin_in = _pinned_copy(wga, d_in)
+    pin_out = wga.PinnedBuffer(n * mcap)
+    key = np.random.default_rng(seed).integers(0, 256, 32, dtype=np.uint8).tobytes()
+    rx, c0 = 0x0E0CAA, 1 + rank * n * nseg
+    state = {}
+
+    def launch():
+        state["r"] = wga.encap_host(pin_in.array, gd, key, rx, c0, nseg, seg, mcap, msgs=pin_out.array)
+
+    def post():
+        _, res, gres, nxt = state["r"]
+        ok = bool(np.all(res["nmsg"] == nseg) and np.all(res["msg_bytes"] == mbytes)
+                  and np.array_equal(res["counter0"], c0 + np.arange(n, dtype=np.uint64) * nseg)
+                  and np.all(gres["status"] == 0))
+        # a sample decrypted back on the device and compared with the split's segments
+        k = 256
+        full = torch.from_numpy(np.concatenate([pin_out.array[i * mcap: i * mcap + (nseg - 1) * mstride]
+                                                for i in range(k)])).to(dev)
+        pt, st = wga.aead_decrypt_batch(full, mstride, key)
+        ref = torch.empty(k * 73216, dtype=torch.uint8, device=dev)
+        gdk = gd[:k].copy()
+        gdk["out_offset"] = np.arange(k, dtype=np.uint64) * 73216
+        wga.gso_split(d_in[: k * in_stride].clone(), torch.from_numpy(gdk.view(np.uint8).copy()).to(dev), ref)
+        segs = torch.cat([ref[i * 73216: i * 73216 + (nseg - 1) * seg] for i in range(k)])
+        torch.cuda.synchronize()
+        same = bool(torch.equal(pt.view(-1, mstride - 32)[:, :seg].reshape(-1), segs))
+        return {"results_ok": ok, "next_counter": int(nxt), "next_counter_expected": int(c0 + n * nseg),
+                "sample_super_buffers_decrypted": k, "sample_plaintexts_equal_segments": same,
+                "sample_status_nonzero": int(torch.count_nonzero(st).item())}
+
+    def sample(_npk):
+        k = min(n, 1024)
+        gk = gd[:k].copy()
+        gk["out_offset"] = np.arange(k, dtype=np.uint64) * 73216
+        return (pin_in.array[: k * in_stride].copy(), pin_out.array[: k * mcap].copy(),
+                ("encap", gk, k * 73216, key, rx, c0, seg, nseg, mcap, mbytes))
+
+    cfg = {"workload": "encap_host: 32,768 tun reads of 64 KiB IPv4/TCP (config 3 shape) in pinned host memory -> "
+                       "wg_encap_host (H2D, GSO split + ChaCha20-Poly1305 per 1460-B segment, messages D2H to pinned "
+                       "memory), one peer", "super_buffers_per_gpu": n, "segments_per_buffer": nseg,
+           "message_stride": mstride, "parallelism": f"shard{world}", "entry": "wg_encap_host",
+           "host_chunk_mb": wga.tune_get("host_chunk_mb")}
+    return Workload(launch, n, n * in_len, n * (in_len + mbytes), cfg, "weak", d_in,
+                    "wg_encap_host pipeline (H2D / wg_encap_batch kernels / D2H on three streams)", rank * n,
+                    sample=sample, counts=[n] * world, post=post,
+                    metric="host-memory GiB/s of tun input, encap step incl. PCIe (SURVEY f3 + A6 + f4)",
+                    pcie={"h2d": n * in_stride, "d2h": n * mcap})
+
+
+def build_decap_host(wga, torch, rank: int, world: int, dev) -> Workload:
+    """The decap worker's step from host memory (SURVEY §8 f3 with f4 + f1,
+    worker/decap.cpp:90-156 -> worker/decap_ref.cpp:53-89): a UDP GRO batch
+    of 1,048,576 data messages (1,504-B inner IPv4/IPv6 x TCP/UDP packets, a
+    multiple of 16 so every gate runs) in a pinned buffer -> wg_decap_host
+    (chunked H2D, decrypt + verify gates fused on the device, plaintext and
+    verdicts D2H into pinned memory).  value = GiB/s of UDP messages."""
+    import numpy as np
+
+    n, s2, seed = 1 << 20, 1504, 0x5EED00D4
+    m2 = wga.aead_message_stride(s2)
+    pk = torch.empty(n * s2, dtype=torch.uint8, device=dev)
+    wga.synth_fill(pk, seed, counter_base=rank * n * s2)
+    d2 = wga.synth_desc_stride(n, s2, s2, 1, seed, rank * n, device=dev)
+    wga.synth_headers(pk, d2, seed, rank * n)
+    wga.store_l4csum(pk, d2, wga.calc_l4_checksum_desc(pk, d2))
+    key = np.random.default_rng(seed).integers(0, 256, 32, dtype=np.uint8).tobytes()
+    msgs, _ = wga.aead_encrypt_batch(pk, s2, key, 0x1D, 77 + rank * n)
+    torch.cuda.synchronize()
+    pin_m = _pinned_copy(wga, msgs[: n * m2])
+    del msgs
+    pin_p = wga.PinnedBuffer(n * s2)
+    state = {}
+
+    def launch():
+        state["r"] = wga.decap_host(pin_m.array, m2, key, verify=True, plain=pin_p.array)
+
+    def post():
+        _, st, ver, l4 = state["r"]
+        same = bool(torch.equal(torch.from_numpy(pin_p.array).to(dev), pk))
+        return {"status_nonzero": int(np.count_nonzero(st)), "verify_failures": int(np.count_nonzero((ver & 3) != 3)),
+                "l4_nonzero": int(np.count_nonzero(l4)), "plaintext_equal_packets": same}
+
+    def sample(_npk):
+        k = 1 << 16
+        _, st, ver, l4 = state["r"] if "r" in state else wga.decap_host(pin_m.array, m2, key, plain=pin_p.array)
+        return (None, (st[:k].copy(), ver[:k].copy(), l4[:k].copy()),
+                ("decap", key, m2, pin_m.array[: k * m2].copy()))
+
+    cfg = {"workload": "decap_host: a UDP GRO batch of 1,048,576 WireGuard data messages (1,504-B inner IPv4/IPv6 x "
+                       "TCP/UDP packets) in pinned host memory -> wg_decap_host (H2D, decrypt + verify gates fused, "
+                       "plaintext + verdicts D2H to pinned memory)", "messages_per_gpu": n, "message_stride": m2,
+           "parallelism": f"shard{world}", "entry": "wg_decap_host", "host_chunk_mb": wga.tune_get("host_chunk_mb")}
+    return Workload(launch, n, n * m2, n * (m2 + s2 + 4), cfg, "weak", pk,
+                    "wg_decap_host pipeline (H2D / aead_kernel<..,dec,verify> / D2H on three streams)", rank * n,
+                    sample=sample, counts=[n] * world, post=post,
+                    metric="host-memory GiB/s of UDP data messages, decap step incl. PCIe (SURVEY f3 + f4 + f1)",
+                    pcie={"h2d": n * m2, "d2h": n * (s2 + 4)})
 
 
 def build_encap(wga, torch, rank: int, world: int, dev, fused: bool = True) -> Workload:
@@ -735,9 +961,35 @@ def wga_stride(seg: int) -> int:
     return 16 + (seg + 15) // 16 * 16 + 16
 
 
-def cpu_baseline(sample_fn, seconds: float):
+def _rep_rates(fn, units: float, seconds: float, reps: int) -> list:
+    """`reps` repetitions, each running fn() back to back until `seconds` of
+    wall time have passed; the rate (units per second) of each repetition."""
+    out = []
+    for _ in range(reps):
+        k, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            k += 1
+            t = time.perf_counter() - t0
+            if t >= seconds:
+                break
+        out.append(units * k / t)
+    return out
+
+
+def _spread(rates: list, scale: float) -> dict:
+    r = sorted(x * scale for x in rates)
+    med = r[len(r) // 2] if len(r) % 2 else 0.5 * (r[len(r) // 2 - 1] + r[len(r) // 2])
+    return {"median": med, "min": r[0], "max": r[-1], "reps": len(r),
+            "spread_pct": round(100.0 * max(med - r[0], r[-1] - med) / med, 2) if med else None}
+
+
+def cpu_baseline(sample_fn, seconds: float, reps: int = 5):
     """The oracle (C restatement of checksum.cpp + a fastcsum-class nofold) on
-    the host cores of this box, on a bounded sample of the same workload."""
+    the host cores of this box, on a bounded sample of the same workload.
+    All cores: `reps` repetitions of >= `seconds` each, the median is the
+    value (min / max beside it: a 16-core share of a 256-core host moves with
+    its neighbours); one core: 3 repetitions of >= seconds / 2."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import numpy as np
     import oracle  # test infrastructure: the CPU baseline leg only
@@ -748,27 +1000,19 @@ def cpu_baseline(sample_fn, seconds: float):
     host, gpu_out, kind = sample_fn(npk)
     cores = oracle.host_cores()
     threads = cores["threads"]
+    one_scale = 1.0  # the 1-core leg runs on 1/one_scale of the sample
+    extra = {}
     if kind[0] == "uniform":
         _, seg, cs, fl = kind
         exp = oracle.l4_uniform(host, seg, cs, fl, threads)
-        t1c = oracle.time_l4_uniform(host, seg, cs, fl, 1, 1)
-        reps1 = max(1, int(seconds / 3 / max(t1c, 1e-6)))
-        t_1core = oracle.time_l4_uniform(host, seg, cs, fl, 1, reps1) / reps1
-        tall1 = oracle.time_l4_uniform(host, seg, cs, fl, threads, 1)
-        reps = max(1, int(math.ceil(seconds / max(tall1, 1e-6))))
-        t_all = oracle.time_l4_uniform(host, seg, cs, fl, threads, reps) / reps
+        run_all = lambda: oracle.l4_uniform(host, seg, cs, fl, threads)  # noqa: E731
+        run_one = lambda: oracle.l4_uniform(host, seg, cs, fl, 1)  # noqa: E731
         nbytes = host.size
     elif kind[0] == "verify":
         d = kind[1]
         exp_v, exp_l4 = oracle.verify_desc(host, d, threads)
-        t0 = time.perf_counter()
-        oracle.verify_desc(host, d, 1)
-        t_1core = time.perf_counter() - t0
-        reps = max(1, int(seconds * threads / max(t_1core, 1e-6)))
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            oracle.verify_desc(host, d, threads)
-        t_all = (time.perf_counter() - t0) / reps
+        run_all = lambda: oracle.verify_desc(host, d, threads)  # noqa: E731
+        run_one = lambda: oracle.verify_desc(host, d, 1)  # noqa: E731
         nbytes = int(np.ascontiguousarray(d).view(oracle.PKT_DESC)["len"].astype(np.int64).sum())
         exp = np.concatenate([exp_v.astype(np.int64), exp_l4.astype(np.int64)])
         gpu_out = np.concatenate([gpu_out[0].astype(np.int64), gpu_out[1].astype(np.int64)])
@@ -779,16 +1023,11 @@ def cpu_baseline(sample_fn, seconds: float):
         gk, out_bytes = kind[1], kind[2]
         cpu_out = np.zeros(out_bytes, np.uint8)
         st = oracle.gso_split_desc(host, gk, cpu_out, threads)
-        exp, gpu_out = cpu_out, gpu_out
+        exp = cpu_out.copy()
         sub = gk[: max(1, gk.size // 8)]
-        t0 = time.perf_counter()
-        oracle.gso_split_desc(host, sub, cpu_out, 1)
-        t_1core = (time.perf_counter() - t0) * gk.size / sub.size
-        reps = max(1, int(seconds * threads / max(t_1core, 1e-6)))
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            oracle.gso_split_desc(host, gk, cpu_out, threads)
-        t_all = (time.perf_counter() - t0) / reps
+        one_scale = sub.size / gk.size
+        run_all = lambda: oracle.gso_split_desc(host, gk, cpu_out, threads)  # noqa: E731
+        run_one = lambda: oracle.gso_split_desc(host, sub, cpu_out, 1)  # noqa: E731
         nbytes = int(gk["in_len"].astype(np.int64).sum())
         npk = gk.size
         if np.any(st != 0):
@@ -801,18 +1040,14 @@ def cpu_baseline(sample_fn, seconds: float):
         # timed region (finalize is idempotent: re-running it on finalized
         # headers rewrites the same bytes)
         hw, dw = oracle.gro_working_copies(host, d)
-        t0 = time.perf_counter()
-        oracle.gro_finalize_desc_inplace(hw, dw, 1)
-        t_1core = time.perf_counter() - t0
-        reps = max(1, int(seconds * threads / max(t_1core, 1e-6)))
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            oracle.gro_finalize_desc_inplace(hw, dw, threads)
-        t_all = (time.perf_counter() - t0) / reps
+        run_all = lambda: oracle.gro_finalize_desc_inplace(hw, dw, threads)  # noqa: E731
+        run_one = lambda: oracle.gro_finalize_desc_inplace(hw, dw, 1)  # noqa: E731
+        run_one()
         if not (np.array_equal(hw, hdr_after) and np.array_equal(dw["status"], st)):
             gpu_out = None  # the timed in-place runs must reproduce the checked answer
         nbytes = d.size  # flows
-        gpu_out = np.concatenate([gpu_out[0].astype(np.int64), gpu_out[1].astype(np.int64)])
+        if gpu_out is not None:
+            gpu_out = np.concatenate([gpu_out[0].astype(np.int64), gpu_out[1].astype(np.int64)])
     elif kind[0] == "aead":
         # Peer::encrypt per segment: the oracle (scalar RFC 8439 restatement,
         # the bit-exact checker) and, as the stronger CPU comparator of
@@ -820,27 +1055,22 @@ def cpu_baseline(sample_fn, seconds: float):
         _, key, rx, c0, seg = kind
         cpu_out = np.zeros(gpu_out.size + 64, np.uint8)
         oracle.wg_encrypt_batch_mt(key, rx, c0, host, seg, cpu_out, threads)
-        exp, gpu_out = cpu_out[: gpu_out.size], gpu_out
+        exp = cpu_out[: gpu_out.size].copy()
         sub = host[: host.size // 8 // seg * seg]
-        t0 = time.perf_counter()
-        oracle.wg_encrypt_batch_mt(key, rx, c0, sub, seg, cpu_out, 1)
-        t_1core = (time.perf_counter() - t0) * host.size / sub.size
-        t0 = time.perf_counter()
-        oracle.wg_encrypt_batch_mt(key, rx, c0, host, seg, cpu_out, threads)
-        t_all = time.perf_counter() - t0
-        oss = {}
+        one_scale = sub.size / host.size
+        run_all = lambda: oracle.wg_encrypt_batch_mt(key, rx, c0, host, seg, cpu_out, threads)  # noqa: E731
+        run_one = lambda: oracle.wg_encrypt_batch_mt(key, rx, c0, sub, seg, cpu_out, 1)  # noqa: E731
         try:
-            t0 = time.perf_counter()
-            oracle.openssl_encrypt_batch(key, rx, c0, sub, seg, cpu_out, 1)
-            oss1 = (time.perf_counter() - t0) * host.size / sub.size
-            t0 = time.perf_counter()
-            oracle.openssl_encrypt_batch(key, rx, c0, host, seg, cpu_out, threads)
-            ossn = time.perf_counter() - t0
-            oss = {"openssl_evp_chacha20_poly1305": {
-                "value": host.size / ossn * 2.0**-30, "value_1core": host.size / oss1 * 2.0**-30, "unit": "GiB/s",
+            oss_all = _spread(_rep_rates(lambda: oracle.openssl_encrypt_batch(key, rx, c0, host, seg, cpu_out,
+                                                                              threads), host.size, seconds, 3), 2.0**-30)
+            oss_one = _spread(_rep_rates(lambda: oracle.openssl_encrypt_batch(key, rx, c0, sub, seg, cpu_out, 1),
+                                         sub.size, seconds / 2, 3), 2.0**-30)
+            extra = {"openssl_evp_chacha20_poly1305": {
+                "value": oss_all["median"], "value_1core": oss_one["median"], "unit": "GiB/s",
+                "spread": oss_all, "spread_1core": oss_one,
                 "bit_exact_vs_oracle": bool(np.array_equal(cpu_out[: gpu_out.size], exp))}}
         except Exception as e:  # noqa: BLE001 - a comparator, never the checker
-            oss = {"openssl_evp_chacha20_poly1305": f"unavailable: {e}"}
+            extra = {"openssl_evp_chacha20_poly1305": f"unavailable: {e}"}
         nbytes = host.size
         npk = host.size // seg
     elif kind[0] == "encap":
@@ -862,78 +1092,102 @@ def cpu_baseline(sample_fn, seconds: float):
         segs = np.ascontiguousarray(seg_out.reshape(gk.size, ostride)[:, : nseg * seg]).reshape(-1)
         enc_out = np.zeros(gk.size * nseg * wga_stride(seg) + 64, np.uint8)
         sub = gk[: max(1, gk.size // 8)]
-        t0 = time.perf_counter()
-        oracle.gso_split_desc(host, sub, seg_out, 1)
-        t_g1 = (time.perf_counter() - t0) * gk.size / sub.size
-        t0 = time.perf_counter()
-        oracle.gso_split_desc(host, gk, seg_out, threads)
-        t_gn = time.perf_counter() - t0
-        ssub = segs[: segs.size // 8 // seg * seg]
-        t0 = time.perf_counter()
-        oracle.openssl_encrypt_batch(key, rx, c0, ssub, seg, enc_out, 1)
-        t_e1 = (time.perf_counter() - t0) * segs.size / ssub.size
-        t0 = time.perf_counter()
-        oracle.openssl_encrypt_batch(key, rx, c0, segs, seg, enc_out, threads)
-        t_en = time.perf_counter() - t0
-        t_1core, t_all = t_g1 + t_e1, t_gn + t_en
+        ssub = segs[: sub.size * nseg * seg]
+        one_scale = sub.size / gk.size
+
+        def run_all():
+            oracle.gso_split_desc(host, gk, seg_out, threads)
+            oracle.openssl_encrypt_batch(key, rx, c0, segs, seg, enc_out, threads)
+
+        def run_one():
+            oracle.gso_split_desc(host, sub, seg_out, 1)
+            oracle.openssl_encrypt_batch(key, rx, c0, ssub, seg, enc_out, 1)
+
         nbytes = int(gk["in_len"].astype(np.int64).sum())
         npk = gk.size
         if np.any(st != 0):
             gpu_out = None
+    elif kind[0] == "decap":
+        # Peer::decrypt + evaluate_packet per message: OpenSSL's EVP
+        # ChaCha20-Poly1305 decrypt, then the verify-gate restatement over
+        # the plaintexts (timed); parity against the oracle's decrypt + verify
+        _, key, seg, msgs_host = kind
+        n_m = (msgs_host.size + seg - 1) // seg
+        pt, st = oracle.wg_decrypt_batch(key, msgs_host, seg)
+        d = np.zeros(n_m, dtype=oracle.PKT_DESC)
+        d["offset"] = np.arange(n_m, dtype=np.uint64) * (seg - 32)
+        d["len"] = [min(seg, msgs_host.size - i * seg) - 32 for i in range(n_m)]
+        ev, el4 = oracle.verify_desc(pt, d, threads)
+        ev[st != 0], el4[st != 0] = 0, 0
+        exp = np.concatenate([st.astype(np.int64), ev.astype(np.int64), el4.astype(np.int64)])
+        gpu_out = np.concatenate([np.asarray(x).astype(np.int64) for x in gpu_out])
+        pt_buf = np.zeros(n_m * (seg - 32) + 64, np.uint8)
+        st_buf = np.zeros(n_m, np.int8)
+        sub_m = msgs_host[: max(1, n_m // 8) * seg]
+        one_scale = sub_m.size / msgs_host.size
+
+        def run_all():
+            oracle.openssl_decrypt_batch(key, msgs_host, seg, pt_buf, st_buf, threads)
+            oracle.verify_desc(pt_buf, d, threads)
+
+        def run_one():
+            oracle.openssl_decrypt_batch(key, sub_m, seg, pt_buf, st_buf, 1)
+            oracle.verify_desc(pt_buf, d[: sub_m.size // seg], 1)
+
+        run_all()
+        extra = {"openssl_decrypt_status_equal_oracle": bool(np.array_equal(st_buf, st))}
+        nbytes = msgs_host.size
+        npk = n_m
     elif kind[0] == "checksum":
         # checksum(buf, 0) per buffer (BASELINE config 1)
         d = kind[1]
         exp = oracle.checksum_desc(host, d, threads)
-        t0 = time.perf_counter()
-        oracle.checksum_desc(host, d, 1)
-        t_1core = time.perf_counter() - t0
-        reps = max(1, int(seconds * threads / max(t_1core, 1e-6)))
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            oracle.checksum_desc(host, d, threads)
-        t_all = (time.perf_counter() - t0) / reps
+        run_all = lambda: oracle.checksum_desc(host, d, threads)  # noqa: E731
+        run_one = lambda: oracle.checksum_desc(host, d, 1)  # noqa: E731
         nbytes = int(np.ascontiguousarray(d).view(oracle.PKT_DESC)["len"].astype(np.int64).sum())
         npk = d.size
     else:
         d = kind[1]
         exp = oracle.l4_desc(host, d, threads)
-        t0 = time.perf_counter()
-        oracle.l4_desc(host, d, 1)
-        t_1core = time.perf_counter() - t0
-        reps = max(1, int(seconds * threads / max(t_1core, 1e-6)))
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            oracle.l4_desc(host, d, threads)
-        t_all = (time.perf_counter() - t0) / reps
+        run_all = lambda: oracle.l4_desc(host, d, threads)  # noqa: E731
+        run_one = lambda: oracle.l4_desc(host, d, 1)  # noqa: E731
         nbytes = int(np.ascontiguousarray(d).view(oracle.PKT_DESC)["len"].astype(np.int64).sum())
     parity = gpu_out is not None and bool(np.array_equal(exp, gpu_out))
+    scale, unit = (1e-6, "Mflows/s") if kind[0] == "gro" else (2.0**-30, "GiB/s")
+    run_all()  # first touch / warm-up, untimed
+    all_s = _spread(_rep_rates(run_all, nbytes, seconds, reps), scale)
+    one_s = _spread(_rep_rates(run_one, nbytes * one_scale, seconds / 2, 3), scale)
     try:
         cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except Exception:
         cpu_model = "unknown"
-    scale, unit = (1e-6, "Mflows/s") if kind[0] == "gro" else (2.0**-30, "GiB/s")
     what = {"verify": "decap verify gates restatement (orc_verify)", "gro": "GRO finalize restatement",
             "gso": "do_tun_gso_split restatement, output bytes compared",
             "checksum": "checksum(span, 0) restatement",
             "aead": "Peer::encrypt restatement over RFC 8439 (scalar C), message bytes compared",
             "encap": "do_tun_gso_split restatement + OpenSSL EVP ChaCha20-Poly1305 timed; messages compared with "
-                     "the RFC 8439 restatement"}.get(
+                     "the RFC 8439 restatement",
+            "decap": "OpenSSL EVP ChaCha20-Poly1305 decrypt + verify-gate restatement timed; plaintext statuses, "
+                     "verdicts and L4 results compared with the RFC 8439 restatement + orc_verify"}.get(
                 kind[0], "calc_l4_checksum restatement")
     nofold = "AVX2 vector nofold (oracle/csum_oracle.c nofold_avx2)" if oracle.have_avx2() else "scalar nofold"
     return {
-        "value": nbytes / t_all * scale,
+        "value": all_s["median"],
         "unit": unit,
         "cores": threads,
         "kind": "port",
-        "value_1core": nbytes / t_1core * scale,
+        "value_1core": one_s["median"],
+        "spread": all_s,
+        "spread_1core": one_s,
         "cpu_model": cpu_model,
         "host_cores": cores,
         "sample": f"first {npk} units of the same batch, oracle/csum_oracle.c "
                   f"({what}; {nofold} for spans >= 256 B), {threads} pthreads "
-                  f"(sched_getaffinity {cores['affinity']}, cgroup quota {cores['cgroup_quota_cpus']}), "
-                  f"~{seconds:.1f} s wall; bit-exact vs GPU: {parity}",
+                  f"(sched_getaffinity {cores['affinity']}, cgroup quota {cores['cgroup_quota_cpus']}); "
+                  f"value = median of {reps} repetitions of >= {seconds:.1f} s, 1 core: median of 3 of "
+                  f">= {seconds / 2:.1f} s; bit-exact vs GPU: {parity}",
         "parity_with_gpu": parity,
-        **(oss if kind[0] == "aead" else {}),
+        **extra,
     }
 
 
@@ -1072,22 +1326,26 @@ def time_steps(torch, wl: Workload, args, world: int, dev) -> dict:
     return {"settled": settled, "wall": wall, "kern_ms": kern_ms, "kern_ms_isolated": kern_ms_isolated,
             "kern_ms_per_rank": [round(r[0], 5) for r in per_rank],
             "wall_s_per_rank": [round(r[1], 6) for r in per_rank],
-            "kern_ms_max": max(r[0] for r in per_rank), "total_payload": total_payload}
+            "kern_ms_max": max(r[0] for r in per_rank), "total_payload": total_payload,
+            "payload_per_rank": [r[2] for r in per_rank]}
 
 
-def strong_scaling(torch, wga, args, rank: int, world: int, dev) -> dict:
-    """BASELINE config 5 (16,777,216 x 1500 B mixed v4/v6 x TCP/UDP, split
-    across the ranks) timed like the main line: whole-job GiB/s
-    = all ranks' packet bytes / max-over-ranks wall time."""
+def strong_scaling(torch, wga, args, rank: int, world: int, dev, name: str = "config5") -> dict:
+    """A batch of fixed total size split across the ranks, timed like the
+    main line: whole-job GiB/s = all ranks' packet bytes / max-over-ranks
+    wall time.  config5: BASELINE config 5 (16,777,216 x 1500 B mixed v4/v6 x
+    TCP/UDP, count = byte balance); config4strong: config 4's one bimodal
+    64 B / 9000 B batch, split by bytes."""
     from wireglider_amd import dist as wdist
 
-    wl = build_workload(wga, torch, "config5", rank, world, dev)
+    wl = build_workload(wga, torch, name, rank, world, dev)
     torch.cuda.synchronize()
     t = time_steps(torch, wl, args, world, dev)
     h = wdist.allreduce_hash(wdist.result_hash(wl.out, wl.first_index), device=dev)
     out = {
         "workload": wl.cfg["workload"], "scaling": "strong", "packets_total": wl.cfg["packets_total"],
         "packets_per_rank": wl.counts,
+        "bytes_per_rank": [int(b) for b in t["payload_per_rank"]],
         "value": round(t["total_payload"] * args.steps / t["wall"] * 2.0**-30, 3), "unit": "GiB/s",
         "ms_per_step": round(t["wall"] / args.steps * 1e3, 5),
         "kernel_ms_per_rank": t["kern_ms_per_rank"],
@@ -1142,7 +1400,21 @@ def main():
     value = t["total_payload"] * args.steps / wall * wl.value_scale
     achieved = wl.alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args.workload)
-    probe = measured_read_peak(torch, wga, wl.buf, run_bytes=wl.probe_run) if rank == 0 else None
+    pcie = None
+    if wl.pcie:
+        # host-memory workloads: the bound is PCIe, not HBM — the achieved
+        # rate is the step's PCIe bytes over the wall time, against the raw
+        # copy rates of this box (both directions at once: PCIe is full duplex)
+        ceil = pcie_ceiling(torch, wl.pcie["h2d"], wl.pcie["d2h"])
+        pb = wl.pcie["h2d"] + wl.pcie["d2h"]
+        ach = pb / (wall / args.steps) / 1e9
+        pcie = {"bound": "pcie", "achieved": round(ach, 2), "peak": ceil["both_GBps"], "unit": "GB/s",
+                "frac": round(ach / ceil["both_GBps"], 4), "traffic": pb,
+                "peak_source": "raw hipMemcpyAsync H2D + D2H of the step's bytes at once on two streams, pinned, "
+                               "this box", "pcie_ceiling": ceil,
+                "spec_peak_GBps": 128.0, "frac_of_spec": round(ach / 128.0, 4),
+                "spec_source": "PCIe Gen5 x16: 64 GB/s per direction"}
+    probe = measured_read_peak(torch, wga, wl.buf, run_bytes=wl.probe_run) if rank == 0 and not wl.pcie else None
     read_peak = probe["best"] if probe else None
     # The CPU baseline samples the batch as the timed launches saw it, so it
     # runs before post_checks (whose verify pass stores the checksums into the
@@ -1152,10 +1424,12 @@ def main():
         cpu = cpu_baseline(wl.sample, args.cpu_seconds)
     post = post_checks(torch, wga, wl, world, dev)
     meta = {"metric": wl.metric or "device-resident GiB/s, L4 checksum over packet batch; 1/2/4/8 MI355X",
+            "pcie": pcie,
             "unit": wl.unit, "scaling": wl.scaling, "config": wl.cfg, "kernel": wl.kernel, "alg_bytes": wl.alg_bytes}
     del wl
     torch.cuda.empty_cache()
     strong = None if args.no_strong else strong_scaling(torch, wga, args, rank, world, dev)
+    strong4 = None if args.no_strong else strong_scaling(torch, wga, args, rank, world, dev, "config4strong")
     line = {
         "metric": meta["metric"],
         "value": round(value, 3),
@@ -1209,8 +1483,13 @@ def main():
             "unit": "T wave64-instructions/s", "frac": round(ach / VALU_PEAK_WINST, 4),
             "instructions_per_launch": valu["valu_winst_per_launch"],
             "source": f"profiles/valu_{args.workload}.json (rocprofv3 SQ_INSTS_VALU, {valu.get('kernel')})"}
+    if meta["pcie"] is not None:
+        # the device roofline does not apply to a host-memory pipeline
+        line["roofline_device"] = line["roofline"]
+        line["roofline"] = meta["pcie"]
     if strong is not None:
         line["strong_scaling"] = strong
+        line["strong_scaling_config4"] = strong4
     if rank == 0:
         line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)

@@ -368,6 +368,13 @@ int wg_host_release(void);
 int wg_host_alloc(void **ptr, uint64_t bytes);
 int wg_host_free(void *ptr);
 
+/* Per-call placement counters of the drop-in symbol wireglider::calc_l4_checksum
+ * (checksum.cpp:8-36, exported by this library): calls answered by the GPU
+ * round trip (WG_PERCALL=gpu), calls that fell back to the host because that
+ * round trip failed, and calls answered on the host by placement (the
+ * default).  Process-wide, since load; any pointer may be NULL.  Always WG_OK. */
+int wg_percall_stats(uint64_t *gpu_answered, uint64_t *host_fallback, uint64_t *host_answered);
+
 /* ------------------------------------------------------------------------
  * Synthetic batches (benchmark / test data, written on the device; not part
  * of the reference interface).  Deterministic in `seed` and in the global

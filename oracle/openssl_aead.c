@@ -85,3 +85,75 @@ int oss_wg_encrypt_batch(const uint8_t key[32], uint32_t rx, uint64_t c0, const 
     }
     return rc;
 }
+
+typedef struct {
+    const uint8_t *key;
+    const uint8_t *in;
+    uint64_t total;
+    uint32_t seg;
+    uint8_t *out;
+    int8_t *status;
+    uint64_t lo, hi;
+    int rc;
+} djob;
+
+/* Peer::decrypt (proto/proto.cpp:496-523) per message of a GRO batch: the
+ * header / counter checks, then EVP decrypt with the tag; a failed message
+ * gets status -1 (plaintext zeroed on a bad tag, as libsodium leaves it). */
+static void *drun(void *arg) {
+    djob *j = (djob *)arg;
+    EVP_CIPHER_CTX *ctx = EVP_CIPHER_CTX_new();
+    const uint64_t ostride = j->seg > 32 ? j->seg - 32 : 0;
+    j->rc = ctx && EVP_DecryptInit_ex(ctx, EVP_chacha20_poly1305(), NULL, j->key, NULL) == 1 ? 0 : -1;
+    for (uint64_t i = j->lo; i < j->hi && !j->rc; i++) {
+        const uint64_t off = i * j->seg;
+        const size_t len = j->total - off < j->seg ? (size_t)(j->total - off) : j->seg;
+        const uint8_t *m = j->in + off;
+        uint8_t *o = j->out + i * ostride;
+        uint64_t counter = 0;
+        if (len >= 16)
+            for (int b = 7; b >= 0; b--) counter = (counter << 8) | m[8 + b];
+        if (len < 32 || counter > UINT64_MAX - (1ull << 13)) {
+            j->status[i] = -1;
+            continue;
+        }
+        uint8_t nonce[12] = {0};
+        memcpy(nonce + 4, m + 8, 8);
+        const size_t clen = len - 32;
+        int n = 0, ok = EVP_DecryptInit_ex(ctx, NULL, NULL, NULL, nonce) == 1 &&
+                        EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_SET_TAG, 16, (void *)(m + 16 + clen)) == 1 &&
+                        (!clen || EVP_DecryptUpdate(ctx, o, &n, m + 16, (int)clen) == 1) &&
+                        EVP_DecryptFinal_ex(ctx, o + n, &n) == 1;
+        if (!ok)
+            memset(o, 0, clen);
+        j->status[i] = ok ? 0 : -1;
+    }
+    EVP_CIPHER_CTX_free(ctx);
+    return NULL;
+}
+
+/* 0, or -1 if OpenSSL could not be set up; plaintext i at out + i * (seg - 32). */
+int oss_wg_decrypt_batch(const uint8_t key[32], const uint8_t *in, uint64_t total, uint32_t seg, uint8_t *out,
+                         int8_t *status, int threads) {
+    const uint64_t n = (total + seg - 1) / seg;
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    if ((uint64_t)threads > n) threads = n ? (int)n : 1;
+    pthread_t tid[256];
+    djob jobs[256];
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (djob){key, in, total, seg, out, status, n * (uint64_t)t / (uint64_t)threads,
+                         n * (uint64_t)(t + 1) / (uint64_t)threads, 0};
+        if (threads == 1)
+            drun(&jobs[t]);
+        else
+            pthread_create(&tid[t], NULL, drun, &jobs[t]);
+    }
+    int rc = 0;
+    for (int t = 0; t < threads; t++) {
+        if (threads > 1)
+            pthread_join(tid[t], NULL);
+        rc |= jobs[t].rc;
+    }
+    return rc;
+}

@@ -412,11 +412,7 @@ def wg_decrypt_batch_mt(key: bytes, buf: np.ndarray, segment_size: int, out: np.
 _OSS = None
 
 
-def openssl_encrypt_batch(key: bytes, receiver_index: int, counter0: int, buf: np.ndarray, segment_size: int,
-                          out: np.ndarray, threads: int) -> None:
-    """The same batch over the system OpenSSL's EVP_chacha20_poly1305
-    (oracle/openssl_aead.c): an optimised RFC 8439 of libsodium's class, the
-    f4 CPU comparator."""
+def _oss():
     global _OSS
     if _OSS is None:
         path = HERE / "build" / "libaead_openssl.so"
@@ -426,8 +422,35 @@ def openssl_encrypt_batch(key: bytes, receiver_index: int, counter0: int, buf: n
         _OSS.oss_wg_encrypt_batch.restype = ctypes.c_int
         _OSS.oss_wg_encrypt_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
                                               ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int]
+        _OSS.oss_wg_decrypt_batch.restype = ctypes.c_int
+        _OSS.oss_wg_decrypt_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    return _OSS
+
+
+def openssl_encrypt_batch(key: bytes, receiver_index: int, counter0: int, buf: np.ndarray, segment_size: int,
+                          out: np.ndarray, threads: int) -> None:
+    """The same batch over the system OpenSSL's EVP_chacha20_poly1305
+    (oracle/openssl_aead.c): an optimised RFC 8439 of libsodium's class, the
+    f4 CPU comparator."""
+    _oss()
     k, a = _b(key), _u8(buf)
     rc = _OSS.oss_wg_encrypt_batch(k.ctypes.data, receiver_index, counter0, a.ctypes.data, a.size, segment_size,
                                    out.ctypes.data, threads)
+    if rc != 0:
+        raise RuntimeError("OpenSSL EVP_chacha20_poly1305 failed")
+
+
+def openssl_decrypt_batch(key: bytes, buf: np.ndarray, segment_size: int, out: np.ndarray, status: np.ndarray,
+                          threads: int) -> None:
+    """Peer::decrypt per message of a GRO batch over OpenSSL's
+    EVP_chacha20_poly1305 (the decap CPU comparator): plaintext i at
+    i * (segment_size - 32) of `out`, status 0 / -1 per message."""
+    _oss()
+    k, a = _b(key), _u8(buf)
+    n = (a.size + segment_size - 1) // segment_size
+    assert out.size >= n * max(segment_size - 32, 0) and status.size >= n and status.dtype == np.int8
+    rc = _OSS.oss_wg_decrypt_batch(k.ctypes.data, a.ctypes.data, a.size, segment_size, out.ctypes.data,
+                                   status.ctypes.data, threads)
     if rc != 0:
         raise RuntimeError("OpenSSL EVP_chacha20_poly1305 failed")

@@ -4,7 +4,8 @@
 // through the reference's C++ symbol wireglider::calc_l4_checksum.
 //
 // stdin: records {u32 len, u8 isv6, u8 istcp, u16 csum_start, len bytes}
-// stdout: one hex result per record.
+// stdout: one hex result per record; stderr: the library's per-call
+// placement counters (wg_percall_stats) at the end.
 #include <cstdint>
 #include <cstdio>
 #include <vector>
@@ -26,5 +27,9 @@ int main() {
         uint16_t r = wireglider::calc_l4_checksum(std::span<const uint8_t>(pkt), v6 != 0, tcp != 0, cs);
         printf("%04x\n", r);
     }
+    uint64_t gpu = 0, fallback = 0, host = 0;
+    wg_percall_stats(&gpu, &fallback, &host);
+    fprintf(stderr, "percall gpu=%llu fallback=%llu host=%llu\n", (unsigned long long)gpu,
+            (unsigned long long)fallback, (unsigned long long)host);
     return 0;
 }

@@ -64,14 +64,25 @@ def _worker(rank, world, port, n, q):
         bounds = wdist.shard_bounds_by_bytes(d["len"], world)
         lo, hi = bounds[rank]
         local = torch.from_numpy(oracle.l4_desc(buf, d[lo:hi], threads=1).astype(np.int32)).to(torch.uint16)
-        full = wdist.gather_results(local, [b - a for a, b in bounds])
+        sent = []
+        real = dist.all_gather
+
+        def spy(parts, t, group=None):
+            sent.append((str(t.dtype), t.numel() * t.element_size()))
+            return real(parts, t, group=group)
+
+        dist.all_gather = spy
+        try:
+            full = wdist.gather_results(local, [b - a for a, b in bounds])
+        finally:
+            dist.all_gather = real
         h = wdist.allreduce_hash(wdist.result_hash(local, lo))
         # far from zero: per-rank hashes near 2^61 must not overflow the reduction
         h_big = wdist.allreduce_hash(wdist.result_hash(local, lo + BIG_OFFSET))
         t = wdist.max_over_ranks(float(rank + 1))
         per = wdist.all_gather_floats([float(rank), 0.5 * rank])
         if rank == 0:
-            q.put((full.numpy().astype(np.uint16).tobytes(), h, h_big, t, bounds, per))
+            q.put((full.numpy().astype(np.uint16).tobytes(), h, h_big, t, bounds, per, sent))
     finally:
         dist.destroy_process_group()
 
@@ -87,7 +98,7 @@ def test_sharded_equals_single_process(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
     for p in procs:
         p.start()
-    full_bytes, h, h_big, t, bounds, per = q.get(timeout=240)
+    full_bytes, h, h_big, t, bounds, per, sent = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -99,6 +110,8 @@ def test_sharded_equals_single_process(world):
     assert h_big == exact_hash(ref, BIG_OFFSET)
     assert t == float(world)
     assert per == [[float(r), 0.5 * r] for r in range(world)]  # per-rank bench times, in rank order
+    # the gather moves 2 B per packet of the longest shard
+    assert sent == [("torch.uint8", 2 * max(b - a for a, b in bounds))]
     # byte balance: each shard within one max-size packet of the mean
     per = [int(d["len"][a:b].astype(np.int64).sum()) for a, b in bounds]
     assert max(per) - min(per) <= 2 * int(d["len"].max())
@@ -161,3 +174,29 @@ def test_bench_refuses_more_ranks_than_gpus():
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2, r.stderr
     assert "GPU(s) visible" in r.stderr
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_config4_strong_shards(world):
+    """bench.py's config 4 strong companion: ONE 4 M-packet bimodal batch
+    split by bytes; every rank's shard buffer starts at the 16-B-aligned
+    global byte its synth_fill counter base needs, its descriptors rebased
+    onto it, so the shards together are the N = 1 batch; per-rank byte
+    totals within one 9000-B packet of each other."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+
+    lens, offs = bench.config4_lengths()
+    assert lens.size == 1 << 22 and set(np.unique(lens)) == {64, 9000}
+    bounds = wdist.shard_bounds_by_bytes(lens, world)
+    assert bounds[0][0] == 0 and bounds[-1][1] == lens.size
+    per = [int(lens[a:b].sum()) for a, b in bounds]
+    assert sum(per) == int(lens.sum()) and max(per) - min(per) <= 9000
+    for a, b in bounds:
+        base = int(offs[a]) & ~15
+        assert base % 16 == 0 and 0 <= int(offs[a]) - base < 16
+        rel = offs[a:b] - base
+        assert rel[0] < 16 and np.all(np.diff(rel) == lens[a:b - 1])

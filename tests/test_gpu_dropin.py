@@ -3,7 +3,9 @@ include/wireglider/checksum.hpp and linked to libwireglider_amd.so through the
 reference's symbol wireglider::calc_l4_checksum (checksum.cpp:8), with
 WG_PERCALL=gpu (every call through the host-memory GPU path), returns the
 RFC textbook checksum for every packet, and verify-to-zero holds for the
-reference test's packets (tests/test-checksum.cpp:53-82).  The per-call
+reference test's packets (tests/test-checksum.cpp:53-82); the library's
+placement counters (wg_percall_stats) show every call answered by the GPU,
+none by the host fallback.  The per-call
 latency of both placements is printed for DESIGN.md."""
 import json
 import os
@@ -54,6 +56,16 @@ def test_dropin_calc_l4_checksum_on_gpu(gpu, tmp_path):
     assert r.returncode == 0, r.stderr.decode()
     got = [int(x, 16) for x in r.stdout.decode().split()]
     assert got == exp
+    # every call was answered by the GPU round trip: none fell back to the
+    # host (which would give the same checksums by construction)
+    stats = dict(kv.split("=") for kv in r.stderr.decode().split("percall ")[-1].split())
+    assert stats == {"gpu": str(len(recs)), "fallback": "0", "host": "0"}, stats
+    # and the default placement answers on the host, with no GPU round trip
+    r = subprocess.run([str(exe)], input=blob, capture_output=True, timeout=300,
+                       env={k: v for k, v in os.environ.items() if k != "WG_PERCALL"})
+    assert r.returncode == 0 and [int(x, 16) for x in r.stdout.decode().split()] == exp
+    stats = dict(kv.split("=") for kv in r.stderr.decode().split("percall ")[-1].split())
+    assert stats == {"gpu": "0", "fallback": "0", "host": str(len(recs))}, stats
 
 
 def test_percall_latency_both_placements(gpu, tmp_path):

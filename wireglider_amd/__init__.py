@@ -49,6 +49,7 @@ EXPORTED_SYMBOLS = (
     "wg_decap_host",
     "wg_encap_host",
     "wg_host_release",
+    "wg_percall_stats",
     "wg_host_alloc",
     "wg_host_free",
     "wg_synth_fill",
@@ -129,6 +130,7 @@ def _load() -> ctypes.CDLL:
         "wg_encap_host": (i32, [u8p, vp, u64, ctypes.c_char_p, u32, u64, u32, u32, u32, vp, vp, vp,
                                 ctypes.POINTER(u64)]),
         "wg_host_release": (i32, []),
+        "wg_percall_stats": (i32, [ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "wg_host_alloc": (i32, [ctypes.POINTER(ctypes.c_void_p), u64]),
         "wg_host_free": (i32, [vp]),
         "wg_synth_fill": (i32, [u8p, u64, u64, u64, vp]),

@@ -27,8 +27,13 @@ def shard_bounds(n: int, world: int, rank: int) -> tuple[int, int]:
 
 def shard_bounds_by_bytes(lengths: Sequence[int], world: int) -> list[tuple[int, int]]:
     """Split packets 0..n-1 into `world` contiguous ranges of near-equal byte
-    totals.  Every range boundary is the first packet whose byte prefix sum
-    reaches rank * total / world, so the largest imbalance is one packet."""
+    totals.  Each boundary is one of the two packet boundaries around
+    rank * total / world (the prefix sums just below and at-or-above it);
+    of those 2^(world-1) choices (world <= 12; else the nearer one each) the
+    one with the smallest spread of shard byte totals wins, so a shard is off
+    the mean by at most about one packet."""
+    import itertools
+
     import numpy as np
 
     lens = np.asarray(lengths, dtype=np.int64)
@@ -37,15 +42,28 @@ def shard_bounds_by_bytes(lengths: Sequence[int], world: int) -> list[tuple[int,
         raise ValueError("world must be >= 1")
     csum = np.concatenate([[0], np.cumsum(lens)])
     total = int(csum[-1])
-    cuts = [0]
+    cands = []
     for r in range(1, world):
         target = total * r // world
-        cuts.append(int(np.searchsorted(csum, target, side="left")))
-    cuts.append(n)
-    cuts = [min(max(c, 0), n) for c in cuts]
-    for i in range(1, len(cuts)):  # monotone
-        cuts[i] = max(cuts[i], cuts[i - 1])
-    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+        j = int(np.searchsorted(csum, target, side="left"))
+        lo_c, hi_c = max(j - 1, 0), min(j, n)
+        if world > 12:  # the nearer boundary only
+            near = lo_c if target - int(csum[lo_c]) <= int(csum[hi_c]) - target else hi_c
+            cands.append((near,))
+        else:
+            cands.append(tuple(sorted({lo_c, hi_c})))
+    best, best_spread = None, None
+    for choice in itertools.product(*cands) if cands else [()]:
+        cuts = [0, *choice, n]
+        if any(cuts[i] > cuts[i + 1] for i in range(world)):
+            continue
+        per = [int(csum[cuts[i + 1]] - csum[cuts[i]]) for i in range(world)]
+        spread = max(per) - min(per)
+        if best_spread is None or spread < best_spread:
+            best, best_spread = cuts, spread
+    if best is None:  # (cannot happen: the all-lower choice is monotone) fall back to count balance
+        best = [n * r // world for r in range(world + 1)]
+    return [(best[r], best[r + 1]) for r in range(world)]
 
 
 def result_hash(results, global_offset: int) -> int:
@@ -89,18 +107,21 @@ def allreduce_hash(local_hash: int, group=None, device=None) -> int:
 
 def gather_results(local, counts: Sequence[int], group=None):
     """All-gather variable-size uint16 shards into the full result array
-    (padded all_gather, then trimmed).  `counts[r]` = packets of rank r."""
+    (padded all_gather, then trimmed).  `counts[r]` = packets of rank r.
+    The shards travel as their raw bytes (a uint8 view of even length), so
+    the gather moves 2 B per packet, plus the padding of the
+    shorter shards up to the longest."""
     import torch
     import torch.distributed as dist
 
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return local.clone()
     mx = max(counts)
-    buf = torch.zeros(mx, dtype=torch.int32, device=local.device)
-    buf[: local.numel()] = local.to(torch.int32)
+    buf = torch.zeros(2 * mx, dtype=torch.uint8, device=local.device)
+    buf[: 2 * local.numel()] = local.reshape(-1).contiguous().view(torch.uint8)
     parts = [torch.empty_like(buf) for _ in counts]
     dist.all_gather(parts, buf, group=group)
-    return torch.cat([p[:c] for p, c in zip(parts, counts)]).to(torch.uint16)
+    return torch.cat([p[: 2 * c] for p, c in zip(parts, counts)]).view(torch.uint16)
 
 
 def max_over_ranks(x: float, device=None, group=None) -> float:
