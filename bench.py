@@ -455,6 +455,24 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
         d_desc = torch.from_numpy(gd.view(np.uint8).copy()).to(dev)
         hdr_bytes = int(hdr_len.sum())
         written = int(np.where(isv6, 4, 6).sum() + 2 * (~istcp).sum())  # length fields, ip_sum, seed
+        # Memory-side floor per flow (profiles/r02_store_granularity.json,
+        # profiles/pmc_gro.json): the 24-B descriptor, the header chunks read
+        # in 64-B memory blocks, the stores in 32-B sectors (the kernel's wide
+        # stores: v4 bytes [0, 16), v6 [4, 8); UDP length + seed [cs+4, cs+8),
+        # TCP seed [cs+16, cs+18)).
+        ho = gd["hdr_offset"].astype(np.int64)
+        need = np.where(isv6, 40, cs)
+        c0 = ho & ~15
+        c1 = c0 + 16 * (((ho & 15) + need - 1) // 16 + 1)
+        rblk = (c1 - 1) // 64 - c0 // 64 + 1
+        st_lo = np.where(isv6, ho + 4, ho)
+        st_hi = np.where(isv6, ho + 8, ho + 16)
+        f_lo = ho + cs + np.where(istcp, 16, 4)
+        f_hi = f_lo + np.where(istcp, 2, 4)
+        s1, s2 = st_lo // 32, (st_hi - 1) // 32
+        t1, t2 = f_lo // 32, (f_hi - 1) // 32
+        wsec = (s2 - s1 + 1) + (t2 - t1 + 1) - np.maximum(0, np.minimum(s2, t2) - np.maximum(s1, t1) + 1)
+        phys = int(24 * n + 64 * rblk.sum() + 32 * wsec.sum())
 
         def launch():
             wga.gro_finalize(d_hdr, d_desc)
@@ -479,8 +497,10 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
         cfg = {"workload": "gro (SURVEY §8 f2): 4,194,304 coalesced flows per GPU, headers in 64 B slots, "
                            "mixed IPv4/IPv6 x TCP/UDP, in-place finalize (wg_gro_finalize)",
                "flows_per_gpu": n, "slot_bytes": slot, "parallelism": f"shard{world}"}
-        return Workload(launch, n, n, n * 24 + hdr_bytes + written + n, cfg, "weak", d_hdr,
-                        "wg::gro_finalize_lds_kernel<true>", rank * n, sample=sample, counts=[n] * world,
+        cfg["alg_bytes_fields_only"] = n * 24 + hdr_bytes + written + n  # round 1-2 count: bytes the code touches
+        cfg["alg_bytes_model"] = "24-B descriptor + header chunks in 64-B read blocks + stores in 32-B write sectors"
+        return Workload(launch, n, n, phys, cfg, "weak", d_hdr,
+                        "wg::gro_finalize_lds_kernel<true,5>", rank * n, sample=sample, counts=[n] * world,
                         metric="device-resident Mflows/s, GRO finalize (SURVEY f2)", unit="Mflows/s",
                         value_scale=1e-6, post=post)
     if name == "config4strong":

@@ -291,6 +291,108 @@ __global__ __launch_bounds__(kGroBlock) void gro_finalize_lds_kernel(uint8_t *hd
         reinterpret_cast<int8_t *>(desc)[i * sizeof(wg_gro_desc) + offsetof(wg_gro_desc, status)] = st;
 }
 
+// Wave-owned variant (knob gro_lds = 2): the same cooperative chunk loads,
+// but each wave owns 64 flows and stages only its own chunks, so no block
+// barrier sits between the descriptor round trip and the chunk round trip
+// (the LDS kernel's block of 256 flows waits for its slowest wave twice).
+// The per-flow chunk geometry reaches the loading lanes by ds_bpermute and
+// the chunks their flow's lane through a wave-private LDS tile; LDS ops of
+// one wave execute in order, so a wave-scope fence is all the ordering the
+// tile needs.  kIters > 1: each wave takes kIters groups of 64 flows a grid
+// stride apart and loads the next group's descriptors while the current
+// group's chunks are in flight.
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool kWide, int kIters>
+__global__ __launch_bounds__(kGroBlock) void gro_finalize_wave_kernel(uint8_t *hdrs, wg_gro_desc *desc, uint64_t n) {
+    constexpr uint32_t K = 5;
+    __shared__ v4u s_tile[kGroBlock / 64][64 * K];
+    const uint32_t lane = lane_id(), w = wave_in_block();
+    v4u *tile = s_tile[w];
+    const uint64_t wave = (uint64_t)blockIdx.x * (kGroBlock / 64) + w;
+    const uint64_t gstride = (uint64_t)gridDim.x * kGroBlock;  // flows between a wave's groups
+    uint64_t i = wave * 64u + lane;
+    wg_gro_desc d{};
+    if (i < n)
+        d = desc[i];
+    for (int it = 0; it < kIters; it++) {
+        const bool live = i < n;
+        bool fast = false, v6 = false, tcp = false;
+        int8_t st = 0;
+        uint32_t need = 0, cs = 0, l4off = 0;
+        uint8_t *h = hdrs;
+        if (live) {
+            h = hdrs + d.hdr_offset;
+            const uint32_t H = d.hdr_len;
+            cs = d.csum_start;
+            l4off = cs + d.csum_offset;
+            v6 = d.flags & WG_PKT_V6;
+            tcp = d.flags & WG_PKT_TCP;
+            const uint32_t iph = v6 ? 40u : 20u;
+            if (cs < iph || cs > H || l4off < cs || l4off + 2 > H || (!tcp && cs + 8 > H))
+                st = -3;
+            else {
+                need = v6 ? 40u : cs;
+                fast = need <= kFastNeed;
+            }
+        }
+        const uintptr_t hp = reinterpret_cast<uintptr_t>(h);
+        const uint64_t a0 = (uint64_t)(hp & ~(uintptr_t)15);
+        const uint32_t last = fast ? (uint32_t)(((hp & 15u) + need - 1) >> 4) : 0xffu;
+        // slot k * 64 + lane = chunk c of flow f = slot / 5: every load issued
+        // before any is used, branch-free (no-stage slots read the zero chunk)
+        v4u v[K];
+#pragma unroll
+        for (uint32_t k = 0; k < K; k++) {
+            const uint32_t slot = 64u * k + lane;
+            const uint32_t f = (slot * 52429u) >> 18;  // slot / 5
+            const uint32_t c = slot - 5u * f;
+            const uint32_t lf = bperm(last, f);
+            const uint64_t af = ((uint64_t)bperm((uint32_t)(a0 >> 32), f) << 32) | bperm((uint32_t)a0, f);
+            const uintptr_t a = lf != 0xffu ? (uintptr_t)(af + 16u * (c < lf ? c : lf))
+                                            : reinterpret_cast<uintptr_t>(&g_gro_zero);
+            v[k] = ld16(a);
+        }
+        // the next group's descriptors, in flight under this group's chunks
+        const uint64_t inext = i + gstride;
+        wg_gro_desc dn{};
+        if (kIters > 1 && it + 1 < kIters && inext < n)
+            dn = desc[inext];
+#pragma unroll
+        for (uint32_t k = 0; k < K; k++)
+            tile[64u * k + lane] = v[k];
+        wave_lds_sync();
+        if (live) {
+            if (st == 0) {
+                const uint64_t l4len = (uint64_t)(d.hdr_len - cs) + d.payload_bytes;  // :84
+                if (!tcp && !(kWide && fast))
+                    st_be16(h + cs + 4, (uint32_t)l4len);  // udp->len (uint16), :85-86
+                if (fast) {
+                    const v4u *kk = &tile[lane * K];
+                    gro_fields<kWide>(h, d, v6, tcp, l4len, kk[0], kk[1], kk[2], kk[3], kk[4]);
+                } else {
+                    gro_slow(h, d.hdr_len, cs, l4off, d.payload_bytes, v6, l4len);
+                }
+            }
+            if (d.status != st)  // leave descriptor lines clean when the caller pre-zeroed status
+                reinterpret_cast<int8_t *>(desc)[i * sizeof(wg_gro_desc) + offsetof(wg_gro_desc, status)] = st;
+        }
+        if (kIters == 1)
+            break;
+        wave_lds_sync();  // this group's tile reads before the next group's writes
+        i = inext;
+        d = dn;
+    }
+}
+
 }  // namespace wg
 
 using namespace wg;
@@ -304,6 +406,21 @@ extern "C" int wg_gro_finalize(uint8_t *dev_hdrs, wg_gro_desc *dev_desc, uint64_
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
     const Tune t = tune();
+    if (t.gro_lds == 2) {
+        const uint32_t it = t.gro_iters;
+        uint64_t b = (blocks + it - 1) / it;
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        if (it == 2)
+            hipLaunchKernelGGL((gro_finalize_wave_kernel<true, 2>), dim3((unsigned)b), dim3(kGroBlock), 0, st,
+                               dev_hdrs, dev_desc, n);
+        else if (it == 4)
+            hipLaunchKernelGGL((gro_finalize_wave_kernel<true, 4>), dim3((unsigned)b), dim3(kGroBlock), 0, st,
+                               dev_hdrs, dev_desc, n);
+        else
+            hipLaunchKernelGGL((gro_finalize_wave_kernel<true, 1>), dim3((unsigned)blocks), dim3(kGroBlock), 0, st,
+                               dev_hdrs, dev_desc, n);
+        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+    }
     if (t.gro_lds && t.gro_wide && t.gro_chunks == 4)
         hipLaunchKernelGGL((gro_finalize_lds_kernel<true, 4>), dim3((unsigned)blocks), dim3(kGroBlock), 0,
                            static_cast<hipStream_t>(stream), dev_hdrs, dev_desc, n);
