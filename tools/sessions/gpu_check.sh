@@ -1,9 +1,9 @@
 #!/bin/bash
 # One GPU-box session: parity tests, smoke, bench line, rocprofv3 kernel stats.
 # Every GPU step has its own time limit; a crash/fault/timeout ends the script.
-# usage: tools/gpu_check.sh [tag] [pytest-args...]
+# usage: tools/sessions/gpu_check.sh [tag] [pytest-args...]
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 ROOT=$(pwd)
 TAG=${1:-r01}
 OUT=$ROOT/gpurun_out/$TAG

@@ -1,9 +1,9 @@
 #!/bin/bash
 # The fused encap step (wg_encap_batch): parity tests, the fused and two-call
 # bench lines on one box, and a kernel-trace profile of the fused one.
-# usage: tools/gpu_encap_fused.sh TAG
+# usage: tools/sessions/gpu_encap_fused.sh TAG
 set -euo pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/$1
 mkdir -p "$OUT"

@@ -6,7 +6,7 @@
 # lines that follow carry it, then the bench lines: the default run (config 2)
 # and configs 3/4/5, verify, GRO.  Each GPU step has its own time limit; the
 # first failure ends it.
-# usage: tools/gpu_evidence.sh [outdir-name]
+# usage: tools/sessions/gpu_evidence.sh [outdir-name]
 set -u
 cd "${GRAFT_REPO_ROOT}"
 O=$(pwd)/gpurun_out/${1:-evidence}; mkdir -p $O

@@ -1,9 +1,9 @@
 #!/bin/bash
 # GSO split on raw buffer ops: parity (GSO + encap suites) then a same-box
 # A/B against a library built from another revision.
-# usage: tools/gpu_gso_buf.sh TAG <libA (old)> [rounds]
+# usage: tools/sessions/gpu_gso_buf.sh TAG <libA (old)> [rounds]
 set -euo pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/$1; OLD=$2; R=${3:-3}
 mkdir -p "$OUT"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Interleaved A/B (tools/ab.py) of knob variants on workloads.
-# usage: tools/gpu_r02_ab.sh TAG "workload variants..." ["workload variants..."]
+# usage: tools/sessions/gpu_r02_ab.sh TAG "workload variants..." ["workload variants..."]
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT}"
 TAG=$1; shift

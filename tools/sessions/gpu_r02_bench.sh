@@ -4,9 +4,9 @@
 # GSO variant, and a 2-rank rehearsal of the self-spawning multi-rank path
 # (gloo, both ranks on the one GPU).  Every GPU step has its own time limit;
 # the first failure ends the script.
-# usage: tools/gpu_r02_bench.sh TAG [workloads...]
+# usage: tools/sessions/gpu_r02_bench.sh TAG [workloads...]
 set -euo pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-r02}
 shift || true
 OUT=gpurun_out/$TAG

@@ -1,9 +1,9 @@
 #!/bin/bash
 # Bench lines only (no tests) for the given workloads, each under its own
 # limit; the first failure ends the script.
-# usage: tools/gpu_r02_benches.sh TAG workload [workload...]
+# usage: tools/sessions/gpu_r02_benches.sh TAG workload [workload...]
 set -euo pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=$1
 shift
 OUT=gpurun_out/$TAG

@@ -2,9 +2,9 @@
 # Round-2 evidence session: GPU tests, host-path rates, bench lines for the
 # given workloads (the first is profiled with rocprofv3 kernel stats, same
 # box).  Every GPU step has its own limit; the first failure ends the script.
-# usage: tools/gpu_r02_evidence.sh TAG workload [workload...]
+# usage: tools/sessions/gpu_r02_evidence.sh TAG workload [workload...]
 set -euo pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 ROOT=$(pwd)
 TAG=$1
 shift
