@@ -72,9 +72,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="config2",
-                    choices=["config1", "config2", "config3", "config3udp", "config4", "config4strong", "config5",
+                    choices=["config1", "config2", "config3", "config3udp", "config4", "config4small", "config4strong",
+                             "config5",
                              "verify", "gro", "encap", "encap_2call", "aead", "encap_host", "decap_host"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-post", action="store_true",
+                    help="skip the workload's own post-checks (PMC passes: only the step's launches of its kernels)")
     ap.add_argument("--no-strong", action="store_true", help="skip the config 5 strong-scaling companion")
     ap.add_argument("--cpu-seconds", type=float, default=2.0,
                     help="wall seconds of each CPU baseline repetition (5 on all cores, 3 on one)")
@@ -104,6 +107,7 @@ class Workload:
     post: Optional[Callable] = None   # workload-specific post-check
     probe_run: int = 0                # packet size for the kernel-shaped read probe (0: contiguous only)
     pcie: Optional[dict] = None       # host-memory workloads: PCIe bytes per step {"h2d": B, "d2h": B}
+    rw: Optional[tuple] = None        # (read, written) algorithmic bytes per launch, when both directions count
 
 
 def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workload:
@@ -227,7 +231,8 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
         alg = n * in_len + n * out_len + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES)
         return Workload(launch, n, n * in_len, alg, cfg, "weak", buf,
                         "wg::gso_plan_kernel + wg::gso_split_kernel<4,4,0> + wg::gso_finalize_kernel (one wg_gso_split call)",
-                        rank * n, sample=sample, counts=[n] * world, post=post)
+                        rank * n, sample=sample, counts=[n] * world, post=post,
+                        rw=(n * in_len + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES), n * out_len))
     if name == "aead":
         # worker/encap.cpp:136-141: Peer::encrypt for every 1500-B segment of a
         # PacketBatch (config 2's packets), counters encrypt_nonce++ per call
@@ -503,6 +508,8 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                         "wg::gro_finalize_lds_kernel<true,5>", rank * n, sample=sample, counts=[n] * world,
                         metric="device-resident Mflows/s, GRO finalize (SURVEY f2)", unit="Mflows/s",
                         value_scale=1e-6, post=post)
+    if name == "config4small":
+        return build_config4_small(wga, torch, rank, world, dev)
     if name == "config4strong":
         return build_config4_strong(wga, torch, rank, world, dev)
     if name == "encap_host":
@@ -660,6 +667,51 @@ def build_config4_strong(wga, torch, rank: int, world: int, dev) -> Workload:
            "layout": "descriptor", "parallelism": f"shard{world} (byte-balanced contiguous ranges)"}
     return Workload(launch, n, payload, payload + 18 * n, cfg, "strong", buf,
                     "wg::l4csum_split_kernel<1,nt> (l4_small=5)", lo, out, desc, None, counts)
+
+
+def build_config4_small(wga, torch, rank: int, world: int, dev) -> Workload:
+    """Config 4's 64-B sub-batch as a workload of its own, so
+    PMC and kernel stats cover it: the 2,098,300 64-B packets of config 4's
+    batch, where they lie between the 9000-B ones (8-B aligned), through
+    the default descriptor kernel.  The physical floor is counted beside
+    the algorithmic bytes: each packet touches one or two 64-B memory blocks."""
+    import numpy as np
+
+    seed = 0x5EED0004
+    lens, offs = config4_lengths()
+    idx = np.nonzero(lens == 64)[0]
+    raw = np.zeros((idx.size, 2), dtype=np.int64)
+    raw[:, 0] = offs[idx]
+    raw[:, 1] = 64 | (20 << 32)
+    total = int(offs[-1] + lens[-1])
+    buf = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    wga.synth_fill(buf, seed)
+    full = np.zeros((lens.size, 2), dtype=np.int64)
+    full[:, 0] = offs
+    full[:, 1] = lens | (20 << 32)
+    wga.synth_headers(buf, torch.from_numpy(full).to(dev), seed, 0)
+    desc = torch.from_numpy(raw).to(dev)
+    n = idx.size
+    out = torch.empty(n, dtype=torch.uint16, device=dev)
+
+    def launch():
+        wga.calc_l4_checksum_desc(buf, desc, out=out)
+
+    def sample(npk):
+        k = min(n, npk)
+        end = int(raw[k - 1, 0]) + 64
+        return buf[:end].cpu().numpy(), out[:k].cpu().numpy(), ("desc", raw[:k])
+
+    o = offs[idx]
+    blocks = ((o + 63) // 64 - o // 64 + 1)
+    phys = int(64 * blocks.sum()) + 18 * n
+    cfg = {"workload": "config4small: config 4's 64-B sub-batch (2,098,300 IPv4/UDP packets between its 9000-B ones, "
+                       "8-B aligned), descriptor batch", "packets_per_gpu": int(n), "layout": "descriptor",
+           "physical_floor_bytes": phys,
+           "physical_floor_model": "64-B memory blocks touched by each packet (1 or 2) + 16-B descriptor + 2-B result",
+           "parallelism": f"shard{world}"}
+    return Workload(launch, n, 64 * n, 82 * n, cfg, "weak", buf, "wg::l4csum_split_kernel<1,nt> (l4_small=5)", 0,
+                    out, desc, sample, [n] * world)
 
 
 def _pinned_copy(wga, t):
@@ -1243,12 +1295,12 @@ def load_valu(workload: str):
         return None
 
 
-def post_checks(torch, wga, wl: Workload, world: int, dev):
+def post_checks(torch, wga, wl: Workload, world: int, dev, no_post: bool = False):
     """Outside the timed region: verify pass, result hash, RCCL gather."""
     from wireglider_amd import dist as wdist
 
     info = {}
-    if wl.post is not None:
+    if wl.post is not None and not no_post:
         torch.cuda.synchronize()
         info.update(wl.post())
     if wl.out is None:
@@ -1442,9 +1494,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl.sample is not None:
         cpu = cpu_baseline(wl.sample, args.cpu_seconds)
-    post = post_checks(torch, wga, wl, world, dev)
+    post = post_checks(torch, wga, wl, world, dev, args.no_post)
     meta = {"metric": wl.metric or "device-resident GiB/s, L4 checksum over packet batch; 1/2/4/8 MI355X",
-            "pcie": pcie,
+            "pcie": pcie, "rw": wl.rw,
             "unit": wl.unit, "scaling": wl.scaling, "config": wl.cfg, "kernel": wl.kernel, "alg_bytes": wl.alg_bytes}
     del wl
     torch.cuda.empty_cache()
@@ -1489,6 +1541,11 @@ def main():
             "kernel_ms_source": "HIP events at the two ends of the timed region on the launch stream / K "
                                 "(back-to-back launches)",
             "kernel_ms_isolated": round(t["kern_ms_isolated"], 5),
+            **({"read_bytes_per_launch": meta["rw"][0], "write_bytes_per_launch": meta["rw"][1],
+                "read_achieved": round(meta["rw"][0] / (kern_ms * 1e-3) / 1e9, 2),
+                "write_achieved": round(meta["rw"][1] / (kern_ms * 1e-3) / 1e9, 2),
+                "read_write_note": "SURVEY §8(d): read-only and read+write rates stated separately; `achieved` is "
+                                   "read + write"} if meta["rw"] else {}),
         },
         "post_checks": post,
     }

@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 cd /tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$C" -o run -- \
-      python3 "$ROOT/bench.py" --no-cpu-baseline "$@" > "$OUT/pmc_$C.log" 2>&1
+      python3 "$ROOT/bench.py" --no-cpu-baseline --no-post "$@" > "$OUT/pmc_$C.log" 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "rocprofv3 --pmc $C failed rc=$rc"; tail -20 "$OUT/pmc_$C.log"; exit $rc; fi
 done

@@ -15,14 +15,31 @@ import sys
 from pathlib import Path
 
 
-def per_dispatch(path_glob, kernel_sub):
-    vals = []
+def per_kernel(path_glob):
+    """Kernel name -> list of per-dispatch counter values."""
+    vals = {}
     for f in glob.glob(path_glob, recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if kernel_sub in row.get("Kernel_Name", ""):
-                    vals.append(float(row["Counter_Value"]))
+                vals.setdefault(row.get("Kernel_Name", ""), []).append(float(row["Counter_Value"]))
     return vals
+
+
+# the kernels one step of each workload launches (substrings of the kernel
+# names); their per-dispatch medians add up to the step's HBM bytes
+STEP_KERNELS = {
+    "config1": ["l4csum_coop_kernel"],
+    "config2": ["l4csum_kernel<"],
+    "config3": ["gso_plan_kernel", "gso_split_kernel", "gso_finalize_kernel"],
+    "config3udp": ["gso_plan_kernel", "gso_split_kernel", "gso_finalize_kernel"],
+    "config4": ["l4csum_split_kernel"],
+    "config4strong": ["l4csum_split_kernel"],
+    "config4small": ["l4csum_split_kernel"],
+    "config5": ["l4csum_split_kernel"],
+    "verify": ["verify_"],
+    "gro": ["gro_finalize"],
+    "aead": ["aead_kernel"],
+}
 
 
 def main():
@@ -31,28 +48,30 @@ def main():
     workload = "config2"
     if "--workload" in args:
         workload = args[args.index("--workload") + 1]
-    res = {"workload": workload, "bench_args": args}
-    for kern in ("l4csum_kernel", "l4csum_split_kernel", "l4csum_coop_kernel", "gso_split_kernel", "verify_kernel", "gro_finalize",
-                 "aead_kernel"):
-        f = per_dispatch(str(out / "pmc_FETCH_SIZE" / "**" / "*counter_collection.csv"), kern)
-        w = per_dispatch(str(out / "pmc_WRITE_SIZE" / "**" / "*counter_collection.csv"), kern)
-        if not f:
+    res = {"workload": workload, "bench_args": args, "kernels": {}}
+    f_all = per_kernel(str(out / "pmc_FETCH_SIZE" / "**" / "*counter_collection.csv"))
+    w_all = per_kernel(str(out / "pmc_WRITE_SIZE" / "**" / "*counter_collection.csv"))
+    subs = STEP_KERNELS.get(workload, ["l4csum_kernel<"])
+    rd = wr = 0.0
+    for name, f in sorted(f_all.items()):
+        if not any(x in name for x in subs):
             continue
         fk = statistics.median(f)
+        w = w_all.get(name, [])
         wk = statistics.median(w) if w else 0.0
-        res[kern] = {
+        res["kernels"][name] = {
             "dispatches": len(f),
             "FETCH_SIZE_KiB_median": fk,
             "WRITE_SIZE_KiB_median": wk,
             "read_bytes_corrected": 2 * fk * 1024,
             "write_bytes": wk * 1024,
-            "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024,
         }
-    main_k = {"config3": "gso_split_kernel", "config3udp": "gso_split_kernel", "verify": "verify_kernel",
-              "gro": "gro_finalize", "config1": "l4csum_coop_kernel", "config4": "l4csum_split_kernel",
-              "config5": "l4csum_split_kernel", "aead": "aead_kernel"}.get(workload, "l4csum_kernel")
-    if main_k in res:
-        res["hbm_bytes_per_launch"] = res[main_k]["hbm_bytes_per_launch"]
+        rd += 2 * fk * 1024
+        wr += wk * 1024
+    if res["kernels"]:
+        res["read_bytes_per_launch"] = rd
+        res["write_bytes_per_launch"] = wr
+        res["hbm_bytes_per_launch"] = rd + wr
     res["correction"] = "gfx950: read bytes = 2 x FETCH_SIZE KiB x 1024 (MI355X_MICROARCH.md §HBM); write = WRITE_SIZE KiB x 1024"
     if workload == "gro":
         res["calibration_note"] = ("gro_finalize stages its header chunks with 16 B/lane loads, consecutive lanes on "
