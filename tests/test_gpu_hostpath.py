@@ -87,13 +87,19 @@ def check_encap(cases, caps, key, rx, c0, msgs, res, gres, nxt):
     assert nxt == ctr and ctr - c0 > 300
 
 
-def test_encap_host_matches_oracle(gpu, small_chunks):
+@pytest.mark.parametrize("parts", [1, 3])
+def test_encap_host_matches_oracle(gpu, small_chunks, parts):
     wga = _wga()
     cases, caps, desc, inbuf = encap_case(21)
     assert inbuf.size > 4 << 20  # more 1-MiB chunks than device slots
     key = bytes(range(1, 33))
     c0 = (1 << 32) - 100  # counters cross 2^32 on the way
-    msgs, res, gres, nxt = wga.encap_host(inbuf, desc, key, 0xABCD, c0, MAX_SEG, MAX_SIZE, MSG_CAP)
+    saved = wga.tune_get("encap_parts")
+    wga.tune_set("encap_parts", parts)  # each chunk's device step pipelined in slices too
+    try:
+        msgs, res, gres, nxt = wga.encap_host(inbuf, desc, key, 0xABCD, c0, MAX_SEG, MAX_SIZE, MSG_CAP)
+    finally:
+        wga.tune_set("encap_parts", saved)
     check_encap(cases, caps, key, 0xABCD, c0, msgs, res, gres, nxt)
 
 

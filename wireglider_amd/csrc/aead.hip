@@ -1176,6 +1176,33 @@ extern "C" int wg_encap_encrypt(const uint8_t *dev_in, const uint8_t *dev_seg, c
 
 namespace wg {
 
+// Side stream + events for the pipelined encap step (knob encap_parts): one
+// set per host thread and device, created on first use and kept.
+struct EncapSide {
+    int device = -1;
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr;
+    hipEvent_t split_done[8] = {};
+};
+static thread_local EncapSide g_side;
+
+static int encap_side(EncapSide &e) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        return WG_ERR_NODEV;
+    if (e.device == dev)
+        return WG_OK;
+    e = EncapSide{};  // a new device: the old objects are left to the runtime (device switches are rare)
+    if (hipStreamCreateWithFlags(&e.side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&e.fork, hipEventDisableTiming) != hipSuccess)
+        return WG_ERR_RUNTIME;
+    for (hipEvent_t &ev : e.split_done)
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+            return WG_ERR_RUNTIME;
+    e.device = dev;
+    return WG_OK;
+}
+
 int encap_batch_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
                        wg_gso_result *dev_gso_res, const uint8_t key[32], uint32_t receiver_index, uint64_t counter0,
                        const uint64_t *dev_msg_offset, uint32_t msg_cap, uint32_t max_segments,
@@ -1186,12 +1213,51 @@ int encap_batch_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n,
         return WG_ERR_INVALID;
     if (!n)
         return WG_OK;
-    const int rc = gso_split_launch(dev_in, dev_desc, n, dev_out, dev_gso_res, true, st);
+    const uint32_t parts = tune().encap_parts;
+    if (parts <= 1 || n < 2ull * parts) {
+        const int rc = gso_split_launch(dev_in, dev_desc, n, dev_out, dev_gso_res, true, st);
+        if (rc != WG_OK)
+            return rc;
+        return encap_launch(dev_in, dev_out, dev_desc, dev_gso_res, n, key, receiver_index, counter0, dev_msg_offset,
+                            msg_cap, max_segments, max_segment_size, dev_msgs, dev_res, dev_work, dev_total, 2u,
+                            dev_base, st);
+    }
+    // Pipelined: the batch in `parts` slices of super-buffers; slice k's
+    // headers-only split runs on a side stream while slice k-1's scans and
+    // AEAD run on the caller's stream (the split waits on memory, the AEAD on
+    // VALU issue).  Counters chain on the device: slice k starts at
+    // counter0 + *base + the messages of slices < k (ctr[k], kept at the end
+    // of dev_work past every slice's scan area), the last slice writing
+    // *dev_total.
+    EncapSide &e = g_side;
+    int rc = encap_side(e);
     if (rc != WG_OK)
         return rc;
-    return encap_launch(dev_in, dev_out, dev_desc, dev_gso_res, n, key, receiver_index, counter0, dev_msg_offset,
-                        msg_cap, max_segments, max_segment_size, dev_msgs, dev_res, dev_work, dev_total, 2u, dev_base,
-                        st);
+    // dev_work is 4 * (n + 1024) bytes; a slice's scan uses [0, cnt + cnt / 1024 + 1) dwords
+    // and cnt <= n / 2 here, so the last 2 * (parts + 2) dwords are free (8-B aligned below)
+    const uintptr_t wend = reinterpret_cast<uintptr_t>(dev_work) + 4ull * (n + 1024);
+    uint64_t *ctr = reinterpret_cast<uint64_t *>((wend - 8ull * (parts + 2)) & ~(uintptr_t)7);
+    if (hipMemsetAsync(ctr, 0, sizeof(uint64_t), st) != hipSuccess)
+        return WG_ERR_RUNTIME;
+    if (dev_base && hipMemcpyAsync(ctr, dev_base, sizeof(uint64_t), hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return WG_ERR_RUNTIME;
+    if (hipEventRecord(e.fork, st) != hipSuccess || hipStreamWaitEvent(e.side, e.fork, 0) != hipSuccess)
+        return WG_ERR_RUNTIME;
+    for (uint32_t k = 0; k < parts; k++) {
+        const uint64_t i0 = n * k / parts, cnt = n * (k + 1) / parts - i0;
+        rc = gso_split_launch(dev_in, dev_desc + i0, cnt, dev_out, dev_gso_res + i0, true, e.side);
+        if (rc != WG_OK)
+            return rc;
+        if (hipEventRecord(e.split_done[k], e.side) != hipSuccess ||
+            hipStreamWaitEvent(st, e.split_done[k], 0) != hipSuccess)
+            return WG_ERR_RUNTIME;
+        rc = encap_launch(dev_in, dev_out, dev_desc + i0, dev_gso_res + i0, cnt, key, receiver_index, counter0,
+                          dev_msg_offset + i0, msg_cap, max_segments, max_segment_size, dev_msgs, dev_res + i0,
+                          dev_work, k + 1 == parts ? dev_total : ctr + k + 1, 2u, ctr + k, st);
+        if (rc != WG_OK)
+            return rc;
+    }
+    return WG_OK;
 }
 
 }  // namespace wg

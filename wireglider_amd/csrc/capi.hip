@@ -29,7 +29,7 @@ struct Knob {
 
 static const uint64_t kPpw[] = {1, 2, 4, 8}, kOcc[] = {0, 7, 8}, kVOcc[] = {0, 6, 8}, kDm[] = {0, 2},
                       kWaves[] = {1, 2, 4, 8}, kAbl[] = {0, 1, 32},
-                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {0, 1, 2, 3, 4}, kSplitW[] = {4, 8}, kGroIt[] = {1, 2, 4};
+                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {0, 1, 2, 3, 4}, kSplitW[] = {4, 8}, kGroIt[] = {1, 2, 4}, kParts[] = {1, 2, 3, 4, 8};
 #define WG_N(a) (sizeof(a) / sizeof(a[0]))
 static const Knob kKnobs[] = {
     {"l4_blocks", &Tune::l4_blocks, nullptr, 1, 1u << 20, nullptr, 0},
@@ -62,6 +62,7 @@ static const Knob kKnobs[] = {
     {"aead_k", nullptr, &Tune::aead_k, 0, 0, kAeadK, WG_N(kAeadK)},
     {"aead_pair", nullptr, &Tune::aead_pair, 0, 1, nullptr, 0},
     {"aead_flex", nullptr, &Tune::aead_flex, 0, 1, nullptr, 0},
+    {"encap_parts", nullptr, &Tune::encap_parts, 0, 0, kParts, WG_N(kParts)},
 };
 #undef WG_N
 
@@ -166,6 +167,7 @@ static Tune &tune_storage() {
         x.aead_k = 0;
         x.aead_pair = 1;
         x.aead_flex = 1;
+        x.encap_parts = 1;
         // environment overrides: WG_<KNOB> (upper case), same accepted values
         // as wg_tune_set; anything else is ignored
         for (const Knob &k : kKnobs) {
