@@ -10,6 +10,8 @@
 #                      command gives the line and the kernel stats, and the line's `traffic` is
 #                      the PMC file of this session
 #   n2                 bench.py --gpus 2 with gloo (two ranks on the one GPU)
+#   abuild:NAME:W1,W2  tools/ab_builds.sh: tools/exp/variant_NAME/libwireglider_amd.so (A) against the
+#                      tree's library (B), alternating processes, 3 rounds, on workloads W1, W2...
 # usage: tools/gpu_r03.sh TAG step [step...]
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -56,6 +58,12 @@ for step in "$@"; do
         || fail "evidence bench $W" "$OUT/bench_$W.err"
       cut -c1-300 "$OUT/bench_$W.json"
       find "$OUT/stats_$W" -name "*kernel_stats.csv" -exec head -6 {} \; ;;
+    abuild)
+      N=${rest%%:*}
+      W=${rest#*:}
+      timeout -k 10 900 bash tools/ab_builds.sh "$OUT/abuild_$N.jsonl" 3 "tools/exp/variant_$N/libwireglider_amd.so" \
+        "$ROOT/wireglider_amd/lib/libwireglider_amd.so" ${W//,/ } > "$OUT/abuild_$N.txt" 2>&1 || fail "abuild $N" "$OUT/abuild_$N.txt"
+      cat "$OUT/abuild_$N.txt" ;;
     n2)
       WG_DIST_BACKEND=gloo timeout -k 10 500 python3 -u bench.py --gpus 2 --steps 10 --no-cpu-baseline \
         > "$OUT/bench_n2.json" 2> "$OUT/bench_n2.err" || fail n2 "$OUT/bench_n2.err"

@@ -194,6 +194,59 @@ __device__ __forceinline__ L5 l5_mul(const L5 &a, const L5 &b) {
     return h;
 }
 
+// The Horner step x = (x + m + 2^128) * r mod p for one 16-B block, in
+// radix 2^32 (four 32-bit words + a small fifth): r is CLAMPED (RFC 8439
+// §2.5: r_j < 2^28, r_1..r_3 divisible by 4), so 2^128 r_j = 2^130 (r_j / 4)
+// == 5 r_j / 4 = s_j (mod p) folds the columns past 2^128 back exactly, each
+// column is four or five products below 2^60.4 (no 64-bit overflow), and the
+// product takes 16 + 3 multiplies instead of radix 2^26's 25 (the layout of
+// OpenSSL's 32-bit Poly1305).  h[4] stays <= 4 between steps.
+struct P32 {
+    uint32_t h[5];
+};
+
+__device__ __forceinline__ P32 p32_step(const P32 &x, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3,
+                                        const uint32_t r[4], const uint32_t sr[4]) {
+    uint64_t a = (uint64_t)x.h[0] + m0;
+    const uint32_t t0 = (uint32_t)a;
+    a = (a >> 32) + x.h[1] + m1;
+    const uint32_t t1 = (uint32_t)a;
+    a = (a >> 32) + x.h[2] + m2;
+    const uint32_t t2 = (uint32_t)a;
+    a = (a >> 32) + x.h[3] + m3;
+    const uint32_t t3 = (uint32_t)a;
+    const uint32_t t4 = x.h[4] + 1u + (uint32_t)(a >> 32);  // + 2^128: the block's pad bit
+    uint64_t d0 = (uint64_t)t0 * r[0] + (uint64_t)t1 * sr[3] + (uint64_t)t2 * sr[2] + (uint64_t)t3 * sr[1];
+    uint64_t d1 = (uint64_t)t0 * r[1] + (uint64_t)t1 * r[0] + (uint64_t)t2 * sr[3] + (uint64_t)t3 * sr[2] +
+                  (uint64_t)(t4 * sr[1]);
+    uint64_t d2 = (uint64_t)t0 * r[2] + (uint64_t)t1 * r[1] + (uint64_t)t2 * r[0] + (uint64_t)t3 * sr[3] +
+                  (uint64_t)(t4 * sr[2]);
+    uint64_t d3 = (uint64_t)t0 * r[3] + (uint64_t)t1 * r[2] + (uint64_t)t2 * r[1] + (uint64_t)t3 * r[0] +
+                  (uint64_t)(t4 * sr[3]);
+    uint32_t h4 = t4 * r[0];
+    d1 += d0 >> 32;
+    d2 += d1 >> 32;
+    d3 += d2 >> 32;
+    h4 += (uint32_t)(d3 >> 32);
+    const uint32_t c = (h4 >> 2) + (h4 & ~3u);  // 5 * (h4 >> 2): 2^130 == 5
+    P32 o;
+    uint64_t e = (uint64_t)(uint32_t)d0 + c;
+    o.h[0] = (uint32_t)e;
+    e = (e >> 32) + (uint32_t)d1;
+    o.h[1] = (uint32_t)e;
+    e = (e >> 32) + (uint32_t)d2;
+    o.h[2] = (uint32_t)e;
+    e = (e >> 32) + (uint32_t)d3;
+    o.h[3] = (uint32_t)e;
+    o.h[4] = (h4 & 3u) + (uint32_t)(e >> 32);
+    return o;
+}
+
+// radix 2^32 -> five 26-bit limbs (h[4] <= 4: limb 4 < 2^27)
+__device__ __forceinline__ L5 p32_to_l5(const P32 &x) {
+    return l5_from_words(x.h[0], x.h[1], x.h[2], x.h[3], x.h[4]);
+}
+
 // Shuffles within groups of G lanes (ds_bpermute).
 template <int G>
 __device__ __forceinline__ uint32_t grp_down(uint32_t v, uint32_t lane, uint32_t off) {
@@ -607,6 +660,7 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     rw[2] &= 0x0ffffffcu;
     rw[3] &= 0x0ffffffcu;
     const L5 r = l5_from_words(rw[0], rw[1], rw[2], rw[3], 0u);
+    const uint32_t srw[4] = {0u, rw[1] + (rw[1] >> 2), rw[2] + (rw[2] >> 2), rw[3] + (rw[3] >> 2)};  // 5 r_j / 4
 
     const uint32_t nblk = (pad + 63u) / 64u;  // payload blocks: counters 1 .. nblk
     const uint32_t npass = G == 64 ? (nblk + kPass) / kPass : 1u;  // (nblk + 1) counters
@@ -682,8 +736,8 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             F = l5_mul(F, Sall);
         }
 
-        // the lane's K blocks: keystream, XOR, store, Horner with r
-        L5 x = l5_zero();
+        // the lane's K blocks: keystream, XOR, store, Horner with r (radix 2^32)
+        P32 x{{0u, 0u, 0u, 0u, 0u}};
         auto block = [&](uint32_t c, uint32_t kb[16]) {
             const uint32_t d = c - 1u;  // payload block
             const bool has = act && c >= 1u && d < nblk;
@@ -719,10 +773,10 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             const uint32_t nqj = nct / 16u;
 #pragma unroll
             for (uint32_t q = 0; q < 4; q++) {
-                const L5 blk = l5_from_words(W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3], 1u);
-                const L5 t = l5_mul(l5_add(x, blk), r);
-                if (q < nqj)
-                    x = t;
+                const P32 t = p32_step(x, W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3], rw, srw);
+#pragma unroll
+                for (int k = 0; k < 5; k++)
+                    x.h[k] = q < nqj ? t.h[k] : x.h[k];
             }
         };
         uint32_t j0 = 0;
@@ -760,7 +814,7 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
         // common factor r (the length block after everything) is applied
         // once to the group's sum
         if (nq)
-            acc = l5_add(acc, l5_mul(x, EF));
+            acc = l5_add(acc, l5_mul(p32_to_l5(x), EF));
     }
     // the length block: le64(0) || le64(pad / payload length), times r
     const uint32_t mlen = kDec ? plen : pad;  // AEAD ct length (encrypt: the padded plaintext)
