@@ -205,40 +205,34 @@ struct P32 {
     uint32_t h[5];
 };
 
+__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
+
+// 32-bit carry chains (v_add_co / v_addc_co) and the column carries folded
+// into the next column's multiply-add chain as its addend: no 64-bit adds of
+// zero-extended words (each of those cost a register-pair move).
 __device__ __forceinline__ P32 p32_step(const P32 &x, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3,
                                         const uint32_t r[4], const uint32_t sr[4]) {
-    uint64_t a = (uint64_t)x.h[0] + m0;
-    const uint32_t t0 = (uint32_t)a;
-    a = (a >> 32) + x.h[1] + m1;
-    const uint32_t t1 = (uint32_t)a;
-    a = (a >> 32) + x.h[2] + m2;
-    const uint32_t t2 = (uint32_t)a;
-    a = (a >> 32) + x.h[3] + m3;
-    const uint32_t t3 = (uint32_t)a;
-    const uint32_t t4 = x.h[4] + 1u + (uint32_t)(a >> 32);  // + 2^128: the block's pad bit
-    uint64_t d0 = (uint64_t)t0 * r[0] + (uint64_t)t1 * sr[3] + (uint64_t)t2 * sr[2] + (uint64_t)t3 * sr[1];
-    uint64_t d1 = (uint64_t)t0 * r[1] + (uint64_t)t1 * r[0] + (uint64_t)t2 * sr[3] + (uint64_t)t3 * sr[2] +
-                  (uint64_t)(t4 * sr[1]);
-    uint64_t d2 = (uint64_t)t0 * r[2] + (uint64_t)t1 * r[1] + (uint64_t)t2 * r[0] + (uint64_t)t3 * sr[3] +
-                  (uint64_t)(t4 * sr[2]);
-    uint64_t d3 = (uint64_t)t0 * r[3] + (uint64_t)t1 * r[2] + (uint64_t)t2 * r[1] + (uint64_t)t3 * r[0] +
-                  (uint64_t)(t4 * sr[3]);
-    uint32_t h4 = t4 * r[0];
-    d1 += d0 >> 32;
-    d2 += d1 >> 32;
-    d3 += d2 >> 32;
-    h4 += (uint32_t)(d3 >> 32);
-    const uint32_t c = (h4 >> 2) + (h4 & ~3u);  // 5 * (h4 >> 2): 2^130 == 5
+    uint32_t c;
+    const uint32_t t0 = __builtin_addc(x.h[0], m0, 0u, &c);
+    const uint32_t t1 = __builtin_addc(x.h[1], m1, c, &c);
+    const uint32_t t2 = __builtin_addc(x.h[2], m2, c, &c);
+    const uint32_t t3 = __builtin_addc(x.h[3], m3, c, &c);
+    const uint32_t t4 = x.h[4] + 1u + c;  // + 2^128: the block's pad bit
+    const uint64_t d0 = mad64(t3, sr[1], mad64(t2, sr[2], mad64(t1, sr[3], (uint64_t)t0 * r[0])));
+    const uint64_t d1 =
+        mad64(t4, sr[1], mad64(t3, sr[2], mad64(t2, sr[3], mad64(t1, r[0], mad64(t0, r[1], d0 >> 32)))));
+    const uint64_t d2 =
+        mad64(t4, sr[2], mad64(t3, sr[3], mad64(t2, r[0], mad64(t1, r[1], mad64(t0, r[2], d1 >> 32)))));
+    const uint64_t d3 =
+        mad64(t4, sr[3], mad64(t3, r[0], mad64(t2, r[1], mad64(t1, r[2], mad64(t0, r[3], d2 >> 32)))));
+    const uint32_t h4 = t4 * r[0] + (uint32_t)(d3 >> 32);
+    const uint32_t cc = (h4 >> 2) + (h4 & ~3u);  // 5 * (h4 >> 2): 2^130 == 5
     P32 o;
-    uint64_t e = (uint64_t)(uint32_t)d0 + c;
-    o.h[0] = (uint32_t)e;
-    e = (e >> 32) + (uint32_t)d1;
-    o.h[1] = (uint32_t)e;
-    e = (e >> 32) + (uint32_t)d2;
-    o.h[2] = (uint32_t)e;
-    e = (e >> 32) + (uint32_t)d3;
-    o.h[3] = (uint32_t)e;
-    o.h[4] = (h4 & 3u) + (uint32_t)(e >> 32);
+    o.h[0] = __builtin_addc((uint32_t)d0, cc, 0u, &c);
+    o.h[1] = __builtin_addc((uint32_t)d1, 0u, c, &c);
+    o.h[2] = __builtin_addc((uint32_t)d2, 0u, c, &c);
+    o.h[3] = __builtin_addc((uint32_t)d3, 0u, c, &c);
+    o.h[4] = (h4 & 3u) + c;
     return o;
 }
 
@@ -364,18 +358,33 @@ __device__ __forceinline__ uint32_t keep_below(uint32_t w, uint32_t m, uint32_t 
 }
 
 // The 64 bytes at a (of which the first `n` belong to the packet, n may be
-// 0..64; the rest read as zero) as 16 dwords: the aligned 16-B chunks
-// covering them, clamped onto the last one holding a packet byte (so no load
-// leaves the packet's own aligned chunks), funnel-shifted.
+// 0..64; the rest read as zero) as 16 dwords.  The aligned 16-B chunks
+// covering them are loaded; chunks past the packet's last byte read the
+// zero chunk, and only the chunk holding that last byte has bytes to clear
+// (those at or past a + n: another packet's), masked there BEFORE the
+// funnel shift — one chunk's four masks instead of a byte mask on each of
+// the sixteen shifted dwords.  No load leaves the packet's own aligned chunks.
 __device__ __forceinline__ void load64(uintptr_t a, uint32_t n, uint32_t W[16]) {
     const uintptr_t a0 = a & ~(uintptr_t)15;
-    const uintptr_t alast = n ? (a + n - 1) & ~(uintptr_t)15 : a0;
     const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_aead_zero16);
-    const v4u c0 = ld16(n ? (a0 + 0u > alast ? alast : a0 + 0u) : zero);
-    const v4u c1 = ld16(n ? (a0 + 16u > alast ? alast : a0 + 16u) : zero);
-    const v4u c2 = ld16(n ? (a0 + 32u > alast ? alast : a0 + 32u) : zero);
-    const v4u c3 = ld16(n ? (a0 + 48u > alast ? alast : a0 + 48u) : zero);
-    const v4u c4 = ld16(n ? (a0 + 64u > alast ? alast : a0 + 64u) : zero);
+    const uint32_t e = (uint32_t)a % 16u + n;          // end of the packet's bytes, relative to a0 (<= 79)
+    const uint32_t cl = n ? (e - 1u) >> 4 : 5u;         // chunk holding the last byte (5: none)
+    const uint32_t eb = e - 16u * cl;                   // its bytes to keep: [0, eb), 1..16
+    uint32_t mk[4];
+#pragma unroll
+    for (uint32_t d = 0; d < 4; d++) {
+        const uint32_t k = eb > 4u * d ? (eb - 4u * d < 4u ? eb - 4u * d : 4u) : 0u;
+        mk[d] = k >= 4u ? ~0u : (1u << (8u * k)) - 1u;
+    }
+    v4u c[5];
+#pragma unroll
+    for (uint32_t k = 0; k < 5; k++) {
+        c[k] = ld16(k <= cl && cl < 5u ? a0 + 16u * k : zero);
+#pragma unroll
+        for (uint32_t d = 0; d < 4; d++)
+            c[k][d] = k == cl ? c[k][d] & mk[d] : c[k][d];
+    }
+    const v4u c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3], c4 = c[4];
     // dword m of the result funnels dwords m + q and m + q + 1 of the chunks,
     // q = (a / 4) mod 4 per lane: chosen by q's two bits over NAMED values
     // (selects between elements of an array became a scratch array indexed
@@ -401,22 +410,22 @@ __device__ __forceinline__ void load64(uintptr_t a, uint32_t n, uint32_t W[16]) 
     const uint32_t t16 = q1 ? c4[1] : c4[0];
     const uint32_t t17 = q1 ? c4[2] : c4[1];
     const uint32_t t18 = q1 ? c4[3] : c4[2];
-    W[0] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t3 : t1, q2 ? t2 : t0, sh), 0u, n);
-    W[1] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t4 : t2, q2 ? t3 : t1, sh), 1u, n);
-    W[2] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t5 : t3, q2 ? t4 : t2, sh), 2u, n);
-    W[3] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t6 : t4, q2 ? t5 : t3, sh), 3u, n);
-    W[4] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t7 : t5, q2 ? t6 : t4, sh), 4u, n);
-    W[5] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t8 : t6, q2 ? t7 : t5, sh), 5u, n);
-    W[6] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t9 : t7, q2 ? t8 : t6, sh), 6u, n);
-    W[7] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t10 : t8, q2 ? t9 : t7, sh), 7u, n);
-    W[8] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t11 : t9, q2 ? t10 : t8, sh), 8u, n);
-    W[9] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t12 : t10, q2 ? t11 : t9, sh), 9u, n);
-    W[10] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t13 : t11, q2 ? t12 : t10, sh), 10u, n);
-    W[11] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t14 : t12, q2 ? t13 : t11, sh), 11u, n);
-    W[12] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t15 : t13, q2 ? t14 : t12, sh), 12u, n);
-    W[13] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t16 : t14, q2 ? t15 : t13, sh), 13u, n);
-    W[14] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t17 : t15, q2 ? t16 : t14, sh), 14u, n);
-    W[15] = keep_below(__builtin_amdgcn_alignbyte(q2 ? t18 : t16, q2 ? t17 : t15, sh), 15u, n);
+    W[0] = __builtin_amdgcn_alignbyte(q2 ? t3 : t1, q2 ? t2 : t0, sh);
+    W[1] = __builtin_amdgcn_alignbyte(q2 ? t4 : t2, q2 ? t3 : t1, sh);
+    W[2] = __builtin_amdgcn_alignbyte(q2 ? t5 : t3, q2 ? t4 : t2, sh);
+    W[3] = __builtin_amdgcn_alignbyte(q2 ? t6 : t4, q2 ? t5 : t3, sh);
+    W[4] = __builtin_amdgcn_alignbyte(q2 ? t7 : t5, q2 ? t6 : t4, sh);
+    W[5] = __builtin_amdgcn_alignbyte(q2 ? t8 : t6, q2 ? t7 : t5, sh);
+    W[6] = __builtin_amdgcn_alignbyte(q2 ? t9 : t7, q2 ? t8 : t6, sh);
+    W[7] = __builtin_amdgcn_alignbyte(q2 ? t10 : t8, q2 ? t9 : t7, sh);
+    W[8] = __builtin_amdgcn_alignbyte(q2 ? t11 : t9, q2 ? t10 : t8, sh);
+    W[9] = __builtin_amdgcn_alignbyte(q2 ? t12 : t10, q2 ? t11 : t9, sh);
+    W[10] = __builtin_amdgcn_alignbyte(q2 ? t13 : t11, q2 ? t12 : t10, sh);
+    W[11] = __builtin_amdgcn_alignbyte(q2 ? t14 : t12, q2 ? t13 : t11, sh);
+    W[12] = __builtin_amdgcn_alignbyte(q2 ? t15 : t13, q2 ? t14 : t12, sh);
+    W[13] = __builtin_amdgcn_alignbyte(q2 ? t16 : t14, q2 ? t15 : t13, sh);
+    W[14] = __builtin_amdgcn_alignbyte(q2 ? t17 : t15, q2 ? t16 : t14, sh);
+    W[15] = __builtin_amdgcn_alignbyte(q2 ? t18 : t16, q2 ? t17 : t15, sh);
 }
 
 __device__ __forceinline__ void st16(uintptr_t addr, v4u v) {
@@ -749,14 +758,17 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             // payload; kGso == 2: blocks below hl from the segment slot
             const uintptr_t bsrc = kGso == 2 && boff < hl ? hsrc : src;
             load64(bsrc + boff, nin, W);
+            const uint32_t nqc = nct / 16u;  // whole 16-B Poly1305 chunks in the block (nct is a multiple of 16)
 #pragma unroll
             for (int m = 0; m < 16; m++) {
                 if constexpr (!kDec) {
                     // padding plaintext bytes are zero (proto.cpp:568-572):
                     // their ciphertext is the keystream itself
-                    W[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nct);  // ciphertext, what Poly1305 sees
+                    W[m] = (uint32_t)m / 4u < nqc ? W[m] ^ kb[m] : 0u;  // ciphertext, what Poly1305 sees
+                } else if constexpr (kVer) {
+                    kb[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nin);  // plaintext (the gates read it whole)
                 } else {
-                    kb[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nin);  // plaintext
+                    kb[m] = W[m] ^ kb[m];  // plaintext; store_n writes its first nin bytes only
                 }
             }
             if constexpr (kVer) {
