@@ -40,8 +40,8 @@ def encap_case(seed, n=300):
     wga = _wga()
     rng = np.random.default_rng(seed)
     cases = [random_case(rng) for _ in range(n)]
-    # a few config-3-shaped tun reads (64 KiB TCP super-buffers, 1,460-B segments)
-    for k in range(6):
+    # config-3-shaped tun reads (64 KiB TCP super-buffers, 1,460-B segments)
+    for k in range(60):
         p = pktbuild.build(False, True, rng.integers(0, 256, 65495, dtype=np.uint8).tobytes(),
                            pktbuild.ipv4_addr("10.0.0.1"), pktbuild.ipv4_addr("10.0.0.2"), seq=k * 7919,
                            fill_l4=False)
