@@ -146,6 +146,7 @@ VERIFY_VARIANTS = [{"verify_dm": 0, "verify_occ": 8, "verify_hdr": 1}, {"verify_
                    {"verify_dm": 2, "verify_occ": 6, "l4_iters": 4}, {"verify_dm": 2, "verify_occ": 0, "l4_iters": 3},
                    {"verify_small": 0}, {"verify_small": 1}, {"verify_small": 2}, {"verify_small": 3},
                    {"verify_small": 3, "verify_occ": 0}, {"verify_small": 4}, {"verify_small": 4, "verify_occ": 0},
+                   {"verify_small": 4, "verify_wblk": 16},
                    {"verify_small": 5}, {"verify_small": 5, "verify_occ": 0}]
 
 

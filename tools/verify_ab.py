@@ -10,7 +10,9 @@ Every packet carries a valid checksum.  Times are back-to-back launches
 between one event pair (as bench.py), median of rounds; every variant's
 verdicts and L4 results are compared with variant 0's.
 
-usage: verify_ab.py [variants, default 0,3,4,5] [--rounds R]
+usage: verify_ab.py [variant ...] [--rounds R]
+  a variant is key=value[,key=value...] of wg_tune_set keys (default: the
+  verify_small values 0, 3, 4, 5)
 """
 import json
 import statistics
@@ -64,10 +66,14 @@ def main():
     import wireglider_amd as wga
 
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    if "--rounds" in sys.argv:
+        args.remove(sys.argv[sys.argv.index("--rounds") + 1])
     rounds = int(sys.argv[sys.argv.index("--rounds") + 1]) if "--rounds" in sys.argv else 5
-    variants = [int(x) for x in (args[0].split(",") if args else ["0", "3", "4", "5"])]
+    specs = args or ["verify_small=0", "verify_small=3", "verify_small=4", "verify_small=5"]
+    variants = [tuple((kv.split("=")[0], int(kv.split("=")[1])) for kv in a.split(",")) for a in specs]
+    keys = sorted({k for v in variants for k, _ in v})
     dev = torch.device("cuda:0")
-    saved = wga.tune_get("verify_small")
+    saved = {k: wga.tune_get(k) for k in keys}
     out = {}
     for name in ("1500B", "64B", "c4mix", "alt"):
         buf, desc, n, alg = build(wga, torch, dev, name)
@@ -82,7 +88,10 @@ def main():
         bench.settle(torch, launch, 0.2)
         for _ in range(rounds):
             for v in variants:
-                wga.tune_set("verify_small", v)
+                for k in keys:
+                    wga.tune_set(k, saved[k])
+                for k, x in v:
+                    wga.tune_set(k, x)
                 for _ in range(3):
                     launch()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -99,14 +108,15 @@ def main():
                     passing = int(torch.count_nonzero((got[0] & 3) == 3).item())
                 exact[v] = exact.get(v, True) and bool(torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]))
         out[name] = {"packets": n, "alg_bytes": alg, "packets_passing": passing,
-                     "variants": {f"verify_small={v}": {
+                     "variants": {",".join(f"{k}={x}" for k, x in v): {
                          "ms_med": round(statistics.median(times[v]), 5), "ms_min": round(min(times[v]), 5),
                          "roofline_frac": round(alg / (statistics.median(times[v]) * 1e-3) / 8e12, 4),
                          "bit_exact_vs_first": exact[v]} for v in variants}}
         print(json.dumps({name: out[name]}), flush=True)
         del buf, desc, verdict, l4
         torch.cuda.empty_cache()
-    wga.tune_set("verify_small", saved)
+    for k in keys:
+        wga.tune_set(k, saved[k])
     print(json.dumps({"verify_ab": out}), flush=True)
 
 

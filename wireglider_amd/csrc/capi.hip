@@ -29,7 +29,7 @@ struct Knob {
 
 static const uint64_t kPpw[] = {1, 2, 4, 8}, kOcc[] = {0, 7, 8}, kVOcc[] = {0, 6, 8}, kDm[] = {0, 2},
                       kWaves[] = {1, 2, 4, 8}, kAbl[] = {0, 1, 32},
-                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {0, 1, 2, 3, 4}, kSplitW[] = {4, 8}, kGroIt[] = {1, 2, 4}, kParts[] = {1, 2, 3, 4, 8};
+                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {0, 1, 2, 3, 4}, kSplitW[] = {4, 8}, kGroIt[] = {1, 2, 4}, kParts[] = {1, 2, 3, 4, 8}, kWblk[] = {4, 16};
 #define WG_N(a) (sizeof(a) / sizeof(a[0]))
 static const Knob kKnobs[] = {
     {"l4_blocks", &Tune::l4_blocks, nullptr, 1, 1u << 20, nullptr, 0},
@@ -49,6 +49,7 @@ static const Knob kKnobs[] = {
     {"verify_occ", nullptr, &Tune::verify_occ, 0, 0, kVOcc, WG_N(kVOcc)},
     {"verify_hdr", nullptr, &Tune::verify_hdr, 0, 1, nullptr, 0},
     {"verify_small", nullptr, &Tune::verify_small, 0, 5, nullptr, 0},
+    {"verify_wblk", nullptr, &Tune::verify_wblk, 0, 0, kWblk, WG_N(kWblk)},
     {"gro_lds", nullptr, &Tune::gro_lds, 0, 2, nullptr, 0},
     {"gro_iters", nullptr, &Tune::gro_iters, 0, 0, kGroIt, WG_N(kGroIt)},
     {"gro_wide", nullptr, &Tune::gro_wide, 0, 1, nullptr, 0},
@@ -133,6 +134,7 @@ static Tune &tune_storage() {
         x.verify_dm = 0;
         x.verify_hdr = 1;
         x.verify_small = 0;
+        x.verify_wblk = 4;
         x.gro_lds = 1;
         x.gro_wide = 1;
         x.gro_chunks = 5;

@@ -1123,10 +1123,10 @@ __global__ __launch_bounds__(256) void verify_lane_kernel(VerifyParams p) {
     verify_lane_role(p, (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 256u + threadIdx.x);
 }
 
-template <int O = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_long_kernel(
+template <int O = 0, int BW = 4>  // BW: waves per block (4, or 16: fewer workgroups to dispatch)
+__global__ __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_long_kernel(
     VerifyParams p) {
-    const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
+    const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * (uint32_t)BW + wave_in_block();
     if (wave * 4u < p.n)
         verify_wave_role(p, wave * 4u, lane_id());
 }
@@ -1164,10 +1164,15 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
             return WG_ERR_INVALID;
         if (t.verify_small == 4) {
             hipLaunchKernelGGL(verify_lane_kernel, dim3((unsigned)nl), dim3(256), 0, st, p);
-            if (t.verify_occ == 8)
+            if (t.verify_wblk == 16) {
+                uint64_t nw16 = (n + 63) / 64;
+                if (nw16 >= 8) nw16 = (nw16 + 7) & ~7ull;
+                hipLaunchKernelGGL((verify_long_kernel<8, 16>), dim3((unsigned)nw16), dim3(1024), 0, st, p);
+            } else if (t.verify_occ == 8) {
                 hipLaunchKernelGGL(verify_long_kernel<8>, dim3((unsigned)nw), dim3(256), 0, st, p);
-            else
+            } else {
                 hipLaunchKernelGGL(verify_long_kernel<0>, dim3((unsigned)nw), dim3(256), 0, st, p);
+            }
         } else if (t.verify_occ == 8) {
             hipLaunchKernelGGL(verify_roles_kernel<8>, dim3((unsigned)(nl + nw)), dim3(256), 0, st, p, (uint32_t)nl);
         } else {
