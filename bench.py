@@ -73,7 +73,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="config2",
                     choices=["config1", "config2", "config3", "config3udp", "config4", "config4small", "config4strong",
-                             "config5",
+                             "config5", "verify64", "verify1500u",
                              "verify", "gro", "encap", "encap_2call", "aead", "encap_host", "decap_host"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-post", action="store_true",
@@ -508,6 +508,8 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                         "wg::gro_finalize_lds_kernel<true,5>", rank * n, sample=sample, counts=[n] * world,
                         metric="device-resident Mflows/s, GRO finalize (SURVEY f2)", unit="Mflows/s",
                         value_scale=1e-6, post=post)
+    if name in ("verify64", "verify1500u"):
+        return build_verify_uniform(wga, torch, rank, world, dev, 64 if name == "verify64" else 1504)
     if name == "config4small":
         return build_config4_small(wga, torch, rank, world, dev)
     if name == "config4strong":
@@ -712,6 +714,50 @@ def build_config4_small(wga, torch, rank: int, world: int, dev) -> Workload:
            "parallelism": f"shard{world}"}
     return Workload(launch, n, 64 * n, 82 * n, cfg, "weak", buf, "wg::l4csum_split_kernel<1,nt> (l4_small=5)", 0,
                     out, desc, sample, [n] * world)
+
+
+def build_verify_uniform(wga, torch, rank: int, world: int, dev, seg: int) -> Workload:
+    """SURVEY §8 f1 on the decap worker's own batch shape: the plaintexts of
+    one UDP GRO batch are a uniform PacketBatch (worker/decap.cpp:145-151,
+    worker/decap_ref.cpp:78-86), verified by wg_verify_uniform — 1,048,576
+    valid IPv4/IPv6 x TCP/UDP packets of `seg` bytes (64: TCP ACK-sized
+    batches, a lane per packet; 1504: full-size, a wave per packet)."""
+    import numpy as np
+
+    n, seed = 1 << 20, 0x5EED00F3 + seg
+    buf = torch.empty(n * seg, dtype=torch.uint8, device=dev)
+    wga.synth_fill(buf, seed, counter_base=rank * n * seg)
+    desc = wga.synth_desc_stride(n, seg, seg, 1, seed, rank * n, device=dev)  # mixed v4/v6 x TCP/UDP
+    wga.synth_headers(buf, desc, seed, rank * n)
+    wga.store_l4csum(buf, desc, wga.calc_l4_checksum_desc(buf, desc))
+    torch.cuda.synchronize()
+    verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+    l4 = torch.empty(n, dtype=torch.uint16, device=dev)
+
+    def launch():
+        wga.verify_uniform(buf, seg, verdict=verdict, l4=l4)
+
+    def post():
+        bad = int(((verdict & 3) != 3).sum().item()) + int(torch.count_nonzero(l4.to(torch.int32)).item())
+        # the same packets through the descriptor entry (its default kernel), bit-exact
+        v2, l2 = wga.verify_desc(buf, desc)
+        torch.cuda.synchronize()
+        return {"verify_failures": bad, "equal_to_wg_verify_desc": bool(torch.equal(v2, verdict) and torch.equal(l2, l4))}
+
+    def sample(npk):
+        d = desc[:npk].cpu().numpy()
+        v, l = wga.verify_uniform(buf[: npk * seg], seg)
+        torch.cuda.synchronize()
+        return buf[: npk * seg].cpu().numpy(), (v.cpu().numpy(), l.cpu().numpy()), ("verify", d)
+
+    kern = "wg::verify_uniform_lane_kernel (a lane per packet)" if seg <= 64 else "wg::verify_kernel<4,8,0,true,true>"
+    cfg = {"workload": f"verify{'64' if seg <= 64 else '1500u'} (SURVEY §8 f1): 1,048,576 x {seg} B mixed IPv4/IPv6 x "
+                       "TCP/UDP per GPU, checksums stored, a uniform PacketBatch (one GRO batch's plaintexts) through "
+                       "wg_verify_uniform", "packets_per_gpu": n, "segment_size": seg, "layout": "uniform",
+           "parallelism": f"shard{world}"}
+    return Workload(launch, n, n * seg, n * (seg + 3), cfg, "weak", buf, kern, rank * n, sample=sample,
+                    counts=[n] * world, post=post, probe_run=seg if seg <= 2048 else 0,
+                    metric="device-resident GiB/s, decap verify gates over a uniform packet batch (SURVEY f1)")
 
 
 def _pinned_copy(wga, t):

@@ -130,6 +130,16 @@ int wg_checksum_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_desc, uint6
 int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_desc, uint64_t n, uint8_t *dev_verdict,
                    uint16_t *dev_l4, void *stream);
 
+/* The same gates over a uniform PacketBatch (include/worker/offload.hpp:19-29):
+ * packet i = dev_base[i*segment_size, min((i+1)*segment_size, total_len)),
+ * no descriptors.  This is the decap worker's own shape: a UDP GRO batch has
+ * one segment size (worker/decap.cpp:145-151), and its plaintexts lie at
+ * stride segment_size - 32 with that (padded) length (worker/decap_ref.cpp:
+ * 78-86).  The kernel follows the segment size: <= 64 B (TCP ACK-sized
+ * batches) a lane per packet, longer a wave per packet. */
+int wg_verify_uniform(const uint8_t *dev_base, uint64_t total_len, uint32_t segment_size, uint8_t *dev_verdict,
+                      uint16_t *dev_l4, void *stream);
+
 /* ------------------------------------------------------------------------
  * GSO split (TSO/USO segmentation + per-segment checksum fixup), batched.
  * Per super-buffer this is worker_impl::do_tun_gso_split

@@ -306,3 +306,48 @@ def test_gpu_verify_interleaved(gpu, knobs):
     np.testing.assert_array_equal(verdict.cpu().numpy(), ev)
     np.testing.assert_array_equal(l4.cpu().numpy(), el4)
     assert (ev & OK == OK).mean() > 0.3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seg", [1, 7, 20, 28, 40, 48, 60, 63, 64, 65, 100, 1500, 1504, 9000])
+def test_gpu_verify_uniform(gpu, seg):
+    """wg_verify_uniform (a PacketBatch, no descriptors) equals the oracle on
+    the same segments: valid and corrupted packets of every family whose
+    length is the segment size, a short last segment, every alignment of
+    the batch start, both kernels (segment size <= 64: a lane per packet)."""
+    import torch
+
+    import wireglider_amd as wga
+
+    rng = np.random.default_rng(seg)
+    n = 3001
+    pkts = []
+    for _ in range(n):
+        v6, tcp = bool(rng.integers(0, 2)), bool(rng.integers(0, 2))
+        hl = (40 if v6 else 20) + (20 if tcp else 8)
+        al = 16 if v6 else 4
+        if seg >= hl:
+            p = bytearray(pktbuild.build(v6, tcp, rng.integers(0, 256, seg - hl, dtype=np.uint8).tobytes(),
+                                         rng.integers(0, 256, al, dtype=np.uint8).tobytes(),
+                                         rng.integers(0, 256, al, dtype=np.uint8).tobytes()))
+            if rng.integers(0, 5) == 0:
+                p[int(rng.integers(0, seg))] ^= 1 << int(rng.integers(0, 8))
+        else:
+            p = bytearray(rng.integers(0, 256, seg, dtype=np.uint8).tobytes())
+        pkts.append(bytes(p))
+    for lead in (0, 1, 3, 8):
+        total = n * seg - int(rng.integers(0, seg))  # a short last segment
+        buf = np.zeros(lead + n * seg + 16, np.uint8)
+        buf[lead:lead + n * seg] = np.frombuffer(b"".join(pkts), np.uint8)
+        dbuf = torch.from_numpy(buf).to(gpu)
+        verdict, l4 = wga.verify_uniform(dbuf[lead:lead + total], seg)
+        torch.cuda.synchronize()
+        m = (total + seg - 1) // seg
+        d = np.zeros(m, dtype=oracle.PKT_DESC)
+        d["offset"] = lead + np.arange(m, dtype=np.uint64) * seg
+        d["len"] = np.minimum(seg, total - np.arange(m) * seg)
+        ev, el4 = oracle.verify_desc(buf, d)
+        np.testing.assert_array_equal(verdict.cpu().numpy(), ev, err_msg=f"lead {lead}")
+        np.testing.assert_array_equal(l4.cpu().numpy(), el4, err_msg=f"lead {lead}")
+        if seg >= 60:
+            assert (ev & OK == OK).mean() > 0.5

@@ -37,6 +37,8 @@ STEP_KERNELS = {
     "config4small": ["l4csum_split_kernel"],
     "config5": ["l4csum_split_kernel"],
     "verify": ["verify_"],
+    "verify64": ["verify_"],
+    "verify1500u": ["verify_"],
     "gro": ["gro_finalize"],
     "aead": ["aead_kernel"],
 }

@@ -38,6 +38,7 @@ EXPORTED_SYMBOLS = (
     "wg_l4csum_desc",
     "wg_checksum_desc",
     "wg_verify_desc",
+    "wg_verify_uniform",
     "wg_gso_split",
     "wg_gro_finalize",
     "wg_aead_encrypt_batch",
@@ -115,6 +116,7 @@ def _load() -> ctypes.CDLL:
         "wg_l4csum_desc": (i32, [u8p, vp, u64, vp, vp]),
         "wg_checksum_desc": (i32, [u8p, vp, u64, vp, vp]),
         "wg_verify_desc": (i32, [u8p, vp, u64, vp, vp, vp]),
+        "wg_verify_uniform": (i32, [u8p, u64, u32, vp, vp, vp]),
         "wg_gso_split": (i32, [u8p, vp, u64, u8p, vp, vp]),
 
         "wg_gro_finalize": (i32, [u8p, vp, u64, vp]),
@@ -285,6 +287,27 @@ def verify_desc(base, desc, with_l4: bool = True, stream=None, verdict=None, l4=
         rc = lib.wg_verify_desc(base.data_ptr(), desc.data_ptr(), n, verdict.data_ptr(),
                                 l4.data_ptr() if l4 is not None else None, _stream_ptr(stream, base))
     _check(rc, "wg_verify_desc")
+    return verdict, l4
+
+
+def verify_uniform(batch, segment_size: int, with_l4: bool = True, stream=None, verdict=None, l4=None):
+    """Decap verify gates over a uniform PacketBatch (segment i =
+    batch[i*S : min((i+1)*S, len)]), e.g. the plaintexts of one UDP GRO batch.
+    Returns (verdict uint8 tensor, L4 result uint16 tensor or None)."""
+    torch = _torch()
+    _require_cuda(batch, "batch")
+    n = nr_segments(batch.numel(), segment_size)
+    if verdict is None:
+        verdict = torch.empty(max(n, 1), dtype=torch.uint8, device=batch.device)[:n]
+    if l4 is None and with_l4:
+        l4 = torch.empty(max(n, 1), dtype=torch.uint16, device=batch.device)[:n]
+    _check_out(verdict, n, torch.uint8, batch, "verdict")
+    if l4 is not None:
+        _check_out(l4, n, torch.uint16, batch, "l4")
+    with _on(batch):
+        rc = lib.wg_verify_uniform(batch.data_ptr(), batch.numel(), segment_size, verdict.data_ptr(),
+                                   l4.data_ptr() if l4 is not None else None, _stream_ptr(stream, batch))
+    _check(rc, "wg_verify_uniform")
     return verdict, l4
 
 

@@ -711,10 +711,12 @@ static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
 // ---------------------------------------------------------------------------
 struct VerifyParams {
     const uint8_t *base;
-    const wg_pkt_desc *desc;
+    const wg_pkt_desc *desc;  // null: a uniform PacketBatch (seg, total_len)
     uint8_t *verdict;
     uint16_t *l4;
     uint64_t n;
+    uint64_t total_len = 0;
+    uint32_t seg = 0;
 };
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t j) {
@@ -830,7 +832,8 @@ __device__ __forceinline__ void verify_group(const uint8_t *base, const uint64_t
 // H: header bytes 0-31 ride in the L4 byte gather's idle lanes (issue<.., kHdr>)
 // and the summed region starts at byte 32 — no separate header load; else a
 // byte load of header bytes 0-39 per packet and the region from byte 40.
-template <int P, int O = 0, int DM = 0, bool H = false>  // O: waves/SIMD target (0 = compiler's choice); DM: descriptor mode 0 / 2
+// kUni: a uniform PacketBatch instead of descriptors (wg_verify_uniform).
+template <int P, int O = 0, int DM = 0, bool H = false, bool kUni = false>  // O: waves/SIMD target (0 = compiler's choice); DM: descriptor mode 0 / 2
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_kernel(
     VerifyParams p) {
     const uint32_t lane = lane_id();
@@ -851,6 +854,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
             doff[j] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)nextd.x, j) |
                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)nextd.y, j) << 32);
             len[j] = i0 + j < p.n ? (uint32_t)__builtin_amdgcn_readlane((int)nextd.z, j) : 0u;
+        }
+    } else if (kUni) {
+        // PacketBatch segment i0 + j (include/util/packets.hpp:23-36)
+#pragma unroll
+        for (int j = 0; j < P; j++) {
+            const uint64_t o = (i0 + j) * (uint64_t)p.seg;
+            doff[j] = i0 + j < p.n ? o : 0u;
+            len[j] = i0 + j < p.n ? (p.total_len - o < p.seg ? (uint32_t)(p.total_len - o) : p.seg) : 0u;
         }
     } else {
 #pragma unroll
@@ -1123,6 +1134,22 @@ __global__ __launch_bounds__(256) void verify_lane_kernel(VerifyParams p) {
     verify_lane_role(p, (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 256u + threadIdx.x);
 }
 
+// wg_verify_uniform with segment_size <= kSmallMax: every segment is small,
+// so a lane per segment decodes it (no descriptors, no wave role).
+__global__ __launch_bounds__(256) void verify_uniform_lane_kernel(VerifyParams p) {
+    const uint64_t i = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 256u + threadIdx.x;
+    const bool live = i < p.n;
+    const uint64_t o = live ? i * (uint64_t)p.seg : 0u;
+    const uint32_t len = live ? (p.total_len - o < p.seg ? (uint32_t)(p.total_len - o) : p.seg) : 0u;
+    uint32_t rv = 0, rc = 0;
+    verify_lane(reinterpret_cast<uintptr_t>(p.base) + o, len, live, rv, rc);
+    if (live) {
+        p.verdict[i] = (uint8_t)rv;
+        if (p.l4)
+            p.l4[i] = (uint16_t)rc;
+    }
+}
+
 template <int O = 0, int BW = 4>  // BW: waves per block (4, or 16: fewer workgroups to dispatch)
 __global__ __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_long_kernel(
     VerifyParams p) {
@@ -1231,6 +1258,31 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
         hipLaunchKernelGGL((verify_kernel<4, 8, 0>), grid, dim3(256), 0, st, p);
     else
         hipLaunchKernelGGL((verify_kernel<4, 0, 0>), grid, dim3(256), 0, st, p);
+    return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+}
+
+extern "C" int wg_verify_uniform(const uint8_t *dev_base, uint64_t total_len, uint32_t segment_size,
+                                 uint8_t *dev_verdict, uint16_t *dev_l4, void *stream) {
+    if (!segment_size || (total_len && (!dev_base || !dev_verdict)))
+        return WG_ERR_INVALID;
+    if (!total_len)
+        return WG_OK;
+    VerifyParams p{dev_base, nullptr, dev_verdict, dev_l4, (total_len + segment_size - 1) / segment_size, total_len,
+                   segment_size};
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (segment_size <= kSmallMax) {  // every segment small: a lane each (knob-free: no long packets to serve)
+        uint64_t b = (p.n + 255) / 256;
+        if (b >= 8) b = (b + 7) & ~7ull;
+        if (b > 0x7fffffffull)
+            return WG_ERR_INVALID;
+        hipLaunchKernelGGL(verify_uniform_lane_kernel, dim3((unsigned)b), dim3(256), 0, st, p);
+    } else {
+        uint64_t blocks = (p.n + 15) / 16;  // one-shot 4-packet waves, as wg_verify_desc's default
+        if (blocks >= 8) blocks = (blocks + 7) & ~7ull;
+        if (blocks > 0x7fffffffull)
+            return WG_ERR_INVALID;
+        hipLaunchKernelGGL((verify_kernel<4, 8, 0, true, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+    }
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }
 
