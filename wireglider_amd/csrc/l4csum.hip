@@ -717,6 +717,7 @@ struct VerifyParams {
     uint64_t n;
     uint64_t total_len = 0;
     uint32_t seg = 0;
+    uint32_t last_len = 0;  // uniform: length of segment n - 1 (the only one that may be short)
 };
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t j) {
@@ -856,12 +857,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
             len[j] = i0 + j < p.n ? (uint32_t)__builtin_amdgcn_readlane((int)nextd.z, j) : 0u;
         }
     } else if (kUni) {
-        // PacketBatch segment i0 + j (include/util/packets.hpp:23-36)
+        // PacketBatch segment i0 + j (include/util/packets.hpp:23-36): one
+        // 64-bit multiply and compare per wave (a 64-bit scalar compare has
+        // no SALU form on gfx9, and this kernel's scalar unit is busy)
+        const uint64_t o0 = i0 * (uint64_t)p.seg;
+        const bool full = i0 + P < p.n;  // every segment of the group whole
 #pragma unroll
         for (int j = 0; j < P; j++) {
-            const uint64_t o = (i0 + j) * (uint64_t)p.seg;
-            doff[j] = i0 + j < p.n ? o : 0u;
-            len[j] = i0 + j < p.n ? (p.total_len - o < p.seg ? (uint32_t)(p.total_len - o) : p.seg) : 0u;
+            doff[j] = o0 + (uint32_t)j * p.seg;
+            len[j] = full ? p.seg : (i0 + j + 1 < p.n ? p.seg : (i0 + j + 1 == p.n ? p.last_len : 0u));
         }
     } else {
 #pragma unroll
@@ -1267,8 +1271,9 @@ extern "C" int wg_verify_uniform(const uint8_t *dev_base, uint64_t total_len, ui
         return WG_ERR_INVALID;
     if (!total_len)
         return WG_OK;
-    VerifyParams p{dev_base, nullptr, dev_verdict, dev_l4, (total_len + segment_size - 1) / segment_size, total_len,
-                   segment_size};
+    const uint64_t nseg = (total_len + segment_size - 1) / segment_size;
+    VerifyParams p{dev_base, nullptr, dev_verdict, dev_l4, nseg, total_len, segment_size,
+                   (uint32_t)(total_len - (nseg - 1) * segment_size)};
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (segment_size <= kSmallMax) {  // every segment small: a lane each (knob-free: no long packets to serve)
         uint64_t b = (p.n + 255) / 256;
