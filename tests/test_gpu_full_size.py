@@ -23,6 +23,10 @@ ROOT = Path(__file__).resolve().parents[1]
 # bench.py's config 5 (16,777,216 x 1500 B, seed 0x5EED0005) results hash,
 # the same at every world size (profiles/r02_n2_gloo_rehearsal.json)
 CONFIG5_HASH = 544385951604289
+# bench.py's config 4 batch (4,194,304 packets, 64 / 9000 B, seed 0x5EED0004)
+# results hash: the config 4 strong companion's at every world size
+# (profiles/r03_n2_gloo_rehearsal.json)
+CONFIG4_HASH = 288304973264214192
 
 
 def _wga():
@@ -92,6 +96,9 @@ def test_config4_full_size(gpu):
     wga.synth_headers(buf, dd, seed, 0)
     out = wga.calc_l4_checksum_desc(buf, dd)
     torch.cuda.synchronize()
+    from wireglider_amd import dist as wdist
+
+    assert wdist.result_hash(out, 0) == CONFIG4_HASH
     _compare_in_slices(buf, d, out, step=1 << 20)
     wga.store_l4csum(buf, dd, out)
     ver = wga.calc_l4_checksum_desc(buf, dd)
@@ -104,8 +111,9 @@ def test_config4_full_size(gpu):
 def test_bench_two_ranks_on_one_gpu(gpu, tmp_path):
     """`bench.py --gpus 2` starts two ranks itself (torch.distributed.run on
     127.0.0.1), they find a 2-rank group, shard config 2 (weak) and config 5
-    (strong), and rank 0 prints one line whose whole-job numbers and result
-    hash are the 8-GPU run's logic at N = 2 (gloo: both ranks share this GPU)."""
+    (strong) and config 4's bimodal batch split by bytes (strong), and rank 0
+    prints one line whose whole-job numbers and result hashes are the 8-GPU
+    run's logic at N = 2 (gloo: both ranks share this GPU)."""
     env = dict(os.environ)
     env["WG_DIST_BACKEND"] = "gloo"
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -120,3 +128,9 @@ def test_bench_two_ranks_on_one_gpu(gpu, tmp_path):
     assert line["post_checks"]["gathered_results"] == 2 * (1 << 20)
     assert line["strong_scaling"]["result_hash"] == CONFIG5_HASH
     assert line["strong_scaling"]["packets_per_rank"] == [1 << 23, 1 << 23]
+    # config 4's one bimodal batch split by bytes: the N = 1 hash, byte totals
+    # within one 9000-B packet
+    s4 = line["strong_scaling_config4"]
+    assert s4["result_hash"] == CONFIG4_HASH
+    assert sum(s4["packets_per_rank"]) == 1 << 22
+    assert max(s4["bytes_per_rank"]) - min(s4["bytes_per_rank"]) <= 9000

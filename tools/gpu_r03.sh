@@ -6,9 +6,9 @@
 #   ab:W:V1:V2...      tools/ab.py W V1 V2 ...  (knob variants, e.g. ab:gro:gro_lds=1:gro_lds=2)
 #   bench:W[:args]     python bench.py --workload W [args, comma-separated]
 #   evidence:W[:args]  PMC passes of bench W (FETCH_SIZE, WRITE_SIZE) -> profiles/pmc_W.json on the
-#                      box, THEN the bench line of W under rocprofv3 --kernel-trace --stats: one
-#                      command gives the line and the kernel stats, and the line's `traffic` is
-#                      the PMC file of this session
+#                      box, THEN the bench line of W (its `traffic` is that PMC file), THEN the same
+#                      bench under rocprofv3 --kernel-trace --stats (its per-dispatch average against
+#                      the line's kernel_ms_isolated) — all on one box
 #   n2                 bench.py --gpus 2 with gloo (two ranks on the one GPU)
 #   abuild:NAME:W1,W2  tools/ab_builds.sh: tools/exp/variant_NAME/libwireglider_amd.so (A) against the
 #                      tree's library (B), alternating processes, 3 rounds, on workloads W1, W2...
@@ -53,11 +53,13 @@ for step in "$@"; do
       bash tools/pmc_profile.sh "$OUT/pmc_$W" --workload "$W" --steps 10 --settle-seconds 0.1 --no-strong \
         > "$OUT/pmc_$W.log" 2>&1 || fail "pmc $W" "$OUT/pmc_$W.log"
       cp "$OUT/pmc_$W/pmc_$W.json" "$ROOT/profiles/pmc_$W.json"
-      (cd /tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/stats_$W" -o run --output-format csv -- \
-        python3 -u "$ROOT/bench.py" --workload "$W" ${A//,/ } > "$OUT/bench_$W.json" 2> "$OUT/bench_$W.err") \
+      timeout -k 10 500 python3 -u bench.py --workload "$W" ${A//,/ } > "$OUT/bench_$W.json" 2> "$OUT/bench_$W.err" \
         || fail "evidence bench $W" "$OUT/bench_$W.err"
       cut -c1-300 "$OUT/bench_$W.json"
-      find "$OUT/stats_$W" -name "*kernel_stats.csv" -exec head -6 {} \; ;;
+      (cd /tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/stats_$W" -o run --output-format csv -- \
+        python3 -u "$ROOT/bench.py" --workload "$W" --no-cpu-baseline --no-post --no-strong > "$OUT/stats_bench_$W.json" \
+        2> "$OUT/stats_bench_$W.err") || fail "evidence stats $W" "$OUT/stats_bench_$W.err"
+      find "$OUT/stats_$W" -name "*kernel_stats.csv" -exec head -4 {} \; ;;
     abuild)
       N=${rest%%:*}
       W=${rest#*:}
