@@ -151,9 +151,9 @@ def _oracle_batch(hdrs, desc):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("lds,wide,chunks,iters", [(1, 1, 5, 1), (1, 1, 4, 1), (1, 0, 5, 1), (0, 0, 5, 1),
-                                                   (2, 1, 5, 1), (2, 1, 5, 2), (2, 1, 5, 4), (3, 1, 5, 1)],
+                                                   (2, 1, 5, 1), (2, 1, 5, 2), (2, 1, 5, 4)],
                          ids=["lds-wide", "lds-wide-4chunks", "lds-narrow", "thread-loads", "wave", "wave-iters2",
-                              "wave-iters4", "coop-stores"])
+                              "wave-iters4"])
 def test_gpu_gro_finalize_parity(gpu, lds, wide, chunks, iters):
     import torch
 
@@ -191,7 +191,7 @@ def test_gpu_gro_finalize_empty(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lds", [1, 2, 3], ids=["lds", "wave", "coop-stores"])
+@pytest.mark.parametrize("lds", [1, 2], ids=["lds", "wave"])
 def test_gpu_gro_finalize_high_addresses(gpu, lds):
     """The same ragged batch placed so its flows straddle bit 31 and 4 GiB of
     a 4.3 GB header buffer (64-bit header offsets, staged-chunk addresses)."""

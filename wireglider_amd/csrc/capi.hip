@@ -50,7 +50,7 @@ static const Knob kKnobs[] = {
     {"verify_hdr", nullptr, &Tune::verify_hdr, 0, 1, nullptr, 0},
     {"verify_small", nullptr, &Tune::verify_small, 0, 5, nullptr, 0},
     {"verify_wblk", nullptr, &Tune::verify_wblk, 0, 0, kWblk, WG_N(kWblk)},
-    {"gro_lds", nullptr, &Tune::gro_lds, 0, 3, nullptr, 0},
+    {"gro_lds", nullptr, &Tune::gro_lds, 0, 2, nullptr, 0},
     {"gro_iters", nullptr, &Tune::gro_iters, 0, 0, kGroIt, WG_N(kGroIt)},
     {"gro_wide", nullptr, &Tune::gro_wide, 0, 1, nullptr, 0},
     {"gro_chunks", nullptr, &Tune::gro_chunks, 4, 5, nullptr, 0},

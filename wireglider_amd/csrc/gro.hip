@@ -291,184 +291,6 @@ __global__ __launch_bounds__(kGroBlock) void gro_finalize_lds_kernel(uint8_t *hd
         reinterpret_cast<int8_t *>(desc)[i * sizeof(wg_gro_desc) + offsetof(wg_gro_desc, status)] = st;
 }
 
-// Header-relative dwords R[0..15] of the staged chunks W[0..19] (see gro_fields).
-__device__ __forceinline__ void gro_rel(uintptr_t h, const v4u *k, uint32_t R[16]) {
-    const uint32_t W[20] = {k[0][0], k[0][1], k[0][2], k[0][3], k[1][0], k[1][1], k[1][2], k[1][3], k[2][0], k[2][1],
-                            k[2][2], k[2][3], k[3][0], k[3][1], k[3][2], k[3][3], k[4][0], k[4][1], k[4][2], k[4][3]};
-    const uint32_t s = (uint32_t)(h & 15u);
-    const uint32_t q = s >> 2, sh = s & 3u;
-#pragma unroll
-    for (int m = 0; m < 16; m++) {
-        const uint32_t lo = q == 0 ? W[m] : q == 1 ? W[m + 1] : q == 2 ? W[m + 2] : W[m + 3];
-        const uint32_t hi = q == 0 ? W[m + 1] : q == 1 ? W[m + 2] : q == 2 ? W[m + 3] : W[m + 4];
-        R[m] = __builtin_amdgcn_alignbyte(hi, lo, sh);
-    }
-}
-
-// Write the 16-bit value v (byte 0 = v & 0xff) at header byte q into the
-// header-relative dwords R: a static walk over R (a run-time index would put
-// R in scratch); a field at q % 4 == 3 straddles two dwords.
-__device__ __forceinline__ void put16(uint32_t R[16], uint32_t q, uint32_t v) {
-    const uint32_t m0 = q >> 2, b = q & 3u;
-#pragma unroll
-    for (uint32_t m = 0; m < 16; m++) {
-        const uint32_t mask = m == m0 ? (0xffffu << (8u * b)) : (b == 3u && m == m0 + 1u ? 0xffu : 0u);
-        const uint32_t val = m == m0 ? (v << (8u * b)) : (v >> 8);
-        R[m] = (R[m] & ~mask) | (val & mask);
-    }
-}
-
-// Coalesced-store variant (knob gro_lds = 3).  The LDS kernel's stores are
-// thread per flow at a 64-B lane stride — 64 cache lines per wave store
-// instruction, the address-processing bound the store-granularity probe
-// shows (profiles/r02_store_granularity.json: ~50 us for 4 M 32-B sector
-// writes).  Here each flow's header [0, hdr_len) (<= 64 B) is rebuilt in
-// LDS with its fields patched in (unchanged bytes keep their values), and
-// the block writes the headers back cooperatively: store slot k = 16-B
-// chunk k % 4 of flow k / 4, so a wave store instruction covers 16 whole
-// headers of consecutive flows.  The same 32-B sectors are written as by
-// the wide stores (a header's fields and its bytes share them), in far fewer
-// address-processing steps.  Headers longer than 64 B keep the per-thread path.
-__global__ __launch_bounds__(kGroBlock) void gro_finalize_coop_kernel(uint8_t *hdrs, wg_gro_desc *desc, uint64_t n) {
-    constexpr uint32_t K = 5;
-    __shared__ v4u s_chunk[kGroBlock * K];  // staged chunks, then (after a barrier) the patched headers, 4 per flow
-    __shared__ uint64_t s_a0[kGroBlock];
-    __shared__ uint32_t s_last[kGroBlock];  // last chunk to load, or 0xff: nothing to stage
-    __shared__ uint64_t s_h[kGroBlock];     // header address for the cooperative store
-    __shared__ uint32_t s_H[kGroBlock];     // its bytes to store (0: this flow stores nothing cooperatively)
-    const uint32_t t = threadIdx.x;
-    const uint64_t i = (uint64_t)blockIdx.x * kGroBlock + t;
-    wg_gro_desc d{};
-    bool live = i < n, fast = false, v6 = false, tcp = false;
-    int8_t st = 0;
-    uint32_t need = 0, cs = 0, l4off = 0;
-    uint8_t *h = hdrs;
-    if (live) {
-        d = desc[i];
-        h = hdrs + d.hdr_offset;
-        const uint32_t H = d.hdr_len;
-        cs = d.csum_start;
-        l4off = cs + d.csum_offset;
-        v6 = d.flags & WG_PKT_V6;
-        tcp = d.flags & WG_PKT_TCP;
-        const uint32_t iph = v6 ? 40u : 20u;
-        if (cs < iph || cs > H || l4off < cs || l4off + 2 > H || (!tcp && cs + 8 > H))
-            st = -3;
-        else {
-            need = v6 ? 40u : cs;
-            fast = need <= kFastNeed;
-        }
-    }
-    // the cooperative store covers [0, hdr_len): stage that much
-    const bool coop = fast && d.hdr_len <= 64u;
-    const uint32_t stage = coop ? d.hdr_len : need;
-    const uintptr_t hp = reinterpret_cast<uintptr_t>(h);
-    s_a0[t] = hp & ~(uintptr_t)15;
-    s_last[t] = fast ? (uint32_t)(((hp & 15u) + stage - 1) >> 4) : 0xffu;
-    __syncthreads();
-    uint32_t lst[K];
-    uint64_t a0[K];
-#pragma unroll
-    for (uint32_t k = 0; k < K; k++) {
-        const uint32_t f = flow_of_slot<K>(t + kGroBlock * k);
-        lst[k] = s_last[f];
-        a0[k] = s_a0[f];
-    }
-    v4u v[K];
-#pragma unroll
-    for (uint32_t k = 0; k < K; k++) {
-        const uint32_t slot = t + kGroBlock * k;
-        const uint32_t c = slot - K * flow_of_slot<K>(slot);
-        const uint32_t last = lst[k];
-        const uintptr_t a = last != 0xffu ? a0[k] + 16u * (c < last ? c : last)
-                                          : reinterpret_cast<uintptr_t>(&g_gro_zero);
-        v[k] = ld16(a);
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < K; k++)
-        s_chunk[t + kGroBlock * k] = v[k];
-    __syncthreads();
-    uint32_t R[16];
-    gro_rel(hp, &s_chunk[t * K], R);
-    if (live && st == 0) {
-        const uint64_t l4len = (uint64_t)(d.hdr_len - cs) + d.payload_bytes;  // :84
-        const uint32_t l16 = (uint32_t)l4len & 0xffffu;
-        if (!fast) {
-            if (!tcp)
-                st_be16(h + cs + 4, l16);  // udp->len (uint16), :85-86
-            gro_slow(h, d.hdr_len, cs, l4off, d.payload_bytes, v6, l4len);
-        } else {
-            // the fields (as gro_fields), patched into R
-            uint32_t sad, proto;
-            if (!v6) {
-                const uint32_t T = (uint32_t)((uint64_t)d.hdr_len + d.payload_bytes) & 0xffffu;
-                uint32_t sip = (R[0] & 0xffffu) + sum16x2(R[1]) + (R[2] & 0xffffu);  // skip ip_len, ip_sum
-#pragma unroll
-                for (int m = 3; m < 16; m++)
-                    sip += sum16x2(keep_below(R[m], m, cs));
-                const uint32_t c = ~fold16_32(sip + bswap16(T)) & 0xffffu;  // :103-106
-                sad = sum16x2(R[3]) + sum16x2(R[4]);
-                proto = (R[2] >> 8) & 0xffu;
-                R[0] = (R[0] & 0xffffu) | (bswap16(T) << 16);
-                R[2] = (R[2] & 0xffffu) | (c << 16);
-            } else {
-                sad = 0;
-#pragma unroll
-                for (int m = 2; m < 10; m++)
-                    sad += sum16x2(R[m]);
-                proto = (R[1] >> 16) & 0xffu;
-                R[1] = (R[1] & 0xffff0000u) | bswap16(l16);  // :95
-            }
-            const uint32_t seed = ~fold16_32(sad + (proto << 8) + bswap16(l16)) & 0xffffu;  // :108-112
-            if (!tcp)
-                put16(R, cs + 4, bswap16(l16));  // udp->len, :85-86
-            put16(R, l4off, seed);             // native order, :114
-            if (!coop) {  // header past 64 B: the fields by the thread itself
-                if (!v6) {
-                    st128_u(h, v4u{R[0], R[1], R[2], R[3]});
-                } else {
-                    st32_u(h + 4, R[1]);
-                }
-                if (!tcp)
-                    st_be16(h + cs + 4, l16);
-                st16_ne(h + l4off, seed);
-            }
-        }
-    }
-    __syncthreads();  // every thread's chunks read: the staging area takes the headers
-    const bool mine = live && st == 0 && coop;
-    if (mine) {
-#pragma unroll
-        for (uint32_t c = 0; c < 4; c++)
-            s_chunk[4 * t + c] = v4u{R[4 * c], R[4 * c + 1], R[4 * c + 2], R[4 * c + 3]};
-    }
-    s_h[t] = hp;
-    s_H[t] = mine ? d.hdr_len : 0u;
-    __syncthreads();
-    // store slot j = t + 256 k: chunk j % 4 of flow j / 4 (16 whole headers per wave store)
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-        const uint32_t j = t + kGroBlock * k;
-        const uint32_t f = j >> 2, c = j & 3u;
-        const uint32_t H = s_H[f];
-        const uint32_t b0 = 16u * c;
-        if (b0 < H) {
-            const v4u x = s_chunk[j];
-            uint8_t *o = reinterpret_cast<uint8_t *>(s_h[f]) + b0;
-            if (b0 + 16u <= H) {
-                st128_u(o, x);
-            } else {
-#pragma unroll
-                for (uint32_t e = 0; e < 15; e++)  // the header's tail: byte stores (static register indices)
-                    if (b0 + e < H)
-                        stb(o + e, x[e >> 2] >> (8u * (e & 3u)));
-            }
-        }
-    }
-    if (live && d.status != st)  // leave descriptor lines clean when the caller pre-zeroed status
-        reinterpret_cast<int8_t *>(desc)[i * sizeof(wg_gro_desc) + offsetof(wg_gro_desc, status)] = st;
-}
-
 // Wave-owned variant (knob gro_lds = 2): the same cooperative chunk loads,
 // but each wave owns 64 flows and stages only its own chunks, so no block
 // barrier sits between the descriptor round trip and the chunk round trip
@@ -584,11 +406,6 @@ extern "C" int wg_gro_finalize(uint8_t *dev_hdrs, wg_gro_desc *dev_desc, uint64_
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
     const Tune t = tune();
-    if (t.gro_lds == 3) {
-        hipLaunchKernelGGL(gro_finalize_coop_kernel, dim3((unsigned)blocks), dim3(kGroBlock), 0,
-                           static_cast<hipStream_t>(stream), dev_hdrs, dev_desc, n);
-        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
-    }
     if (t.gro_lds == 2) {
         const uint32_t it = t.gro_iters;
         uint64_t b = (blocks + it - 1) / it;
