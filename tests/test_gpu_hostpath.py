@@ -4,7 +4,9 @@ segment, worker/encap.cpp:22-170) and wg_decap_host (UDP GRO batch ->
 Peer::decrypt -> evaluate_packet, worker/decap.cpp:90-156,
 worker/decap_ref.cpp:37-107), each against the oracle message for message:
 odd totals, more chunks than the pipeline's three device slots
-(host_chunk_mb = 1), pageable and pinned buffers, two host threads at once."""
+(host_chunk_mb = 1), pageable and pinned buffers (downloads into pinned
+memory by the store kernel or the runtime's copy, knob host_d2h; misaligned
+pinned outputs fall back to the copy), two host threads at once."""
 import threading
 
 import numpy as np
@@ -21,6 +23,15 @@ def _wga():
     import wireglider_amd as wga
 
     return wga
+
+
+@pytest.fixture
+def d2h():
+    """Sets knob host_d2h for one test, restored after."""
+    wga = _wga()
+    saved = wga.tune_get("host_d2h")
+    yield lambda v: wga.tune_set("host_d2h", v)
+    wga.tune_set("host_d2h", saved)
 
 
 @pytest.fixture
@@ -103,10 +114,13 @@ def test_encap_host_matches_oracle(gpu, small_chunks, parts):
     check_encap(cases, caps, key, 0xABCD, c0, msgs, res, gres, nxt)
 
 
-def test_encap_host_pinned_two_threads(gpu, small_chunks):
+@pytest.mark.parametrize("mode", [0, 1])
+def test_encap_host_pinned_two_threads(gpu, small_chunks, d2h, mode):
     """Two host threads, each with its own pipeline, concurrently; one of them
-    reads its tun reads from and writes its messages to pinned buffers."""
+    reads its tun reads from and writes its messages to pinned buffers (by
+    the store kernel when host_d2h = 1)."""
     wga = _wga()
+    d2h(mode)
     work = [encap_case(31), encap_case(32)]
     key = bytes(32)
     out = [None, None]
@@ -136,6 +150,23 @@ def test_encap_host_pinned_two_threads(gpu, small_chunks):
         check_encap(cases, caps, key, 7 + k, 1000 * k, msgs, res, gres, nxt)
     for p in pins:
         p.close()
+
+
+def test_encap_host_pinned_misaligned(gpu, small_chunks, d2h):
+    """Pinned messages buffer 8 bytes off a 16-B boundary: the store kernel
+    is skipped (runtime copy), the bytes around the region stay untouched."""
+    wga = _wga()
+    d2h(1)
+    cases, caps, desc, inbuf = encap_case(33, n=120)
+    need = len(cases) * MSG_CAP
+    pin = wga.PinnedBuffer(need + 32)
+    pin.array[:] = 0x5A
+    key = bytes(range(32))
+    msgs, res, gres, nxt = wga.encap_host(inbuf, desc, key, 3, 0, MAX_SEG, MAX_SIZE, MSG_CAP,
+                                          msgs=pin.array[8:8 + need])
+    check_encap(cases, caps, key, 3, 0, msgs, res, gres, nxt)
+    assert (pin.array[:8] == 0x5A).all() and (pin.array[8 + need:] == 0x5A).all()
+    pin.close()
 
 
 def test_encap_host_empty_and_invalid(gpu):
@@ -216,8 +247,12 @@ def test_decap_host_matches_oracle(gpu, small_chunks, verify):
     check_decap(key, msgs, stride, got)
 
 
-def test_decap_host_pinned_two_threads(gpu, small_chunks):
+@pytest.mark.parametrize("mode", [1, 3])
+def test_decap_host_pinned_two_threads(gpu, small_chunks, d2h, mode):
+    """Two threads; one decrypts from and into pinned buffers (plaintext by the
+    store kernel when host_d2h = 3)."""
     wga = _wga()
+    d2h(mode)
     work = [decap_case(51, 2503, short=1), decap_case(52, 1999, S=1456, short=33)]
     out = [None, None]
     pins = []

@@ -20,7 +20,7 @@ sys.path.insert(0, str(ROOT))
 KEYS = ("l4_blocks", "l4_ppw", "l4_nt", "l4_descv", "l4_iters", "l4_occ", "l4_small", "l4_small_uniform", "verify_small", "gso_blocks", "gso_waves", "gso_split", "gso_spw",
         "gso_groups", "verify_occ", "verify_dm", "verify_hdr", "gro_lds", "gro_wide", "gro_chunks", "gso_ablate",
         "l4_unroll", "host_chunk_mb", "l4_coop", "l4_coop_waves", "aead_k", "aead_pair", "l4_split_waves", "aead_flex",
-        "gro_iters", "encap_parts")
+        "gro_iters", "encap_parts", "host_d2h")
 
 
 def main():

@@ -56,6 +56,7 @@ static const Knob kKnobs[] = {
     {"gro_chunks", nullptr, &Tune::gro_chunks, 4, 5, nullptr, 0},
     {"gso_ablate", nullptr, &Tune::gso_ablate, 0, 0, kAbl, WG_N(kAbl)},
     {"host_chunk_mb", nullptr, &Tune::host_chunk_mb, 1, 4096, nullptr, 0},
+    {"host_d2h", nullptr, &Tune::host_d2h, 0, 3, nullptr, 0},
     {"l4_unroll", nullptr, &Tune::l4_unroll, 0, 0, kUnroll, WG_N(kUnroll)},
     {"l4_coop", &Tune::l4_coop, nullptr, 0, 1u << 20, nullptr, 0},
     {"l4_coop_waves", nullptr, &Tune::l4_coop_waves, 0, 0, kCoopW, WG_N(kCoopW)},
@@ -141,8 +142,14 @@ static Tune &tune_storage() {
         x.gro_iters = 1;
         x.gso_ablate = 0;
         // host pipeline chunk: 128-512 MiB reach 97-98 % of the raw H2D rate
-        // (8 MiB: 70 %, per-chunk overheads; profiles/r02_host_path.json)
-        x.host_chunk_mb = 256;
+        // (8 MiB: 70 %, per-chunk overheads; profiles/r02_host_path.json);
+        // with both directions in flight 64 MiB: decap 35.2 ms vs 37.3 at
+        // 256 MiB (shorter fill and drain), encap within 2 %
+        // (profiles/r03_host_d2h_probe.txt)
+        x.host_chunk_mb = 64;
+        // encap message downloads by the store kernel, decap plaintext by
+        // the runtime's copy (hostpath.hip d2h_store_kernel)
+        x.host_d2h = 1;
         // descriptor batches: 8 loads in flight per lane on a long packet's
         // rest (5 waves/SIMD instead of 6): config 4 -1.4 %, config 1 (64 KiB
         // buffers) -26 %, config 5 (no long packets) unchanged

@@ -230,6 +230,63 @@ int d2h(Pipe &c, void *dst, const void *src, size_t n) {
                                                                                                : WG_ERR_RUNTIME;
 }
 
+// Downloads into pinned host memory by a store kernel on the D2H stream
+// (knob host_d2h, bit 1: encap messages, bit 2: decap plaintext): 16-B
+// loads from the slot, 16-B stores across PCIe, four in flight per lane.
+// The runtime's hipMemcpyAsync picks its copy engine per call (an SDMA
+// engine or a blit kernel); in the encap pipeline its message downloads ran
+// at a fraction of the link while uploads were in flight (2 GiB of tun
+// reads: 101 ms a call, 56 ms with the store kernel), while the decap
+// pipeline's plaintext downloads are faster by SDMA (35.2 vs 38.5 ms)
+// (tools/host_probe.py, profiles/r03_host_d2h_probe.txt).
+__global__ void __launch_bounds__(256) d2h_store_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
+                                                        uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * 1024u;
+    for (uint64_t i = (uint64_t)blockIdx.x * 1024u + threadIdx.x; i < n16; i += stride) {
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (i + k * 256u < n16)
+                v[k] = src[i + k * 256u];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (i + k * 256u < n16)
+                dst[i + k * 256u] = v[k];
+    }
+}
+
+// The device-visible address of a caller's host buffer when it is pinned
+// (hipHostMalloc, wg_host_alloc, hipHostRegister), else nullptr: pageable
+// memory is left to the runtime's staged copies.
+uint8_t *pinned_alias(const void *host) {
+    hipPointerAttribute_t a{};
+    if (!host || hipPointerGetAttributes(&a, host) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer)
+        return nullptr;
+    const auto *h = static_cast<const uint8_t *>(host), *hb = static_cast<const uint8_t *>(a.hostPointer);
+    return h >= hb ? static_cast<uint8_t *>(a.devicePointer) + (h - hb) : nullptr;
+}
+
+// A large download: the store kernel when knob host_d2h has `bit`, the
+// destination is pinned (dst_alias: its device-visible address) and both
+// ends and the length are 16-B multiples, else hipMemcpyAsync.
+int d2h_big(Pipe &c, uint32_t bit, void *dst, uint8_t *dst_alias, const void *src, size_t n) {
+    if (!n)
+        return WG_OK;
+    if (!dst_alias || !(tune().host_d2h & bit) || ((reinterpret_cast<uintptr_t>(dst_alias) | n) & 15) ||
+        (reinterpret_cast<uintptr_t>(src) & 15))
+        return d2h(c, dst, src, n);
+    const uint64_t n16 = n / 16;
+    uint64_t blocks = (n16 + 1023) / 1024;
+    blocks = blocks < 1024 ? blocks : 1024;
+    hipLaunchKernelGGL(d2h_store_kernel, dim3((uint32_t)blocks), dim3(256), 0, c.s[kD2H],
+                       static_cast<const uint4 *>(src), reinterpret_cast<uint4 *>(dst_alias), n16);
+    return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+}
+
 uint64_t chunk_bytes() { return (uint64_t)tune().host_chunk_mb << 20; }
 
 #define WG_TRY(x)                 \
@@ -316,6 +373,7 @@ extern "C" int wg_decap_host(const uint8_t *host_msgs, uint64_t total_len, uint3
     auto *gst = static_cast<int8_t *>(c.gather[kSt].p);
     auto *gver = static_cast<uint8_t *>(c.gather[kVer].p);
     auto *gl4 = static_cast<uint16_t *>(c.gather[kL4].p);
+    uint8_t *const plain_alias = pstride ? pinned_alias(host_plain) : nullptr;
     Flight f(c);
     for (uint64_t off = 0; off < total_len; off += chunk) {
         const int slot = (int)(f.k % kSlots);
@@ -332,7 +390,8 @@ extern "C" int wg_decap_host(const uint8_t *host_msgs, uint64_t total_len, uint3
             WG_TRY(wg_aead_decrypt_batch(dp(c, slot, kIn), len, segment_size, key, dp(c, slot, kPlain),
                                          dp<int8_t>(c, slot, kSt), c.s[kExec]));
         WG_TRY(f.computed(slot));
-        WG_TRY(d2h(c, host_plain + first * pstride, dp(c, slot, kPlain), m * pstride));
+        WG_TRY(d2h_big(c, 2u, host_plain + first * pstride, plain_alias ? plain_alias + first * pstride : nullptr,
+                       dp(c, slot, kPlain), m * pstride));
         WG_TRY(d2h(c, gst + first, dp(c, slot, kSt), m));
         if (ver) {
             WG_TRY(d2h(c, gver + first, dp(c, slot, kVer), m));
@@ -413,6 +472,7 @@ extern "C" int wg_encap_host(const uint8_t *host_in, const wg_gso_desc *host_des
     auto *geres = static_cast<wg_encap_result *>(c.gather[kEres].p);
     auto *ggres = static_cast<wg_gso_result *>(c.gather[kGres].p);
     auto *ctr = static_cast<uint64_t *>(c.ctr.p);
+    uint8_t *const msgs_alias = pinned_alias(host_msgs);
     Flight f(c);
     f.armed = true;
     if (hipMemsetAsync(ctr, 0, sizeof(uint64_t), c.s[kExec]) != hipSuccess)
@@ -445,7 +505,8 @@ extern "C" int wg_encap_host(const uint8_t *host_in, const wg_gso_desc *host_des
                                   dp(c, slot, kMsgs), dp<wg_encap_result>(c, slot, kEres), dp<uint32_t>(c, slot, kWork),
                                   ctr + k + 1, ctr + k, c.s[kExec]));
         WG_TRY(f.computed(slot));
-        WG_TRY(d2h(c, host_msgs + i0 * msg_cap, dp(c, slot, kMsgs), cnt * msg_cap));
+        WG_TRY(d2h_big(c, 1u, host_msgs + i0 * msg_cap, msgs_alias ? msgs_alias + i0 * msg_cap : nullptr,
+                       dp(c, slot, kMsgs), cnt * msg_cap));
         WG_TRY(d2h(c, geres + i0, dp(c, slot, kEres), cnt * sizeof(wg_encap_result)));
         if (host_gso_res)
             WG_TRY(d2h(c, ggres + i0, dp(c, slot, kGres), cnt * sizeof(wg_gso_result)));

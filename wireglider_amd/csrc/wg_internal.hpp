@@ -35,6 +35,7 @@ struct Tune {
     uint32_t gro_chunks;  // 16-B chunks staged per flow by the LDS variant (4, 5)
     uint32_t gro_iters;   // gro_lds = 2: groups of 64 flows per wave (1, 2, 4), next descriptors prefetched
     uint32_t host_chunk_mb;  // host-memory pipeline chunk size, MiB
+    uint32_t host_d2h;    // host pipeline downloads into pinned memory by a store kernel (bit 1 encap messages, bit 2 decap plaintext)
     uint32_t l4_unroll;   // split kernel: loads in flight per lane on a long packet's rest (4, 8)
     uint64_t l4_coop;     // descriptor batches of n <= l4_coop: a block of l4_coop_waves waves per packet (0: never)
     uint32_t l4_coop_waves;  // waves per packet in that mode (2, 4, 8, 16)
