@@ -753,42 +753,74 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             const uint32_t boff = has ? 64u * d : 0u;
             const uint32_t nin = has ? (plen - boff < 64u ? plen - boff : 64u) : 0u;  // payload bytes in the block
             const uint32_t nct = has ? (pad - boff < 64u ? pad - boff : 64u) : 0u;    // Poly1305 bytes in the block
+            // plaintext (encrypt) / ciphertext (decrypt); kGso == 2: blocks
+            // below hl from the segment slot
+            const uintptr_t bsrc = (kGso == 2 && boff < hl ? hsrc : src) + boff;
+            const uintptr_t bdst = kDec ? dst + boff : dst + 16 + boff;
             uint32_t W[16];
-            // plaintext (encrypt) / ciphertext (decrypt), zero past the
-            // payload; kGso == 2: blocks below hl from the segment slot
-            const uintptr_t bsrc = kGso == 2 && boff < hl ? hsrc : src;
-            load64(bsrc + boff, nin, W);
-            const uint32_t nqc = nct / 16u;  // whole 16-B Poly1305 chunks in the block (nct is a multiple of 16)
+            if (nin == 64u) {
+                // A whole block inside the payload (every block of a packet
+                // but its last): four 16-B loads at the source address as it
+                // is (gfx950 global loads take any alignment; all 64 bytes
+                // are the packet's), no masks, four 16-B stores, four
+                // unmasked Poly1305 steps.  Lanes whose block is the packet's
+                // last, or none, take the general path below; per wave that
+                // path runs only in the iterations where some lane needs it.
 #pragma unroll
-            for (int m = 0; m < 16; m++) {
-                if constexpr (!kDec) {
-                    // padding plaintext bytes are zero (proto.cpp:568-572):
-                    // their ciphertext is the keystream itself
-                    W[m] = (uint32_t)m / 4u < nqc ? W[m] ^ kb[m] : 0u;  // ciphertext, what Poly1305 sees
-                } else if constexpr (kVer) {
-                    kb[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nin);  // plaintext (the gates read it whole)
-                } else {
-                    kb[m] = W[m] ^ kb[m];  // plaintext; store_n writes its first nin bytes only
+                for (uint32_t q = 0; q < 4; q++) {
+                    const v4u v = ld16(bsrc + 16u * q);
+#pragma unroll
+                    for (uint32_t e = 0; e < 4; e++) W[4 * q + e] = v[e];
+                }
+#pragma unroll
+                for (int m = 0; m < 16; m++) {
+                    if constexpr (!kDec)
+                        W[m] ^= kb[m];  // ciphertext
+                    else
+                        kb[m] ^= W[m];  // plaintext
+                }
+                const uint32_t *o = kDec ? kb : W;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q++)
+                    st16(bdst + 16u * q, v4u{o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]});
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q++)
+                    x = p32_step(x, W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3], rw, srw);
+            } else if (has) {
+                // zero past the payload
+                load64(bsrc, nin, W);
+                const uint32_t nqc = nct / 16u;  // whole 16-B Poly1305 chunks in the block (nct is a multiple of 16)
+#pragma unroll
+                for (int m = 0; m < 16; m++) {
+                    if constexpr (!kDec) {
+                        // padding plaintext bytes are zero (proto.cpp:568-572):
+                        // their ciphertext is the keystream itself
+                        W[m] = (uint32_t)m / 4u < nqc ? W[m] ^ kb[m] : 0u;  // ciphertext, what Poly1305 sees
+                    } else if constexpr (kVer) {
+                        kb[m] = keep_below(W[m] ^ kb[m], (uint32_t)m, nin);  // plaintext (the gates read it whole)
+                    } else {
+                        kb[m] = W[m] ^ kb[m];  // plaintext; store_n writes its first nin bytes only
+                    }
+                }
+                // decrypt stores the plaintext now; a bad tag zeroes it below
+                // (the final bytes are libsodium's either way)
+                store_n(bdst, kDec ? kb : W, kDec ? nin : nct);
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q++) {
+                    const P32 t = p32_step(x, W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3], rw, srw);
+#pragma unroll
+                    for (int k = 0; k < 5; k++)
+                        x.h[k] = q < nqc ? t.h[k] : x.h[k];
                 }
             }
             if constexpr (kVer) {
                 // the plaintext's words; the first 64 bytes decide the gates
+                if (has) {
 #pragma unroll
-                for (int m = 0; m < 16; m++) vsum += hsum32(kb[m]);
-                if (has && d == 0u)
-                    gate = hdr_gate(kb, plen);
-            }
-            // decrypt stores the plaintext now; a bad tag zeroes it below
-            // (the final bytes are libsodium's either way)
-            if (has)
-                store_n(kDec ? dst + boff : dst + 16 + boff, kDec ? kb : W, kDec ? nin : nct);
-            const uint32_t nqj = nct / 16u;
-#pragma unroll
-            for (uint32_t q = 0; q < 4; q++) {
-                const P32 t = p32_step(x, W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3], rw, srw);
-#pragma unroll
-                for (int k = 0; k < 5; k++)
-                    x.h[k] = q < nqj ? t.h[k] : x.h[k];
+                    for (int m = 0; m < 16; m++) vsum += hsum32(kb[m]);
+                    if (d == 0u)
+                        gate = hdr_gate(kb, plen);
+                }
             }
         };
         uint32_t j0 = 0;
