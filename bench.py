@@ -74,7 +74,7 @@ def parse():
     ap.add_argument("--workload", default="config2",
                     choices=["config1", "config2", "config3", "config3udp", "config4", "config4small", "config4strong",
                              "config5", "verify64", "verify1500u",
-                             "verify", "gro", "encap", "encap_2call", "aead", "encap_host", "decap_host"])
+                             "verify", "verify64d", "gro", "encap", "encap_2call", "aead", "encap_host", "decap_host"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-post", action="store_true",
                     help="skip the workload's own post-checks (PMC passes: only the step's launches of its kernels)")
@@ -360,12 +360,13 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                         "wg::l4csum_coop_kernel<2,nt,4,4> (plain checksum, a 4-wave block per buffer: l4_coop)", rank * n, sample=sample,
                         counts=[n] * world,
                         metric="device-resident GiB/s, checksum(span, 0) over 64 KiB buffers (BASELINE config 1 shape)")
-    if name == "verify":
+    if name in ("verify", "verify64d"):
         n = 1 << 20
         seed = 0x5EED00F1
-        buf = torch.empty(n * SEG, dtype=torch.uint8, device=dev)
-        wga.synth_fill(buf, seed, counter_base=rank * n * SEG)
-        desc = wga.synth_desc_stride(n, SEG, SEG, 1, seed, rank * n, device=dev)  # mixed v4/v6 x TCP/UDP
+        VSEG = SEG if name == "verify" else 64
+        buf = torch.empty(n * VSEG, dtype=torch.uint8, device=dev)
+        wga.synth_fill(buf, seed, counter_base=rank * n * VSEG)
+        desc = wga.synth_desc_stride(n, VSEG, VSEG, 1, seed, rank * n, device=dev)  # mixed v4/v6 x TCP/UDP
         wga.synth_headers(buf, desc, seed, rank * n)
         wga.store_l4csum(buf, desc, wga.calc_l4_checksum_desc(buf, desc))  # received packets are valid
         torch.cuda.synchronize()
@@ -394,8 +395,8 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
             l64 = torch.empty(n, dtype=torch.uint16, device=dev)
             saved = wga.tune_get("verify_small")
             small, ref = {}, None
-            for kname, knob in (("wave_per_packet", 0), ("lane_per_descriptor", 1), ("quad_per_descriptor", 2),
-                                ("split_roles", 3)):
+            for kname, knob in (("wave_per_packet", 0), ("default_auto", 7), ("compacting", 6),
+                                ("lane_per_descriptor", 1), ("split_roles", 3), ("two_role", 4)):
                 wga.tune_set("verify_small", knob)
                 for _ in range(10):
                     wga.verify_desc(b64, d64, verdict=v64, l4=l64)
@@ -424,14 +425,17 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
             d = desc[:npk].cpu().numpy()
             v, l = wga.verify_desc(buf, desc[:npk])
             torch.cuda.synchronize()
-            end = npk * SEG
+            end = npk * VSEG
             return buf[:end].cpu().numpy(), (v.cpu().numpy(), l.cpu().numpy()), ("verify", d)
 
-        cfg = {"workload": "verify (SURVEY §8 f1): 1,048,576 x 1500 B mixed IPv4/IPv6 x TCP/UDP per GPU, "
-                           "checksums stored, evaluate_packet checksum gates (wg_verify_desc)",
-               "packets_per_gpu": n, "segment_size": SEG, "layout": "descriptor", "parallelism": f"shard{world}"}
-        return Workload(launch, n, n * SEG, n * SEG + 16 * n + n + 2 * n, cfg, "weak", buf,
-                        "wg::verify_kernel<4>", rank * n, sample=sample, counts=[n] * world, probe_run=SEG,
+        cfg = {"workload": f"{name} (SURVEY §8 f1): 1,048,576 x {VSEG} B mixed IPv4/IPv6 x TCP/UDP per GPU, "
+                           "checksums stored, evaluate_packet checksum gates (wg_verify_desc, default knobs)",
+               "packets_per_gpu": n, "segment_size": VSEG, "layout": "descriptor", "parallelism": f"shard{world}"}
+        kname = ("wg::verify_kernel<4,8,0,true> (verify_small=7 chose the wave kernel: no small packets sampled)"
+                 if VSEG > 64 else "wg::verify_compact_lane_kernel + wg::verify_compact_long_kernel<8> "
+                 "(verify_small=7 chose the compacting path: 64 of 64 sampled packets small)")
+        return Workload(launch, n, n * VSEG, n * VSEG + 16 * n + n + 2 * n, cfg, "weak", buf,
+                        kname, rank * n, sample=sample, counts=[n] * world, probe_run=VSEG,
                         metric="device-resident GiB/s, decap verify gates over packet batch (SURVEY f1)",
                         post=post)
     if name == "gro":

@@ -147,7 +147,9 @@ VERIFY_VARIANTS = [{"verify_dm": 0, "verify_occ": 8, "verify_hdr": 1}, {"verify_
                    {"verify_small": 0}, {"verify_small": 1}, {"verify_small": 2}, {"verify_small": 3},
                    {"verify_small": 3, "verify_occ": 0}, {"verify_small": 4}, {"verify_small": 4, "verify_occ": 0},
                    {"verify_small": 4, "verify_wblk": 16},
-                   {"verify_small": 5}, {"verify_small": 5, "verify_occ": 0}]
+                   {"verify_small": 5}, {"verify_small": 5, "verify_occ": 0},
+                   {"verify_small": 6}, {"verify_small": 6, "verify_k2min": 8}, {"verify_small": 7},
+                   {"verify_small": 7, "verify_auto_t": 1}]
 
 
 @pytest.mark.gpu
@@ -351,3 +353,81 @@ def test_gpu_verify_uniform(gpu, seg):
         np.testing.assert_array_equal(l4.cpu().numpy(), el4, err_msg=f"lead {lead}")
         if seg >= 60:
             assert (ev & OK == OK).mean() > 0.5
+
+
+def _verify_calls(wga, torch, gpu, batches, knobs, stream=None):
+    """wg_verify_desc over each (buf, desc) in order on one stream under knobs;
+    returns the host copies of every call's verdicts and L4 results."""
+    saved = {k: wga.tune_get(k) for k in knobs}
+    for k, v in knobs.items():
+        wga.tune_set(k, v)
+    out = []
+    try:
+        ctx = torch.cuda.stream(stream) if stream is not None else torch.cuda.stream(torch.cuda.current_stream())
+        with ctx:
+            for buf, d in batches:
+                verdict, l4 = wga.verify_desc(torch.from_numpy(buf).to(gpu),
+                                              torch.from_numpy(d.view(np.int64).reshape(-1, 2).copy()).to(gpu))
+                out.append((verdict, l4))
+        torch.cuda.synchronize()
+    finally:
+        for k, v in saved.items():
+            wga.tune_set(k, v)
+    return [(v.cpu().numpy(), x.cpu().numpy()) for v, x in out]
+
+
+@pytest.mark.gpu
+def test_gpu_verify_auto_switches(gpu):
+    """The default wg_verify_desc (verify_small = 7) picks its kernels per call
+    from the size mix the previous call on the stream sampled: all-small,
+    all-long and interleaved batches back to back, each followed by a
+    different one (every call then runs on a stale sample, including the
+    compacting path's long kernel sized for no long packets at all, with a
+    1-block-per-shard minimum grid), on the default stream and on a side
+    stream — every call's results equal the oracle's."""
+    import torch
+
+    import wireglider_amd as wga
+
+    rng = np.random.default_rng(14)
+
+    def sized(n, lo, hi):
+        pkts = []
+        for _ in range(n):
+            v6, tcp = bool(rng.integers(0, 2)), bool(rng.integers(0, 2))
+            hl = (40 if v6 else 20) + (20 if tcp else 8)
+            al = 16 if v6 else 4
+            plen = int(rng.integers(max(0, lo - hl), max(1, hi - hl)))
+            pkts.append(pktbuild.build(v6, tcp, rng.integers(0, 256, plen, dtype=np.uint8).tobytes(),
+                                       rng.integers(0, 256, al, dtype=np.uint8).tobytes(),
+                                       rng.integers(0, 256, al, dtype=np.uint8).tobytes()))
+        return pkts
+
+    kinds = {"small": sized(9000, 40, 65), "long": sized(9000, 65, 1600), "mixed": interleaved_batch(rng, 9001)}
+    packed = {k: pack(v, rng) for k, v in kinds.items()}
+    order = ["small", "long", "small", "mixed", "mixed", "long", "long", "small", "small", "mixed", "long"]
+    expect = {k: oracle.verify_desc(*packed[k]) for k in kinds}
+    for stream in (None, torch.cuda.Stream(gpu)):
+        got = _verify_calls(wga, torch, gpu, [packed[k] for k in order],
+                            {"verify_small": 7, "verify_auto_t": 4, "verify_k2min": 8}, stream)
+        for k, (v, x) in zip(order, got):
+            np.testing.assert_array_equal(v, expect[k][0], err_msg=k)
+            np.testing.assert_array_equal(x, expect[k][1], err_msg=k)
+    assert (expect["long"][0] & OK == OK).mean() > 0.9 and (expect["small"][0] & OK == OK).mean() > 0.9
+
+
+@pytest.mark.gpu
+def test_gpu_verify_compact_grows(gpu):
+    """The compacting path's entry lists grow with the batch (a batch larger
+    than every earlier one on the stream), and a 1-packet batch after it."""
+    import torch
+
+    import wireglider_amd as wga
+
+    rng = np.random.default_rng(15)
+    batches = [pack(interleaved_batch(rng, n), rng) for n in (300, 70001, 1)]
+    got = _verify_calls(wga, torch, gpu, batches, {"verify_small": 6})
+    for (buf, d), (v, x) in zip(batches, got):
+        ev, el4 = oracle.verify_desc(buf, d)
+        np.testing.assert_array_equal(v, ev)
+        np.testing.assert_array_equal(x, el4)

@@ -6,11 +6,13 @@ batch shapes a decap worker sees, one process, one device:
   c4mix   config 4's 4,194,304 packets, 64 B / 9000 B 50/50 by a seeded draw
   alt     1,048,576 packets alternating 64 B / 1500 B in runs of 1-7 (small
           and long packets interleaved inside every 4-descriptor group)
+  mixP    1,048,576 packets, P % of them 64 B at random among 1500-B ones
+          (P = 3, 12, 25: where the per-call choice of verify_small = 7 flips)
 Every packet carries a valid checksum.  Times are back-to-back launches
 between one event pair (as bench.py), median of rounds; every variant's
 verdicts and L4 results are compared with variant 0's.
 
-usage: verify_ab.py [variant ...] [--rounds R]
+usage: verify_ab.py [variant ...] [--rounds R] [--batches a,b,...]
   a variant is key=value[,key=value...] of wg_tune_set keys (default: the
   verify_small values 0, 3, 4, 5)
 """
@@ -38,6 +40,9 @@ def build(wga, torch, dev, name):
         if name == "c4mix":
             n = 1 << 22
             lens = np.where(rng.random(n) < 0.5, 64, 9000).astype(np.int64)
+        elif name.startswith("mix"):  # mixP: P % of 64-B packets among 1500-B ones, placed at random
+            n = 1 << 20
+            lens = np.where(rng.random(n) < int(name[3:]) / 100, 64, 1500).astype(np.int64)
         else:
             n = 1 << 20
             runs = rng.integers(1, 8, n)
@@ -66,16 +71,20 @@ def main():
     import wireglider_amd as wga
 
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    if "--rounds" in sys.argv:
-        args.remove(sys.argv[sys.argv.index("--rounds") + 1])
+    for opt in ("--rounds", "--batches"):
+        if opt in sys.argv:
+            args.remove(sys.argv[sys.argv.index(opt) + 1])
     rounds = int(sys.argv[sys.argv.index("--rounds") + 1]) if "--rounds" in sys.argv else 5
-    specs = args or ["verify_small=0", "verify_small=3", "verify_small=4", "verify_small=5"]
+    specs = args or ["verify_small=0", "verify_small=7", "verify_small=6", "verify_small=4"]
     variants = [tuple((kv.split("=")[0], int(kv.split("=")[1])) for kv in a.split(",")) for a in specs]
     keys = sorted({k for v in variants for k, _ in v})
     dev = torch.device("cuda:0")
     saved = {k: wga.tune_get(k) for k in keys}
     out = {}
-    for name in ("1500B", "64B", "c4mix", "alt"):
+    names = ("1500B", "64B", "c4mix", "alt", "mix3", "mix12", "mix25")
+    if "--batches" in sys.argv:
+        names = tuple(sys.argv[sys.argv.index("--batches") + 1].split(","))
+    for name in names:
         buf, desc, n, alg = build(wga, torch, dev, name)
         verdict = torch.empty(n, dtype=torch.uint8, device=dev)
         l4 = torch.empty(n, dtype=torch.uint16, device=dev)

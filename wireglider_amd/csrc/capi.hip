@@ -48,7 +48,9 @@ static const Knob kKnobs[] = {
     {"verify_dm", nullptr, &Tune::verify_dm, 0, 0, kDm, WG_N(kDm)},
     {"verify_occ", nullptr, &Tune::verify_occ, 0, 0, kVOcc, WG_N(kVOcc)},
     {"verify_hdr", nullptr, &Tune::verify_hdr, 0, 1, nullptr, 0},
-    {"verify_small", nullptr, &Tune::verify_small, 0, 5, nullptr, 0},
+    {"verify_small", nullptr, &Tune::verify_small, 0, 7, nullptr, 0},
+    {"verify_auto_t", nullptr, &Tune::verify_auto_t, 1, 64, nullptr, 0},
+    {"verify_k2min", nullptr, &Tune::verify_k2min, 8, 65536, nullptr, 0},
     {"verify_wblk", nullptr, &Tune::verify_wblk, 0, 0, kWblk, WG_N(kWblk)},
     {"gro_lds", nullptr, &Tune::gro_lds, 0, 2, nullptr, 0},
     {"gro_iters", nullptr, &Tune::gro_iters, 0, 0, kGroIt, WG_N(kGroIt)},
@@ -134,7 +136,9 @@ static Tune &tune_storage() {
         x.verify_occ = 8;
         x.verify_dm = 0;
         x.verify_hdr = 1;
-        x.verify_small = 0;
+        x.verify_small = 7;
+        x.verify_auto_t = 4;
+        x.verify_k2min = 2048;
         x.verify_wblk = 4;
         x.gro_lds = 1;
         x.gro_wide = 1;

@@ -17,6 +17,8 @@
 // traffic.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include "wg_device.hpp"
 #include "wg_internal.hpp"
 #include "wg_l4wave.hpp"
@@ -718,7 +720,21 @@ struct VerifyParams {
     uint64_t total_len = 0;
     uint32_t seg = 0;
     uint32_t last_len = 0;  // uniform: length of segment n - 1 (the only one that may be short)
+    uint32_t *sample = nullptr;  // host-mapped word: small packets among 64 spread descriptors (verify_sample)
 };
+
+// The size mix of a descriptor batch, for the NEXT call's kernel choice
+// (wg_verify_desc, verify_small = 7): lane k reads descriptor k*n/64 and the
+// wave stores how many of those 64 packets are <= kSmallMax bytes into a
+// host-mapped word (one dword store; the host reads it without waiting).
+__device__ __forceinline__ void verify_sample(const VerifyParams &p, uint32_t lane) {
+    constexpr uint32_t kSmallLen = 64;  // = kSmallMax (declared with the small-packet kernels)
+    const uint64_t i = ((uint64_t)lane * p.n) >> 6;
+    const uint32_t len = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * i).z;
+    const uint32_t s = (uint32_t)__builtin_popcountll(__ballot(len <= kSmallLen));
+    if (lane == 0)
+        __hip_atomic_store(p.sample, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t j) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
@@ -894,6 +910,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
     }
     if constexpr (DM == 0)
         break;
+    }
+    if constexpr (!kUni) {
+        if (p.sample && blockIdx.x == 0 && wave_in_block() == 0)
+            verify_sample(p, lane);
     }
 }
 
@@ -1176,7 +1196,260 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
         verify_wave_role(p, wave * 4u, lane_id());
 }
 
+// ---------------------------------------------------------------------------
+// Compacting verify (verify_small 6; 7 chooses per call between it and the
+// wave kernel).  Two launches whose wave counts follow the batch's size mix
+// instead of its descriptor count:
+//  - verify_compact_lane_kernel, a lane per descriptor (n / 64 waves):
+//    packets of <= kSmallMax bytes are decoded in their lane (verify_lane);
+//    the longer ones are appended as 16-B entries {offset, len, index} to the
+//    list of shard (blockIdx & 31) — one returning atomic per block, after the
+//    block's four waves have counted their long lanes in LDS;
+//  - verify_compact_long_kernel: waves take 4 consecutive entries of their
+//    block's shard through verify_group (the wave kernel's body, 8
+//    waves/SIMD) and store by index, grid-stride over the shard, so any grid
+//    is correct and the host sizes it from the expected long count.
+// A batch of ACK-sized packets thus costs n / 64 lane waves and an almost
+// empty second launch, where n / 4 one-shot waves (the wave kernel, or any
+// role split sized by descriptor count) cost ~30 us of wave launches alone
+// (profiles/r03_verify_ab.json, verify_small 4 / 5 at 64 B).
+// The counters come in two sets; a call uses set `parity` and its lane
+// kernel zeroes the other, which the previous call's long kernel has finished
+// reading (stream order), so no memset is launched per call.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kVShards = 32;  // 4 per XCD: one returning atomic per word saturates at ~88/us
+constexpr uint32_t kVCtrStride = 32;  // words between counters: a 128-B line each
+
+struct VerifyCompact {
+    v4u *ent;            // shard s's list at ent + s * cap
+    uint64_t cap;        // entries per shard (>= 256 * ceil(lane-kernel blocks / 8))
+    uint32_t *ctr;       // this call's counters (kVShards, stride kVCtrStride)
+    uint32_t *ctr_next;  // the next call's, zeroed here
+};
+
+__global__ __launch_bounds__(256) void verify_compact_lane_kernel(VerifyParams p, VerifyCompact c) {
+    __shared__ uint32_t s_cnt[4];
+    __shared__ uint32_t s_base;
+    const uint32_t lane = lane_id();
+    const uint32_t wib = wave_in_block();
+    const uint64_t i = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 256u + threadIdx.x;
+    const bool live = i < p.n;
+    const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0));
+    const uint32_t len = live ? dv.z : 0u;
+    const bool small = live && len <= kSmallMax;
+    const bool lng = live && !small;
+    if (blockIdx.x == 0 && threadIdx.x < kVShards)
+        c.ctr_next[threadIdx.x * kVCtrStride] = 0;
+    // the small packets: loads issued before the block synchronises
+    uint32_t rv = 0, rc = 0;
+    const bool any_small = __ballot(small) != 0;
+    if (any_small)
+        verify_lane(reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)dv.y << 32) | dv.x), small ? len : 0u, small,
+                    rv, rc);
+    // the long packets: block-aggregated append to this block's shard
+    const uint64_t ml = __ballot(lng);
+    if (lane == 0)
+        s_cnt[wib] = (uint32_t)__builtin_popcountll(ml);
+    __syncthreads();
+    const uint32_t tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    if (tot) {  // block-uniform
+        const uint32_t sh = blockIdx.x & (kVShards - 1);
+        if (threadIdx.x == 0)
+            s_base = atomicAdd(&c.ctr[sh * kVCtrStride], tot);
+        __syncthreads();
+        if (lng) {
+            const uint32_t pre = (wib > 0 ? s_cnt[0] : 0u) + (wib > 1 ? s_cnt[1] : 0u) + (wib > 2 ? s_cnt[2] : 0u);
+            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(ml >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ml, 0u));
+            c.ent[sh * c.cap + s_base + pre + r] = v4u{dv.x, dv.y, len, (uint32_t)i};
+        }
+    }
+    if (small) {
+        p.verdict[i] = (uint8_t)rv;
+        if (p.l4)
+            p.l4[i] = (uint16_t)rc;
+    }
+    if (p.sample && blockIdx.x == 0 && wib == 0)
+        verify_sample(p, lane);
+}
+
+template <int O = 8>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_compact_long_kernel(
+    VerifyParams p, VerifyCompact c) {
+    constexpr int P = 4;
+    __shared__ uint32_t s_idx[4][P];
+    const uint32_t lane0 = lane_id();
+    const uint32_t sh = blockIdx.x & (kVShards - 1);
+    const uint32_t nbs = (gridDim.x - sh + kVShards - 1) / kVShards;  // blocks serving this shard
+    const uint64_t step = (uint64_t)nbs * 4u * P;
+    const v4u *e = c.ent + sh * c.cap;
+    uint64_t k0 = ((uint64_t)(blockIdx.x / kVShards) * 4u + wave_in_block()) * P;
+    // the first group's entries load together with the count — no dependent
+    // round trip in front of them (entries past the count are read but not
+    // used; the index is clamped into the list)
+    v4u d[P];
+#pragma unroll
+    for (int j = 0; j < P; j++)
+        d[j] = e[k0 + j < c.cap ? k0 + j : c.cap - 1];
+    const uint32_t cnt = c.ctr[sh * kVCtrStride];
+    while (k0 < cnt) {
+        // the lane id laundered per iteration: the lane-derived constants of
+        // verify_group are then recomputed in the body instead of hoisted and
+        // held across the loop (which spilled at 64 VGPRs)
+        uint32_t lane = lane0;
+        asm volatile("" : "+v"(lane));
+        uint64_t doff[P];
+        uint32_t len[P], tgt[P];
+#pragma unroll
+        for (int j = 0; j < P; j++) {
+            doff[j] = ((uint64_t)d[j].y << 32) | d[j].x;
+            len[j] = k0 + j < cnt ? d[j].z : 0u;
+            tgt[j] = (uint32_t)j;
+        }
+        // the packets' indices parked in this wave's LDS words across the
+        // group (held in registers they spill; re-read from memory they put
+        // a dependent load at the end of every wave)
+        if (lane < (uint32_t)P)
+            s_idx[wave_in_block()][lane] = lane == 0 ? d[0].w : lane == 1 ? d[1].w : lane == 2 ? d[2].w : d[3].w;
+        uint32_t rv = 0, rc = 0;
+        verify_group<P, true>(p.base, doff, len, tgt, lane, rv, rc, [] {});
+        if (lane < (uint32_t)P && k0 + lane < cnt) {
+            const uint32_t at = s_idx[wave_in_block()][lane];
+            p.verdict[at] = (uint8_t)rv;
+            if (p.l4)
+                p.l4[at] = (uint16_t)rc;
+        }
+        k0 += step;
+        if (k0 < cnt) {
+#pragma unroll
+            for (int j = 0; j < P; j++)
+                d[j] = e[k0 + j < c.cap ? k0 + j : c.cap - 1];
+        }
+    }
+}
+
 }  // namespace wg
+
+namespace {
+
+// Per (device, stream) scratch of the compacting verify path: the entry
+// lists, two counter sets, and the host-mapped sample word read by the next
+// call.  Created on first use, grown (after draining the stream) when a
+// batch needs more entries, never freed (a handful per process).  A stream
+// whose state cannot be made (table full, allocation failure) runs the wave
+// kernel: the same results by another kernel, never a host fallback.
+struct VerifyState {
+    int dev = -1;
+    void *stream = nullptr;
+    std::mutex mu;
+    uint32_t *host_sample = nullptr;  // hipHostMalloc'd, mapped
+    uint32_t *dev_sample = nullptr;
+    uint32_t *ctr = nullptr;          // 2 sets x kVShards x kVCtrStride words
+    wg::v4u *ent = nullptr;
+    uint64_t cap = 0;                 // entries per shard
+    uint32_t parity = 0;
+};
+constexpr uint32_t kSampleUnknown = 0xffffffffu;
+constexpr size_t kMaxVerifyStates = 64;
+std::mutex g_vstate_mu;
+VerifyState *g_vstate[kMaxVerifyStates];
+size_t g_nvstate = 0;
+
+VerifyState *verify_state(void *stream) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        return nullptr;
+    std::lock_guard<std::mutex> g(g_vstate_mu);
+    for (size_t k = 0; k < g_nvstate; k++)
+        if (g_vstate[k]->dev == dev && g_vstate[k]->stream == stream)
+            return g_vstate[k];
+    if (g_nvstate == kMaxVerifyStates)
+        return nullptr;
+    VerifyState *s = new VerifyState;
+    s->dev = dev;
+    s->stream = stream;
+    void *h = nullptr, *d = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+        delete s;
+        return nullptr;
+    }
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&s->ctr), 2u * wg::kVShards * wg::kVCtrStride * 4u) != hipSuccess ||
+        hipMemset(s->ctr, 0, 2u * wg::kVShards * wg::kVCtrStride * 4u) != hipSuccess) {
+        (void)hipHostFree(h);
+        if (s->ctr)
+            (void)hipFree(s->ctr);
+        delete s;
+        return nullptr;
+    }
+    s->host_sample = static_cast<uint32_t *>(h);
+    s->dev_sample = static_cast<uint32_t *>(d);
+    __atomic_store_n(s->host_sample, kSampleUnknown, __ATOMIC_RELAXED);
+    g_vstate[g_nvstate++] = s;
+    return s;
+}
+
+// Entry capacity for n descriptors (caller holds s->mu).
+bool verify_reserve(VerifyState *s, uint64_t cap, hipStream_t st) {
+    if (s->cap >= cap)
+        return true;
+    if (s->ent) {
+        if (hipStreamSynchronize(st) != hipSuccess)
+            return false;
+        (void)hipFree(s->ent);
+        s->ent = nullptr;
+        s->cap = 0;
+    }
+    if (hipMalloc(reinterpret_cast<void **>(&s->ent), cap * wg::kVShards * 16u) != hipSuccess) {
+        s->ent = nullptr;
+        return false;
+    }
+    s->cap = cap;
+    return true;
+}
+
+}  // namespace
+
+namespace wg {
+
+// The compacting path (caller holds s->mu).  Grid of the long kernel: est_long
+// expected long packets (grid-stride, so a low estimate is only slower).
+static int verify_compact_launch(VerifyParams p, VerifyState *s, uint64_t est_long, uint64_t kmin,
+                                 hipStream_t st) {
+    uint64_t nl = (p.n + 255) / 256;
+    if (nl >= 8)
+        nl = (nl + 7) & ~7ull;
+    const uint64_t cap = 256u * ((nl + kVShards - 1) / kVShards);
+    if (nl > 0x7fffffffull || p.n >= (1ull << 32) || !verify_reserve(s, cap, st))
+        return WG_ERR_RUNTIME;  // the caller runs the wave kernel instead
+    VerifyCompact c{s->ent, s->cap, s->ctr + s->parity * kVShards * kVCtrStride,
+                    s->ctr + (s->parity ^ 1u) * kVShards * kVCtrStride};
+    s->parity ^= 1u;
+    p.sample = s->dev_sample;
+    hipLaunchKernelGGL(verify_compact_lane_kernel, dim3((unsigned)nl), dim3(256), 0, st, p, c);
+    // long kernel: one 4-entry group per wave for the expected count (+1/8
+    // and 32 waves of slack), at least one block per shard, at most n / 16
+    uint64_t waves = (est_long + 3) / 4;
+    waves += waves / 8 + 32;
+    uint64_t nb = (waves + 3) / 4;
+    nb = nb < kmin ? kmin : nb;  // a stale estimate: still every SIMD busy
+    const uint64_t nbmax = (p.n + 15) / 16;
+    nb = nb > nbmax ? nbmax : nb;
+    nb = (nb + kVShards - 1) & ~(uint64_t)(kVShards - 1);
+    hipLaunchKernelGGL(verify_compact_long_kernel<8>, dim3((unsigned)nb), dim3(256), 0, st, p, c);
+    if (hipGetLastError() != hipSuccess) {
+        // a launch that did not happen may have left a counter set dirty
+        (void)hipMemsetAsync(s->ctr, 0, 2u * kVShards * kVCtrStride * 4u, st);
+        return WG_ERR_LAUNCH;
+    }
+    return WG_OK;
+}
+
+}  // namespace wg
+
+static uint64_t verify_wave_blocks(uint64_t n) {
+    uint64_t blocks = (n + 15) / 16;  // one-shot 4-packet waves
+    return blocks >= 8 ? (blocks + 7) & ~7ull : blocks;
+}
 
 extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_desc, uint64_t n,
                               uint8_t *dev_verdict, uint16_t *dev_l4, void *stream) {
@@ -1186,6 +1459,28 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
         return WG_ERR_INVALID;
     VerifyParams p{dev_base, dev_desc, dev_verdict, dev_l4, n};
     const Tune t = tune();
+    if (t.verify_small >= 6) {
+        // 6: the compacting path; 7 (default): the compacting path when the
+        // previous call on this stream sampled >= verify_auto_t small packets
+        // of 64, else the wave kernel (which samples this batch in turn).
+        // Both give the same results; only the kernels differ.
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        if (VerifyState *s = verify_state(stream)) {
+            std::lock_guard<std::mutex> g(s->mu);
+            const uint32_t smp = __atomic_load_n(s->host_sample, __ATOMIC_RELAXED);
+            const bool known = smp <= 64u;
+            if (t.verify_small == 6 || (known && smp >= t.verify_auto_t)) {
+                const uint64_t est = known ? (n * (64u - smp) + 63u) / 64u : n;
+                const int rc = verify_compact_launch(p, s, est, t.verify_k2min, st);
+                if (rc != WG_ERR_RUNTIME)
+                    return rc;
+            }
+            p.sample = s->dev_sample;
+            hipLaunchKernelGGL((verify_kernel<4, 8, 0, true>), dim3((unsigned)verify_wave_blocks(n)), dim3(256), 0, st,
+                               p);
+            return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+        }
+    }
     if (t.verify_small == 4 || t.verify_small == 5) {
         hipStream_t st = static_cast<hipStream_t>(stream);
         uint64_t nl = (n + 255) / 256, nw = (n + 15) / 16;  // lane-role / wave-role blocks

@@ -29,6 +29,8 @@ struct Tune {
     uint32_t verify_occ;  // waves/SIMD target of the verify kernel (0 = compiler's choice; 8)
     uint32_t verify_small;  // 1: verify by the lane-per-descriptor kernel (packets <= 64 B decoded in a lane)
     uint32_t verify_wblk; // verify_small = 4: waves per block of the wave-role launch (4, 16)
+    uint32_t verify_auto_t;  // verify_small = 7: compacting path when >= this many of 64 sampled packets are small
+    uint32_t verify_k2min;   // compacting path: minimum blocks of the long kernel
     uint32_t verify_hdr;  // 1: header bytes ride in the L4 byte gather (no separate header load)
     uint32_t gro_lds;     // 1: GRO finalize with LDS-staged cooperative header loads
     uint32_t gro_wide;    // 1: GRO finalize fields written by two wide stores (LDS variant)
