@@ -269,7 +269,8 @@ int wg_aead_decrypt_verify_batch(const uint8_t *dev_in, uint64_t total_len, uint
  *   dev_in / dev_seg / dev_desc / dev_gso_res: wg_gso_split's dev_in, dev_out,
  *     dev_desc and dev_res (passthrough batches are read from dev_in);
  *   dev_msg_offset[i]: where super-buffer i's messages go in dev_msgs
- *     (16-B aligned), msg_cap bytes available there; its messages follow each
+ *     (16-B aligned), msg_cap bytes available there (the caller owns this
+ *     extent: nothing here can check it on the device); its messages follow each
  *     other at stride 32 + pad16(segment_size), the last one shorter — the
  *     reference's outbuf layout (worker/encap.cpp:131-141,161-168);
  *   max_segments / max_segment_size: bounds over the batch (super-buffers
@@ -450,11 +451,19 @@ int wg_device_count(void);
  *   "verify_occ" verify waves/SIMD target (0 = compiler, 6, 8)
  *   "verify_hdr" verify header bytes from the L4 byte gather (1) or a
  *                separate byte load (0)
- *   "verify_small" verify by the small-packet kernel: packets of <= 64 B
- *                decoded in one lane (1) or redundantly in a lane quad (2),
- *                longer ones by the wave; 3 = split roles (all-small groups
- *                of 4 descriptors a lane per packet, the rest by the wave);
- *                0 = wave-per-packet kernel (default)
+ *   "verify_small" wg_verify_desc kernels: 7 (default) = per call, the
+ *                compacting path (6) when the previous call on the same
+ *                (device, stream) sampled >= verify_auto_t packets of <= 64 B
+ *                among 64 spread descriptors, else the wave-per-packet kernel
+ *                (0), which samples the batch for the next call; 6 = lane per
+ *                descriptor (<= 64 B decoded in the lane, longer ones
+ *                appended to per-shard lists) + a wave kernel over the lists;
+ *                1 / 2 = packets of <= 64 B decoded in one lane / a lane
+ *                quad, longer ones by the same wave; 3 = split roles;
+ *                4 / 5 = lane and wave roles as two launches / one
+ *   "verify_auto_t" the sample threshold of verify_small 7 (1 .. 64)
+ *   "verify_k2min" compacting path: minimum blocks of its wave kernel
+ *                (8 .. 65536; the grid follows the expected long packets)
  *   "gro_lds", "gro_wide"  GRO finalize: LDS-staged loads, wide field stores
  *   "gro_chunks" 16-B header chunks staged per flow (4, 5; with 4, headers
  *                over 48 bytes take the byte path)

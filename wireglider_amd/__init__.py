@@ -466,6 +466,32 @@ def _encap_outputs(inbuf, gso_desc, gso_results, key, msg_offset, results, work,
     return n, results, work, total
 
 
+def _encap_buffers(inbuf, out, out_name, gso_desc, msgs, msg_offset, msg_cap: int, n: int) -> None:
+    """The byte buffers of an encap call: uint8 on inbuf's device.  The caller
+    owns the message extent (msg_offset[i] + msg_cap <= msgs.numel(), every
+    msg_offset[i] a multiple of 16, as include/wireglider_amd.h documents); it
+    is checked here only with WG_DEBUG_CHECKS=1 in the environment (the check
+    copies msg_offset to the host and waits for it)."""
+    import numpy as np
+
+    torch = _torch()
+    for t, nm in ((out, out_name), (msgs, "msgs"), (gso_desc, "gso_desc")):
+        _require_cuda(t, nm)
+        if t.device != inbuf.device:
+            raise WireGliderError(f"{nm}: expected a tensor on {inbuf.device}, got {t.device}")
+    for t, nm in ((out, out_name), (msgs, "msgs")):
+        if t.dtype != torch.uint8:
+            raise WireGliderError(f"{nm}: expected torch.uint8, got {t.dtype}")
+    if n and msgs.numel() < msg_cap:
+        raise WireGliderError(f"msgs: {msgs.numel()} bytes, smaller than one super-buffer's msg_cap {msg_cap}")
+    if n and os.environ.get("WG_DEBUG_CHECKS") == "1":
+        offs = msg_offset[:n].to("cpu").numpy().astype(np.uint64)
+        if (offs % 16).any():
+            raise WireGliderError("msg_offset: every entry must be a multiple of 16")
+        if int(offs.max()) + msg_cap > msgs.numel():
+            raise WireGliderError(f"msgs: {msgs.numel()} bytes, msg_offset + msg_cap reaches {int(offs.max()) + msg_cap}")
+
+
 def encap_encrypt(inbuf, seg_out, gso_desc, gso_results, key: bytes, receiver_index: int, counter0: int, msg_offset,
                   msg_cap: int, max_segments: int, max_segment_size: int, msgs, results=None, work=None, total=None,
                   stream=None):
@@ -475,8 +501,7 @@ def encap_encrypt(inbuf, seg_out, gso_desc, gso_results, key: bytes, receiver_in
     messages of super-buffer i at msg_offset[i] (uint64 device tensor).
     Returns (results uint8 tensor of wg_encap_result, total uint64 tensor)."""
     n, results, work, total = _encap_outputs(inbuf, gso_desc, gso_results, key, msg_offset, results, work, total)
-    for t, nm in ((seg_out, "seg_out"), (msgs, "msgs"), (gso_desc, "gso_desc")):
-        _require_cuda(t, nm)
+    _encap_buffers(inbuf, seg_out, "seg_out", gso_desc, msgs, msg_offset, msg_cap, n)
     with _on(inbuf):
         rc = lib.wg_encap_encrypt(inbuf.data_ptr(), seg_out.data_ptr(), gso_desc.data_ptr(), gso_results.data_ptr(), n,
                                   bytes(key), receiver_index, counter0 & (2**64 - 1), msg_offset.data_ptr(), msg_cap,
@@ -495,8 +520,7 @@ def encap_batch(inbuf, gso_desc, out, gso_results, key: bytes, receiver_index: i
     payload from `inbuf`.  Same results / messages / total as gso_split +
     encap_encrypt; `out` holds the segment headers only."""
     n, results, work, total = _encap_outputs(inbuf, gso_desc, gso_results, key, msg_offset, results, work, total)
-    for t, nm in ((out, "out"), (msgs, "msgs"), (gso_desc, "gso_desc")):
-        _require_cuda(t, nm)
+    _encap_buffers(inbuf, out, "out", gso_desc, msgs, msg_offset, msg_cap, n)
     with _on(inbuf):
         rc = lib.wg_encap_batch(inbuf.data_ptr(), gso_desc.data_ptr(), n, out.data_ptr(), gso_results.data_ptr(),
                                 bytes(key), receiver_index, counter0 & (2**64 - 1), msg_offset.data_ptr(), msg_cap,
