@@ -137,7 +137,10 @@ static Tune &tune_storage() {
         x.verify_dm = 0;
         x.verify_hdr = 1;
         x.verify_small = 7;
-        x.verify_auto_t = 4;
+        // verify_small 7: the kernel choice follows a cost model of the
+        // sampled size mix (l4csum.hip verify_pick_compact); auto_t = the
+        // fewest small packets among the 64 samples that may pick compaction
+        x.verify_auto_t = 1;
         x.verify_k2min = 2048;
         x.verify_wblk = 4;
         x.gro_lds = 1;

@@ -17,6 +17,7 @@
 // traffic.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <mutex>
 
 #include "wg_device.hpp"
@@ -711,6 +712,10 @@ static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
 // header bytes [ihs, 40) and the pseudo-header addresses are added from the
 // byte load once the header is decoded.
 // ---------------------------------------------------------------------------
+typedef unsigned int v16u __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(4))) const v16u c_v16u;  // constant address space: scalar loads
+typedef __attribute__((address_space(4))) const uint32_t c_u32;
+
 struct VerifyParams {
     const uint8_t *base;
     const wg_pkt_desc *desc;  // null: a uniform PacketBatch (seg, total_len)
@@ -725,15 +730,18 @@ struct VerifyParams {
 
 // The size mix of a descriptor batch, for the NEXT call's kernel choice
 // (wg_verify_desc, verify_small = 7): lane k reads descriptor k*n/64 and the
-// wave stores how many of those 64 packets are <= kSmallMax bytes into a
-// host-mapped word (one dword store; the host reads it without waiting).
+// wave stores into two host-mapped words how many of those 64 packets are
+// <= kSmallMax bytes and the summed length of the others (two dword stores;
+// the host reads them without waiting).
 __device__ __forceinline__ void verify_sample(const VerifyParams &p, uint32_t lane) {
     constexpr uint32_t kSmallLen = 64;  // = kSmallMax (declared with the small-packet kernels)
     const uint64_t i = ((uint64_t)lane * p.n) >> 6;
     const uint32_t len = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * i).z;
-    const uint32_t s = (uint32_t)__builtin_popcountll(__ballot(len <= kSmallLen));
-    if (lane == 0)
-        __hip_atomic_store(p.sample, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const bool small = len <= kSmallLen;
+    const uint32_t s = (uint32_t)__builtin_popcountll(__ballot(small));
+    const uint32_t lb = wave_sum_u32(small ? 0u : (len < 65535u ? len : 65535u));
+    if (lane < 2)
+        __hip_atomic_store(p.sample + lane, lane ? lb : s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t j) {
@@ -850,7 +858,10 @@ __device__ __forceinline__ void verify_group(const uint8_t *base, const uint64_t
 // and the summed region starts at byte 32 — no separate header load; else a
 // byte load of header bytes 0-39 per packet and the region from byte 40.
 // kUni: a uniform PacketBatch instead of descriptors (wg_verify_uniform).
-template <int P, int O = 0, int DM = 0, bool H = false, bool kUni = false>  // O: waves/SIMD target (0 = compiler's choice); DM: descriptor mode 0 / 2
+// kD64: a whole group's 4 descriptors (64 B) by one scalar load instead of a
+// load per descriptor (which the compiler issues one after another, each
+// waited for).
+template <int P, int O = 0, int DM = 0, bool H = false, bool kUni = false, bool kD64 = false>  // O: waves/SIMD target (0 = compiler's choice); DM: descriptor mode 0 / 2
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_kernel(
     VerifyParams p) {
     const uint32_t lane = lane_id();
@@ -882,6 +893,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
         for (int j = 0; j < P; j++) {
             doff[j] = o0 + (uint32_t)j * p.seg;
             len[j] = full ? p.seg : (i0 + j + 1 < p.n ? p.seg : (i0 + j + 1 == p.n ? p.last_len : 0u));
+        }
+    } else if (kD64 && P == 4 && i0 + P <= p.n) {
+        const v16u dd = *reinterpret_cast<const c_v16u *>(reinterpret_cast<uintptr_t>(p.desc + i0));
+#pragma unroll
+        for (int j = 0; j < P; j++) {
+            doff[j] = ((uint64_t)dd[4 * j + 1] << 32) | dd[4 * j];
+            len[j] = dd[4 * j + 2];
         }
     } else {
 #pragma unroll
@@ -1272,25 +1290,22 @@ __global__ __launch_bounds__(256) void verify_compact_lane_kernel(VerifyParams p
         verify_sample(p, lane);
 }
 
-template <int O = 8>
+template <int O = 8, bool kLoop = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_compact_long_kernel(
     VerifyParams p, VerifyCompact c) {
     constexpr int P = 4;
     __shared__ uint32_t s_idx[4][P];
     const uint32_t lane0 = lane_id();
     const uint32_t sh = blockIdx.x & (kVShards - 1);
-    const uint32_t nbs = (gridDim.x - sh + kVShards - 1) / kVShards;  // blocks serving this shard
-    const uint64_t step = (uint64_t)nbs * 4u * P;
-    const v4u *e = c.ent + sh * c.cap;
-    uint64_t k0 = ((uint64_t)(blockIdx.x / kVShards) * 4u + wave_in_block()) * P;
-    // the first group's entries load together with the count — no dependent
-    // round trip in front of them (entries past the count are read but not
-    // used; the index is clamped into the list)
-    v4u d[P];
-#pragma unroll
-    for (int j = 0; j < P; j++)
-        d[j] = e[k0 + j < c.cap ? k0 + j : c.cap - 1];
-    const uint32_t cnt = c.ctr[sh * kVCtrStride];
+    const uint32_t step = (gridDim.x / kVShards) * 4u * P;  // grid: a multiple of kVShards (32-bit: a shard's entries < 2^32)
+    // The list and its count were written by the lane kernel (an earlier
+    // launch) and are only read here: constant-address-space loads, so the
+    // 4 entries (64 B) and the count are two scalar loads issued together.
+    const c_v16u *e = reinterpret_cast<const c_v16u *>(reinterpret_cast<uintptr_t>(c.ent + sh * c.cap));
+    uint32_t k0 = ((blockIdx.x / kVShards) * 4u + wave_in_block()) * P;
+    v16u d = e[(k0 < c.cap ? k0 : c.cap - P) / P];  // past the count: read, not used
+    const uint32_t cnt = *reinterpret_cast<const c_u32 *>(reinterpret_cast<uintptr_t>(c.ctr + sh * kVCtrStride));
+    asm volatile("" ::"s"(d[0]), "s"(cnt));  // both in flight before the first wait
     while (k0 < cnt) {
         // the lane id laundered per iteration: the lane-derived constants of
         // verify_group are then recomputed in the body instead of hoisted and
@@ -1301,15 +1316,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
         uint32_t len[P], tgt[P];
 #pragma unroll
         for (int j = 0; j < P; j++) {
-            doff[j] = ((uint64_t)d[j].y << 32) | d[j].x;
-            len[j] = k0 + j < cnt ? d[j].z : 0u;
+            doff[j] = ((uint64_t)d[4 * j + 1] << 32) | d[4 * j];
+            len[j] = k0 + j < cnt ? d[4 * j + 2] : 0u;
             tgt[j] = (uint32_t)j;
         }
         // the packets' indices parked in this wave's LDS words across the
-        // group (held in registers they spill; re-read from memory they put
-        // a dependent load at the end of every wave)
+        // group (held in registers they spill)
         if (lane < (uint32_t)P)
-            s_idx[wave_in_block()][lane] = lane == 0 ? d[0].w : lane == 1 ? d[1].w : lane == 2 ? d[2].w : d[3].w;
+            s_idx[wave_in_block()][lane] = lane == 0 ? d[3] : lane == 1 ? d[7] : lane == 2 ? d[11] : d[15];
         uint32_t rv = 0, rc = 0;
         verify_group<P, true>(p.base, doff, len, tgt, lane, rv, rc, [] {});
         if (lane < (uint32_t)P && k0 + lane < cnt) {
@@ -1318,12 +1332,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
             if (p.l4)
                 p.l4[at] = (uint16_t)rc;
         }
+        if constexpr (!kLoop)
+            break;
         k0 += step;
-        if (k0 < cnt) {
-#pragma unroll
-            for (int j = 0; j < P; j++)
-                d[j] = e[k0 + j < c.cap ? k0 + j : c.cap - 1];
-        }
+        if (k0 < cnt)
+            d = e[k0 / P];
     }
 }
 
@@ -1384,6 +1397,7 @@ VerifyState *verify_state(void *stream) {
     s->host_sample = static_cast<uint32_t *>(h);
     s->dev_sample = static_cast<uint32_t *>(d);
     __atomic_store_n(s->host_sample, kSampleUnknown, __ATOMIC_RELAXED);
+    __atomic_store_n(s->host_sample + 1, 0u, __ATOMIC_RELAXED);
     g_vstate[g_nvstate++] = s;
     return s;
 }
@@ -1435,7 +1449,7 @@ static int verify_compact_launch(VerifyParams p, VerifyState *s, uint64_t est_lo
     const uint64_t nbmax = (p.n + 15) / 16;
     nb = nb > nbmax ? nbmax : nb;
     nb = (nb + kVShards - 1) & ~(uint64_t)(kVShards - 1);
-    hipLaunchKernelGGL(verify_compact_long_kernel<8>, dim3((unsigned)nb), dim3(256), 0, st, p, c);
+    hipLaunchKernelGGL((verify_compact_long_kernel<0, true>), dim3((unsigned)nb), dim3(256), 0, st, p, c);
     if (hipGetLastError() != hipSuccess) {
         // a launch that did not happen may have left a counter set dirty
         (void)hipMemsetAsync(s->ctr, 0, 2u * kVShards * kVCtrStride * 4u, st);
@@ -1445,6 +1459,25 @@ static int verify_compact_launch(VerifyParams p, VerifyState *s, uint64_t est_lo
 }
 
 }  // namespace wg
+
+// verify_small = 7: the compacting path or the wave kernel, from the previous
+// call's sample (smp of 64 spread packets <= 64 B, the others lb bytes in
+// all).  Cost model, measured on MI355X (profiles/r03_verify_*):
+// the wave kernel spends max(0.88 ns, group bytes / 6.5 TB/s) of chip time
+// per 4-packet group whatever sizes the group mixes; the compacting path pays
+// its lane kernel (~7 ps per descriptor + ~8 ps per small packet) and then
+// the long packets' groups at 1.07x the wave kernel's per-group time.
+static bool verify_pick_compact(uint64_t n, uint32_t smp, uint32_t lb, uint32_t min_small) {
+    if (smp < min_small)
+        return false;
+    const double fs = smp / 64.0;
+    const double l_all = (lb + 48.0 * smp) / 64.0;                   // mean length (small ones ~48 B)
+    const double l_long = smp < 64 ? (double)lb / (64 - smp) : 0.0;  // mean length of the long ones
+    auto group_s = [](double mean_len) { return std::max(0.88e-9, 4.0 * mean_len / 6.5e12); };
+    const double t_wave = n / 4.0 * group_s(l_all);
+    const double t_compact = n * (7e-12 + 8e-12 * fs) + 1.07 * (n * (1.0 - fs) / 4.0) * group_s(l_long);
+    return t_compact < 0.97 * t_wave;
+}
 
 static uint64_t verify_wave_blocks(uint64_t n) {
     uint64_t blocks = (n + 15) / 16;  // one-shot 4-packet waves
@@ -1468,16 +1501,17 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
         if (VerifyState *s = verify_state(stream)) {
             std::lock_guard<std::mutex> g(s->mu);
             const uint32_t smp = __atomic_load_n(s->host_sample, __ATOMIC_RELAXED);
+            const uint32_t lb = __atomic_load_n(s->host_sample + 1, __ATOMIC_RELAXED);
             const bool known = smp <= 64u;
-            if (t.verify_small == 6 || (known && smp >= t.verify_auto_t)) {
+            if (t.verify_small == 6 || (known && verify_pick_compact(n, smp, lb, t.verify_auto_t))) {
                 const uint64_t est = known ? (n * (64u - smp) + 63u) / 64u : n;
                 const int rc = verify_compact_launch(p, s, est, t.verify_k2min, st);
                 if (rc != WG_ERR_RUNTIME)
                     return rc;
             }
             p.sample = s->dev_sample;
-            hipLaunchKernelGGL((verify_kernel<4, 8, 0, true>), dim3((unsigned)verify_wave_blocks(n)), dim3(256), 0, st,
-                               p);
+            hipLaunchKernelGGL((verify_kernel<4, 8, 0, true, false, true>), dim3((unsigned)verify_wave_blocks(n)),
+                               dim3(256), 0, st, p);
             return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
         }
     }
