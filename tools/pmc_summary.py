@@ -36,7 +36,8 @@ STEP_KERNELS = {
     "config4strong": ["l4csum_split_kernel"],
     "config4small": ["l4csum_split_kernel"],
     "config5": ["l4csum_split_kernel"],
-    "verify": ["verify_"],
+    "verify": ["verify_kernel<"],
+    "verify64d": ["verify_compact"],
     "verify64": ["verify_"],
     "verify1500u": ["verify_"],
     "gro": ["gro_finalize"],
