@@ -979,17 +979,31 @@ __device__ __forceinline__ void verify_mask(uint64_t m, uint32_t olo, uint32_t o
 // The lane path of the small-packet verify kernels: packet (a, len), len <=
 // kSmallMax, decoded and checked in one lane; verdict bits into rv, the L4
 // result into rc.
-__device__ __forceinline__ void verify_lane(uintptr_t a, uint32_t len, bool use, uint32_t &rv, uint32_t &rc) {
+// Its loads: the packet's five aligned 16-B chunks (clamped chunks lie past
+// the packet and are zeroed by the decode).
+__device__ __forceinline__ void verify_lane_load(uintptr_t a, uint32_t len, bool use, v4u W[5]) {
     const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
     const uintptr_t a0 = a & ~(uintptr_t)15;
     const uintptr_t alast = (a + len - 1) & ~(uintptr_t)15;
     const bool any = use && len;
-    v4u W[5];
 #pragma unroll
     for (uint32_t c = 0; c < 5; c++) {
         const uintptr_t ca = a0 + 16u * c;
-        W[c] = ld16(any ? (ca > alast ? alast : ca) : zero);  // clamped chunks lie past the packet: zeroed below
+        W[c] = ld16(any ? (ca > alast ? alast : ca) : zero);
     }
+}
+
+__device__ __forceinline__ void verify_lane_decode(const v4u W[5], uintptr_t a, uint32_t len, uint32_t &rv,
+                                                   uint32_t &rc);
+
+__device__ __forceinline__ void verify_lane(uintptr_t a, uint32_t len, bool use, uint32_t &rv, uint32_t &rc) {
+    v4u W[5];
+    verify_lane_load(a, len, use, W);
+    verify_lane_decode(W, a, len, rv, rc);
+}
+
+__device__ __forceinline__ void verify_lane_decode(const v4u W[5], uintptr_t a, uint32_t len, uint32_t &rv,
+                                                   uint32_t &rc) {
     const uint32_t Wd[20] = {W[0][0], W[0][1], W[0][2], W[0][3], W[1][0], W[1][1], W[1][2], W[1][3],
                              W[2][0], W[2][1], W[2][2], W[2][3], W[3][0], W[3][1], W[3][2], W[3][3],
                              W[4][0], W[4][1], W[4][2], W[4][3]};
@@ -1260,8 +1274,7 @@ __global__ __launch_bounds__(256) void verify_compact_lane_kernel(VerifyParams p
         c.ctr_next[threadIdx.x * kVCtrStride] = 0;
     // the small packets: loads issued before the block synchronises
     uint32_t rv = 0, rc = 0;
-    const bool any_small = __ballot(small) != 0;
-    if (any_small)
+    if (__ballot(small))  // wave-uniform
         verify_lane(reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)dv.y << 32) | dv.x), small ? len : 0u, small,
                     rv, rc);
     // the long packets: block-aggregated append to this block's shard
@@ -1429,10 +1442,11 @@ namespace wg {
 // expected long packets (grid-stride, so a low estimate is only slower).
 static int verify_compact_launch(VerifyParams p, VerifyState *s, uint64_t est_long, uint64_t kmin,
                                  hipStream_t st) {
-    uint64_t nl = (p.n + 255) / 256;
+    const uint64_t per_block = 256u;  // descriptors per lane-kernel block
+    uint64_t nl = (p.n + per_block - 1) / per_block;
     if (nl >= 8)
         nl = (nl + 7) & ~7ull;
-    const uint64_t cap = 256u * ((nl + kVShards - 1) / kVShards);
+    const uint64_t cap = per_block * ((nl + kVShards - 1) / kVShards);
     if (nl > 0x7fffffffull || p.n >= (1ull << 32) || !verify_reserve(s, cap, st))
         return WG_ERR_RUNTIME;  // the caller runs the wave kernel instead
     VerifyCompact c{s->ent, s->cap, s->ctr + s->parity * kVShards * kVCtrStride,
@@ -1604,7 +1618,7 @@ extern "C" int wg_verify_uniform(const uint8_t *dev_base, uint64_t total_len, ui
     VerifyParams p{dev_base, nullptr, dev_verdict, dev_l4, nseg, total_len, segment_size,
                    (uint32_t)(total_len - (nseg - 1) * segment_size)};
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (segment_size <= kSmallMax) {  // every segment small: a lane each (knob-free: no long packets to serve)
+    if (segment_size <= kSmallMax) {  // every segment small: a lane each (no long packets to serve)
         uint64_t b = (p.n + 255) / 256;
         if (b >= 8) b = (b + 7) & ~7ull;
         if (b > 0x7fffffffull)
