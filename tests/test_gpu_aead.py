@@ -45,7 +45,7 @@ ENC_CASES = [(1460, 1460 * 40 + 777), (1460, 1460 * 3), (64, 64 * 300 + 1), (1, 
 
 
 @pytest.fixture(params=[(1, 0, 0), (2, 0, 0), (2, 1, 0), (4, 0, 0), (4, 1, 0), (2, 1, 1), (3, 1, 1), (3, 0, 1),
-                        (4, 1, 1), (1, 0, 1)],
+                        (4, 1, 1), (1, 0, 1), (3, 2, 1), (3, 2, 0), (0, 2, 1), (2, 2, 1)],
                 ids=lambda kp: f"aead_k={kp[0]},pair={kp[1]},flex={kp[2]}")
 def aead_k(request):
     """Every lane-blocking variant (consecutive ChaCha20 blocks per lane, the

@@ -567,8 +567,8 @@ constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/prot
 // are (the headers-only split writes exactly those bytes), every later
 // block from the input itself, where plaintext byte q >= hdr_len of segment
 // s is input byte s * gso + q — one source per block, no merge.
-template <int G, int K, bool kDec, bool kP = false, bool kVer = false, int kGso = 0>
-__global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
+template <int G, int K, bool kDec, int kP = 0, bool kVer = false, int kGso = 0>  // kP: 1 pairs, 2 + K = 3's third block up front
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kP == 2 ? 4 : 1, 8))) void aead_kernel(AeadParams p) {
     constexpr bool kFlex = G == 0;
     const uint32_t GG = kFlex ? p.grp : (uint32_t)G;  // lanes per packet
     const uint32_t kPer = kFlex ? 64u / GG : 64u / (uint32_t)(G ? G : 1);  // packets per wave
@@ -651,11 +651,17 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     // kPair (K = 2 or 4, one pass): the lane's blocks two at a time, each
     // pair interleaved (chacha20_block2); the first pair up front
     constexpr bool kPair = kP && K >= 2 && G < 64;
-    uint32_t ks[16], ks1[16];
+    // kP = 2, K = 3, one pass: the lane's third block computed up front too,
+    // so its quarter rounds sit in the same straight-line code as the first
+    // two blocks' XOR / store / Poly1305 chains (dependent multiply-adds)
+    constexpr bool kTri = kP == 2 && K == 3 && G < 64;
+    uint32_t ks[16], ks1[16], ks2[kTri ? 16 : 1];
     if constexpr (kPair)
         chacha20_block2(p.key, g * (uint32_t)K, n0, n1, n2, ks, ks1);
     else
         chacha20_block(p.key, g * (uint32_t)K, n0, n1, n2, ks);
+    if constexpr (kTri)
+        chacha20_block(p.key, g * (uint32_t)K + 2u, n0, n1, n2, ks2);
     const uint32_t base_lane = kFlex ? slot * GG : lane & ~(uint32_t)(G - 1);
     uint32_t rw[4], sw[4];
 #pragma unroll
@@ -830,6 +836,10 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             if constexpr (kPair) {
                 block(cf + 1u, ks1);
                 j0 = 2;
+            }
+            if constexpr (kTri) {
+                block(cf + 2u, ks2);
+                j0 = 3;
             }
         }
         if constexpr (kPair) {
@@ -1054,7 +1064,9 @@ template <int G, int K, bool kDec>
 static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
     if constexpr (!kDec) {
         if (p.eres) {  // encap: GSO segments (with the pair interleave where it applies)
-            constexpr bool kPg = K >= 2 && G < 64;
+            // (the third block up front, aead_pair = 2, spills in this
+            // geometry: encap 19.44 -> 20.09 ms, profiles/r03_aead_tri_ab.json)
+            constexpr int kPg = K >= 2 && G < 64 ? 1 : 0;
             if (p.gmode == 2)
                 hipLaunchKernelGGL((aead_kernel<G, K, false, kPg, false, 2>), dim3((unsigned)blocks), dim3(256), 0,
                                    st, p);
@@ -1066,14 +1078,19 @@ static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
     }
     if constexpr (kDec) {
         if (p.verdict) {  // decrypt + verify (always with the pair interleave where it applies)
-            constexpr bool kPv = K >= 2 && G < 64;
+            constexpr int kPv = K >= 2 && G < 64 ? 1 : 0;
             hipLaunchKernelGGL((aead_kernel<G, K, true, kPv, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
             return;
         }
     }
     if constexpr (K >= 2 && G < 64) {
-        if (tune().aead_pair) {
-            hipLaunchKernelGGL((aead_kernel<G, K, kDec, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+        const uint32_t pair = tune().aead_pair;
+        if (pair == 2 && !kDec) {  // encrypt: 1.297 -> 1.275 ms (profiles/r03_aead_tri_ab.json)
+            hipLaunchKernelGGL((aead_kernel<G, K, kDec, 2>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+            return;
+        }
+        if (pair) {
+            hipLaunchKernelGGL((aead_kernel<G, K, kDec, 1>), dim3((unsigned)blocks), dim3(256), 0, st, p);
             return;
         }
     }

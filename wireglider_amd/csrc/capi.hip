@@ -64,7 +64,7 @@ static const Knob kKnobs[] = {
     {"l4_coop_waves", nullptr, &Tune::l4_coop_waves, 0, 0, kCoopW, WG_N(kCoopW)},
     {"l4_split_waves", nullptr, &Tune::l4_split_waves, 0, 0, kSplitW, WG_N(kSplitW)},
     {"aead_k", nullptr, &Tune::aead_k, 0, 0, kAeadK, WG_N(kAeadK)},
-    {"aead_pair", nullptr, &Tune::aead_pair, 0, 1, nullptr, 0},
+    {"aead_pair", nullptr, &Tune::aead_pair, 0, 2, nullptr, 0},
     {"aead_flex", nullptr, &Tune::aead_flex, 0, 1, nullptr, 0},
     {"encap_parts", nullptr, &Tune::encap_parts, 0, 0, kParts, WG_N(kParts)},
 };
@@ -181,7 +181,10 @@ static Tune &tune_storage() {
         // K = 2 in 16-lane groups 1.506 (profiles/r02_aead_flex_ab.json), the
         // interleave -8 % (profiles/r02_aead_pair_ab.json)
         x.aead_k = 0;
-        x.aead_pair = 1;
+        // 2: encrypt batches also compute a lane's third block (K = 3) up
+        // front with the pair, 128 VGPRs forced (a 20-B spill): -1.7 %
+        // (profiles/r03_aead_tri_ab.json); decrypt and encap keep 1
+        x.aead_pair = 2;
         x.aead_flex = 1;
         x.encap_parts = 1;
         // environment overrides: WG_<KNOB> (upper case), same accepted values
