@@ -567,8 +567,8 @@ constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/prot
 // are (the headers-only split writes exactly those bytes), every later
 // block from the input itself, where plaintext byte q >= hdr_len of segment
 // s is input byte s * gso + q — one source per block, no merge.
-template <int G, int K, bool kDec, int kP = 0, bool kVer = false, int kGso = 0>  // kP: 1 pairs, 2 + K = 3's third block up front
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kP == 2 ? 4 : 1, 8))) void aead_kernel(AeadParams p) {
+template <int G, int K, bool kDec, int kP = 0, bool kVer = false, int kGso = 0>  // kP: 1 pairs; 2 + K = 3's third block up front
+__global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     constexpr bool kFlex = G == 0;
     const uint32_t GG = kFlex ? p.grp : (uint32_t)G;  // lanes per packet
     const uint32_t kPer = kFlex ? 64u / GG : 64u / (uint32_t)(G ? G : 1);  // packets per wave
@@ -653,7 +653,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kP == 2 ? 4
     constexpr bool kPair = kP && K >= 2 && G < 64;
     // kP = 2, K = 3, one pass: the lane's third block computed up front too,
     // so its quarter rounds sit in the same straight-line code as the first
-    // two blocks' XOR / store / Poly1305 chains (dependent multiply-adds)
+    // two blocks' XOR / store / Poly1305 chains (dependent multiply-adds).
+    // 141 VGPRs, 3 waves/SIMD, and still faster: the waves wait on dependent
+    // VALU issue, not on memory (forcing 4 waves/SIMD spills and loses half
+    // the gain; profiles/r03_aead_tri_ab.json)
     constexpr bool kTri = kP == 2 && K == 3 && G < 64;
     uint32_t ks[16], ks1[16], ks2[kTri ? 16 : 1];
     if constexpr (kPair)
@@ -1064,10 +1067,13 @@ template <int G, int K, bool kDec>
 static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
     if constexpr (!kDec) {
         if (p.eres) {  // encap: GSO segments (with the pair interleave where it applies)
-            // (the third block up front, aead_pair = 2, spills in this
-            // geometry: encap 19.44 -> 20.09 ms, profiles/r03_aead_tri_ab.json)
+            // the third block up front too (aead_pair = 2): encap 19.33 ->
+            // 18.55 ms (profiles/r03_aead_tri_ab.json)
             constexpr int kPg = K >= 2 && G < 64 ? 1 : 0;
-            if (p.gmode == 2)
+            if (p.gmode == 2 && kPg && tune().aead_pair == 2)
+                hipLaunchKernelGGL((aead_kernel<G, K, false, 2, false, 2>), dim3((unsigned)blocks), dim3(256), 0,
+                                   st, p);
+            else if (p.gmode == 2)
                 hipLaunchKernelGGL((aead_kernel<G, K, false, kPg, false, 2>), dim3((unsigned)blocks), dim3(256), 0,
                                    st, p);
             else
@@ -1085,7 +1091,7 @@ static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
     }
     if constexpr (K >= 2 && G < 64) {
         const uint32_t pair = tune().aead_pair;
-        if (pair == 2 && !kDec) {  // encrypt: 1.297 -> 1.275 ms (profiles/r03_aead_tri_ab.json)
+        if (pair == 2 && !kDec) {  // encrypt: 1.343 -> 1.256 ms (profiles/r03_aead_tri_ab.json)
             hipLaunchKernelGGL((aead_kernel<G, K, kDec, 2>), dim3((unsigned)blocks), dim3(256), 0, st, p);
             return;
         }
