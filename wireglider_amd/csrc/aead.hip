@@ -124,6 +124,102 @@ __device__ __forceinline__ void chacha20_block2(const AeadKey &key, uint32_t ctr
         o1[m] = y[m] + (m == 12 ? ctr + 1u : init[m]);
     }
 }
+// Columns 1-3 of round 1 involve key, constants and nonce only, never the
+// block counter (state word 12 is column 0's): one lane's blocks share them,
+// so they are computed once per lane and every block starts from them
+// (36 of ~960 quarter-round operations per block).
+struct ChaPre {
+    uint32_t v[12];  // x1 x5 x9 x13, x2 x6 x10 x14, x3 x7 x11 x15 after round 1's column quarter rounds
+};
+
+__device__ __forceinline__ ChaPre chacha_pre(const AeadKey &key, uint32_t n0, uint32_t n1, uint32_t n2) {
+    uint32_t x1 = 0x3320646eu, x5 = key.k[1], x9 = key.k[5], x13 = n0;
+    uint32_t x2 = 0x79622d32u, x6 = key.k[2], x10 = key.k[6], x14 = n1;
+    uint32_t x3 = 0x6b206574u, x7 = key.k[3], x11 = key.k[7], x15 = n2;
+    WG_QR(x1, x5, x9, x13);
+    WG_QR(x2, x6, x10, x14);
+    WG_QR(x3, x7, x11, x15);
+    return ChaPre{{x1, x5, x9, x13, x2, x6, x10, x14, x3, x7, x11, x15}};
+}
+
+// Round 1 of a block from the shared columns: column 0 (the counter's), the
+// precomputed columns 1-3, then the diagonals.
+__device__ __forceinline__ void chacha_round1(const AeadKey &key, uint32_t ctr, const ChaPre &pc, uint32_t x[16]) {
+    x[0] = 0x61707865u;
+    x[4] = key.k[0];
+    x[8] = key.k[4];
+    x[12] = ctr;
+    WG_QR(x[0], x[4], x[8], x[12]);
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        x[1 + c] = pc.v[4 * c];
+        x[5 + c] = pc.v[4 * c + 1];
+        x[9 + c] = pc.v[4 * c + 2];
+        x[13 + c] = pc.v[4 * c + 3];
+    }
+    WG_QR(x[0], x[5], x[10], x[15]);
+    WG_QR(x[1], x[6], x[11], x[12]);
+    WG_QR(x[2], x[7], x[8], x[13]);
+    WG_QR(x[3], x[4], x[9], x[14]);
+}
+
+// chacha20_block / chacha20_block2 from the shared round-1 columns.
+__device__ __forceinline__ void chacha20_block_pre(const AeadKey &key, uint32_t ctr, uint32_t n0, uint32_t n1,
+                                                   uint32_t n2, const ChaPre &pc, uint32_t out[16]) {
+    uint32_t x[16];
+    chacha_round1(key, ctr, pc, x);
+#pragma unroll 3
+    for (int i = 1; i < 10; i++) {
+        WG_QR(x[0], x[4], x[8], x[12]);
+        WG_QR(x[1], x[5], x[9], x[13]);
+        WG_QR(x[2], x[6], x[10], x[14]);
+        WG_QR(x[3], x[7], x[11], x[15]);
+        WG_QR(x[0], x[5], x[10], x[15]);
+        WG_QR(x[1], x[6], x[11], x[12]);
+        WG_QR(x[2], x[7], x[8], x[13]);
+        WG_QR(x[3], x[4], x[9], x[14]);
+    }
+    const uint32_t init[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key.k[0], key.k[1], key.k[2],
+                               key.k[3],    key.k[4],    key.k[5],    key.k[6],    key.k[7], ctr,      n0,
+                               n1,          n2};
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+        out[m] = x[m] + init[m];
+}
+
+__device__ __forceinline__ void chacha20_block2_pre(const AeadKey &key, uint32_t ctr, uint32_t n0, uint32_t n1,
+                                                    uint32_t n2, const ChaPre &pc, uint32_t o0[16], uint32_t o1[16]) {
+    uint32_t x[16], y[16];
+    chacha_round1(key, ctr, pc, x);
+    chacha_round1(key, ctr + 1u, pc, y);
+#pragma unroll 3
+    for (int i = 1; i < 10; i++) {
+        WG_QR(x[0], x[4], x[8], x[12]);
+        WG_QR(y[0], y[4], y[8], y[12]);
+        WG_QR(x[1], x[5], x[9], x[13]);
+        WG_QR(y[1], y[5], y[9], y[13]);
+        WG_QR(x[2], x[6], x[10], x[14]);
+        WG_QR(y[2], y[6], y[10], y[14]);
+        WG_QR(x[3], x[7], x[11], x[15]);
+        WG_QR(y[3], y[7], y[11], y[15]);
+        WG_QR(x[0], x[5], x[10], x[15]);
+        WG_QR(y[0], y[5], y[10], y[15]);
+        WG_QR(x[1], x[6], x[11], x[12]);
+        WG_QR(y[1], y[6], y[11], y[12]);
+        WG_QR(x[2], x[7], x[8], x[13]);
+        WG_QR(y[2], y[7], y[8], y[13]);
+        WG_QR(x[3], x[4], x[9], x[14]);
+        WG_QR(y[3], y[4], y[9], y[14]);
+    }
+    const uint32_t init[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key.k[0], key.k[1], key.k[2],
+                               key.k[3],    key.k[4],    key.k[5],    key.k[6],    key.k[7], ctr,      n0,
+                               n1,          n2};
+#pragma unroll
+    for (int m = 0; m < 16; m++) {
+        o0[m] = x[m] + init[m];
+        o1[m] = y[m] + (m == 12 ? ctr + 1u : init[m]);
+    }
+}
 #undef WG_QR
 
 // ---------------------------------------------------------------------------
@@ -659,12 +755,15 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     // the gain; profiles/r03_aead_tri_ab.json)
     constexpr bool kTri = kP == 2 && K == 3 && G < 64;
     uint32_t ks[16], ks1[16], ks2[kTri ? 16 : 1];
-    if constexpr (kPair)
-        chacha20_block2(p.key, g * (uint32_t)K, n0, n1, n2, ks, ks1);
-    else
-        chacha20_block(p.key, g * (uint32_t)K, n0, n1, n2, ks);
-    if constexpr (kTri)
-        chacha20_block(p.key, g * (uint32_t)K + 2u, n0, n1, n2, ks2);
+    {
+        const ChaPre pc = chacha_pre(p.key, n0, n1, n2);
+        if constexpr (kPair)
+            chacha20_block2_pre(p.key, g * (uint32_t)K, n0, n1, n2, pc, ks, ks1);
+        else
+            chacha20_block_pre(p.key, g * (uint32_t)K, n0, n1, n2, pc, ks);
+        if constexpr (kTri)
+            chacha20_block_pre(p.key, g * (uint32_t)K + 2u, n0, n1, n2, pc, ks2);
+    }
     const uint32_t base_lane = kFlex ? slot * GG : lane & ~(uint32_t)(G - 1);
     uint32_t rw[4], sw[4];
 #pragma unroll

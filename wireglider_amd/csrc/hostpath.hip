@@ -43,11 +43,11 @@ struct DeviceScope {
         if (hipGetDevice(&prev) != hipSuccess)
             prev = -1;
         if (d >= 0 && prev != d)
-            hipSetDevice(d);
+            (void)hipSetDevice(d);
     }
     ~DeviceScope() {
         if (prev >= 0)
-            hipSetDevice(prev);
+            (void)hipSetDevice(prev);
     }
 };
 
@@ -71,11 +71,11 @@ struct Pipe {
 std::atomic<bool> g_exiting{false};
 
 void free_dev(DevBuf &b) {
-    if (b.p) hipFree(b.p);
+    if (b.p) (void)hipFree(b.p);  // teardown: nothing left to report to
     b = DevBuf{};
 }
 void free_pin(DevBuf &b) {
-    if (b.p) hipHostFree(b.p);
+    if (b.p) (void)hipHostFree(b.p);
     b = DevBuf{};
 }
 
@@ -84,20 +84,20 @@ void Pipe::release() {
         return;
     DeviceScope ds(device);
     for (hipStream_t st : s)
-        if (st) hipStreamSynchronize(st);
+        if (st) (void)hipStreamSynchronize(st);
     for (int k = 0; k < kSlots; k++) {
         for (DevBuf &b : dev[k]) free_dev(b);
         free_pin(stage[k]);
-        if (copied[k]) hipEventDestroy(copied[k]);
-        if (computed[k]) hipEventDestroy(computed[k]);
-        if (drained[k]) hipEventDestroy(drained[k]);
+        if (copied[k]) (void)hipEventDestroy(copied[k]);
+        if (computed[k]) (void)hipEventDestroy(computed[k]);
+        if (drained[k]) (void)hipEventDestroy(drained[k]);
         copied[k] = computed[k] = drained[k] = nullptr;
     }
     for (DevBuf &b : gather) free_pin(b);
     free_dev(ctr);
     free_pin(hctr);
     for (hipStream_t &st : s) {
-        if (st) hipStreamDestroy(st);
+        if (st) (void)hipStreamDestroy(st);
         st = nullptr;
     }
     device = -1;
