@@ -1184,13 +1184,16 @@ static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
     if constexpr (kDec) {
         if (p.verdict) {  // decrypt + verify (always with the pair interleave where it applies)
             constexpr int kPv = K >= 2 && G < 64 ? 1 : 0;
-            hipLaunchKernelGGL((aead_kernel<G, K, true, kPv, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+            if (kPv && tune().aead_pair == 2)
+                hipLaunchKernelGGL((aead_kernel<G, K, true, 2, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+            else
+                hipLaunchKernelGGL((aead_kernel<G, K, true, kPv, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
             return;
         }
     }
     if constexpr (K >= 2 && G < 64) {
         const uint32_t pair = tune().aead_pair;
-        if (pair == 2 && !kDec) {  // encrypt: 1.343 -> 1.256 ms (profiles/r03_aead_tri_ab.json)
+        if (pair == 2) {  // encrypt: 1.343 -> 1.256 ms (profiles/r03_aead_tri_ab.json)
             hipLaunchKernelGGL((aead_kernel<G, K, kDec, 2>), dim3((unsigned)blocks), dim3(256), 0, st, p);
             return;
         }
