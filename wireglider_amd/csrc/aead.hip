@@ -1193,7 +1193,7 @@ static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
     }
     if constexpr (K >= 2 && G < 64) {
         const uint32_t pair = tune().aead_pair;
-        if (pair == 2) {  // encrypt: 1.343 -> 1.256 ms (profiles/r03_aead_tri_ab.json)
+        if (pair == 2) {  // encrypt 1.343 -> 1.256 ms, decrypt 1.356 -> 1.316 ms (profiles/r03_aead_tri_*)
             hipLaunchKernelGGL((aead_kernel<G, K, kDec, 2>), dim3((unsigned)blocks), dim3(256), 0, st, p);
             return;
         }

@@ -181,9 +181,10 @@ static Tune &tune_storage() {
         // K = 2 in 16-lane groups 1.506 (profiles/r02_aead_flex_ab.json), the
         // interleave -8 % (profiles/r02_aead_pair_ab.json)
         x.aead_k = 0;
-        // 2: encrypt batches and the encap step also compute a lane's third
-        // block (K = 3) up front with the pair (3 waves/SIMD): encrypt -6.5 %,
-        // encap -4 % (profiles/r03_aead_tri_ab.json); decrypt keeps the pair
+        // 2: a lane's third block (K = 3) computed up front with the pair
+        // too (3 waves/SIMD): encrypt -6.5 %, encap -4 %, decrypt and the
+        // fused decrypt + verify -3-4 % (profiles/r03_aead_tri_ab.json,
+        // profiles/r03_aead_tri_decrypt.txt)
         x.aead_pair = 2;
         x.aead_flex = 1;
         x.encap_parts = 1;
