@@ -278,3 +278,22 @@ def test_decap_host_pinned_two_threads(gpu, small_chunks, d2h, mode):
         check_decap(*work[k], out[k])
     for p in pins:
         p.close()
+
+
+@pytest.mark.gpu
+def test_host_path_keeps_current_device(gpu):
+    """The host-memory entries and wg_host_release set the pipeline's device
+    for their own scope and restore the caller's current device (ADVICE r02:
+    release() had left it switched)."""
+    import torch
+
+    wga = _wga()
+    before = torch.cuda.current_device()
+    buf = bytes(np.random.default_rng(5).integers(0, 256, 1500 * 64, dtype=np.uint8))
+    wga.calc_l4_checksum_host(buf, 1500, False, False, 20)
+    assert torch.cuda.current_device() == before
+    wga.host_release()
+    assert torch.cuda.current_device() == before
+    wga.calc_l4_checksum_host(buf, 1500, False, False, 20)  # the pipeline rebuilt after a release
+    wga.host_release()
+    assert torch.cuda.current_device() == before
