@@ -683,7 +683,7 @@ int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, u
         blocks &= ~7ull;  // the XCD swizzle wants a multiple of 8 (the grid-stride loop covers the rest)
     const dim3 g((unsigned)blocks, t.gso_split);
     if (hdr_only) {
-        switch (t.gso_spw) {
+        switch (t.encap_spw) {  // the encap step's own value: it stores headers only (3 there, 4 for the full split)
         case 1: launch_split<1, kHdrOnly>(p, g, t.gso_waves, st); break;
         case 2: launch_split<2, kHdrOnly>(p, g, t.gso_waves, st); break;
         case 3: launch_split<3, kHdrOnly>(p, g, t.gso_waves, st); break;

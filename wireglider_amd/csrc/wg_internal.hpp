@@ -25,6 +25,7 @@ struct Tune {
     uint32_t gso_split;   // blocks per super-buffer (grid y)
     uint32_t gso_groups;  // blocks per super-buffer, consecutive in the flat grid (one-shot waves)
     uint32_t gso_spw;     // segments per wave step: 0 one at a time, 1 ping-pong pipeline, 2-4 issued together
+    uint32_t encap_spw;   // the same for the encap step's headers-only split
     uint32_t verify_dm;   // verify kernel descriptor mode: 0 one-shot waves, 2 next-iteration prefetch (l4_iters)
     uint32_t verify_occ;  // waves/SIMD target of the verify kernel (0 = compiler's choice; 8)
     uint32_t verify_small;  // 1: verify by the lane-per-descriptor kernel (packets <= 64 B decoded in a lane)
