@@ -447,6 +447,9 @@ int wg_device_count(void);
  *   "gso_waves"  waves per GSO block (1, 2, 4, 8)
  *   "gso_split"  further blocks per super-buffer in grid y (1 .. 64)
  *   "gso_spw"    segments per wave step: 0 serial, 1 ping-pong, 2-4 issued together (4)
+ *   "encap_spw"  the same for wg_encap_batch's headers-only split (3)
+ *   "encap_parts" wg_encap_batch in slices, each split on a side stream under
+ *                the previous slice's AEAD (1 = not pipelined, default; 2-8)
  *   "verify_dm"  verify descriptor mode: 0 one-shot waves, 2 prefetch
  *   "verify_occ" verify waves/SIMD target (0 = compiler, 6, 8)
  *   "verify_hdr" verify header bytes from the L4 byte gather (1) or a
@@ -478,7 +481,8 @@ int wg_device_count(void);
  *   "aead_k"     AEAD kernels: consecutive ChaCha20 blocks per lane (1-4; 0
  *                = 2 or 3, whichever fills a wave better for the batch)
  *   "aead_pair"  a lane's blocks computed two at a time, interleaved (1),
- *                or one after the other (0)
+ *                and with K = 3 the third one up front beside them (2,
+ *                default), or one after the other (0)
  *   "aead_flex"  groups of exactly the lanes a packet needs (1, up to 32)
  *                or the next power of two (0)
  *   "gso_ablate" GSO A/B variants: 1 = non-temporal payload stores, 32 = no
