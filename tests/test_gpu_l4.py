@@ -118,7 +118,9 @@ DESC_VARIANTS = [{"l4_occ": 0}, {"l4_occ": 7}, {"l4_occ": 8}, {"l4_descv": 1}, {
                  {"l4_small": 1, "l4_nt": 0}, {"l4_small": 5}, {"l4_small": 5, "l4_nt": 0},
                  {"l4_coop": 1 << 20, "l4_coop_waves": 2}, {"l4_coop": 1 << 20, "l4_coop_waves": 4, "l4_unroll": 4},
                  {"l4_coop": 1 << 20, "l4_coop_waves": 8, "l4_nt": 0}, {"l4_coop": 1 << 20, "l4_coop_waves": 16},
-                 {"l4_small": 5, "l4_split_waves": 8}, {"l4_small": 5, "l4_split_waves": 8, "l4_unroll": 4}]
+                 {"l4_small": 5, "l4_split_waves": 8}, {"l4_small": 5, "l4_split_waves": 8, "l4_unroll": 4},
+                 {"l4_small": 6}, {"l4_small": 6, "l4_unroll": 4}, {"l4_small": 6, "l4_nt": 0},
+                 {"l4_small": 7}, {"l4_small": 7, "l4_unroll": 4}]
 
 
 @pytest.mark.parametrize("knobs", DESC_VARIANTS, ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()))
@@ -188,7 +190,7 @@ def test_uniform_small_segments(gpu, seg, knob):
         wga.tune_set("l4_small_uniform", saved)
 
 
-@pytest.mark.parametrize("small", [0, 1, 2, 3, 4, 5, 58])
+@pytest.mark.parametrize("small", [0, 1, 2, 3, 4, 5, 58, 6, 7])
 @pytest.mark.parametrize("seed", [5, 6])
 def test_desc_small_packets(gpu, small, seed):
     """Batches of mostly small packets (0-130 B, every alignment, csum_start

@@ -149,7 +149,10 @@ VERIFY_VARIANTS = [{"verify_dm": 0, "verify_occ": 8, "verify_hdr": 1}, {"verify_
                    {"verify_small": 4, "verify_wblk": 16},
                    {"verify_small": 5}, {"verify_small": 5, "verify_occ": 0},
                    {"verify_small": 6}, {"verify_small": 6, "verify_k2min": 8}, {"verify_small": 7},
-                   {"verify_small": 7, "verify_auto_t": 1}]
+                   {"verify_small": 7, "verify_auto_t": 1},
+                   {"verify_small": 8}, {"verify_small": 8, "verify_occ": 0}, {"verify_small": 8, "verify_dm": 2},
+                   {"verify_small": 9}, {"verify_small": 9, "verify_occ": 0},
+                   {"verify_small": 10}, {"verify_small": 10, "verify_occ": 0}]
 
 
 @pytest.mark.gpu

@@ -38,7 +38,7 @@ static const Knob kKnobs[] = {
     {"l4_descv", nullptr, &Tune::l4_descv, 0, 2, nullptr, 0},
     {"l4_iters", nullptr, &Tune::l4_iters, 1, 64, nullptr, 0},
     {"l4_occ", nullptr, &Tune::l4_occ, 0, 0, kOcc, WG_N(kOcc)},
-    {"l4_small", nullptr, &Tune::l4_small, 0, 5, nullptr, 0},
+    {"l4_small", nullptr, &Tune::l4_small, 0, 7, nullptr, 0},
     {"l4_small_uniform", nullptr, &Tune::l4_small_uniform, 0, 2, nullptr, 0},
     {"gso_blocks", &Tune::gso_blocks, nullptr, 1, 1u << 23, nullptr, 0},
     {"gso_waves", nullptr, &Tune::gso_waves, 0, 0, kWaves, WG_N(kWaves)},
@@ -49,7 +49,7 @@ static const Knob kKnobs[] = {
     {"verify_dm", nullptr, &Tune::verify_dm, 0, 0, kDm, WG_N(kDm)},
     {"verify_occ", nullptr, &Tune::verify_occ, 0, 0, kVOcc, WG_N(kVOcc)},
     {"verify_hdr", nullptr, &Tune::verify_hdr, 0, 1, nullptr, 0},
-    {"verify_small", nullptr, &Tune::verify_small, 0, 7, nullptr, 0},
+    {"verify_small", nullptr, &Tune::verify_small, 0, 10, nullptr, 0},
     {"verify_auto_t", nullptr, &Tune::verify_auto_t, 1, 64, nullptr, 0},
     {"verify_k2min", nullptr, &Tune::verify_k2min, 8, 65536, nullptr, 0},
     {"verify_wblk", nullptr, &Tune::verify_wblk, 0, 0, kWblk, WG_N(kWblk)},

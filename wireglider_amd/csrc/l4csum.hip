@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 
 #include "wg_device.hpp"
@@ -507,6 +508,115 @@ __global__ __launch_bounds__(64 * kW) void l4csum_split_kernel(L4Params p) {
     }
 }
 
+// Walking descriptor kernel (knob l4_small = 6).  A wave per 64 descriptors
+// whatever their sizes, laid out so that the waves resident at any moment
+// touch one narrow window of the batch: lane l of wave w (of G) owns
+// descriptor ((l >> 2) * G + w) * 4 + (l & 3) — sixteen 4-descriptor groups a
+// sixteenth of the batch apart.  Small packets (<= kSmallMax) are summed in
+// their lane (lane_chunks / lane_sum); the wave then walks its long packets in
+// group order, 4 at a time, through the wave-per-packet issue / finish
+// machinery.  An all-small batch costs n / 64 waves (the split kernel's n / 16
+// waves spend three of every four on one descriptor load), an all-long batch
+// 16 groups per wave.
+template <int kKind, bool kNT, int U = 4>
+__global__ __launch_bounds__(256) void l4csum_walk_kernel(L4Params p) {
+    constexpr bool kL4 = kKind != kDescPlain;
+    const uint32_t lane = lane_id();
+    const uint64_t G = (uint64_t)gridDim.x * 4u;
+    const uint64_t w = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
+    const uint64_t i = ((uint64_t)(lane >> 2) * G + w) * 4u + (lane & 3u);
+    const bool live = i < p.n;
+    const v4u d = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0u));
+    const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + (live ? off : 0u);
+    const uint32_t len = live ? d.z : 0u;
+    const uint32_t cs = kL4 && live ? (d.w & 0xffffu) : 0u;
+    const uint32_t fl = live ? (d.w >> 16) & 0xffu : 0u;
+    const bool small = live && len <= kSmallMax;
+    uint32_t res = 0;
+    if (__ballot(small)) {  // wave-uniform
+        v4u W[5];
+        lane_chunks(a, len, small && len, W);
+        const uint32_t t = lane_sum<kL4>(W, a, small ? len : 0u, cs, fl);
+        res = ~fold16_32(t) & 0xffffu;
+    }
+    wave_long<kL4, kNT, 4, U>(__ballot(live && !small), a, len, cs, fl, p.base, lane, res);
+    if (live)
+        p.out[i] = (uint16_t)res;
+}
+
+// Persistent walking kernel (knob l4_small = 7): the walking kernel's lane /
+// wave split, but the grid is the device's resident wave capacity (or n / 64
+// waves if fewer) and each wave takes ROUNDS of 16 groups — in round r lane l
+// owns descriptor ((16 r + (l >> 2)) * G + w) * 4 + (l & 3) — so every wave
+// gets the same number of groups to within one, whatever n (a grid of n / 64
+// waves is 2.3 generations of resident waves for 1 M descriptors: its last
+// partial generation ran at a third of the chip), and the waves resident at
+// any moment still work on one narrow window of the batch.
+template <int kKind, bool kNT, int U = 4>
+__global__ __launch_bounds__(256) void l4csum_persist_kernel(L4Params p) {
+    constexpr bool kL4 = kKind != kDescPlain;
+    const uint64_t G = (uint64_t)gridDim.x * 4u;
+    const uint64_t w = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
+    for (uint64_t r0 = 0; r0 * G * 4u < p.n; r0 += 16) {
+        uint32_t lane = lane_id();
+        asm volatile("" : "+v"(lane));  // lane-derived values recomputed per round, not held across it
+        const uint64_t i = ((r0 + (lane >> 2)) * G + w) * 4u + (lane & 3u);
+        const bool live = i < p.n;
+        const v4u d = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0u));
+        const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + (live ? off : 0u);
+        const uint32_t len = live ? d.z : 0u;
+        const uint32_t cs = kL4 && live ? (d.w & 0xffffu) : 0u;
+        const uint32_t fl = live ? (d.w >> 16) & 0xffu : 0u;
+        const bool small = live && len <= kSmallMax;
+        uint32_t res = 0;
+        if (__ballot(small)) {  // wave-uniform
+            v4u W[5];
+            lane_chunks(a, len, small && len, W);
+            const uint32_t t = lane_sum<kL4>(W, a, small ? len : 0u, cs, fl);
+            res = ~fold16_32(t) & 0xffffu;
+        }
+        wave_long<kL4, kNT, 4, U>(__ballot(live && !small), a, len, cs, fl, p.base, lane, res);
+        if (live)
+            p.out[i] = (uint16_t)res;
+    }
+}
+
+// Resident 256-thread blocks of `kernel` on the current device (occupancy
+// query x CUs), cached per device; 0 when the runtime cannot say.
+template <typename K>
+static uint64_t resident_blocks(K kernel) {
+    static std::atomic<int64_t> cache[16];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0)
+        return 0;
+    if (dev < 16) {
+        const int64_t c = cache[dev].load(std::memory_order_relaxed);
+        if (c > 0)
+            return (uint64_t)c;
+    }
+    int cus = 0, nb = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, 256, 0) != hipSuccess || cus <= 0 || nb <= 0)
+        return 0;
+    const int64_t v = (int64_t)cus * nb;
+    if (dev < 16)
+        cache[dev].store(v, std::memory_order_relaxed);
+    return (uint64_t)v;
+}
+
+// Grid of a persistent walking kernel: n / 256 blocks, capped at the resident
+// capacity, a multiple of 8 (XCD swizzle) when >= 8.
+static uint64_t persist_grid(uint64_t n, uint64_t cap) {
+    uint64_t b = (n + 255) / 256;
+    if (cap >= 8 && b > (cap & ~7ull))
+        b = cap & ~7ull;
+    if (b >= 8)
+        b = (b + 7) & ~7ull;  // <= the capped value: that is a multiple of 8
+    return b;
+}
+
 // Block-per-descriptor kernel for batches of FEW, LONG packets (knob l4_coop:
 // descriptor batches of n <= l4_coop; BASELINE config 1: 16,384 x 64 KiB).
 // The split kernel sizes its grid by descriptor count — 1,024 waves for
@@ -627,11 +737,29 @@ static int launch_small(const L4Params &p, uint32_t mode, hipStream_t st) {
         if (blocks >= 8)
             blocks = (blocks + 7) & ~7ull;  // XCD swizzle bijective; surplus blocks have no live lane
     }
+    if (mode == 6) {  // walking kernel: a wave per 64 descriptors
+        blocks = (p.n + 255) / 256;
+        if (blocks >= 8)
+            blocks = (blocks + 7) & ~7ull;
+    }
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
     const dim3 grid((unsigned)blocks), blk(256);
     const Tune t = tune();
-    if (mode == 5 && t.l4_split_waves == 8) {
+    if (mode == 7) {
+        if (t.l4_unroll == 8) {
+            auto k = l4csum_persist_kernel<kKind, kNT, 8>;
+            hipLaunchKernelGGL(k, dim3((unsigned)persist_grid(p.n, resident_blocks(k))), blk, 0, st, p);
+        } else {
+            auto k = l4csum_persist_kernel<kKind, kNT, 4>;
+            hipLaunchKernelGGL(k, dim3((unsigned)persist_grid(p.n, resident_blocks(k))), blk, 0, st, p);
+        }
+    } else if (mode == 6) {
+        if (t.l4_unroll == 8)
+            hipLaunchKernelGGL((l4csum_walk_kernel<kKind, kNT, 8>), grid, blk, 0, st, p);
+        else
+            hipLaunchKernelGGL((l4csum_walk_kernel<kKind, kNT, 4>), grid, blk, 0, st, p);
+    } else if (mode == 5 && t.l4_split_waves == 8) {
         if (t.l4_unroll == 8)
             hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 8, 8>), grid, dim3(512), 0, st, q);
         else
@@ -1353,6 +1481,238 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
     }
 }
 
+// Walking verify (verify_small = 8): one launch of n / 64 waves whatever the
+// size mix, the layout of l4csum_walk_kernel (lane l of wave w of G owns
+// descriptor ((l >> 2) * G + w) * 4 + (l & 3): the resident waves work on one
+// narrow window of the batch).  Packets of <= kSmallMax bytes are decoded in
+// their lane (verify_lane); the wave then walks its longer packets in group
+// order, 4 at a time, through verify_group.  Stateless: no host sample, no
+// lists, nothing carried between calls.
+// One round of the walking verify: lane l holds descriptor i (of group
+// g = i / 4); small packets in their lane, long ones 4 at a time through
+// verify_group with their offsets / lengths parked in LDS (s_geo: this wave's
+// 3 x 64 words), results stored by index.
+__device__ __forceinline__ void verify_walk_round(const VerifyParams &p, uint64_t i, uint32_t *s_geo) {
+    const uint32_t lane = lane_id();
+    const bool live = i < p.n;
+    const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0u));
+    const uint32_t len = live ? dv.z : 0u;
+    const uint32_t olo = live ? dv.x : 0u, ohi = live ? dv.y : 0u;
+    const bool small = live && len <= kSmallMax;
+    uint32_t rv = 0, rc = 0;
+    if (__ballot(small))  // wave-uniform
+        verify_lane(reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)ohi << 32) | olo), small ? len : 0u, small, rv,
+                    rc);
+    uint32_t r = rv | (rc << 8);  // one register across the walk
+    uint64_t m = __ballot(live && !small);
+    if (m) {
+        s_geo[lane] = olo;
+        s_geo[64 + lane] = ohi;
+        s_geo[128 + lane] = len;
+    }
+    while (m) {
+        uint32_t ln = lane_id();
+        asm volatile("" : "+v"(ln));
+        uint64_t doff[4];
+        uint32_t lg[4], tgt[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const bool have = m != 0;
+            const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
+            m = have ? m & (m - 1) : m;
+            tgt[k] = have ? j : 64u;
+            const uint32_t x = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[j]);
+            const uint32_t y = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[64 + j]);
+            const uint32_t z = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[128 + j]);
+            doff[k] = have ? (((uint64_t)y << 32) | x) : 0u;
+            lg[k] = have ? z : 0u;
+        }
+        uint32_t v2 = 0, c2 = 0;
+        verify_group<4, true>(p.base, doff, lg, tgt, ln, v2, c2, [] {});
+        r = (ln == tgt[0] || ln == tgt[1] || ln == tgt[2] || ln == tgt[3]) ? (v2 | (c2 << 8)) : r;
+    }
+    if (live) {
+        p.verdict[i] = (uint8_t)r;
+        if (p.l4)
+            p.l4[i] = (uint16_t)(r >> 8);
+    }
+}
+
+// Persistent walking verify (verify_small = 9): the grid is the resident
+// capacity (or n / 64 waves if fewer); wave w takes rounds of 16 groups,
+// lane l of round r holding descriptor ((16 r + (l >> 2)) * G + w) * 4 + (l & 3):
+// every wave gets the same number of groups to within one (l4csum_persist_kernel).
+template <int O = 8>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_persist_kernel(
+    VerifyParams p) {
+    __shared__ uint32_t s_geo[4][3 * 64];
+    const uint64_t G = (uint64_t)gridDim.x * 4u;
+    const uint32_t wib = wave_in_block();
+    const uint64_t w = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wib;
+    for (uint64_t r0 = 0; r0 * G * 4u < p.n; r0 += 16) {
+        uint32_t lane = lane_id();
+        asm volatile("" : "+v"(lane));
+        verify_walk_round(p, ((r0 + (lane >> 2)) * G + w) * 4u + (lane & 3u), s_geo[wib]);
+    }
+}
+
+// Walk the long packets of mask m 4 at a time through verify_group, their
+// geometry (olo / ohi / len of lane j) read from this wave's LDS words; each
+// packet's verdict | L4 result << 8 lands in its lane's r.
+__device__ __forceinline__ void verify_walk_lds(const VerifyParams &p, uint64_t m, const uint32_t *s_geo,
+                                                uint32_t &r) {
+    while (m) {
+        // the lane id laundered per iteration: verify_group's lane-derived
+        // constants are recomputed in the body, not held across the loop
+        uint32_t ln = lane_id();
+        asm volatile("" : "+v"(ln));
+        uint64_t doff[4];
+        uint32_t lg[4], tgt[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const bool have = m != 0;
+            const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
+            m = have ? m & (m - 1) : m;
+            tgt[k] = have ? j : 64u;
+            const uint32_t x = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[j]);
+            const uint32_t y = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[64 + j]);
+            const uint32_t z = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[128 + j]);
+            doff[k] = have ? (((uint64_t)y << 32) | x) : 0u;
+            lg[k] = have ? z : 0u;
+        }
+        uint32_t v2 = 0, c2 = 0;
+        verify_group<4, true>(p.base, doff, lg, tgt, ln, v2, c2, [] {});
+        r = (ln == tgt[0] || ln == tgt[1] || ln == tgt[2] || ln == tgt[3]) ? (v2 | (c2 << 8)) : r;
+    }
+}
+
+// Split-role verify at 8 waves/SIMD (verify_small = 10): the layout of
+// l4csum_split_kernel — block b owns the 16 descriptors [q*Q + 16b, +16) of
+// each quarter q; wave k walks its own group of each quarter that holds a
+// packet longer than kSmallMax (4 groups a quarter batch apart, as the
+// wave-per-packet kernel's waves would take them); wave 0 then decodes the
+// block's all-small groups a lane per packet.  The descriptors' geometry is
+// parked in LDS across both roles (held in registers, verify_split_kernel
+// spilled 60 B at 8 waves/SIMD).  An all-small batch costs n / 64 lane-waves
+// (and three one-load waves per block), an all-long one the wave kernel's
+// groups, 4 per wave.
+template <int O = 8>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_split2_kernel(
+    VerifyParams p, uint64_t Q) {
+    __shared__ uint32_t s_geo[4][3 * 64];
+    const uint32_t wib = wave_in_block();
+    const uint64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
+    uint64_t m_mine, m_small;
+    {
+        const uint32_t lane = lane_id();
+        const uint32_t qq = wib == 0 ? lane >> 4 : (lane >> 2) & 3u;
+        const uint32_t oo = wib == 0 ? lane & 15u : 4u * wib + (lane & 3u);
+        const uint64_t i = (uint64_t)qq * Q + 16u * blk + oo;
+        const bool live = (wib == 0 || lane < 16u) && 16u * blk < Q && i < p.n;
+        const v4u d = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0u));
+        const uint32_t len = live ? d.z : 0u;
+        const uint64_t gl = __ballot(live && len > kSmallMax);
+        const bool grp_long = ((gl >> (lane & ~3u)) & 0xfu) != 0;
+        const bool own = wib == 0 ? (lane & 15u) < 4u : true;
+        m_mine = __ballot(live && own && grp_long);
+        m_small = __ballot(wib == 0 && live && !grp_long);
+        s_geo[wib][lane] = live ? d.x : 0u;
+        s_geo[wib][64 + lane] = live ? d.y : 0u;
+        s_geo[wib][128 + lane] = len;
+    }
+    uint32_t r = 0;
+    verify_walk_lds(p, m_mine, s_geo[wib], r);
+    if (m_small) {  // wave-uniform; never true on waves 1-3
+        uint32_t lane = lane_id();
+        asm volatile("" : "+v"(lane));
+        const bool small = (m_small >> lane) & 1u;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) +
+                            (((uint64_t)s_geo[wib][64 + lane] << 32) | s_geo[wib][lane]);
+        uint32_t sv = 0, sc = 0;
+        verify_lane(a, small ? s_geo[wib][128 + lane] : 0u, small, sv, sc);
+        r = small ? (sv | (sc << 8)) : r;
+    }
+    uint32_t lane = lane_id();
+    asm volatile("" : "+v"(lane));
+    if (((m_mine | m_small) >> lane) & 1u) {
+        const uint32_t qq = wib == 0 ? lane >> 4 : (lane >> 2) & 3u;
+        const uint32_t oo = wib == 0 ? lane & 15u : 4u * wib + (lane & 3u);
+        const uint64_t i = (uint64_t)qq * Q + 16u * blk + oo;
+        p.verdict[i] = (uint8_t)r;
+        if (p.l4)
+            p.l4[i] = (uint16_t)(r >> 8);
+    }
+}
+
+template <int O = 0, bool kLds = false>  // kLds: the long lanes' offsets / lengths parked in LDS across the walk
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_walk_kernel(
+    VerifyParams p) {
+    __shared__ uint32_t s_geo[kLds ? 4 : 1][kLds ? 3 * 64 : 1];
+    const uint32_t lane = lane_id();
+    const uint64_t G = (uint64_t)gridDim.x * 4u;
+    const uint64_t w = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
+    const uint64_t i = ((uint64_t)(lane >> 2) * G + w) * 4u + (lane & 3u);
+    const bool live = i < p.n;
+    const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0u));
+    const uint32_t len = live ? dv.z : 0u;
+    const uint32_t olo = live ? dv.x : 0u, ohi = live ? dv.y : 0u;
+    const bool small = live && len <= kSmallMax;
+    uint32_t rv = 0, rc = 0;
+    if (__ballot(small))  // wave-uniform
+        verify_lane(reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)ohi << 32) | olo), small ? len : 0u, small, rv,
+                    rc);
+    // one register across the walk: verdict | L4 result << 8
+    uint32_t r = rv | (rc << 8);
+    uint64_t m = __ballot(live && !small);
+    if constexpr (kLds) {
+        const uint32_t wib = wave_in_block();
+        if (m) {
+            s_geo[wib][lane] = olo;
+            s_geo[wib][64 + lane] = ohi;
+            s_geo[wib][128 + lane] = len;
+        }
+    }
+    while (m) {  // the long packets, 4 at a time in group order (verify_mask)
+        // the lane id laundered per iteration: verify_group's lane-derived
+        // constants are recomputed in the body, not held across the loop
+        uint32_t ln = lane_id();
+        asm volatile("" : "+v"(ln));
+        uint64_t doff[4];
+        uint32_t lg[4], tgt[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const bool have = m != 0;
+            const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
+            m = have ? m & (m - 1) : m;
+            tgt[k] = have ? j : 64u;
+            if constexpr (kLds) {
+                // same-address LDS reads (broadcast), made wave-uniform
+                const uint32_t wib = wave_in_block();
+                const uint32_t x = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[wib][j]);
+                const uint32_t y = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[wib][64 + j]);
+                const uint32_t z = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[wib][128 + j]);
+                doff[k] = have ? (((uint64_t)y << 32) | x) : 0u;
+                lg[k] = have ? z : 0u;
+            } else {
+                doff[k] = have ? (((uint64_t)rdl(ohi, j) << 32) | rdl(olo, j)) : 0u;
+                lg[k] = have ? rdl(len, j) : 0u;
+            }
+        }
+        uint32_t v2 = 0, c2 = 0;
+        verify_group<4, true>(p.base, doff, lg, tgt, ln, v2, c2, [] {});
+        r = (ln == tgt[0] || ln == tgt[1] || ln == tgt[2] || ln == tgt[3]) ? (v2 | (c2 << 8)) : r;
+    }
+    // the index recomputed from a laundered lane id (held across the walk it spilled)
+    uint32_t l2 = lane_id();
+    asm volatile("" : "+v"(l2));
+    const uint64_t i2 = ((uint64_t)(l2 >> 2) * G + w) * 4u + (l2 & 3u);
+    if (i2 < p.n) {
+        p.verdict[i2] = (uint8_t)r;
+        if (p.l4)
+            p.l4[i2] = (uint16_t)(r >> 8);
+    }
+}
+
 }  // namespace wg
 
 namespace {
@@ -1506,6 +1866,46 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
         return WG_ERR_INVALID;
     VerifyParams p{dev_base, dev_desc, dev_verdict, dev_l4, n};
     const Tune t = tune();
+    if (t.verify_small == 10) {  // split roles at 8 waves/SIMD: one stateless launch
+        const uint64_t Q = ((n + 3) / 4 + 15) & ~15ull;  // as l4csum_split_kernel's quarters
+        uint64_t sb = Q / 16;
+        if (sb >= 8)
+            sb = (sb + 7) & ~7ull;
+        if (sb > 0x7fffffffull)
+            return WG_ERR_INVALID;
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        if (t.verify_occ == 8)
+            hipLaunchKernelGGL(verify_split2_kernel<8>, dim3((unsigned)sb), dim3(256), 0, st, p, Q);
+        else
+            hipLaunchKernelGGL(verify_split2_kernel<0>, dim3((unsigned)sb), dim3(256), 0, st, p, Q);
+        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+    }
+    if (t.verify_small == 9) {  // persistent walking verify: one stateless launch at the resident capacity
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        if (t.verify_occ == 8) {
+            auto k = verify_persist_kernel<8>;
+            hipLaunchKernelGGL(k, dim3((unsigned)persist_grid(n, resident_blocks(k))), dim3(256), 0, st, p);
+        } else {
+            auto k = verify_persist_kernel<0>;
+            hipLaunchKernelGGL(k, dim3((unsigned)persist_grid(n, resident_blocks(k))), dim3(256), 0, st, p);
+        }
+        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+    }
+    if (t.verify_small == 8) {  // walking verify: one stateless launch of n / 64 waves
+        uint64_t blocks = (n + 255) / 256;
+        if (blocks >= 8)
+            blocks = (blocks + 7) & ~7ull;
+        if (blocks > 0x7fffffffull)
+            return WG_ERR_INVALID;
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        if (t.verify_occ == 8 && t.verify_dm == 2)  // (experiment) geometry parked in LDS
+            hipLaunchKernelGGL((verify_walk_kernel<8, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+        else if (t.verify_occ == 8)
+            hipLaunchKernelGGL(verify_walk_kernel<8>, dim3((unsigned)blocks), dim3(256), 0, st, p);
+        else
+            hipLaunchKernelGGL(verify_walk_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, st, p);
+        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+    }
     if (t.verify_small >= 6) {
         // 6: the compacting path; 7 (default): the compacting path when the
         // previous call on this stream sampled >= verify_auto_t small packets
