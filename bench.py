@@ -80,7 +80,7 @@ def parse():
                     help="skip the workload's own post-checks (PMC passes: only the step's launches of its kernels)")
     ap.add_argument("--no-strong", action="store_true", help="skip the config 5 strong-scaling companion")
     ap.add_argument("--cpu-seconds", type=float, default=2.0,
-                    help="wall seconds of each CPU baseline repetition (5 on all cores, 3 on one)")
+                    help="wall seconds of each CPU baseline repetition on all cores (half on one core); 8 repetitions each, the first dropped")
     ap.add_argument("--settle-seconds", type=float, default=0.3,
                     help="untimed back-to-back launches before the warmup (clock/memory settle)")
     return ap.parse_args()
@@ -108,6 +108,7 @@ class Workload:
     probe_run: int = 0                # packet size for the kernel-shaped read probe (0: contiguous only)
     pcie: Optional[dict] = None       # host-memory workloads: PCIe bytes per step {"h2d": B, "d2h": B}
     rw: Optional[tuple] = None        # (read, written) algorithmic bytes per launch, when both directions count
+    copy_dst: Optional[object] = None  # read+write workloads: a device buffer the copy probe may overwrite
 
 
 def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workload:
@@ -232,7 +233,8 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
         return Workload(launch, n, n * in_len, alg, cfg, "weak", buf,
                         "wg::gso_plan_kernel + wg::gso_split_kernel<4,4,0> + wg::gso_finalize_kernel (one wg_gso_split call)",
                         rank * n, sample=sample, counts=[n] * world, post=post,
-                        rw=(n * in_len + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES), n * out_len))
+                        rw=(n * in_len + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES), n * out_len),
+                        copy_dst=outb)
     if name == "aead":
         # worker/encap.cpp:136-141: Peer::encrypt for every 1500-B segment of a
         # PacketBatch (config 2's packets), counters encrypt_nonce++ per call
@@ -395,8 +397,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
             l64 = torch.empty(n, dtype=torch.uint16, device=dev)
             saved = wga.tune_get("verify_small")
             small, ref = {}, None
-            for kname, knob in (("wave_per_packet", 0), ("default_auto", 7), ("compacting", 6),
-                                ("lane_per_descriptor", 1), ("split_roles", 3), ("two_role", 4)):
+            for kname, knob in (("wave_kernel", 0), ("default_auto", 7), ("compacting", 6), ("walking", 8)):
                 wga.tune_set("verify_small", knob)
                 for _ in range(10):
                     wga.verify_desc(b64, d64, verdict=v64, l4=l64)
@@ -431,9 +432,9 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
         cfg = {"workload": f"{name} (SURVEY §8 f1): 1,048,576 x {VSEG} B mixed IPv4/IPv6 x TCP/UDP per GPU, "
                            "checksums stored, evaluate_packet checksum gates (wg_verify_desc, default knobs)",
                "packets_per_gpu": n, "segment_size": VSEG, "layout": "descriptor", "parallelism": f"shard{world}"}
-        kname = ("wg::verify_kernel<4,8,0,true> (verify_small=7 chose the wave kernel: no small packets sampled)"
-                 if VSEG > 64 else "wg::verify_compact_lane_kernel + wg::verify_compact_long_kernel<8> "
-                 "(verify_small=7 chose the compacting path: 64 of 64 sampled packets small)")
+        kname = ("wg::verify_kernel<false> (verify_small=7 chose the wave kernel: no small packets sampled)"
+                 if VSEG > 64 else "wg::verify_walk_kernel (verify_small=7 chose the walking kernel: 64 of 64 "
+                 "sampled packets small)")
         return Workload(launch, n, n * VSEG, n * VSEG + 16 * n + n + 2 * n, cfg, "weak", buf,
                         kname, rank * n, sample=sample, counts=[n] * world, probe_run=VSEG,
                         metric="device-resident GiB/s, decap verify gates over packet batch (SURVEY f1)",
@@ -548,7 +549,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
     def post():
         """the small-only and large-only sub-batches
         (same buffer, the descriptors of one size class) and the whole batch,
-        under the default wave-per-packet kernel and the thread-per-packet one
+        under the split-role kernel (default) and the wave-per-packet one
         (knob l4_small), timed like the main line (back-to-back launches
         between one event pair on the launch stream), each checked bit-exact
         against the main line's results."""
@@ -561,8 +562,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
             o_sub = torch.empty(len(idx), dtype=torch.uint16, device=dev)
             nbytes = int(lens[idx].sum())
             alg = nbytes + 18 * len(idx)  # bytes read + u16 written + 16-B descriptor
-            for kname, small in (("wave_per_packet", 0), ("thread_per_packet", 1), ("thread_per_packet_q4", 2),
-                                 ("quad_per_packet_q4", 3), ("quad_late", 4), ("split_roles", 5)):
+            for kname, small in (("wave_per_packet", 0), ("split_roles", 5)):
                 wga.tune_set("l4_small", small)
                 for _ in range(10):
                     wga.calc_l4_checksum_desc(buf, d_sub, out=o_sub)
@@ -593,8 +593,7 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
         res = {}
         ref = None
         nt0 = wga.tune_get("l4_nt")
-        for kname, knob, nt in (("wave_per_packet", 0, nt0), ("small_kernel_quad", 1, nt0),
-                                ("small_kernel_lane", 2, nt0)):
+        for kname, knob, nt in (("wave_per_packet", 0, nt0), ("small_kernel_lane", 2, nt0)):
             wga.tune_set("l4_small_uniform", knob)
             wga.tune_set("l4_nt", nt)
             for _ in range(10):
@@ -1022,7 +1021,7 @@ def build_encap(wga, torch, rank: int, world: int, dev, fused: bool = True) -> W
     return Workload(launch, n, n * in_len, alg, cfg, "weak", buf,
                     ("wg_encap_batch (3 split kernels, headers only, + 2 scan kernels + %s)" if fused else
                      "wg_gso_split (3 kernels) + wg_encap_encrypt (2 scan kernels + %s)") % aead_k,
-                    rank * n, sample=sample, counts=[n] * world, post=post,
+                    rank * n, sample=sample, counts=[n] * world, post=post, copy_dst=msgs,
                     metric="device-resident GiB/s of tun input, GSO split + data-message encryption (encap worker)")
 
 
@@ -1078,6 +1077,29 @@ def measured_read_peak(torch, wga, buf, iters: int = 30, run_bytes: int = 0) -> 
     return {"best": max(rates.values()), "variants": rates, "bytes": int(buf.numel())}
 
 
+def measured_copy_peak(torch, wga, src, dst, iters: int = 3) -> dict:
+    """Copy-roofline probe over the workload's own buffers, in the same run:
+    dst = src over min(len) bytes by one-shot waves (wg_probe_copy), non-temporal
+    and default-policy loads / stores at 1 / 2 / 4 KiB per wave; best of 3
+    interleaved passes per variant.  Rate = bytes read + bytes written per
+    second, the unit of a read+write kernel's `achieved`.  Overwrites dst."""
+    n = min(src.numel(), dst.numel()) // 16 * 16
+    s, d = src[:n], dst[:n]
+    variants = [(f"{pol}_{k}KiB", k, pol == "default") for pol in ("nt", "default") for k in (1, 2, 4)]
+    rates = {}
+    for _ in range(3):
+        for name, kib, dflt in variants:
+            wga.probe_copy(s, d, kib, default_policy=dflt)  # warm-up launch
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                wga.probe_copy(s, d, kib, default_policy=dflt)
+            e1.record()
+            torch.cuda.synchronize()
+            rates[name] = max(rates.get(name, 0.0), round(2 * n * iters / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1))
+    return {"best": max(rates.values()), "variants": rates, "bytes_each_way": int(n)}
+
+
 def wga_stride(seg: int) -> int:
     """Peer::expected_encrypt_size (include/proto/proto.hpp:266-269)."""
     return 16 + (seg + 15) // 16 * 16 + 16
@@ -1100,18 +1122,24 @@ def _rep_rates(fn, units: float, seconds: float, reps: int) -> list:
 
 
 def _spread(rates: list, scale: float) -> dict:
-    r = sorted(x * scale for x in rates)
+    """Median / min / max of the repetitions after the first (dropped: first
+    touch of the pages, thread start-up); every value is kept in the line."""
+    vals = [x * scale for x in rates]
+    r = sorted(vals[1:] if len(vals) > 1 else vals)
     med = r[len(r) // 2] if len(r) % 2 else 0.5 * (r[len(r) // 2 - 1] + r[len(r) // 2])
     return {"median": med, "min": r[0], "max": r[-1], "reps": len(r),
-            "spread_pct": round(100.0 * max(med - r[0], r[-1] - med) / med, 2) if med else None}
+            "spread_pct": round(100.0 * max(med - r[0], r[-1] - med) / med, 2) if med else None,
+            "values": [round(v, 3) for v in vals], "dropped_first": len(vals) > 1}
 
 
-def cpu_baseline(sample_fn, seconds: float, reps: int = 5):
+def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
     """The oracle (C restatement of checksum.cpp + a fastcsum-class nofold) on
     the host cores of this box, on a bounded sample of the same workload.
-    All cores: `reps` repetitions of >= `seconds` each, the median is the
-    value (min / max beside it: a 16-core share of a 256-core host moves with
-    its neighbours); one core: 3 repetitions of >= seconds / 2."""
+    All cores: `reps` repetitions of >= `seconds` each, the first dropped,
+    the median of the rest is the value (min / max and every repetition beside
+    it: a 16-core share of a 256-core host moves with its neighbours); one
+    core: the same count of >= seconds / 2.  Worker thread t is pinned to the
+    t-th CPU of the affinity mask (oracle/orc_pin.h)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import numpy as np
     import oracle  # test infrastructure: the CPU baseline leg only
@@ -1184,9 +1212,9 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 5):
         run_one = lambda: oracle.wg_encrypt_batch_mt(key, rx, c0, sub, seg, cpu_out, 1)  # noqa: E731
         try:
             oss_all = _spread(_rep_rates(lambda: oracle.openssl_encrypt_batch(key, rx, c0, host, seg, cpu_out,
-                                                                              threads), host.size, seconds, 3), 2.0**-30)
+                                                                              threads), host.size, seconds, 4), 2.0**-30)
             oss_one = _spread(_rep_rates(lambda: oracle.openssl_encrypt_batch(key, rx, c0, sub, seg, cpu_out, 1),
-                                         sub.size, seconds / 2, 3), 2.0**-30)
+                                         sub.size, seconds / 2, 4), 2.0**-30)
             extra = {"openssl_evp_chacha20_poly1305": {
                 "value": oss_all["median"], "value_1core": oss_one["median"], "unit": "GiB/s",
                 "spread": oss_all, "spread_1core": oss_one,
@@ -1278,7 +1306,7 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 5):
     scale, unit = (1e-6, "Mflows/s") if kind[0] == "gro" else (2.0**-30, "GiB/s")
     run_all()  # first touch / warm-up, untimed
     all_s = _spread(_rep_rates(run_all, nbytes, seconds, reps), scale)
-    one_s = _spread(_rep_rates(run_one, nbytes * one_scale, seconds / 2, 3), scale)
+    one_s = _spread(_rep_rates(run_one, nbytes * one_scale, seconds / 2, reps), scale)
     try:
         cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except Exception:
@@ -1306,8 +1334,9 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 5):
         "sample": f"first {npk} units of the same batch, oracle/csum_oracle.c "
                   f"({what}; {nofold} for spans >= 256 B), {threads} pthreads "
                   f"(sched_getaffinity {cores['affinity']}, cgroup quota {cores['cgroup_quota_cpus']}); "
-                  f"value = median of {reps} repetitions of >= {seconds:.1f} s, 1 core: median of 3 of "
-                  f">= {seconds / 2:.1f} s; bit-exact vs GPU: {parity}",
+                  f"value = median of {reps - 1} repetitions of >= {seconds:.1f} s after a dropped first one, "
+                  f"1 core: the same of >= {seconds / 2:.1f} s; worker t pinned to CPU t of the affinity mask; "
+                  f"bit-exact vs GPU: {parity}",
         "parity_with_gpu": parity,
         **extra,
     }
@@ -1538,6 +1567,14 @@ def main():
                 "spec_source": "PCIe Gen5 x16: 64 GB/s per direction"}
     probe = measured_read_peak(torch, wga, wl.buf, run_bytes=wl.probe_run) if rank == 0 and not wl.pcie else None
     read_peak = probe["best"] if probe else None
+    copy = None
+    if rank == 0 and wl.copy_dst is not None:
+        # the same-run read+write ceiling; the probe
+        # overwrites the workload's output, so one more launch restores it
+        # before the CPU baseline and post-checks read it
+        copy = measured_copy_peak(torch, wga, wl.buf, wl.copy_dst)
+        wl.launch()
+        torch.cuda.synchronize()
     # The CPU baseline samples the batch as the timed launches saw it, so it
     # runs before post_checks (whose verify pass stores the checksums into the
     # packets).
@@ -1586,6 +1623,12 @@ def main():
             "measured_read_peak": round(read_peak, 1) if read_peak else None,
             "read_probe_variants": probe["variants"] if probe else None,
             "frac_of_measured_read_peak": round(achieved / read_peak, 4) if read_peak else None,
+            **({"measured_copy_peak": copy["best"], "copy_probe_variants": copy["variants"],
+                "copy_probe_bytes_each_way": copy["bytes_each_way"],
+                "frac_of_measured_copy_peak": round(achieved / copy["best"], 4),
+                "copy_probe_note": "wg_probe_copy over this workload's own input and output buffers in this run, "
+                                   "best variant of 3 passes; rate = bytes read + written per second, like "
+                                   "`achieved`"} if copy else {}),
             "kernel_ms_avg": round(kern_ms, 5),
             "kernel_ms_avg_max_over_ranks": round(t["kern_ms_max"], 5),
             "kernel_ms_source": "HIP events at the two ends of the timed region on the launch stream / K "

@@ -422,26 +422,23 @@ const char *wg_strerror(int code);
 int wg_device_count(void);
 
 /* Launch-geometry knobs.  Each key is also read once, at the first launch,
- * from the environment as WG_<KEY> (e.g. WG_L4_PPW=2); the environment and
+ * from the environment as WG_<KEY> (e.g. WG_L4_NT=0); the environment and
  * wg_tune_set accept the same values and ignore / reject (WG_ERR_INVALID)
- * anything else.  Results never depend on them.
- *   "l4_blocks"  grid cap of the L4 kernels (1 .. 2^20)
- *   "l4_ppw"     packets per wave iteration (1, 2, 4, 8)
+ * anything else.  Results never depend on them.  (Variants measured and
+ * rejected were removed in round 4; DESIGN.md keeps their numbers.)
+ *   "l4_blocks"  grid cap of the wave-per-packet L4 kernel (1 .. 2^20)
  *   "l4_nt"      non-temporal packet loads (0, 1)
- *   "l4_descv"   descriptor batches: 0 scalar loads, 1 one vector load per
- *                iteration, 2 vector prefetch of the next iteration
- *   "l4_iters"   iterations per wave in descriptor mode 2 (1 .. 64)
- *   "l4_occ"     waves/SIMD target at 4 packets/wave (0 = compiler, 7, 8)
  *   "l4_small"   descriptor-batch kernel: 5 (default) split roles — groups
  *                of 4 descriptors whose packets are all <= 64 B are summed a
  *                lane per packet, every other group wave-per-packet; 0 =
- *                wave-per-packet for all; 1-4 the thread-per-packet variants
- *                (a lane per descriptor, long packets 2 (1) or 4 (2) at a
- *                time; 3: a lane quad per descriptor; 4: as 3, lane loads in
- *                flight during the long packets)
- *   "l4_small_uniform" uniform batches with segment_size <= 64 by the
- *                small-packet kernel, a lane quad (1) or a lane (2) per
- *                segment, or by the wave-per-packet kernel (0)
+ *                wave-per-packet for all
+ *   "l4_small_uniform" uniform batches with segment_size <= 64: a lane per
+ *                segment (2, default) or the wave-per-packet kernel (0)
+ *   "l4_unroll"  descriptor batches: 16-B loads in flight per lane while
+ *                streaming a packet's bytes past its first 2 KiB (4, 8)
+ *   "l4_coop"    descriptor batches of n <= l4_coop descriptors: a block of
+ *                l4_coop_waves waves per packet (few, long packets; 0 never)
+ *   "l4_coop_waves" waves sharing one packet in that mode (2, 4, 8, 16)
  *   "gso_blocks" grid cap of the GSO split kernel (1 .. 2^23)
  *   "gso_groups" blocks per super-buffer, consecutive in the flat grid (1 .. 64)
  *   "gso_waves"  waves per GSO block (1, 2, 4, 8)
@@ -450,34 +447,23 @@ int wg_device_count(void);
  *   "encap_spw"  the same for wg_encap_batch's headers-only split (3)
  *   "encap_parts" wg_encap_batch in slices, each split on a side stream under
  *                the previous slice's AEAD (1 = not pipelined, default; 2-8)
- *   "verify_dm"  verify descriptor mode: 0 one-shot waves, 2 prefetch
- *   "verify_occ" verify waves/SIMD target (0 = compiler, 6, 8)
- *   "verify_hdr" verify header bytes from the L4 byte gather (1) or a
- *                separate byte load (0)
- *   "verify_small" wg_verify_desc kernels: 7 (default) = per call, the
- *                compacting path (6) when the previous call on the same
- *                (device, stream) sampled >= verify_auto_t packets of <= 64 B
- *                among 64 spread descriptors, else the wave-per-packet kernel
- *                (0), which samples the batch for the next call; 6 = lane per
+ *   "verify_small" wg_verify_desc kernels: 7 (default) = per call, from the
+ *                size mix the previous call on the same (device, stream)
+ *                sampled: the walking kernel (8) on the stream's first call
+ *                and when all 64 sampled packets are <= 64 B, else the
+ *                cheaper of the wave kernel (0) and the compacting path (6)
+ *                by a cost model; calls under stream capture take a
+ *                stateless kernel.  0 = one-shot 4-packet waves; 6 = lane per
  *                descriptor (<= 64 B decoded in the lane, longer ones
  *                appended to per-shard lists) + a wave kernel over the lists;
- *                1 / 2 = packets of <= 64 B decoded in one lane / a lane
- *                quad, longer ones by the same wave; 3 = split roles;
- *                4 / 5 = lane and wave roles as two launches / one
- *   "verify_auto_t" the sample threshold of verify_small 7 (1 .. 64)
+ *                8 = a wave per 64 descriptors, small packets in lanes, the
+ *                long ones walked 4 at a time
+ *   "verify_auto_t" the sample threshold of verify_small 7's compacting path (1 .. 64)
  *   "verify_k2min" compacting path: minimum blocks of its wave kernel
  *                (8 .. 65536; the grid follows the expected long packets)
- *   "gro_lds", "gro_wide"  GRO finalize: LDS-staged loads, wide field stores
- *   "gro_chunks" 16-B header chunks staged per flow (4, 5; with 4, headers
- *                over 48 bytes take the byte path)
- *   "host_chunk_mb" wg_l4csum_uniform_host chunk size in MiB (1 .. 4096)
- *   "l4_unroll"  descriptor batches: 16-B loads in flight per lane while
- *                streaming a packet's bytes past its first 2 KiB (4, 8)
- *   "l4_coop"    descriptor batches of n <= l4_coop descriptors: a block of
- *                l4_coop_waves waves per packet (few, long packets; 0 never)
- *   "l4_coop_waves" waves sharing one packet in that mode (2, 4, 8, 16)
- *   "l4_split_waves" split-role descriptor kernel: waves per block, 4 (16
- *                descriptors per wave) or 8 (8 per wave)
+ *   "host_chunk_mb" host-memory pipeline chunk size in MiB (1 .. 4096)
+ *   "host_d2h"   host pipeline downloads into pinned memory by a store
+ *                kernel: bit 1 encap messages (default), bit 2 decap plaintext
  *   "aead_k"     AEAD kernels: consecutive ChaCha20 blocks per lane (1-4; 0
  *                = 2 or 3, whichever fills a wave better for the batch)
  *   "aead_pair"  a lane's blocks computed two at a time, interleaved (1),
@@ -505,8 +491,10 @@ int wg_probe_read(const uint8_t *dev, uint64_t nbytes, uint64_t *dev_out, uint32
                   uint32_t run_bytes, void *stream);
 
 /* Copy-roofline probe: dst[0, nbytes) = src[0, nbytes) by one-shot waves of
- * `kib_per_wave` (1/2/4) KiB, non-temporal loads and stores; the measured
- * read+write ceiling for the GSO split kernel. */
+ * `kib_per_wave` (1/2/4) KiB, non-temporal loads and stores, or the default
+ * cache policy with WG_PROBE_DEFAULT_POLICY or'ed into kib_per_wave; the
+ * measured read+write ceiling for the GSO split and encap kernels. */
+#define WG_PROBE_DEFAULT_POLICY 0x100u
 int wg_probe_copy(const uint8_t *src, uint8_t *dst, uint64_t nbytes, uint32_t kib_per_wave, void *stream);
 
 #ifdef __cplusplus

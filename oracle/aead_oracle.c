@@ -11,6 +11,7 @@
  * RFC 8439 test vectors and by vectors generated with the system OpenSSL's
  * independent implementation (tests/golden/aead/).
  */
+#include "orc_pin.h"
 #include "csum_oracle.h"
 
 #include <pthread.h>
@@ -319,8 +320,10 @@ static void aead_parallel(aead_job proto, uint64_t n, int threads) {
         jobs[t].hi = n * (uint64_t)(t + 1) / (uint64_t)threads;
         if (threads == 1)
             aead_job_run(&jobs[t]);
-        else
+        else {
             pthread_create(&tid[t], NULL, aead_job_run, &jobs[t]);
+            orc_pin_thread(tid[t], t);
+        }
     }
     if (threads > 1)
         for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);

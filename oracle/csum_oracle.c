@@ -9,6 +9,7 @@
  */
 #define _GNU_SOURCE
 #include "csum_oracle.h"
+#include "orc_pin.h"
 
 #include <pthread.h>
 #include <string.h>
@@ -340,6 +341,7 @@ static void run_parallel(job_t proto, uint64_t n, int threads) {
         jobs[t].lo = n * (uint64_t)t / (uint64_t)threads;
         jobs[t].hi = n * (uint64_t)(t + 1) / (uint64_t)threads;
         pthread_create(&tids[t], NULL, job_thread, &jobs[t]);
+        orc_pin_thread(tids[t], t);
     }
     for (int t = 0; t < threads; t++)
         pthread_join(tids[t], NULL);

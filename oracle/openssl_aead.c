@@ -6,6 +6,7 @@
  * not installed here).  TEST INFRASTRUCTURE ONLY: bench.py's f4 CPU
  * comparator and an extra checker in tests/; never part of the product.
  */
+#include "orc_pin.h"
 #include <openssl/evp.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -75,7 +76,7 @@ int oss_wg_encrypt_batch(const uint8_t key[32], uint32_t rx, uint64_t c0, const 
         if (threads == 1)
             run(&jobs[t]);
         else
-            pthread_create(&tid[t], NULL, run, &jobs[t]);
+            pthread_create(&tid[t], NULL, run, &jobs[t]), orc_pin_thread(tid[t], t);
     }
     int rc = 0;
     for (int t = 0; t < threads; t++) {
@@ -147,7 +148,7 @@ int oss_wg_decrypt_batch(const uint8_t key[32], const uint8_t *in, uint64_t tota
         if (threads == 1)
             drun(&jobs[t]);
         else
-            pthread_create(&tid[t], NULL, drun, &jobs[t]);
+            pthread_create(&tid[t], NULL, drun, &jobs[t]), orc_pin_thread(tid[t], t);
     }
     int rc = 0;
     for (int t = 0; t < threads; t++) {

@@ -170,13 +170,19 @@ def test_tune_knobs_validate_and_round_trip():
     import wireglider_amd as wga
 
     keys = re.findall(r'^ \*   "(\w+)"', HDR.read_text(), flags=re.M)
-    keys += re.findall(r'"(gro_wide)"', HDR.read_text())
-    assert {"l4_ppw", "gso_groups", "verify_hdr", "gro_lds", "gro_wide", "gso_ablate"} <= set(keys)
+    assert {"l4_nt", "gso_groups", "verify_small", "l4_small", "host_d2h", "gso_ablate"} <= set(keys)
+    # round 4 removed the rejected variants' knobs: no longer accepted
+    for gone in ("l4_ppw", "l4_occ", "l4_descv", "l4_iters", "l4_split_waves", "verify_dm", "verify_occ",
+                 "verify_hdr", "verify_wblk", "gro_lds", "gro_wide", "gro_chunks", "gro_iters"):
+        assert gone not in keys
+        with pytest.raises(Exception):
+            wga.tune_get(gone)
     for k in keys:
         v = wga.tune_get(k)
         wga.tune_set(k, v)
         assert wga.tune_get(k) == v
-    for k, bad in (("l4_ppw", 3), ("l4_occ", 6), ("gso_groups", 0), ("gso_groups", 65), ("verify_hdr", 2),
+    for k, bad in (("l4_small", 1), ("l4_small", 4), ("verify_small", 3), ("l4_small_uniform", 1),
+                   ("gso_groups", 0), ("gso_groups", 65),
                    ("gso_waves", 16), ("gso_ablate", 7), ("gso_ablate", 2), ("l4_coop_waves", 3),
                    ("l4_coop_waves", 32)):
         v = wga.tune_get(k)
@@ -200,11 +206,11 @@ def test_tune_environment_overrides():
     import sys
 
     code = ("import wireglider_amd as w; print(w.tune_get('l4_nt'), w.tune_get('gso_groups'), "
-            "w.tune_get('l4_ppw'), w.tune_get('verify_hdr'))")
+            "w.tune_get('l4_small'), w.tune_get('verify_small'))")
     code += "; print(w.tune_get('gso_ablate'))"
-    env = dict(os.environ, WG_L4_NT="0", WG_GSO_GROUPS="5", WG_L4_PPW="3", WG_VERIFY_HDR="0x0", WG_GSO_ABLATE="2")
+    env = dict(os.environ, WG_L4_NT="0", WG_GSO_GROUPS="5", WG_L4_SMALL="3", WG_VERIFY_SMALL="0x8", WG_GSO_ABLATE="2")
     out = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT, capture_output=True, text=True, check=True)
-    nt, groups, ppw, hdr, abl = map(int, out.stdout.split())
-    assert (nt, groups, hdr) == (0, 5, 0)
+    nt, groups, small, vs, abl = map(int, out.stdout.split())
+    assert (nt, groups, vs) == (0, 5, 8)
     assert abl == 0  # WG_GSO_ABLATE=2 is not an accepted value: ignored
-    assert ppw == 4  # 3 is not an accepted value: default kept
+    assert small == 5  # 3 is not an accepted value: default kept

@@ -34,7 +34,7 @@ def _load(dev):
     return buf, d, kind, exp, man, dbuf, dd
 
 
-L4_VARIANTS = [{}, {"l4_coop": 0}, {"l4_coop": 0, "l4_small": 0}, {"l4_coop": 0, "l4_small": 6}]
+L4_VARIANTS = [{}, {"l4_coop": 0}, {"l4_coop": 0, "l4_small": 0}, {"l4_coop": 0, "l4_nt": 0}]
 
 
 @pytest.mark.parametrize("knobs", L4_VARIANTS, ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()) or "default")
@@ -70,7 +70,7 @@ def test_l4csum_uniform_runs_equal_reference(gpu):
         np.testing.assert_array_equal(out.cpu().numpy(), exp[run["first"]:run["first"] + cnt], err_msg=run["group"])
 
 
-@pytest.mark.parametrize("vs", [None, 0])
+@pytest.mark.parametrize("vs", [None, 0, 6, 8])
 def test_verify_desc_equals_reference(gpu, vs):
     import torch
 

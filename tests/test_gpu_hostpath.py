@@ -297,3 +297,79 @@ def test_host_path_keeps_current_device(gpu):
     wga.calc_l4_checksum_host(buf, 1500, False, False, 20)  # the pipeline rebuilt after a release
     wga.host_release()
     assert torch.cuda.current_device() == before
+
+
+@pytest.mark.gpu
+def test_pipeline_build_failure(gpu):
+    """A pipeline whose build fails part-way (the third event creation, forced
+    by the WG_TEST_PIPE_FAIL hook, as under resource exhaustion) returns an
+    error and leaves nothing half-built: the thread's next call builds the
+    pipeline again and its results are bit-exact (a failed build
+    had left the device marked, so later calls ran with null streams and
+    events).  In a child process, since the hook is read once per process."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    code = (
+        "import sys, numpy as np\n"
+        f"sys.path[:0] = [{str(root)!r}, {str(root / 'oracle')!r}]\n"
+        "import wireglider_amd as wga, oracle\n"
+        "buf = np.random.default_rng(5).integers(0, 256, 1500 * 300, dtype=np.uint8)\n"
+        "try:\n"
+        "    wga.calc_l4_checksum_host(buf.tobytes(), 1500, False, False, 20)\n"
+        "    print('FIRST ok')\n"
+        "except wga.WireGliderError as e:\n"
+        "    print('FIRST failed:', e)\n"
+        "out = wga.calc_l4_checksum_host(buf.tobytes(), 1500, False, False, 20)\n"
+        "print('SECOND', bool(np.array_equal(out, oracle.l4_uniform(buf, 1500, 20, 0))))\n")
+    env = dict(os.environ, WG_TEST_PIPE_FAIL="3")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "FIRST failed" in r.stdout and "HIP runtime failure" in r.stdout, r.stdout
+    assert "SECOND True" in r.stdout, r.stdout
+
+
+@pytest.mark.gpu
+def test_encap_host_small_reads_large_msg_cap(gpu, small_chunks):
+    """Many ACK-sized tun reads with a msg_cap sized for 64-KiB TSO reads
+    (ADVICE r03): chunks close on their output bytes too (messages at msg_cap
+    each within twice the chunk budget), so the slots stay small; every
+    message still matches the oracle, counters consecutive across chunks."""
+    wga = _wga()
+    rng = np.random.default_rng(33)
+    cases = []
+    for k in range(3000):
+        v6, tcp = bool(rng.integers(0, 2)), bool(rng.integers(0, 2))
+        p = pktbuild.build(v6, tcp, rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8).tobytes(),
+                           rng.integers(0, 256, 16 if v6 else 4, dtype=np.uint8).tobytes(),
+                           rng.integers(0, 256, 16 if v6 else 4, dtype=np.uint8).tobytes(), fill_l4=False)
+        cases.append((p, dict(flags=1, gso_type=0, csum_start=40 if v6 else 20, csum_offset=16 if tcp else 6), 4096))
+    desc = np.zeros(len(cases), dtype=wga.GSO_DESC_DTYPE)
+    off, caps = 5, []
+    for k, (pkt, vnet, cap) in enumerate(cases):
+        caps.append(cap)
+        desc[k]["in_offset"], desc[k]["in_len"], desc[k]["out_cap"] = off, len(pkt), cap
+        for f in ("flags", "gso_type", "hdr_len", "gso_size", "csum_start", "csum_offset"):
+            desc[k]["vnet"][f] = vnet.get(f, 0)
+        off += len(pkt) + int(rng.integers(0, 9))
+    inbuf = np.zeros(off + 7, np.uint8)
+    for k, (pkt, _, _) in enumerate(cases):
+        inbuf[int(desc[k]["in_offset"]):int(desc[k]["in_offset"]) + len(pkt)] = np.frombuffer(pkt, np.uint8)
+    assert len(cases) * MSG_CAP > 2 * (2 << 20)  # the messages alone span many 2-MiB output budgets
+    key = bytes(range(7, 39))
+    msgs, res, gres, nxt = wga.encap_host(inbuf, desc, key, 0x77, 5, MAX_SEG, MAX_SIZE, MSG_CAP)
+    ctr = 5
+    for i, (pkt, vnet, _) in enumerate(cases):
+        st, o_in, o_out, _, r = oracle.gso_split(np.frombuffer(pkt, np.uint8), vnet, caps[i])
+        assert int(gres[i]["status"]) == st == 0, i
+        ol, S = int(r["out_len"]), int(r["segment_size"])
+        nb = 32 + (ol + 15) // 16 * 16
+        assert (int(res[i]["nmsg"]), int(res[i]["msg_bytes"]), int(res[i]["counter0"])) == (1, nb, ctr), i
+        src = o_in if r["passthrough"] else o_out
+        np.testing.assert_array_equal(msgs[i * MSG_CAP:i * MSG_CAP + nb], oracle.wg_encrypt_batch(key, 0x77, ctr,
+                                                                                                  src[:ol], S))
+        ctr += 1
+    assert nxt == ctr

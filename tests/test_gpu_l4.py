@@ -86,14 +86,11 @@ def test_reference_golden_vectors(gpu):
 SEGS = [1, 7, 20, 21, 28, 40, 48, 59, 64, 100, 127, 128, 1460, 1500, 1501, 4096, 9000, 9001]
 
 
-@pytest.mark.parametrize("occ", [0, 7])
 @pytest.mark.parametrize("seg", SEGS)
-def test_uniform_geometry_sweep(gpu, seg, occ):
+def test_uniform_geometry_sweep(gpu, seg):
     import torch
 
     wga = _wga()
-    saved = wga.tune_get("l4_occ")
-    wga.tune_set("l4_occ", occ)
     rng = np.random.default_rng(seg)
     for trial in range(6):
         nseg = int(rng.integers(1, 40))
@@ -109,18 +106,12 @@ def test_uniform_geometry_sweep(gpu, seg, occ):
         exp = oracle.l4_uniform(buf, seg, cs, flags)
         np.testing.assert_array_equal(out.cpu().numpy(), exp,
                                       err_msg=f"seg={seg} total={total} pad={pad} cs={cs} flags={flags}")
-    wga.tune_set("l4_occ", saved)
 
 
-DESC_VARIANTS = [{"l4_occ": 0}, {"l4_occ": 7}, {"l4_occ": 8}, {"l4_descv": 1}, {"l4_descv": 2, "l4_iters": 2},
-                 {"l4_descv": 2, "l4_iters": 3, "l4_occ": 0}, {"l4_descv": 2, "l4_iters": 8, "l4_ppw": 2},
-                 {"l4_small": 0}, {"l4_small": 1}, {"l4_small": 2}, {"l4_small": 3}, {"l4_small": 4},
-                 {"l4_small": 1, "l4_nt": 0}, {"l4_small": 5}, {"l4_small": 5, "l4_nt": 0},
+DESC_VARIANTS = [{"l4_small": 0}, {"l4_small": 0, "l4_nt": 0}, {"l4_small": 5}, {"l4_small": 5, "l4_nt": 0},
+                 {"l4_small": 5, "l4_unroll": 4},
                  {"l4_coop": 1 << 20, "l4_coop_waves": 2}, {"l4_coop": 1 << 20, "l4_coop_waves": 4, "l4_unroll": 4},
-                 {"l4_coop": 1 << 20, "l4_coop_waves": 8, "l4_nt": 0}, {"l4_coop": 1 << 20, "l4_coop_waves": 16},
-                 {"l4_small": 5, "l4_split_waves": 8}, {"l4_small": 5, "l4_split_waves": 8, "l4_unroll": 4},
-                 {"l4_small": 6}, {"l4_small": 6, "l4_unroll": 4}, {"l4_small": 6, "l4_nt": 0},
-                 {"l4_small": 7}, {"l4_small": 7, "l4_unroll": 4}]
+                 {"l4_coop": 1 << 20, "l4_coop_waves": 8, "l4_nt": 0}, {"l4_coop": 1 << 20, "l4_coop_waves": 16}]
 
 
 @pytest.mark.parametrize("knobs", DESC_VARIANTS, ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()))
@@ -131,8 +122,7 @@ def test_desc_random(gpu, knobs):
     import torch
 
     wga = _wga()
-    saved = {k: wga.tune_get(k) for k in ("l4_occ", "l4_descv", "l4_iters", "l4_ppw", "l4_blocks", "l4_small",
-                                          "l4_nt", "l4_coop", "l4_coop_waves", "l4_unroll", "l4_split_waves")}
+    saved = {k: wga.tune_get(k) for k in ("l4_blocks", "l4_small", "l4_nt", "l4_coop", "l4_coop_waves", "l4_unroll")}
     for k, v in knobs.items():
         wga.tune_set(k, v)
     rng = np.random.default_rng(1234)
@@ -160,7 +150,7 @@ def test_desc_random(gpu, knobs):
     np.testing.assert_array_equal(plain.cpu().numpy(), oracle.checksum_desc(buf, d))
 
 
-@pytest.mark.parametrize("knob", [0, 1, 2])
+@pytest.mark.parametrize("knob", [0, 2])
 @pytest.mark.parametrize("seg", [1, 2, 3, 15, 16, 17, 20, 33, 40, 47, 60, 63, 64, 65])
 def test_uniform_small_segments(gpu, seg, knob):
     """PacketBatches of small segments (<= 64 B go to the small-packet kernel
@@ -190,7 +180,7 @@ def test_uniform_small_segments(gpu, seg, knob):
         wga.tune_set("l4_small_uniform", saved)
 
 
-@pytest.mark.parametrize("small", [0, 1, 2, 3, 4, 5, 58, 6, 7])
+@pytest.mark.parametrize("small", [0, 5])
 @pytest.mark.parametrize("seed", [5, 6])
 def test_desc_small_packets(gpu, small, seed):
     """Batches of mostly small packets (0-130 B, every alignment, csum_start
@@ -201,9 +191,9 @@ def test_desc_small_packets(gpu, small, seed):
     import torch
 
     wga = _wga()
-    saved = {k: wga.tune_get(k) for k in ("l4_small", "l4_split_waves")}
-    wga.tune_set("l4_small", 5 if small == 58 else small)  # 58: the split kernel with 8-wave blocks
-    wga.tune_set("l4_split_waves", 8 if small == 58 else 4)
+    saved = {k: wga.tune_get(k) for k in ("l4_small", "l4_coop")}
+    wga.tune_set("l4_small", small)
+    wga.tune_set("l4_coop", 0)
     rng = np.random.default_rng(seed)
     n = 30001
     lens = rng.integers(0, 131, n)

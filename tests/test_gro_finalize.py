@@ -150,22 +150,13 @@ def _oracle_batch(hdrs, desc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lds,wide,chunks,iters", [(1, 1, 5, 1), (1, 1, 4, 1), (1, 0, 5, 1), (0, 0, 5, 1),
-                                                   (2, 1, 5, 1), (2, 1, 5, 2), (2, 1, 5, 4)],
-                         ids=["lds-wide", "lds-wide-4chunks", "lds-narrow", "thread-loads", "wave", "wave-iters2",
-                              "wave-iters4"])
-def test_gpu_gro_finalize_parity(gpu, lds, wide, chunks, iters):
+@pytest.mark.parametrize("seed", [2024, 2025])
+def test_gpu_gro_finalize_parity(gpu, seed):
     import torch
 
     import wireglider_amd as wg
 
-    saved = {k: wg.tune_get(k) for k in ("gro_lds", "gro_wide", "gro_chunks", "gro_iters")}
-    wg.tune_set("gro_lds", lds)
-    wg.tune_set("gro_wide", wide)
-    wg.tune_set("gro_chunks", chunks)
-    wg.tune_set("gro_iters", iters)
-
-    rng = np.random.default_rng(2024)
+    rng = np.random.default_rng(seed)
     hdrs, desc = _batch(rng, 3000)
     want, want_st = _oracle_batch(hdrs, desc)
     assert (want_st == -3).any() and (want_st == 0).any()
@@ -173,8 +164,6 @@ def test_gpu_gro_finalize_parity(gpu, lds, wide, chunks, iters):
     dd = torch.from_numpy(desc.view(np.uint8)).to(gpu)
     wg.gro_finalize(dh, dd)
     torch.cuda.synchronize()
-    for k, v in saved.items():
-        wg.tune_set(k, v)
     got = dh.cpu().numpy()
     got_desc = dd.cpu().numpy().view(wg.GRO_DESC_DTYPE)
     assert np.array_equal(got_desc["status"], want_st)
@@ -191,16 +180,12 @@ def test_gpu_gro_finalize_empty(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lds", [1, 2], ids=["lds", "wave"])
-def test_gpu_gro_finalize_high_addresses(gpu, lds):
+def test_gpu_gro_finalize_high_addresses(gpu):
     """The same ragged batch placed so its flows straddle bit 31 and 4 GiB of
     a 4.3 GB header buffer (64-bit header offsets, staged-chunk addresses)."""
     import torch
 
     import wireglider_amd as wg
-
-    saved = wg.tune_get("gro_lds")
-    wg.tune_set("gro_lds", lds)
 
     rng = np.random.default_rng(2031)
     hdrs, desc = _batch(rng, 3000)
@@ -215,6 +200,5 @@ def test_gpu_gro_finalize_high_addresses(gpu, lds):
         torch.cuda.synchronize()
         assert np.array_equal(dd.cpu().numpy().view(wg.GRO_DESC_DTYPE)["status"], want_st)
         assert np.array_equal(big[base:base + hdrs.size].cpu().numpy(), want)
-    wg.tune_set("gro_lds", saved)
     del big
     torch.cuda.empty_cache()

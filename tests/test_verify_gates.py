@@ -141,18 +141,8 @@ def test_oracle_verify_desc_matches_scalar():
         assert (verdict[i], l4[i]) == V.verify(p)
 
 
-VERIFY_VARIANTS = [{"verify_dm": 0, "verify_occ": 8, "verify_hdr": 1}, {"verify_dm": 0, "verify_occ": 0, "verify_hdr": 1},
-                   {"verify_dm": 0, "verify_occ": 8, "verify_hdr": 0}, {"verify_dm": 0, "verify_occ": 0, "verify_hdr": 0},
-                   {"verify_dm": 2, "verify_occ": 6, "l4_iters": 4}, {"verify_dm": 2, "verify_occ": 0, "l4_iters": 3},
-                   {"verify_small": 0}, {"verify_small": 1}, {"verify_small": 2}, {"verify_small": 3},
-                   {"verify_small": 3, "verify_occ": 0}, {"verify_small": 4}, {"verify_small": 4, "verify_occ": 0},
-                   {"verify_small": 4, "verify_wblk": 16},
-                   {"verify_small": 5}, {"verify_small": 5, "verify_occ": 0},
-                   {"verify_small": 6}, {"verify_small": 6, "verify_k2min": 8}, {"verify_small": 7},
-                   {"verify_small": 7, "verify_auto_t": 1},
-                   {"verify_small": 8}, {"verify_small": 8, "verify_occ": 0}, {"verify_small": 8, "verify_dm": 2},
-                   {"verify_small": 9}, {"verify_small": 9, "verify_occ": 0},
-                   {"verify_small": 10}, {"verify_small": 10, "verify_occ": 0}]
+VERIFY_VARIANTS = [{"verify_small": 0}, {"verify_small": 6}, {"verify_small": 6, "verify_k2min": 8},
+                   {"verify_small": 7}, {"verify_small": 7, "verify_auto_t": 64}, {"verify_small": 8}]
 
 
 @pytest.mark.gpu
@@ -381,12 +371,13 @@ def _verify_calls(wga, torch, gpu, batches, knobs, stream=None):
 
 @pytest.mark.gpu
 def test_gpu_verify_auto_switches(gpu):
-    """The default wg_verify_desc (verify_small = 7) picks its kernels per call
-    from the size mix the previous call on the stream sampled: all-small,
+    """The default wg_verify_desc (verify_small = 7) picks its kernel per call
+    from the size mix the previous call on the stream sampled (the walking
+    kernel on a stream's first call and after an all-small sample): all-small,
     all-long and interleaved batches back to back, each followed by a
     different one (every call then runs on a stale sample, including the
     compacting path's long kernel sized for no long packets at all, with a
-    1-block-per-shard minimum grid), on the default stream and on a side
+    1-block-per-shard minimum grid), on the default stream and on a fresh side
     stream — every call's results equal the oracle's."""
     import torch
 
@@ -434,3 +425,46 @@ def test_gpu_verify_compact_grows(gpu):
         ev, el4 = oracle.verify_desc(buf, d)
         np.testing.assert_array_equal(v, ev)
         np.testing.assert_array_equal(x, el4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("warm", [False, True])
+def test_gpu_verify_under_graph_capture(gpu, warm):
+    """wg_verify_desc captured into a HIP graph (torch.cuda.graph) on a side
+    stream — with no per-stream state yet (warm False) or after eager calls
+    gave the stream a sample (warm True): captured calls take a stateless
+    kernel (no entry lists, no counter sets frozen into the graph, nothing
+    allocated while capturing), and every replay equals the oracle (ADVICE
+    r03: a replayed compacting path reused one counter set without zeroing
+    it; a missing state fell through to a kernel the comment did not name)."""
+    import torch
+
+    import wireglider_amd as wga
+
+    rng = np.random.default_rng(16 + warm)
+    for pkts in (interleaved_batch(rng, 5000), random_verify_batch(rng, 3000),
+                 [p for p in interleaved_batch(rng, 6000) if len(p) <= 64][:3000]):
+        buf, d = pack(pkts, rng)
+        dbuf = torch.from_numpy(buf).to(gpu)
+        dd = torch.from_numpy(d.view(np.int64).reshape(-1, 2).copy()).to(gpu)
+        n = len(d)
+        verdict = torch.empty(n, dtype=torch.uint8, device=gpu)
+        l4 = torch.empty(n, dtype=torch.uint16, device=gpu)
+        s = torch.cuda.Stream(gpu)
+        if warm:
+            with torch.cuda.stream(s):
+                for _ in range(3):  # the stream's state and sample exist before the capture
+                    wga.verify_desc(dbuf, dd, verdict=verdict, l4=l4)
+            torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            wga.verify_desc(dbuf, dd, verdict=verdict, l4=l4)
+        ev, el4 = oracle.verify_desc(buf, d)
+        for _ in range(3):
+            verdict.zero_()
+            l4.zero_()
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(verdict.cpu().numpy(), ev)
+            np.testing.assert_array_equal(l4.cpu().numpy(), el4)

@@ -4,7 +4,7 @@ bench.py workload, one process, one device.
 
 usage: ab.py <workload> [key=value[,key=value...] ...]
   e.g. ab.py config3 gso_groups=1 gso_groups=6 gso_groups=12,gso_waves=8
-       ab.py config5 l4_ppw=2 l4_ppw=4
+       ab.py config5 l4_small=0 l4_small=5
 Every variant starts from the library's defaults; rounds interleave the
 variants so clock / thermal drift hits them alike.  Prints one JSON object:
 variant -> median kernel ms and algorithmic GB/s.
@@ -17,10 +17,9 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
-KEYS = ("l4_blocks", "l4_ppw", "l4_nt", "l4_descv", "l4_iters", "l4_occ", "l4_small", "l4_small_uniform", "verify_small", "gso_blocks", "gso_waves", "gso_split", "gso_spw",
-        "gso_groups", "verify_occ", "verify_dm", "verify_hdr", "gro_lds", "gro_wide", "gro_chunks", "gso_ablate",
-        "l4_unroll", "host_chunk_mb", "l4_coop", "l4_coop_waves", "aead_k", "aead_pair", "l4_split_waves", "aead_flex",
-        "gro_iters", "encap_parts", "host_d2h")
+KEYS = ("l4_blocks", "l4_nt", "l4_small", "l4_small_uniform", "verify_small", "verify_auto_t", "verify_k2min",
+        "gso_blocks", "gso_waves", "gso_split", "gso_spw", "encap_spw", "gso_groups", "gso_ablate", "l4_unroll",
+        "host_chunk_mb", "l4_coop", "l4_coop_waves", "aead_k", "aead_pair", "aead_flex", "encap_parts", "host_d2h")
 
 
 def main():

@@ -14,7 +14,7 @@ verdicts and L4 results are compared with variant 0's.
 
 usage: verify_ab.py [variant ...] [--rounds R] [--batches a,b,...]
   a variant is key=value[,key=value...] of wg_tune_set keys (default: the
-  verify_small values 0, 3, 4, 5)
+  verify_small values 0, 7, 6, 8)
 """
 import json
 import statistics
@@ -75,7 +75,7 @@ def main():
         if opt in sys.argv:
             args.remove(sys.argv[sys.argv.index(opt) + 1])
     rounds = int(sys.argv[sys.argv.index("--rounds") + 1]) if "--rounds" in sys.argv else 5
-    specs = args or ["verify_small=0", "verify_small=7", "verify_small=6", "verify_small=4"]
+    specs = args or ["verify_small=0", "verify_small=7", "verify_small=6", "verify_small=8"]
     variants = [tuple((kv.split("=")[0], int(kv.split("=")[1])) for kv in a.split(",")) for a in specs]
     keys = sorted({k for v in variants for k, _ in v})
     dev = torch.device("cuda:0")

@@ -27,43 +27,30 @@ struct Knob {
     size_t nset;
 };
 
-static const uint64_t kPpw[] = {1, 2, 4, 8}, kOcc[] = {0, 7, 8}, kVOcc[] = {0, 6, 8}, kDm[] = {0, 2},
+static const uint64_t kL4Small[] = {0, 5}, kL4SU[] = {0, 2}, kVSmall[] = {0, 6, 7, 8},
                       kWaves[] = {1, 2, 4, 8}, kAbl[] = {0, 1, 32},
-                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {0, 1, 2, 3, 4}, kSplitW[] = {4, 8}, kGroIt[] = {1, 2, 4}, kParts[] = {1, 2, 3, 4, 8}, kWblk[] = {4, 16};
+                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {0, 1, 2, 3, 4}, kParts[] = {1, 2, 3, 4, 8};
 #define WG_N(a) (sizeof(a) / sizeof(a[0]))
 static const Knob kKnobs[] = {
     {"l4_blocks", &Tune::l4_blocks, nullptr, 1, 1u << 20, nullptr, 0},
-    {"l4_ppw", nullptr, &Tune::l4_ppw, 0, 0, kPpw, WG_N(kPpw)},
     {"l4_nt", nullptr, &Tune::l4_nt, 0, 1, nullptr, 0},
-    {"l4_descv", nullptr, &Tune::l4_descv, 0, 2, nullptr, 0},
-    {"l4_iters", nullptr, &Tune::l4_iters, 1, 64, nullptr, 0},
-    {"l4_occ", nullptr, &Tune::l4_occ, 0, 0, kOcc, WG_N(kOcc)},
-    {"l4_small", nullptr, &Tune::l4_small, 0, 7, nullptr, 0},
-    {"l4_small_uniform", nullptr, &Tune::l4_small_uniform, 0, 2, nullptr, 0},
+    {"l4_small", nullptr, &Tune::l4_small, 0, 0, kL4Small, WG_N(kL4Small)},
+    {"l4_small_uniform", nullptr, &Tune::l4_small_uniform, 0, 0, kL4SU, WG_N(kL4SU)},
     {"gso_blocks", &Tune::gso_blocks, nullptr, 1, 1u << 23, nullptr, 0},
     {"gso_waves", nullptr, &Tune::gso_waves, 0, 0, kWaves, WG_N(kWaves)},
     {"gso_split", nullptr, &Tune::gso_split, 1, 64, nullptr, 0},
     {"gso_groups", nullptr, &Tune::gso_groups, 1, 64, nullptr, 0},
     {"gso_spw", nullptr, &Tune::gso_spw, 0, 4, nullptr, 0},
     {"encap_spw", nullptr, &Tune::encap_spw, 0, 4, nullptr, 0},
-    {"verify_dm", nullptr, &Tune::verify_dm, 0, 0, kDm, WG_N(kDm)},
-    {"verify_occ", nullptr, &Tune::verify_occ, 0, 0, kVOcc, WG_N(kVOcc)},
-    {"verify_hdr", nullptr, &Tune::verify_hdr, 0, 1, nullptr, 0},
-    {"verify_small", nullptr, &Tune::verify_small, 0, 10, nullptr, 0},
+    {"verify_small", nullptr, &Tune::verify_small, 0, 0, kVSmall, WG_N(kVSmall)},
     {"verify_auto_t", nullptr, &Tune::verify_auto_t, 1, 64, nullptr, 0},
     {"verify_k2min", nullptr, &Tune::verify_k2min, 8, 65536, nullptr, 0},
-    {"verify_wblk", nullptr, &Tune::verify_wblk, 0, 0, kWblk, WG_N(kWblk)},
-    {"gro_lds", nullptr, &Tune::gro_lds, 0, 2, nullptr, 0},
-    {"gro_iters", nullptr, &Tune::gro_iters, 0, 0, kGroIt, WG_N(kGroIt)},
-    {"gro_wide", nullptr, &Tune::gro_wide, 0, 1, nullptr, 0},
-    {"gro_chunks", nullptr, &Tune::gro_chunks, 4, 5, nullptr, 0},
     {"gso_ablate", nullptr, &Tune::gso_ablate, 0, 0, kAbl, WG_N(kAbl)},
     {"host_chunk_mb", nullptr, &Tune::host_chunk_mb, 1, 4096, nullptr, 0},
     {"host_d2h", nullptr, &Tune::host_d2h, 0, 3, nullptr, 0},
     {"l4_unroll", nullptr, &Tune::l4_unroll, 0, 0, kUnroll, WG_N(kUnroll)},
     {"l4_coop", &Tune::l4_coop, nullptr, 0, 1u << 20, nullptr, 0},
     {"l4_coop_waves", nullptr, &Tune::l4_coop_waves, 0, 0, kCoopW, WG_N(kCoopW)},
-    {"l4_split_waves", nullptr, &Tune::l4_split_waves, 0, 0, kSplitW, WG_N(kSplitW)},
     {"aead_k", nullptr, &Tune::aead_k, 0, 0, kAeadK, WG_N(kAeadK)},
     {"aead_pair", nullptr, &Tune::aead_pair, 0, 2, nullptr, 0},
     {"aead_flex", nullptr, &Tune::aead_flex, 0, 1, nullptr, 0},
@@ -107,21 +94,14 @@ static Tune &tune_storage() {
         // wave, non-temporal loads: 7.26 TB/s vs 5.6 TB/s for a 2048-block
         // grid-stride launch with default-policy loads.
         x.l4_blocks = 1u << 20;
-        x.l4_ppw = 4;
         x.l4_nt = 1;
-        // Descriptor batches: each wave takes 4 iterations and prefetches the
-        // next iteration's descriptors by one vector load during the current
-        // one's finish (+3-5 % on config 5, profiles/r01_ab_session2.json).
-        x.l4_descv = 2;
-        x.l4_occ = 0;
         // Descriptor batches: the split-role kernel (l4_small = 5): small
         // packets of all-small groups a lane each, the rest wave-per-packet.
         // Config 4's 64-B sub-batch 0.336 -> 0.061 ms (35 % of the roofline);
         // config 5 and config 4's mixed batch within 0.6 % of the
         // wave-per-packet kernel (interleaved A/B, profiles/r02_small_ab.json).
         x.l4_small = 5;
-        x.l4_small_uniform = 2;  // lane per segment: 64-B PacketBatch 0.342 -> 0.043 ms (quad 0.074)
-        x.l4_iters = 4;
+        x.l4_small_uniform = 2;  // lane per segment: 64-B PacketBatch 0.342 -> 0.043 ms (a lane quad: 0.074)
         x.gso_blocks = 1u << 23;
         // GSO: three 4-wave blocks per super-buffer (3 groups -2.5 % vs 1 on
         // two boxes once the per-wave setup is one scalar round trip), each
@@ -137,20 +117,14 @@ static Tune &tune_storage() {
         // encap 18.37 -> 18.13 ms (profiles/r03_encap_gso_ab.json)
         x.encap_spw = 3;
         x.gso_groups = 3;
-        x.verify_occ = 8;
-        x.verify_dm = 0;
-        x.verify_hdr = 1;
+        // verify_small 7: per call the walking kernel (first call on a stream,
+        // all-small sample), the wave kernel or the compacting path, from a
+        // cost model of the previous call's sampled size mix (l4csum.hip
+        // wg_verify_desc); auto_t = the fewest small packets among the 64
+        // samples that may pick compaction
         x.verify_small = 7;
-        // verify_small 7: the kernel choice follows a cost model of the
-        // sampled size mix (l4csum.hip verify_pick_compact); auto_t = the
-        // fewest small packets among the 64 samples that may pick compaction
         x.verify_auto_t = 1;
         x.verify_k2min = 2048;
-        x.verify_wblk = 4;
-        x.gro_lds = 1;
-        x.gro_wide = 1;
-        x.gro_chunks = 5;
-        x.gro_iters = 1;
         x.gso_ablate = 0;
         // host pipeline chunk: 128-512 MiB reach 97-98 % of the raw H2D rate
         // (8 MiB: 70 %, per-chunk overheads; profiles/r02_host_path.json);
@@ -174,9 +148,6 @@ static Tune &tune_storage() {
         // of 1,500 B the split kernel wins 2x (profiles/r02_coop_probe.json)
         x.l4_coop = 16384;
         x.l4_coop_waves = 4;
-        // split kernel: 4-wave blocks (16 descriptors per wave); 8-wave blocks
-        // (8 per wave) config 4 -1.5 %, config 5 +13 % (profiles/r02_split_waves_ab.json)
-        x.l4_split_waves = 4;
         // AEAD: K consecutive ChaCha20 blocks per lane, chosen per batch (0:
         // 2 or 3, whichever fills the wave better), each lane's blocks two at
         // a time with interleaved quarter rounds (the kernel waits on
@@ -292,9 +263,10 @@ __global__ __launch_bounds__(256) void probe_read_runs_kernel(const uint8_t *dev
     if (lane == 0 && s == 0xFFFFFFFFu) *out = s;
 }
 
-// Copy-roofline probe: one-shot waves, each copying U contiguous KiB
-// (non-temporal loads, all issued first, then non-temporal stores).
-template <int U>
+// Copy-roofline probe: one-shot waves, each copying U contiguous KiB (all
+// loads issued first, then the stores; non-temporal loads and stores, or the
+// default cache policy when kNT is false).
+template <int U, bool kNT = true>
 __global__ __launch_bounds__(256) void probe_copy_kernel(const uint8_t *src, uint8_t *dst, uint64_t nchunks) {
     const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
     const uint64_t c0 = wave * (uint64_t)U * 64u;
@@ -306,13 +278,18 @@ __global__ __launch_bounds__(256) void probe_copy_kernel(const uint8_t *src, uin
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint64_t c = c0 + (uint64_t)u * 64u + lane;
-        v[u] = ld16_nt(s + 16u * (c < nchunks ? c : nchunks - 1));
+        v[u] = ld16x<kNT>(s + 16u * (c < nchunks ? c : nchunks - 1));
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint64_t c = c0 + (uint64_t)u * 64u + lane;
-        if (c < nchunks)
-            __builtin_nontemporal_store(v[u], reinterpret_cast<__attribute__((address_space(1))) v4u *>(d + 16u * c));
+        auto *p = reinterpret_cast<__attribute__((address_space(1))) v4u *>(d + 16u * c);
+        if (c < nchunks) {
+            if constexpr (kNT)
+                __builtin_nontemporal_store(v[u], p);
+            else
+                *p = v[u];
+        }
     }
 }
 
@@ -325,13 +302,20 @@ extern "C" int wg_probe_copy(const uint8_t *src, uint8_t *dst, uint64_t nbytes, 
         return WG_ERR_INVALID;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const uint64_t nch = nbytes >> 4;
+    const bool dflt = kib_per_wave & WG_PROBE_DEFAULT_POLICY;  // default cache policy instead of non-temporal
+    kib_per_wave &= ~WG_PROBE_DEFAULT_POLICY;
     const uint32_t U = kib_per_wave == 2 || kib_per_wave == 4 ? kib_per_wave : 1;
     uint64_t blocks = (nch + 256ull * U - 1) / (256ull * U);
     if (blocks >= 8) blocks = (blocks + 7) & ~7ull;
-    switch (U) {
-    case 2: hipLaunchKernelGGL(probe_copy_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, nch); break;
-    case 4: hipLaunchKernelGGL(probe_copy_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, nch); break;
-    default: hipLaunchKernelGGL(probe_copy_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, nch); break;
+    if (blocks > 0x7fffffffull) return WG_ERR_INVALID;
+    const dim3 g((unsigned)blocks), b(256);
+    switch (U * 2 + (dflt ? 1 : 0)) {
+    case 4: hipLaunchKernelGGL((probe_copy_kernel<2, true>), g, b, 0, st, src, dst, nch); break;
+    case 5: hipLaunchKernelGGL((probe_copy_kernel<2, false>), g, b, 0, st, src, dst, nch); break;
+    case 8: hipLaunchKernelGGL((probe_copy_kernel<4, true>), g, b, 0, st, src, dst, nch); break;
+    case 9: hipLaunchKernelGGL((probe_copy_kernel<4, false>), g, b, 0, st, src, dst, nch); break;
+    case 3: hipLaunchKernelGGL((probe_copy_kernel<1, false>), g, b, 0, st, src, dst, nch); break;
+    default: hipLaunchKernelGGL((probe_copy_kernel<1, true>), g, b, 0, st, src, dst, nch); break;
     }
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }

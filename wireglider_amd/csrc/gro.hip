@@ -10,7 +10,8 @@
 // overload and sums the std::span objects (pointer + size) instead —
 // pointer-dependent, not reproduced.
 //
-// Header-only work (tens of bytes per flow): one thread per flow.
+// Header-only work (tens of bytes per flow): one thread per flow, header
+// chunks staged cooperatively through LDS.
 #include <hip/hip_runtime.h>
 
 #include "wg_device.hpp"
@@ -64,15 +65,15 @@ __device__ __forceinline__ void st128_u(uint8_t *p, v4u v) {
     *reinterpret_cast<__attribute__((address_space(1))) v4u *>(reinterpret_cast<uintptr_t>(p)) = v;
 }
 
-// kWide: the fields go out in two wide stores instead of four or five
-// narrow ones (stores at a 64-B lane stride are address-processing bound,
-// so instructions, not bytes, are the cost): IPv4 header bytes [0, 16)
-// (ip_len and ip_sum with the 12 unchanged bytes around them) or the IPv6
-// payload length as one dword, and for UDP the length and the seed as one
-// dword (csum_offset 6, adjacent fields).  Every byte written lies in the
-// flow's own header and the unchanged ones get their own values back.  The
-// caller writes udp->len itself when !kWide.
-template <bool kWide>
+// The fields go out in two wide stores instead of four or five narrow ones
+// (stores at a 64-B lane stride are address-processing bound, so
+// instructions, not bytes, are the cost; narrow stores of the changed 2-B
+// fields only measured the same, profiles/r02_store_granularity.json): IPv4
+// header bytes [0, 16) (ip_len and ip_sum with the 12 unchanged bytes around
+// them) or the IPv6 payload length as one dword, and for UDP the length and
+// the seed as one dword (csum_offset 6, adjacent fields).  Every byte written
+// lies in the flow's own header and the unchanged ones get their own values
+// back.
 __device__ __forceinline__ void gro_fields(uint8_t *h, const wg_gro_desc &d, bool v6, bool tcp, uint64_t l4len,
                                            v4u k0, v4u k1, v4u k2, v4u k3, v4u k4) {
     const uint32_t W[20] = {k0[0], k0[1], k0[2], k0[3], k1[0], k1[1], k1[2], k1[3], k2[0], k2[1],
@@ -96,19 +97,11 @@ __device__ __forceinline__ void gro_fields(uint8_t *h, const wg_gro_desc &d, boo
         for (int m = 3; m < 16; m++)
             sip += sum16x2(keep_below(R[m], m, cs));
         const uint32_t c = ~fold16_32(sip + bswap16(T)) & 0xffffu;  // :103-106
-        if constexpr (kWide) {
-            st128_u(h, v4u{(R[0] & 0xffffu) | (bswap16(T) << 16), R[1], (R[2] & 0xffffu) | (c << 16), R[3]});
-        } else {
-            st16_ne(h + 2, bswap16(T));
-            st16_ne(h + 10, c);  // native order
-        }
+        st128_u(h, v4u{(R[0] & 0xffffu) | (bswap16(T) << 16), R[1], (R[2] & 0xffffu) | (c << 16), R[3]});
         sad = sum16x2(R[3]) + sum16x2(R[4]);
         proto = (R[2] >> 8) & 0xffu;
     } else {
-        if constexpr (kWide)
-            st32_u(h + 4, (R[1] & 0xffff0000u) | bswap16(l16));  // :95
-        else
-            st16_ne(h + 4, bswap16(l16));  // :95
+        st32_u(h + 4, (R[1] & 0xffff0000u) | bswap16(l16));  // :95
         sad = 0;
 #pragma unroll
         for (int m = 2; m < 10; m++)
@@ -116,24 +109,13 @@ __device__ __forceinline__ void gro_fields(uint8_t *h, const wg_gro_desc &d, boo
         proto = (R[1] >> 16) & 0xffu;
     }
     const uint32_t seed = ~fold16_32(sad + (proto << 8) + bswap16(l16)) & 0xffffu;  // :108-112
-    if (kWide && !tcp && d.csum_offset == 6) {
+    if (!tcp && d.csum_offset == 6) {
         st32_u(h + cs + 4, bswap16(l16) | (seed << 16));  // udp->len (:85-86) + seed (:114)
         return;
     }
-    if (kWide && !tcp)
-        st_be16(h + cs + 4, l16);               // udp->len, :85-86
+    if (!tcp)
+        st_be16(h + cs + 4, l16);           // udp->len, :85-86
     st16_ne(h + cs + d.csum_offset, seed);  // native order, :114
-}
-
-__device__ __forceinline__ void gro_fast(uint8_t *h, const wg_gro_desc &d, bool v6, uint64_t l4len, uint32_t need) {
-    const uint64_t addr = (uint64_t)(uintptr_t)h;
-    const uintptr_t a0 = (uintptr_t)(addr & ~15ull);
-    const uintptr_t alast = (uintptr_t)((addr + need - 1) & ~15ull);
-    auto chunk = [&](uint32_t c) {
-        const uintptr_t a = a0 + 16u * c;
-        return ld16(a > alast ? alast : a);
-    };
-    gro_fields<false>(h, d, v6, true, l4len, chunk(0), chunk(1), chunk(2), chunk(3), chunk(4));
 }
 
 // General path (header fields beyond 64 bytes): byte loop in reference order.
@@ -166,56 +148,27 @@ __device__ __noinline__ void gro_slow(uint8_t *h, uint32_t H, uint32_t cs, uint3
     stb(h + l4off + 1, seed >> 8);
 }
 
-__global__ __launch_bounds__(256) void gro_finalize_kernel(uint8_t *hdrs, wg_gro_desc *desc, uint64_t n) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n)
-        return;
-    const wg_gro_desc d = desc[i];
-    uint8_t *h = hdrs + d.hdr_offset;
-    const uint32_t H = d.hdr_len, cs = d.csum_start, l4off = (uint32_t)d.csum_start + d.csum_offset;
-    const bool v6 = d.flags & WG_PKT_V6, tcp = d.flags & WG_PKT_TCP;
-    const uint32_t iph = v6 ? 40u : 20u;
-    int8_t st = 0;
-    if (cs < iph || cs > H || l4off < cs || l4off + 2 > H || (!tcp && cs + 8 > H)) {
-        st = -3;
-    } else {
-        const uint64_t l4len = (uint64_t)(H - cs) + d.payload_bytes;  // :84
-        if (!tcp)
-            st_be16(h + cs + 4, (uint32_t)l4len);  // udp->len (uint16), :85-86
-        const uint32_t need = v6 ? 40u : cs;
-        if (need <= kFastNeed)
-            gro_fast(h, d, v6, l4len, need);
-        else
-            gro_slow(h, H, cs, l4off, d.payload_bytes, v6, l4len);
-    }
-    if (d.status != st)  // leave descriptor lines clean when the caller pre-zeroed status
-        reinterpret_cast<int8_t *>(desc)[i * sizeof(wg_gro_desc) + offsetof(wg_gro_desc, status)] = st;
-}
-
-// LDS-staged variant.  Thread per flow, but the header chunks are fetched
-// cooperatively: the block's 256 flows need up to 5 aligned 16-B chunks
-// each; lane L loads chunk slots L, L+256, ... (slot k = chunk k % 5 of flow
-// k / 5), so consecutive lanes read consecutive chunks of one flow and a
+// The kernel: a thread per flow for the arithmetic, but the header chunks
+// are fetched cooperatively: the block's 256 flows need up to 5 aligned 16-B
+// chunks each; lane L loads chunk slots L, L+256, ... (slot k = chunk k % 5 of
+// flow k / 5), so consecutive lanes read consecutive chunks of one flow and a
 // wave-instruction touches a few contiguous lines instead of 64 scattered
 // ones (thread-per-flow loads at a 64-B lane stride are address-processing
 // bound: about one cache line per cycle per CU).  The chunks go through LDS
-// to their flow's thread, which then runs the same arithmetic.
-// K = chunks staged per flow: 5 covers every header the fast path takes (<= 64
-// bytes at any alignment); 4 covers <= 48 bytes (v6, v4 with up to 28 B of
-// options; longer go to the byte path) in 19 KB of LDS instead of 23 KB, i.e.
-// 8 resident blocks per CU instead of 6.
+// to their flow's thread, which then runs gro_fields.  Five chunks cover
+// every header of <= 64 bytes at any alignment; longer ones take the byte
+// path.  (Measured and dropped: thread-per-flow loads, 4 chunks per flow,
+// wave-owned staging without the block barrier, narrow field stores.)
 constexpr uint32_t kGroBlock = 256;
+constexpr uint32_t kGroChunks = 5;
 static __device__ v4u g_gro_zero;  // load target of slots with nothing to stage
 
-template <uint32_t K>
-__device__ __forceinline__ uint32_t flow_of_slot(uint32_t slot) {  // slot / K for slot < 256 * K
-    return K == 4 ? slot >> 2 : (slot * 52429u) >> 18;
+__device__ __forceinline__ uint32_t flow_of_slot(uint32_t slot) {  // slot / 5 for slot < 256 * 5
+    return (slot * 52429u) >> 18;
 }
 
-template <bool kWide, uint32_t kGroChunks = 5>
 __global__ __launch_bounds__(kGroBlock) void gro_finalize_lds_kernel(uint8_t *hdrs, wg_gro_desc *desc, uint64_t n) {
-    static_assert(kGroChunks == 4 || kGroChunks == 5, "4 or 5 chunks per flow");
-    constexpr uint32_t kNeedMax = kGroChunks == 5 ? kFastNeed : 48u;
+    constexpr uint32_t kNeedMax = kFastNeed;
     __shared__ v4u s_chunk[kGroBlock * kGroChunks];
     __shared__ uint64_t s_a0[kGroBlock];
     __shared__ uint32_t s_last[kGroBlock];  // last chunk index to load, or 0xff: nothing to stage
@@ -253,7 +206,7 @@ __global__ __launch_bounds__(kGroBlock) void gro_finalize_lds_kernel(uint8_t *hd
     uint64_t a0[kGroChunks];
 #pragma unroll
     for (uint32_t k = 0; k < kGroChunks; k++) {  // every LDS read first (unconditional), then the loads
-        const uint32_t f = flow_of_slot<kGroChunks>(t + kGroBlock * k);
+        const uint32_t f = flow_of_slot(t + kGroBlock * k);
         lst[k] = s_last[f];
         a0[k] = s_a0[f];
     }
@@ -261,7 +214,7 @@ __global__ __launch_bounds__(kGroBlock) void gro_finalize_lds_kernel(uint8_t *hd
 #pragma unroll
     for (uint32_t k = 0; k < kGroChunks; k++) {
         const uint32_t slot = t + kGroBlock * k;
-        const uint32_t c = slot - kGroChunks * flow_of_slot<kGroChunks>(slot);
+        const uint32_t c = slot - kGroChunks * flow_of_slot(slot);
         const uint32_t last = lst[k];
         const uintptr_t a = last != 0xffu ? a0[k] + 16u * (c < last ? c : last)
                                           : reinterpret_cast<uintptr_t>(&g_gro_zero);
@@ -275,122 +228,17 @@ __global__ __launch_bounds__(kGroBlock) void gro_finalize_lds_kernel(uint8_t *hd
         return;
     if (st == 0) {
         const uint64_t l4len = (uint64_t)(d.hdr_len - cs) + d.payload_bytes;  // :84
-        if (!tcp && !(kWide && fast))
-            st_be16(h + cs + 4, (uint32_t)l4len);  // udp->len (uint16), :85-86
         if (fast) {
             const v4u *k = &s_chunk[t * kGroChunks];
-            // K = 4: header bytes >= 48 are never used (need <= 48; the
-            // v4 sum masks bytes >= csum_start), so chunk 4 may be zero
-            gro_fields<kWide>(h, d, v6, tcp, l4len, k[0], k[1], k[2], k[3],
-                              kGroChunks == 5 ? k[kGroChunks - 1] : v4u{0, 0, 0, 0});
+            gro_fields(h, d, v6, tcp, l4len, k[0], k[1], k[2], k[3], k[4]);
         } else {
+            if (!tcp)
+                st_be16(h + cs + 4, (uint32_t)l4len);  // udp->len (uint16), :85-86
             gro_slow(h, d.hdr_len, cs, l4off, d.payload_bytes, v6, l4len);
         }
     }
     if (d.status != st)  // leave descriptor lines clean when the caller pre-zeroed status
         reinterpret_cast<int8_t *>(desc)[i * sizeof(wg_gro_desc) + offsetof(wg_gro_desc, status)] = st;
-}
-
-// Wave-owned variant (knob gro_lds = 2): the same cooperative chunk loads,
-// but each wave owns 64 flows and stages only its own chunks, so no block
-// barrier sits between the descriptor round trip and the chunk round trip
-// (the LDS kernel's block of 256 flows waits for its slowest wave twice).
-// The per-flow chunk geometry reaches the loading lanes by ds_bpermute and
-// the chunks their flow's lane through a wave-private LDS tile; LDS ops of
-// one wave execute in order, so a wave-scope fence is all the ordering the
-// tile needs.  kIters > 1: each wave takes kIters groups of 64 flows a grid
-// stride apart and loads the next group's descriptors while the current
-// group's chunks are in flight.
-__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
-    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
-}
-
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-template <bool kWide, int kIters>
-__global__ __launch_bounds__(kGroBlock) void gro_finalize_wave_kernel(uint8_t *hdrs, wg_gro_desc *desc, uint64_t n) {
-    constexpr uint32_t K = 5;
-    __shared__ v4u s_tile[kGroBlock / 64][64 * K];
-    const uint32_t lane = lane_id(), w = wave_in_block();
-    v4u *tile = s_tile[w];
-    const uint64_t wave = (uint64_t)blockIdx.x * (kGroBlock / 64) + w;
-    const uint64_t gstride = (uint64_t)gridDim.x * kGroBlock;  // flows between a wave's groups
-    uint64_t i = wave * 64u + lane;
-    wg_gro_desc d{};
-    if (i < n)
-        d = desc[i];
-    for (int it = 0; it < kIters; it++) {
-        const bool live = i < n;
-        bool fast = false, v6 = false, tcp = false;
-        int8_t st = 0;
-        uint32_t need = 0, cs = 0, l4off = 0;
-        uint8_t *h = hdrs;
-        if (live) {
-            h = hdrs + d.hdr_offset;
-            const uint32_t H = d.hdr_len;
-            cs = d.csum_start;
-            l4off = cs + d.csum_offset;
-            v6 = d.flags & WG_PKT_V6;
-            tcp = d.flags & WG_PKT_TCP;
-            const uint32_t iph = v6 ? 40u : 20u;
-            if (cs < iph || cs > H || l4off < cs || l4off + 2 > H || (!tcp && cs + 8 > H))
-                st = -3;
-            else {
-                need = v6 ? 40u : cs;
-                fast = need <= kFastNeed;
-            }
-        }
-        const uintptr_t hp = reinterpret_cast<uintptr_t>(h);
-        const uint64_t a0 = (uint64_t)(hp & ~(uintptr_t)15);
-        const uint32_t last = fast ? (uint32_t)(((hp & 15u) + need - 1) >> 4) : 0xffu;
-        // slot k * 64 + lane = chunk c of flow f = slot / 5: every load issued
-        // before any is used, branch-free (no-stage slots read the zero chunk)
-        v4u v[K];
-#pragma unroll
-        for (uint32_t k = 0; k < K; k++) {
-            const uint32_t slot = 64u * k + lane;
-            const uint32_t f = (slot * 52429u) >> 18;  // slot / 5
-            const uint32_t c = slot - 5u * f;
-            const uint32_t lf = bperm(last, f);
-            const uint64_t af = ((uint64_t)bperm((uint32_t)(a0 >> 32), f) << 32) | bperm((uint32_t)a0, f);
-            const uintptr_t a = lf != 0xffu ? (uintptr_t)(af + 16u * (c < lf ? c : lf))
-                                            : reinterpret_cast<uintptr_t>(&g_gro_zero);
-            v[k] = ld16(a);
-        }
-        // the next group's descriptors, in flight under this group's chunks
-        const uint64_t inext = i + gstride;
-        wg_gro_desc dn{};
-        if (kIters > 1 && it + 1 < kIters && inext < n)
-            dn = desc[inext];
-#pragma unroll
-        for (uint32_t k = 0; k < K; k++)
-            tile[64u * k + lane] = v[k];
-        wave_lds_sync();
-        if (live) {
-            if (st == 0) {
-                const uint64_t l4len = (uint64_t)(d.hdr_len - cs) + d.payload_bytes;  // :84
-                if (!tcp && !(kWide && fast))
-                    st_be16(h + cs + 4, (uint32_t)l4len);  // udp->len (uint16), :85-86
-                if (fast) {
-                    const v4u *kk = &tile[lane * K];
-                    gro_fields<kWide>(h, d, v6, tcp, l4len, kk[0], kk[1], kk[2], kk[3], kk[4]);
-                } else {
-                    gro_slow(h, d.hdr_len, cs, l4off, d.payload_bytes, v6, l4len);
-                }
-            }
-            if (d.status != st)  // leave descriptor lines clean when the caller pre-zeroed status
-                reinterpret_cast<int8_t *>(desc)[i * sizeof(wg_gro_desc) + offsetof(wg_gro_desc, status)] = st;
-        }
-        if (kIters == 1)
-            break;
-        wave_lds_sync();  // this group's tile reads before the next group's writes
-        i = inext;
-        d = dn;
-    }
 }
 
 }  // namespace wg
@@ -405,33 +253,7 @@ extern "C" int wg_gro_finalize(uint8_t *dev_hdrs, wg_gro_desc *dev_desc, uint64_
     const uint64_t blocks = (n + 255) / 256;
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
-    const Tune t = tune();
-    if (t.gro_lds == 2) {
-        const uint32_t it = t.gro_iters;
-        uint64_t b = (blocks + it - 1) / it;
-        hipStream_t st = static_cast<hipStream_t>(stream);
-        if (it == 2)
-            hipLaunchKernelGGL((gro_finalize_wave_kernel<true, 2>), dim3((unsigned)b), dim3(kGroBlock), 0, st,
-                               dev_hdrs, dev_desc, n);
-        else if (it == 4)
-            hipLaunchKernelGGL((gro_finalize_wave_kernel<true, 4>), dim3((unsigned)b), dim3(kGroBlock), 0, st,
-                               dev_hdrs, dev_desc, n);
-        else
-            hipLaunchKernelGGL((gro_finalize_wave_kernel<true, 1>), dim3((unsigned)blocks), dim3(kGroBlock), 0, st,
-                               dev_hdrs, dev_desc, n);
-        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
-    }
-    if (t.gro_lds && t.gro_wide && t.gro_chunks == 4)
-        hipLaunchKernelGGL((gro_finalize_lds_kernel<true, 4>), dim3((unsigned)blocks), dim3(kGroBlock), 0,
-                           static_cast<hipStream_t>(stream), dev_hdrs, dev_desc, n);
-    else if (t.gro_lds && t.gro_wide)
-        hipLaunchKernelGGL(gro_finalize_lds_kernel<true>, dim3((unsigned)blocks), dim3(kGroBlock), 0,
-                           static_cast<hipStream_t>(stream), dev_hdrs, dev_desc, n);
-    else if (t.gro_lds)
-        hipLaunchKernelGGL(gro_finalize_lds_kernel<false>, dim3((unsigned)blocks), dim3(kGroBlock), 0,
-                           static_cast<hipStream_t>(stream), dev_hdrs, dev_desc, n);
-    else
-        hipLaunchKernelGGL(gro_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
-                           dev_hdrs, dev_desc, n);
+    hipLaunchKernelGGL(gro_finalize_lds_kernel, dim3((unsigned)blocks), dim3(kGroBlock), 0,
+                       static_cast<hipStream_t>(stream), dev_hdrs, dev_desc, n);
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -122,15 +123,34 @@ int pipe_init(Pipe &c) {
     c.release();  // first use on this thread, or the thread switched devices (current device kept)
     static std::once_flag once;
     std::call_once(once, [] { std::atexit([] { g_exiting.store(true); }); });
-    c.device = dev;
+    // Test hook (WG_TEST_PIPE_FAIL=k, read once): the process's first
+    // pipeline build fails at its k-th event creation, as under resource
+    // exhaustion (tests/test_gpu_hostpath.py::test_pipeline_build_failure).
+    static std::atomic<int> fail_at{[] {
+        const char *v = std::getenv("WG_TEST_PIPE_FAIL");
+        return v && *v ? std::atoi(v) : 0;
+    }()};
+    int nev = 0;
+    auto mk_event = [&](hipEvent_t *e) {
+        if (++nev == fail_at.load() && fail_at.exchange(0) != 0) {
+            *e = nullptr;
+            return false;
+        }
+        return hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+    };
+    // Every handle is created before the pipeline is marked as built for
+    // this device: a failure part-way releases what exists, so the next call
+    // builds it again instead of finding null streams or events.
+    bool ok = true;
     for (hipStream_t &st : c.s)
-        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
-            return WG_ERR_RUNTIME;
-    for (int k = 0; k < kSlots; k++)
-        if (hipEventCreateWithFlags(&c.copied[k], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c.computed[k], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c.drained[k], hipEventDisableTiming) != hipSuccess)
-            return WG_ERR_RUNTIME;
+        ok = ok && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+    for (int k = 0; k < kSlots && ok; k++)
+        ok = mk_event(&c.copied[k]) && mk_event(&c.computed[k]) && mk_event(&c.drained[k]);
+    c.device = dev;  // release() below, or the built pipeline
+    if (!ok) {
+        c.release();
+        return WG_ERR_RUNTIME;
+    }
     return WG_OK;
 }
 
@@ -427,8 +447,12 @@ extern "C" int wg_encap_host(const uint8_t *host_in, const wg_gso_desc *host_des
             return WG_ERR_INVALID;
     // chunk boundaries: super-buffers until ~host_chunk_mb MiB of input (at
     // least one per chunk), every chunk's message count within the scan's
-    // 32-bit index and n <= 2^20 per device call
+    // 32-bit index and n <= 2^20 per device call; and the chunk's per-slot
+    // OUTPUT buffers (messages at msg_cap each, split headers at out_cap
+    // each) within twice that budget, so many small tun reads with a msg_cap
+    // sized for 64-KiB TSO reads do not size a slot at tens of GiB
     const uint64_t cb = chunk_bytes();
+    const uint64_t ob = 2 * cb;
     const uint64_t max_cnt_call = (((1ull << 32) - 1) / max_segments) < (1ull << 20)
                                       ? (((1ull << 32) - 1) / max_segments)
                                       : (1ull << 20);
@@ -442,7 +466,8 @@ extern "C" int wg_encap_host(const uint8_t *host_in, const wg_gso_desc *host_des
         do {
             segb += host_desc[i].out_cap;
             i++;
-        } while (i < n && i - i0 < max_cnt_call && host_desc[i].in_offset + host_desc[i].in_len - s0 <= cb);
+        } while (i < n && i - i0 < max_cnt_call && host_desc[i].in_offset + host_desc[i].in_len - s0 <= cb &&
+                 (i - i0 + 1) * (uint64_t)msg_cap <= ob && segb + host_desc[i].out_cap <= ob);
         const uint64_t span = host_desc[i - 1].in_offset + host_desc[i - 1].in_len - s0;
         bounds.push_back(i);
         max_cnt = i - i0 > max_cnt ? i - i0 : max_cnt;

@@ -94,16 +94,15 @@ __device__ __forceinline__ void geoms_from_vec(const L4Params &p, uint64_t i0, c
     }
 }
 
-// Descriptor modes (kDM): 0 = scalar loads per iteration; 1 = one vector load
-// per iteration (measured slower: the readlanes wait on it); 2 = scalar loads
-// for a wave's first iteration, and each iteration's vector load of the NEXT
-// iteration's descriptors issued right after its own packet loads, so from
-// the second iteration on a wave starts its packet loads with no descriptor
-// round trip in front of them (the launcher gives each wave l4_iters
-// iterations).
-template <int kKind, int P, bool kNT, int kDM, int O = 0>  // O: waves/SIMD target (0 = compiler's choice)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void l4csum_kernel(
-    L4Params p) {
+// Descriptor modes (kDM): 0 = scalar descriptor loads per iteration (uniform
+// batches need none); 2 = scalar loads for a wave's first iteration, and each
+// iteration's vector load of the NEXT iteration's descriptors issued right
+// after its own packet loads, so from the second iteration on a wave starts
+// its packet loads with no descriptor round trip in front of them (the
+// launcher gives each wave 4 iterations; one vector load per iteration
+// without the prefetch measured slower: the readlanes wait on it).
+template <int kKind, int P, bool kNT, int kDM>
+__global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
     constexpr bool kL4 = kKind != kDescPlain;
     constexpr int DM = kKind == kUniformL4 ? 0 : kDM;
     const uint32_t lane = lane_id();
@@ -114,9 +113,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
     for (uint64_t i0 = wave0 * P; i0 < p.n; i0 += step) {
         Geom g[P];
         Front f[P];
-        if constexpr (DM == 1) {
-            geoms_from_vec<kKind, P>(p, i0, load_desc_vec<P>(p, i0, lane), g);
-        } else if constexpr (DM == 2) {
+        if constexpr (DM == 2) {
             if (have_next) {
                 geoms_from_vec<kKind, P>(p, i0, nextd, g);
             } else {
@@ -155,67 +152,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
     }
 }
 
-template <int kKind, int P, bool kNT, int DM>
-static void launch_occ(const L4Params &p, uint64_t blocks, hipStream_t st) {
-    const uint32_t occ = tune().l4_occ;
-    if constexpr (P == 4 && kNT) {
-        if (occ == 7) {
-            hipLaunchKernelGGL((l4csum_kernel<kKind, P, kNT, DM, 7>), dim3((unsigned)blocks), dim3(256), 0, st, p);
-            return;
-        }
-        if (occ == 8) {
-            hipLaunchKernelGGL((l4csum_kernel<kKind, P, kNT, DM, 8>), dim3((unsigned)blocks), dim3(256), 0, st, p);
-            return;
-        }
-    }
-    hipLaunchKernelGGL((l4csum_kernel<kKind, P, kNT, DM>), dim3((unsigned)blocks), dim3(256), 0, st, p);
-}
-
-template <int kKind, int P, bool kNT>
-static void launch_variant(const L4Params &p, uint64_t blocks, hipStream_t st) {
-    const uint32_t dm = kKind == kUniformL4 ? 0u : tune().l4_descv;
-    if (dm == 1)
-        launch_occ<kKind, P, kNT, 1>(p, blocks, st);
-    else if (dm == 2)
-        launch_occ<kKind, P, kNT, 2>(p, blocks, st);
-    else
-        launch_occ<kKind, P, kNT, 0>(p, blocks, st);
-}
-
-template <int kKind>
-static void launch_kind(const L4Params &p, uint64_t blocks, uint32_t P, bool nt, hipStream_t st) {
-    switch (P) {
-    case 1: nt ? launch_variant<kKind, 1, true>(p, blocks, st) : launch_variant<kKind, 1, false>(p, blocks, st); break;
-    case 2: nt ? launch_variant<kKind, 2, true>(p, blocks, st) : launch_variant<kKind, 2, false>(p, blocks, st); break;
-    case 8: nt ? launch_variant<kKind, 8, true>(p, blocks, st) : launch_variant<kKind, 8, false>(p, blocks, st); break;
-    default: nt ? launch_variant<kKind, 4, true>(p, blocks, st) : launch_variant<kKind, 4, false>(p, blocks, st); break;
-    }
-}
-
 // ---------------------------------------------------------------------------
-// Small-packet descriptor kernel (knob l4_small; SURVEY §8(d) config 4's
-// small-packet stress).  A wave per packet spends ~150 wave-instructions
-// (half of them on the CU's one scalar unit) on a 64-B packet, so 64-B
-// batches are issue-bound at ~6 % of the HBM roofline.  Here a lane (or a
-// lane quad, G below) takes one descriptor: a packet of <= kSmallMax bytes is
-// summed from (at most) five aligned 16-B chunks — by a lane as 16
-// packet-relative dwords funnel-shifted out of them, by a quad as masked
-// absolute dwords — over the summed region and the pseudo-header address
-// bytes; the lanes whose packet is longer are then taken by the whole wave,
-// Q at a time, through the same issue / finish machinery as l4csum_kernel.
-// Uniform PacketBatches with segment_size <= kSmallMax use it too (every
-// segment is small).  Same arithmetic model (wg_device.hpp): one byte swap of
-// a folded sum whose pairing starts at an odd position.
+// Small packets (SURVEY §8(d) config 4's small-packet stress).  A wave per
+// packet spends ~150 wave-instructions (half of them on the CU's one scalar
+// unit) on a 64-B packet, so 64-B batches are issue-bound at ~6 % of the HBM
+// roofline by l4csum_kernel.  A lane takes a packet of <= kSmallMax bytes
+// instead: summed from (at most) five aligned 16-B chunks funnel-shifted into
+// 16 packet-relative dwords, over the summed region and the pseudo-header
+// address bytes.  Same arithmetic model (wg_device.hpp): one byte swap of a
+// folded sum whose pairing starts at an odd position.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSmallMax = 64;  // bytes: five aligned 16-B chunks at any alignment
-
-// Bytes of the dword at relative position p (a multiple of 4) that lie in [lo, hi).
-__device__ __forceinline__ uint32_t dword_mask(uint32_t p, uint32_t lo, uint32_t hi) {
-    const int a = (int)lo - (int)p, b = (int)hi - (int)p;
-    const uint32_t mh = b >= 4 ? ~0u : (b <= 0 ? 0u : (1u << (8 * b)) - 1u);
-    const uint32_t ml = a >= 4 ? ~0u : (a <= 0 ? 0u : (1u << (8 * a)) - 1u);
-    return mh & ~ml;
-}
 
 __device__ __forceinline__ uint32_t half_sum(uint32_t w) { return (w & 0xffffu) + (w >> 16); }
 
@@ -326,124 +273,22 @@ __device__ __forceinline__ void wave_long(uint64_t m, uintptr_t a, uint32_t len,
     }
 }
 
-// G: lanes per descriptor.  G = 1: a lane loads all five chunks; G = 4: a
-// quad shares one descriptor, lane q of the quad loads chunks q and (q = 0)
-// chunk 4, and the quad's partial sums meet by DPP — a wave then carries 16
-// descriptors instead of 64, so its serial walk over the long packets is as
-// short as the wave-per-packet kernel's four iterations.
-template <int kKind, bool kNT, int Q, int G, bool kLate = false>  // Q: long packets the wave takes at a time (2, 4)
-__global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
-    static_assert(G == 1 || G == 4, "lanes per descriptor");
-    constexpr bool kL4 = kKind != kDescPlain;
-    const uint32_t lane = lane_id();
-    const uint32_t q = lane & (uint32_t)(G - 1);
-    const uint64_t i = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * (256u / G) + threadIdx.x / G;
+// Uniform PacketBatches of small segments (segment_size <= kSmallMax; knob
+// l4_small_uniform = 2): every segment is small, so a lane per segment, summed
+// by lane_chunks / lane_sum — no descriptors, no wave role.
+__global__ __launch_bounds__(256) void l4csum_uniform_small_kernel(L4Params p) {
+    const uint64_t i = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 256u + threadIdx.x;
     const bool live = i < p.n;
-    uintptr_t a;
-    uint32_t len, cs, fl;
-    if constexpr (kKind == kUniformL4) {  // PacketBatch segment i (include/util/packets.hpp:23-36)
-        const uint64_t off = live ? i * (uint64_t)p.seg : 0u;
-        const uint64_t rem = p.total_len - off;
-        a = reinterpret_cast<uintptr_t>(p.base) + off;
-        len = live ? (rem < p.seg ? (uint32_t)rem : p.seg) : 0u;
-        cs = live ? p.cs : 0u;
-        fl = live ? p.flags : 0u;
-    } else {
-        const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0));
-        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
-        a = reinterpret_cast<uintptr_t>(p.base) + (live ? off : 0u);
-        len = live ? dv.z : 0u;
-        cs = kL4 && live ? (dv.w & 0xffffu) : 0u;
-        fl = live ? (dv.w >> 16) & 0xffu : 0u;
-    }
-    const bool small = len <= kSmallMax;
-
-    // ---- lane path: the packet's aligned chunks, all issued at once.
-    // kLate: the loads go out before the wave path and are summed after it,
-    // so they fly under the long packets' loads; otherwise loaded and summed
-    // here, skipped by waves whose packets are all long (uniform branch).
-    uint32_t res = 0;
-    const bool any_small = __ballot(live && small) != 0;
-    constexpr uint32_t kC = G == 1 ? 5u : 2u;  // chunks per lane
-    v4u W[kC];
-    uint32_t cidx[kC];
-    const uint32_t s = (uint32_t)(a & 15u);
-    auto load_chunks = [&]() {
-        if constexpr (G == 1) {
-            lane_chunks(a, len, small && len, W);
-            return;
-        }
-        const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
-        const uintptr_t a0 = a & ~(uintptr_t)15;
-        const uintptr_t alast = (a + len - 1) & ~(uintptr_t)15;
-        const bool any = small && len;
-#pragma unroll
-        for (uint32_t k = 0; k < kC; k++) {
-            cidx[k] = G == 1 ? k : q + 4u * k;  // G = 4: chunks q and q + 4 (< 5 only for q = 0)
-            const uintptr_t ca = a0 + 16u * cidx[k];
-            const bool use = any && cidx[k] < 5u;
-            // default-policy loads, not kNT: a small packet's 128-B lines are
-            // shared with its neighbours' lanes (and the clamped duplicates),
-            // so non-temporal loads fetched them again (64-B PacketBatch
-            // 42.9 -> 24.3 us with cached loads)
-            W[k] = ld16(use ? (ca > alast ? alast : ca) : zero);  // clamped chunks are masked below
-        }
-    };
-    auto sum_chunks = [&]() {
-        if constexpr (G == 1) {
-            const uint32_t t = lane_sum<kL4>(W, a, len, cs, fl);
-            if (small)
-                res = ~fold16_32(t) & 0xffffu;
-            return;
-        }
-        const uint32_t o0 = cs < len ? cs : len;
-        const bool v6 = fl & WG_PKT_V6;
-        const uint32_t ao = v6 ? 8u : 12u, al = v6 ? 32u : 8u;
-        const uint32_t aend = ao + al < len ? ao + al : len;  // address bytes past the packet end are absent
-        uint32_t sr = 0, sq = 0;
-        uint32_t rodd;  // the region's pairing is odd relative to the summed dwords
-        {
-#pragma unroll
-            for (uint32_t k = 0; k < kC; k++) {
-#pragma unroll
-                for (uint32_t d = 0; d < 4; d++) {
-                    const uint32_t pos = 16u * cidx[k] + 4u * d, w = W[k][d];
-                    sr += half_sum(w & dword_mask(pos, s + o0, s + len));
-                    if (kL4)
-                        sq += half_sum(w & dword_mask(pos, s + ao, s + (aend > ao ? aend : ao)));
-                }
-            }
-            sr = group_sum_u32<4>(sr);  // the quad's partial sums (each < 2^20: no overflow)
-            sq = group_sum_u32<4>(sq);
-            rodd = (s + o0) & 1u;  // absolute-address pairing
-        }
-        sr = fold16_32(sr);
-        if (rodd)  // the region pairs from an odd position
-            sr = bswap16(sr);
-        uint32_t t = sr;
-        if (kL4) {
-            sq = fold16_32(sq);
-            if (G > 1 && (s & 1u))  // absolute pairing: the addresses pair from the packet start
-                sq = bswap16(sq);
-            const uint32_t proto = (fl & WG_PKT_TCP) ? 6u : 17u;
-            t += sq + (proto << 8) + bswap16((len - cs) & 0xffffu);  // checksum.hpp:111-114, checksum.cpp:23,33
-        }
-        if (small)
-            res = ~fold16_32(t) & 0xffffu;
-    };
-    if (kLate) {
-        load_chunks();
-    } else if (any_small) {
-        load_chunks();
-        sum_chunks();
-    }
-
-    // ---- wave path: the longer packets of this wave, Q at a time
-    wave_long<kL4, kNT, Q>(__ballot(live && !small && q == 0), a, len, cs, fl, p.base, lane, res);
-    if (kLate && any_small)
-        sum_chunks();
-    if (live && q == 0)
-        p.out[i] = (uint16_t)res;
+    // PacketBatch segment i (include/util/packets.hpp:23-36)
+    const uint64_t off = live ? i * (uint64_t)p.seg : 0u;
+    const uint64_t rem = p.total_len - off;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + off;
+    const uint32_t len = live ? (rem < p.seg ? (uint32_t)rem : p.seg) : 0u;
+    v4u W[5];
+    lane_chunks(a, len, live && len, W);
+    const uint32_t t = lane_sum<true>(W, a, len, live ? p.cs : 0u, live ? p.flags : 0u);
+    if (live)
+        p.out[i] = (uint16_t)(~fold16_32(t) & 0xffffu);
 }
 
 // Split-role descriptor kernel (knob l4_small = 5).  Descriptors come in
@@ -466,21 +311,18 @@ __global__ __launch_bounds__(256) void l4csum_small_kernel(L4Params p) {
 // batch keeps a lane per packet (waves 1-3 leave after one descriptor load),
 // an all-long one keeps the short 16-packet waves with every descriptor in
 // one vector load.  One launch, no host knowledge of the mix.
-// kW = 8: 512-thread blocks, wave k owning group (k mod 4) of quarters
-// 2 (k / 4) and 2 (k / 4) + 1 — 8 descriptors per wave, shorter-lived waves.
-template <int kKind, bool kNT, int U = 4, int kW = 4>  // U: loads in flight per lane on a long packet's rest
-__global__ __launch_bounds__(64 * kW) void l4csum_split_kernel(L4Params p) {
+template <int kKind, bool kNT, int U = 4>  // U: loads in flight per lane on a long packet's rest
+__global__ __launch_bounds__(256) void l4csum_split_kernel(L4Params p) {
     constexpr bool kL4 = kKind != kDescPlain;
-    constexpr uint32_t kQpw = 16u / kW;  // quarters per wave in the wave role (4 or 2)
     const uint32_t lane = lane_id();
     const uint32_t wib = wave_in_block();
     const uint64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
     const uint64_t Q = p.quarter;
     // lane -> (quarter, offset in the block's 16 of that quarter)
-    const uint32_t qq = wib == 0 ? lane >> 4 : kQpw * (wib >> 2) + ((lane >> 2) & (kQpw - 1u));
-    const uint32_t oo = wib == 0 ? lane & 15u : 4u * (wib & 3u) + (lane & 3u);
+    const uint32_t qq = wib == 0 ? lane >> 4 : (lane >> 2) & 3u;
+    const uint32_t oo = wib == 0 ? lane & 15u : 4u * wib + (lane & 3u);
     const uint64_t i = (uint64_t)qq * Q + 16u * blk + oo;
-    const bool live = (wib == 0 || lane < 4u * kQpw) && 16u * blk < Q && i < p.n;
+    const bool live = (wib == 0 || lane < 16u) && 16u * blk < Q && i < p.n;
     const v4u d = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : p.n - 1));
     const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
     const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + (live ? off : 0u);
@@ -491,7 +333,7 @@ __global__ __launch_bounds__(64 * kW) void l4csum_split_kernel(L4Params p) {
     const uint64_t gl = __ballot(live && len > kSmallMax);
     const bool grp_long = ((gl >> (lane & ~3u)) & 0xfu) != 0;
     // ---- wave role: this wave's groups that hold a long packet
-    const bool own = wib == 0 ? (lane & 15u) < 4u && (lane >> 4) < kQpw : true;
+    const bool own = wib == 0 ? (lane & 15u) < 4u : true;
     const bool mine = live && own && grp_long;
     uint32_t res = 0;
     wave_long<kL4, kNT, 4, U>(__ballot(mine), a, len, cs, fl, p.base, lane, res);
@@ -506,115 +348,6 @@ __global__ __launch_bounds__(64 * kW) void l4csum_split_kernel(L4Params p) {
         if (small)
             p.out[i] = (uint16_t)(~fold16_32(t) & 0xffffu);
     }
-}
-
-// Walking descriptor kernel (knob l4_small = 6).  A wave per 64 descriptors
-// whatever their sizes, laid out so that the waves resident at any moment
-// touch one narrow window of the batch: lane l of wave w (of G) owns
-// descriptor ((l >> 2) * G + w) * 4 + (l & 3) — sixteen 4-descriptor groups a
-// sixteenth of the batch apart.  Small packets (<= kSmallMax) are summed in
-// their lane (lane_chunks / lane_sum); the wave then walks its long packets in
-// group order, 4 at a time, through the wave-per-packet issue / finish
-// machinery.  An all-small batch costs n / 64 waves (the split kernel's n / 16
-// waves spend three of every four on one descriptor load), an all-long batch
-// 16 groups per wave.
-template <int kKind, bool kNT, int U = 4>
-__global__ __launch_bounds__(256) void l4csum_walk_kernel(L4Params p) {
-    constexpr bool kL4 = kKind != kDescPlain;
-    const uint32_t lane = lane_id();
-    const uint64_t G = (uint64_t)gridDim.x * 4u;
-    const uint64_t w = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
-    const uint64_t i = ((uint64_t)(lane >> 2) * G + w) * 4u + (lane & 3u);
-    const bool live = i < p.n;
-    const v4u d = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0u));
-    const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + (live ? off : 0u);
-    const uint32_t len = live ? d.z : 0u;
-    const uint32_t cs = kL4 && live ? (d.w & 0xffffu) : 0u;
-    const uint32_t fl = live ? (d.w >> 16) & 0xffu : 0u;
-    const bool small = live && len <= kSmallMax;
-    uint32_t res = 0;
-    if (__ballot(small)) {  // wave-uniform
-        v4u W[5];
-        lane_chunks(a, len, small && len, W);
-        const uint32_t t = lane_sum<kL4>(W, a, small ? len : 0u, cs, fl);
-        res = ~fold16_32(t) & 0xffffu;
-    }
-    wave_long<kL4, kNT, 4, U>(__ballot(live && !small), a, len, cs, fl, p.base, lane, res);
-    if (live)
-        p.out[i] = (uint16_t)res;
-}
-
-// Persistent walking kernel (knob l4_small = 7): the walking kernel's lane /
-// wave split, but the grid is the device's resident wave capacity (or n / 64
-// waves if fewer) and each wave takes ROUNDS of 16 groups — in round r lane l
-// owns descriptor ((16 r + (l >> 2)) * G + w) * 4 + (l & 3) — so every wave
-// gets the same number of groups to within one, whatever n (a grid of n / 64
-// waves is 2.3 generations of resident waves for 1 M descriptors: its last
-// partial generation ran at a third of the chip), and the waves resident at
-// any moment still work on one narrow window of the batch.
-template <int kKind, bool kNT, int U = 4>
-__global__ __launch_bounds__(256) void l4csum_persist_kernel(L4Params p) {
-    constexpr bool kL4 = kKind != kDescPlain;
-    const uint64_t G = (uint64_t)gridDim.x * 4u;
-    const uint64_t w = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
-    for (uint64_t r0 = 0; r0 * G * 4u < p.n; r0 += 16) {
-        uint32_t lane = lane_id();
-        asm volatile("" : "+v"(lane));  // lane-derived values recomputed per round, not held across it
-        const uint64_t i = ((r0 + (lane >> 2)) * G + w) * 4u + (lane & 3u);
-        const bool live = i < p.n;
-        const v4u d = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0u));
-        const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
-        const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + (live ? off : 0u);
-        const uint32_t len = live ? d.z : 0u;
-        const uint32_t cs = kL4 && live ? (d.w & 0xffffu) : 0u;
-        const uint32_t fl = live ? (d.w >> 16) & 0xffu : 0u;
-        const bool small = live && len <= kSmallMax;
-        uint32_t res = 0;
-        if (__ballot(small)) {  // wave-uniform
-            v4u W[5];
-            lane_chunks(a, len, small && len, W);
-            const uint32_t t = lane_sum<kL4>(W, a, small ? len : 0u, cs, fl);
-            res = ~fold16_32(t) & 0xffffu;
-        }
-        wave_long<kL4, kNT, 4, U>(__ballot(live && !small), a, len, cs, fl, p.base, lane, res);
-        if (live)
-            p.out[i] = (uint16_t)res;
-    }
-}
-
-// Resident 256-thread blocks of `kernel` on the current device (occupancy
-// query x CUs), cached per device; 0 when the runtime cannot say.
-template <typename K>
-static uint64_t resident_blocks(K kernel) {
-    static std::atomic<int64_t> cache[16];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0)
-        return 0;
-    if (dev < 16) {
-        const int64_t c = cache[dev].load(std::memory_order_relaxed);
-        if (c > 0)
-            return (uint64_t)c;
-    }
-    int cus = 0, nb = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, 256, 0) != hipSuccess || cus <= 0 || nb <= 0)
-        return 0;
-    const int64_t v = (int64_t)cus * nb;
-    if (dev < 16)
-        cache[dev].store(v, std::memory_order_relaxed);
-    return (uint64_t)v;
-}
-
-// Grid of a persistent walking kernel: n / 256 blocks, capped at the resident
-// capacity, a multiple of 8 (XCD swizzle) when >= 8.
-static uint64_t persist_grid(uint64_t n, uint64_t cap) {
-    uint64_t b = (n + 255) / 256;
-    if (cap >= 8 && b > (cap & ~7ull))
-        b = cap & ~7ull;
-    if (b >= 8)
-        b = (b + 7) & ~7ull;  // <= the capped value: that is a multiple of 8
-    return b;
 }
 
 // Block-per-descriptor kernel for batches of FEW, LONG packets (knob l4_coop:
@@ -725,57 +458,20 @@ static int launch_coop(const L4Params &p, const Tune &t, hipStream_t st) {
 }
 
 template <int kKind, bool kNT>
-static int launch_small(const L4Params &p, uint32_t mode, hipStream_t st) {
-    const uint32_t per_block = mode >= 3 ? 64u : 256u;  // descriptors per 256-thread block
-    uint64_t blocks = (p.n + per_block - 1) / per_block;
+static int launch_split(const L4Params &p, hipStream_t st) {
+    // quarters of Q descriptors (a multiple of 16: block b owns
+    // [q*Q + 16b, +16) of each quarter, whole 4-descriptor groups); 4 Q >= n
     L4Params q = p;
-    if (mode == 5) {
-        // quarters of Q descriptors (a multiple of 16: block b owns
-        // [q*Q + 16b, +16) of each quarter, whole 4-descriptor groups); 4 Q >= n
-        q.quarter = ((p.n + 3) / 4 + 15) & ~15ull;
-        blocks = q.quarter / 16;
-        if (blocks >= 8)
-            blocks = (blocks + 7) & ~7ull;  // XCD swizzle bijective; surplus blocks have no live lane
-    }
-    if (mode == 6) {  // walking kernel: a wave per 64 descriptors
-        blocks = (p.n + 255) / 256;
-        if (blocks >= 8)
-            blocks = (blocks + 7) & ~7ull;
-    }
+    q.quarter = ((p.n + 3) / 4 + 15) & ~15ull;
+    uint64_t blocks = q.quarter / 16;
+    if (blocks >= 8)
+        blocks = (blocks + 7) & ~7ull;  // XCD swizzle bijective; surplus blocks have no live lane
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
-    const dim3 grid((unsigned)blocks), blk(256);
-    const Tune t = tune();
-    if (mode == 7) {
-        if (t.l4_unroll == 8) {
-            auto k = l4csum_persist_kernel<kKind, kNT, 8>;
-            hipLaunchKernelGGL(k, dim3((unsigned)persist_grid(p.n, resident_blocks(k))), blk, 0, st, p);
-        } else {
-            auto k = l4csum_persist_kernel<kKind, kNT, 4>;
-            hipLaunchKernelGGL(k, dim3((unsigned)persist_grid(p.n, resident_blocks(k))), blk, 0, st, p);
-        }
-    } else if (mode == 6) {
-        if (t.l4_unroll == 8)
-            hipLaunchKernelGGL((l4csum_walk_kernel<kKind, kNT, 8>), grid, blk, 0, st, p);
-        else
-            hipLaunchKernelGGL((l4csum_walk_kernel<kKind, kNT, 4>), grid, blk, 0, st, p);
-    } else if (mode == 5 && t.l4_split_waves == 8) {
-        if (t.l4_unroll == 8)
-            hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 8, 8>), grid, dim3(512), 0, st, q);
-        else
-            hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 4, 8>), grid, dim3(512), 0, st, q);
-    } else if (mode == 5 && t.l4_unroll == 8)
-        hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 8>), grid, blk, 0, st, q);
-    else if (mode == 5)
-        hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT>), grid, blk, 0, st, q);
-    else if (mode == 4)
-        hipLaunchKernelGGL((l4csum_small_kernel<kKind, kNT, 4, 4, true>), grid, blk, 0, st, p);
-    else if (mode == 3)
-        hipLaunchKernelGGL((l4csum_small_kernel<kKind, kNT, 4, 4>), grid, blk, 0, st, p);
-    else if (mode == 2)
-        hipLaunchKernelGGL((l4csum_small_kernel<kKind, kNT, 4, 1>), grid, blk, 0, st, p);
+    if (tune().l4_unroll == 8)
+        hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 8>), dim3((unsigned)blocks), dim3(256), 0, st, q);
     else
-        hipLaunchKernelGGL((l4csum_small_kernel<kKind, kNT, 2, 1>), grid, blk, 0, st, p);
+        hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 4>), dim3((unsigned)blocks), dim3(256), 0, st, q);
     return WG_OK;
 }
 
@@ -783,47 +479,52 @@ static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
     if (p.n == 0)
         return WG_OK;
     const Tune t = tune();
+    int rc = WG_OK;
     if (kind == kUniformL4 && p.seg <= kSmallMax && t.l4_small_uniform) {
-        // every segment is small: the small-packet kernel, no trade-off
-        const uint32_t mode = t.l4_small_uniform == 2 ? 2u : 3u;  // 1: lane quad per segment, 2: lane per segment
-        const int rc = t.l4_nt ? launch_small<kUniformL4, true>(p, mode, st) : launch_small<kUniformL4, false>(p, mode, st);
-        if (rc != WG_OK)
-            return rc;
-        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
-    }
-    if (kind != kUniformL4 && p.n <= t.l4_coop) {
+        // every segment is small: a lane per segment, no trade-off
+        uint64_t b = (p.n + 255) / 256;
+        if (b >= 8)
+            b = (b + 7) & ~7ull;
+        if (b > 0x7fffffffull)
+            return WG_ERR_INVALID;
+        hipLaunchKernelGGL(l4csum_uniform_small_kernel, dim3((unsigned)b), dim3(256), 0, st, p);
+    } else if (kind != kUniformL4 && p.n <= t.l4_coop) {
         // few descriptors: a block per packet (config 1's 64 KiB buffers)
-        const int rc = kind == kDescL4 ? (t.l4_nt ? launch_coop<kDescL4, true>(p, t, st) : launch_coop<kDescL4, false>(p, t, st))
-                                       : (t.l4_nt ? launch_coop<kDescPlain, true>(p, t, st)
-                                                  : launch_coop<kDescPlain, false>(p, t, st));
-        if (rc != WG_OK)
-            return rc;
-        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
-    }
-    if (kind != kUniformL4 && t.l4_small) {
-        int rc;
-        if (kind == kDescL4)
-            rc = t.l4_nt ? launch_small<kDescL4, true>(p, t.l4_small, st) : launch_small<kDescL4, false>(p, t.l4_small, st);
+        rc = kind == kDescL4 ? (t.l4_nt ? launch_coop<kDescL4, true>(p, t, st) : launch_coop<kDescL4, false>(p, t, st))
+                             : (t.l4_nt ? launch_coop<kDescPlain, true>(p, t, st)
+                                        : launch_coop<kDescPlain, false>(p, t, st));
+    } else if (kind != kUniformL4 && t.l4_small) {
+        // descriptor batches: the split-role kernel (l4_small = 5, default)
+        rc = kind == kDescL4 ? (t.l4_nt ? launch_split<kDescL4, true>(p, st) : launch_split<kDescL4, false>(p, st))
+                             : (t.l4_nt ? launch_split<kDescPlain, true>(p, st)
+                                        : launch_split<kDescPlain, false>(p, st));
+    } else {
+        // one wave per packet, 4 packets per wave (uniform batches, and
+        // descriptor batches under l4_small = 0: 4 iterations per wave with
+        // the next iteration's descriptors prefetched)
+        uint64_t want = (p.n + 15) / 16;
+        if (kind != kUniformL4)
+            want = (want + 3) / 4;
+        uint64_t blocks = want < t.l4_blocks ? want : t.l4_blocks;
+        if (blocks >= 8)
+            blocks &= ~7ull;  // keep the XCD swizzle bijective
+        const dim3 g((unsigned)blocks), b(256);
+        const bool nt = t.l4_nt != 0;
+        if (kind == kUniformL4 && nt)
+            hipLaunchKernelGGL((l4csum_kernel<kUniformL4, 4, true, 0>), g, b, 0, st, p);
+        else if (kind == kUniformL4)
+            hipLaunchKernelGGL((l4csum_kernel<kUniformL4, 4, false, 0>), g, b, 0, st, p);
+        else if (kind == kDescL4 && nt)
+            hipLaunchKernelGGL((l4csum_kernel<kDescL4, 4, true, 2>), g, b, 0, st, p);
+        else if (kind == kDescL4)
+            hipLaunchKernelGGL((l4csum_kernel<kDescL4, 4, false, 2>), g, b, 0, st, p);
+        else if (nt)
+            hipLaunchKernelGGL((l4csum_kernel<kDescPlain, 4, true, 2>), g, b, 0, st, p);
         else
-            rc = t.l4_nt ? launch_small<kDescPlain, true>(p, t.l4_small, st)
-                         : launch_small<kDescPlain, false>(p, t.l4_small, st);
-        if (rc != WG_OK)
-            return rc;
-        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+            hipLaunchKernelGGL((l4csum_kernel<kDescPlain, 4, false, 2>), g, b, 0, st, p);
     }
-    const uint32_t P = t.l4_ppw;
-    uint64_t want = (p.n + 4ull * P - 1) / (4ull * P);
-    if (kind != kUniformL4 && t.l4_descv == 2)  // l4_iters iterations per wave (descriptor prefetch)
-        want = (want + t.l4_iters - 1) / t.l4_iters;
-    uint64_t blocks = want < t.l4_blocks ? want : t.l4_blocks;
-    if (blocks >= 8)
-        blocks &= ~7ull;  // keep the XCD swizzle bijective
-    const bool nt = t.l4_nt != 0;
-    switch (kind) {
-    case kUniformL4: launch_kind<kUniformL4>(p, blocks, P, nt, st); break;
-    case kDescL4: launch_kind<kDescL4>(p, blocks, P, nt, st); break;
-    default: launch_kind<kDescPlain>(p, blocks, P, nt, st); break;
-    }
+    if (rc != WG_OK)
+        return rc;
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }
 
@@ -881,11 +582,10 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t j) {
 // prefetch), then decode + finish; packet j's verdict and L4 result land in
 // lane tgt[j]'s rv / rc.  Shared by verify_kernel and the long packets of
 // verify_small_kernel.
-template <int P, bool H, typename Mid>
+template <int P, typename Mid>
 __device__ __forceinline__ void verify_group(const uint8_t *base, const uint64_t *doff, const uint32_t *len,
                                              const uint32_t *tgt, uint32_t lane, uint32_t &rv, uint32_t &rc,
                                              Mid mid) {
-    const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
     Geom g[P];
     Front f[P];
     uint32_t hv[P];
@@ -900,20 +600,13 @@ __device__ __forceinline__ void verify_group(const uint8_t *base, const uint64_t
         const uintptr_t a = reinterpret_cast<uintptr_t>(base) + doff[j];
         g[j].a = a;
         g[j].fl = 0;
-        if constexpr (H) {
-            // longer packets fail the size gate (evaluator.hpp:118-121): only
-            // their header bytes are read (region [32, 32) is empty)
-            g[j].len = len[j] <= 65535u ? len[j] : 32u;
-            g[j].cs = 32;
-            issue<false, true, true>(g[j], lane, f[j]);
-            hv[j] = f[j].hb;
-        } else {
-            const uint32_t hl = len[j] < 40u ? len[j] : 40u;
-            hv[j] = ld8(hl ? a + (lane < hl ? lane : 0u) : zero);
-            g[j].len = len[j] <= 65535u ? len[j] : 0u;
-            g[j].cs = 40;
-            issue<false, true>(g[j], lane, f[j]);
-        }
+        // header bytes 0-31 ride in the byte gather's idle lanes; longer
+        // packets fail the size gate (evaluator.hpp:118-121): only their
+        // header bytes are read (region [32, 32) is empty)
+        g[j].len = len[j] <= 65535u ? len[j] : 32u;
+        g[j].cs = 32;
+        issue<false, true, true>(g[j], lane, f[j]);
+        hv[j] = f[j].hb;
     }
     mid();
     // decode (wave-uniform) and finish every packet
@@ -925,7 +618,7 @@ __device__ __forceinline__ void verify_group(const uint8_t *base, const uint64_t
         uint32_t ihs = 20, proto = 0;
         // header byte `lane` in packet pairing (from byte 0); zero from lane
         // 32 (H) / 40 on and past the packet
-        constexpr uint32_t kHdrEnd = H ? 32u : 40u;
+        constexpr uint32_t kHdrEnd = 32u;
         const uint32_t hb = lane < L && lane < kHdrEnd ? hv[j] << (8u * (lane & 1u)) : 0u;
         // IPv4 header sum over bytes 0-19
         const uint32_t hs = wave_sum_u32(lane < 20u ? hb : 0u);
@@ -982,80 +675,57 @@ __device__ __forceinline__ void verify_group(const uint8_t *base, const uint64_t
     }
 }
 
-// H: header bytes 0-31 ride in the L4 byte gather's idle lanes (issue<.., kHdr>)
-// and the summed region starts at byte 32 — no separate header load; else a
-// byte load of header bytes 0-39 per packet and the region from byte 40.
-// kUni: a uniform PacketBatch instead of descriptors (wg_verify_uniform).
-// kD64: a whole group's 4 descriptors (64 B) by one scalar load instead of a
-// load per descriptor (which the compiler issues one after another, each
-// waited for).
-template <int P, int O = 0, int DM = 0, bool H = false, bool kUni = false, bool kD64 = false>  // O: waves/SIMD target (0 = compiler's choice); DM: descriptor mode 0 / 2
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_kernel(
-    VerifyParams p) {
+// The wave kernel: one-shot waves of 4 packets (one group) at 8 waves per
+// SIMD.  Header bytes 0-31 ride in the L4 byte gather's idle lanes
+// (verify_group) — no separate header load.  A group's 4 descriptors come by
+// one 64-B scalar load (a load per descriptor, the compiler issues one after
+// another, each waited for).  kUni: a uniform PacketBatch instead of
+// descriptors (wg_verify_uniform).
+template <bool kUni>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void verify_kernel(VerifyParams p) {
+    constexpr int P = 4;
     const uint32_t lane = lane_id();
-    const uint64_t wave0 = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
-    const uint64_t step = (uint64_t)gridDim.x * 4u * P;
-    const uintptr_t zero = reinterpret_cast<uintptr_t>(&g_zero16);
-    // DM 2 (as the descriptor-batch L4 kernel): the next iteration's
-    // descriptors by one vector load, in flight during this one's finish.
-    // DM 0: one iteration per wave (the launcher covers the batch).
-    v4u nextd = v4u{0, 0, 0, 0};
-    bool have_next = false;
-    for (uint64_t i0 = wave0 * P; i0 < p.n; i0 += step) {
-    uint32_t len[P];
-    uint64_t doff[P];
-    if (DM == 2 && have_next) {
+    const uint64_t i0 = ((uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block()) * P;
+    if (i0 < p.n) {
+        uint32_t len[P];
+        uint64_t doff[P];
+        if constexpr (kUni) {
+            // PacketBatch segment i0 + j (include/util/packets.hpp:23-36): one
+            // 64-bit multiply and compare per wave (a 64-bit scalar compare
+            // has no SALU form on gfx9, and this kernel's scalar unit is busy)
+            const uint64_t o0 = i0 * (uint64_t)p.seg;
+            const bool full = i0 + P < p.n;  // every segment of the group whole
 #pragma unroll
-        for (int j = 0; j < P; j++) {
-            doff[j] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)nextd.x, j) |
-                      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)nextd.y, j) << 32);
-            len[j] = i0 + j < p.n ? (uint32_t)__builtin_amdgcn_readlane((int)nextd.z, j) : 0u;
-        }
-    } else if (kUni) {
-        // PacketBatch segment i0 + j (include/util/packets.hpp:23-36): one
-        // 64-bit multiply and compare per wave (a 64-bit scalar compare has
-        // no SALU form on gfx9, and this kernel's scalar unit is busy)
-        const uint64_t o0 = i0 * (uint64_t)p.seg;
-        const bool full = i0 + P < p.n;  // every segment of the group whole
+            for (int j = 0; j < P; j++) {
+                doff[j] = o0 + (uint32_t)j * p.seg;
+                len[j] = full ? p.seg : (i0 + j + 1 < p.n ? p.seg : (i0 + j + 1 == p.n ? p.last_len : 0u));
+            }
+        } else if (i0 + P <= p.n) {
+            const v16u dd = *reinterpret_cast<const c_v16u *>(reinterpret_cast<uintptr_t>(p.desc + i0));
 #pragma unroll
-        for (int j = 0; j < P; j++) {
-            doff[j] = o0 + (uint32_t)j * p.seg;
-            len[j] = full ? p.seg : (i0 + j + 1 < p.n ? p.seg : (i0 + j + 1 == p.n ? p.last_len : 0u));
-        }
-    } else if (kD64 && P == 4 && i0 + P <= p.n) {
-        const v16u dd = *reinterpret_cast<const c_v16u *>(reinterpret_cast<uintptr_t>(p.desc + i0));
+            for (int j = 0; j < P; j++) {
+                doff[j] = ((uint64_t)dd[4 * j + 1] << 32) | dd[4 * j];
+                len[j] = dd[4 * j + 2];
+            }
+        } else {
 #pragma unroll
-        for (int j = 0; j < P; j++) {
-            doff[j] = ((uint64_t)dd[4 * j + 1] << 32) | dd[4 * j];
-            len[j] = dd[4 * j + 2];
+            for (int j = 0; j < P; j++) {
+                const wg_pkt_desc d = p.desc[i0 + j < p.n ? i0 + j : p.n - 1];
+                doff[j] = d.offset;
+                len[j] = i0 + j < p.n ? d.len : 0u;
+            }
         }
-    } else {
+        uint32_t rv = 0, rc = 0;
+        uint32_t tgt[P];
 #pragma unroll
-        for (int j = 0; j < P; j++) {
-            const wg_pkt_desc d = p.desc[i0 + j < p.n ? i0 + j : p.n - 1];
-            doff[j] = d.offset;
-            len[j] = i0 + j < p.n ? d.len : 0u;
+        for (int j = 0; j < P; j++)
+            tgt[j] = (uint32_t)j;
+        verify_group<P>(p.base, doff, len, tgt, lane, rv, rc, [] {});
+        if (lane < (uint32_t)P && i0 + lane < p.n) {
+            p.verdict[i0 + lane] = (uint8_t)rv;
+            if (p.l4)
+                p.l4[i0 + lane] = (uint16_t)rc;
         }
-    }
-    uint32_t rv = 0, rc = 0;
-    uint32_t tgt[P];
-#pragma unroll
-    for (int j = 0; j < P; j++)
-        tgt[j] = (uint32_t)j;
-    verify_group<P, H>(p.base, doff, len, tgt, lane, rv, rc, [&]() {
-        if constexpr (DM == 2) {
-            have_next = i0 + step < p.n;
-            const uint64_t di = (have_next ? i0 + step : i0) + (lane & (uint32_t)(P - 1));
-            nextd = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (di < p.n ? di : p.n - 1));
-        }
-    });
-    if (lane < (uint32_t)P && i0 + lane < p.n) {
-        p.verdict[i0 + lane] = (uint8_t)rv;
-        if (p.l4)
-            p.l4[i0 + lane] = (uint16_t)rc;
-    }
-    if constexpr (DM == 0)
-        break;
     }
     if constexpr (!kUni) {
         if (p.sample && blockIdx.x == 0 && wave_in_block() == 0)
@@ -1068,41 +738,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
 using namespace wg;
 
 namespace wg {
-
-// Small-packet verify (knob verify_small; the same split as
-// l4csum_small_kernel): a lane per descriptor.  A packet of <= kSmallMax
-// bytes is decoded and summed in its lane from its five aligned 16-B chunks,
-// funnel-shifted (v_alignbyte) into 16 packet-relative dwords R[0..15] with
-// the bytes past the packet zeroed, so every gate field sits at a static
-// byte position and every summed range (header [0, 20), L4 [ihs, len), the
-// addresses) starts at an even packet offset: packet pairing throughout, as
-// the reference pairs them.  The wave then takes the lanes with longer
-// packets Q at a time through verify_group.
-
-// G = 4: a lane quad per descriptor, every lane of it decoding the same
-// packet (its loads hit the same addresses): a wave owns 16 descriptors, so
-// its serial walk over the long packets is 4 groups instead of 16.
-// The packets of the lanes in mask m (lane j: offset ohi:olo, length len),
-// Q at a time through verify_group; packet j's verdict / L4 result land in
-// lane j's rv / rc.
-template <int Q>
-__device__ __forceinline__ void verify_mask(uint64_t m, uint32_t olo, uint32_t ohi, uint32_t len, const uint8_t *base,
-                                            uint32_t lane, uint32_t &rv, uint32_t &rc) {
-    while (m) {
-        uint64_t doff[Q];
-        uint32_t ln[Q], tgt[Q];
-#pragma unroll
-        for (int k = 0; k < Q; k++) {
-            const bool have = m != 0;
-            const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
-            m = have ? m & (m - 1) : m;
-            tgt[k] = have ? j : 64u;
-            doff[k] = have ? (((uint64_t)rdl(ohi, j) << 32) | rdl(olo, j)) : 0u;
-            ln[k] = have ? rdl(len, j) : 0u;
-        }
-        verify_group<Q, true>(base, doff, ln, tgt, lane, rv, rc, [] {});
-    }
-}
 
 // The lane path of the small-packet verify kernels: packet (a, len), len <=
 // kSmallMax, decoded and checked in one lane; verdict bits into rv, the L4
@@ -1194,130 +829,6 @@ __device__ __forceinline__ void verify_lane_decode(const v4u W[5], uintptr_t a, 
     rc = c;
 }
 
-template <int Q, int G = 1>
-__global__ __launch_bounds__(256) void verify_small_kernel(VerifyParams p) {
-    static_assert(G == 1 || G == 4, "lanes per descriptor");
-    const uint32_t lane = lane_id();
-    const uint32_t q = lane & (uint32_t)(G - 1);
-    const uint64_t i = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * (256u / G) + threadIdx.x / G;
-    const bool live = i < p.n;
-    const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0));
-    const uint32_t len = live ? dv.z : 0u;
-    const uint32_t olo = live ? dv.x : 0u, ohi = live ? dv.y : 0u;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)ohi << 32) | olo);
-    const bool small = len <= kSmallMax;
-    uint32_t rv = 0, rc = 0;
-    if (__ballot(live && small))
-        verify_lane(a, len, small, rv, rc);
-    // the longer packets of this wave, Q at a time
-    verify_mask<Q>(__ballot(live && !small && q == 0), olo, ohi, len, p.base, lane, rv, rc);
-    if (live && q == 0) {
-        p.verdict[i] = (uint8_t)rv;
-        if (p.l4)
-            p.l4[i] = (uint16_t)rc;
-    }
-}
-
-// Split-role verify kernel (knob verify_small = 3; the layout and the role
-// split of l4csum_split_kernel): block b owns the 16 descriptors at
-// [q*Q + 16b, +16) of each quarter q; groups of 4 consecutive descriptors
-// whose packets are all <= kSmallMax bytes are decoded a lane per packet by
-// wave 0, every other group by its wave through verify_group, 4 at a time.
-template <int O = 0>  // O: waves/SIMD target (0 = compiler's choice)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_split_kernel(VerifyParams p, uint64_t Q) {
-    const uint32_t lane = lane_id();
-    const uint32_t wib = wave_in_block();
-    const uint64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
-    const uint32_t qq = wib == 0 ? lane >> 4 : (lane >> 2) & 3u;
-    const uint32_t oo = wib == 0 ? lane & 15u : 4u * wib + (lane & 3u);
-    const uint64_t i = (uint64_t)qq * Q + 16u * blk + oo;
-    const bool live = (wib == 0 || lane < 16u) && 16u * blk < Q && i < p.n;
-    const v4u d = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : p.n - 1));
-    const uint32_t len = live ? d.z : 0u;
-    const uint32_t olo = live ? d.x : 0u, ohi = live ? d.y : 0u;
-    const uint64_t gl = __ballot(live && len > kSmallMax);
-    const bool grp_long = ((gl >> (lane & ~3u)) & 0xfu) != 0;
-    const bool own = wib == 0 ? (lane & 15u) < 4u : true;
-    const bool mine = live && own && grp_long;
-    uint32_t rv = 0, rc = 0;
-    verify_mask<4>(__ballot(mine), olo, ohi, len, p.base, lane, rv, rc);
-    const bool small = wib == 0 && live && !grp_long;
-    if (__ballot(small)) {  // wave-uniform; never true on waves 1-3
-        uint32_t sv = 0, sc = 0;
-        verify_lane(reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)ohi << 32) | olo), small ? len : 0u, small, sv,
-                    sc);
-        rv = small ? sv : rv;
-        rc = small ? sc : rc;
-    }
-    if (mine || small) {
-        p.verdict[i] = (uint8_t)rv;
-        if (p.l4)
-            p.l4[i] = (uint16_t)rc;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Two-role verify (knob verify_small 4 and 5).  The wave-per-packet kernel is
-// fastest on long packets as one-shot 4-packet waves at 8 waves/SIMD, and the
-// lane decode is fastest on small ones at 64 descriptors per wave; any layout
-// that puts both roles in one wave costs the long packets occupancy or
-// one-shot waves (verify_small 1-3).  Here the roles get separate waves:
-//  - LANE role: a lane per descriptor; packets of <= kSmallMax bytes are
-//    decoded in their lane (verify_lane), longer ones left alone;
-//  - WAVE role: one-shot waves of 4 consecutive descriptors through
-//    verify_group (the default kernel's body), taking only the packets longer
-//    than kSmallMax; a wave whose 4 packets are all small exits after its
-//    descriptor load.
-// Every descriptor's result is stored by exactly one role.  verify_small = 4
-// runs the roles as two launches, 5 as the two block ranges of one launch.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void verify_lane_role(const VerifyParams &p, uint64_t i) {
-    const bool live = i < p.n;
-    const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0));
-    const uint32_t len = live ? dv.z : 0u;
-    const bool small = live && len <= kSmallMax;
-    if (!__ballot(small))  // wave-uniform: nothing small here
-        return;
-    uint32_t rv = 0, rc = 0;
-    verify_lane(reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)dv.y << 32) | dv.x), small ? len : 0u, small, rv,
-                rc);
-    if (small) {
-        p.verdict[i] = (uint8_t)rv;
-        if (p.l4)
-            p.l4[i] = (uint16_t)rc;
-    }
-}
-
-__device__ __forceinline__ void verify_wave_role(const VerifyParams &p, uint64_t i0, uint32_t lane) {
-    constexpr int P = 4;
-    uint64_t doff[P];
-    uint32_t len[P], tgt[P];
-    uint32_t keep = 0;
-#pragma unroll
-    for (int j = 0; j < P; j++) {
-        const wg_pkt_desc d = p.desc[i0 + j < p.n ? i0 + j : p.n - 1];
-        const uint32_t L = i0 + j < p.n ? d.len : 0u;
-        const bool lg = L > kSmallMax;
-        keep |= (uint32_t)lg << j;
-        doff[j] = d.offset;
-        len[j] = lg ? L : 0u;  // the lane role's packets: nothing issued
-        tgt[j] = (uint32_t)j;
-    }
-    if (!keep)
-        return;
-    uint32_t rv = 0, rc = 0;
-    verify_group<P, true>(p.base, doff, len, tgt, lane, rv, rc, [] {});
-    if (lane < (uint32_t)P && ((keep >> lane) & 1u)) {
-        p.verdict[i0 + lane] = (uint8_t)rv;
-        if (p.l4)
-            p.l4[i0 + lane] = (uint16_t)rc;
-    }
-}
-
-__global__ __launch_bounds__(256) void verify_lane_kernel(VerifyParams p) {
-    verify_lane_role(p, (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 256u + threadIdx.x);
-}
-
 // wg_verify_uniform with segment_size <= kSmallMax: every segment is small,
 // so a lane per segment decodes it (no descriptors, no wave role).
 __global__ __launch_bounds__(256) void verify_uniform_lane_kernel(VerifyParams p) {
@@ -1332,28 +843,6 @@ __global__ __launch_bounds__(256) void verify_uniform_lane_kernel(VerifyParams p
         if (p.l4)
             p.l4[i] = (uint16_t)rc;
     }
-}
-
-template <int O = 0, int BW = 4>  // BW: waves per block (4, or 16: fewer workgroups to dispatch)
-__global__ __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_long_kernel(
-    VerifyParams p) {
-    const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * (uint32_t)BW + wave_in_block();
-    if (wave * 4u < p.n)
-        verify_wave_role(p, wave * 4u, lane_id());
-}
-
-// One launch: blocks [0, nl) lane role (256 descriptors each), the rest wave
-// role (16 descriptors each); both ranges multiples of 8 blocks (XCD swizzle).
-template <int O = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_roles_kernel(
-    VerifyParams p, uint32_t nl) {
-    if (blockIdx.x < nl) {
-        verify_lane_role(p, (uint64_t)xcd_swizzle(blockIdx.x, nl) * 256u + threadIdx.x);
-        return;
-    }
-    const uint64_t wave = (uint64_t)xcd_swizzle(blockIdx.x - nl, gridDim.x - nl) * 4u + wave_in_block();
-    if (wave * 4u < p.n)
-        verify_wave_role(p, wave * 4u, lane_id());
 }
 
 // ---------------------------------------------------------------------------
@@ -1419,7 +908,12 @@ __global__ __launch_bounds__(256) void verify_compact_lane_kernel(VerifyParams p
         if (lng) {
             const uint32_t pre = (wib > 0 ? s_cnt[0] : 0u) + (wib > 1 ? s_cnt[1] : 0u) + (wib > 2 ? s_cnt[2] : 0u);
             const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(ml >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ml, 0u));
-            c.ent[sh * c.cap + s_base + pre + r] = v4u{dv.x, dv.y, len, (uint32_t)i};
+            // A shard receives at most cap entries per call (the host sizes
+            // cap from the blocks per shard) when its counter started at 0,
+            // which stream order guarantees (captured calls never come here);
+            // the bound keeps a broken protocol from writing past the list.
+            if (s_base + pre + r < c.cap)
+                c.ent[sh * c.cap + s_base + pre + r] = v4u{dv.x, dv.y, len, (uint32_t)i};
         }
     }
     if (small) {
@@ -1445,8 +939,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
     const c_v16u *e = reinterpret_cast<const c_v16u *>(reinterpret_cast<uintptr_t>(c.ent + sh * c.cap));
     uint32_t k0 = ((blockIdx.x / kVShards) * 4u + wave_in_block()) * P;
     v16u d = e[(k0 < c.cap ? k0 : c.cap - P) / P];  // past the count: read, not used
-    const uint32_t cnt = *reinterpret_cast<const c_u32 *>(reinterpret_cast<uintptr_t>(c.ctr + sh * kVCtrStride));
-    asm volatile("" ::"s"(d[0]), "s"(cnt));  // both in flight before the first wait
+    const uint32_t cnt0 = *reinterpret_cast<const c_u32 *>(reinterpret_cast<uintptr_t>(c.ctr + sh * kVCtrStride));
+    asm volatile("" ::"s"(d[0]), "s"(cnt0));  // both in flight before the first wait
+    const uint32_t cnt = cnt0 < c.cap ? cnt0 : (uint32_t)c.cap;  // never past the list (see the lane kernel)
     while (k0 < cnt) {
         // the lane id laundered per iteration: the lane-derived constants of
         // verify_group are then recomputed in the body instead of hoisted and
@@ -1466,7 +961,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
         if (lane < (uint32_t)P)
             s_idx[wave_in_block()][lane] = lane == 0 ? d[3] : lane == 1 ? d[7] : lane == 2 ? d[11] : d[15];
         uint32_t rv = 0, rc = 0;
-        verify_group<P, true>(p.base, doff, len, tgt, lane, rv, rc, [] {});
+        verify_group<P>(p.base, doff, len, tgt, lane, rv, rc, [] {});
         if (lane < (uint32_t)P && k0 + lane < cnt) {
             const uint32_t at = s_idx[wave_in_block()][lane];
             p.verdict[at] = (uint8_t)rv;
@@ -1481,173 +976,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
     }
 }
 
-// Walking verify (verify_small = 8): one launch of n / 64 waves whatever the
-// size mix, the layout of l4csum_walk_kernel (lane l of wave w of G owns
-// descriptor ((l >> 2) * G + w) * 4 + (l & 3): the resident waves work on one
-// narrow window of the batch).  Packets of <= kSmallMax bytes are decoded in
-// their lane (verify_lane); the wave then walks its longer packets in group
-// order, 4 at a time, through verify_group.  Stateless: no host sample, no
-// lists, nothing carried between calls.
-// One round of the walking verify: lane l holds descriptor i (of group
-// g = i / 4); small packets in their lane, long ones 4 at a time through
-// verify_group with their offsets / lengths parked in LDS (s_geo: this wave's
-// 3 x 64 words), results stored by index.
-__device__ __forceinline__ void verify_walk_round(const VerifyParams &p, uint64_t i, uint32_t *s_geo) {
-    const uint32_t lane = lane_id();
-    const bool live = i < p.n;
-    const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0u));
-    const uint32_t len = live ? dv.z : 0u;
-    const uint32_t olo = live ? dv.x : 0u, ohi = live ? dv.y : 0u;
-    const bool small = live && len <= kSmallMax;
-    uint32_t rv = 0, rc = 0;
-    if (__ballot(small))  // wave-uniform
-        verify_lane(reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)ohi << 32) | olo), small ? len : 0u, small, rv,
-                    rc);
-    uint32_t r = rv | (rc << 8);  // one register across the walk
-    uint64_t m = __ballot(live && !small);
-    if (m) {
-        s_geo[lane] = olo;
-        s_geo[64 + lane] = ohi;
-        s_geo[128 + lane] = len;
-    }
-    while (m) {
-        uint32_t ln = lane_id();
-        asm volatile("" : "+v"(ln));
-        uint64_t doff[4];
-        uint32_t lg[4], tgt[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const bool have = m != 0;
-            const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
-            m = have ? m & (m - 1) : m;
-            tgt[k] = have ? j : 64u;
-            const uint32_t x = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[j]);
-            const uint32_t y = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[64 + j]);
-            const uint32_t z = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[128 + j]);
-            doff[k] = have ? (((uint64_t)y << 32) | x) : 0u;
-            lg[k] = have ? z : 0u;
-        }
-        uint32_t v2 = 0, c2 = 0;
-        verify_group<4, true>(p.base, doff, lg, tgt, ln, v2, c2, [] {});
-        r = (ln == tgt[0] || ln == tgt[1] || ln == tgt[2] || ln == tgt[3]) ? (v2 | (c2 << 8)) : r;
-    }
-    if (live) {
-        p.verdict[i] = (uint8_t)r;
-        if (p.l4)
-            p.l4[i] = (uint16_t)(r >> 8);
-    }
-}
-
-// Persistent walking verify (verify_small = 9): the grid is the resident
-// capacity (or n / 64 waves if fewer); wave w takes rounds of 16 groups,
-// lane l of round r holding descriptor ((16 r + (l >> 2)) * G + w) * 4 + (l & 3):
-// every wave gets the same number of groups to within one (l4csum_persist_kernel).
-template <int O = 8>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_persist_kernel(
-    VerifyParams p) {
-    __shared__ uint32_t s_geo[4][3 * 64];
-    const uint64_t G = (uint64_t)gridDim.x * 4u;
-    const uint32_t wib = wave_in_block();
-    const uint64_t w = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wib;
-    for (uint64_t r0 = 0; r0 * G * 4u < p.n; r0 += 16) {
-        uint32_t lane = lane_id();
-        asm volatile("" : "+v"(lane));
-        verify_walk_round(p, ((r0 + (lane >> 2)) * G + w) * 4u + (lane & 3u), s_geo[wib]);
-    }
-}
-
-// Walk the long packets of mask m 4 at a time through verify_group, their
-// geometry (olo / ohi / len of lane j) read from this wave's LDS words; each
-// packet's verdict | L4 result << 8 lands in its lane's r.
-__device__ __forceinline__ void verify_walk_lds(const VerifyParams &p, uint64_t m, const uint32_t *s_geo,
-                                                uint32_t &r) {
-    while (m) {
-        // the lane id laundered per iteration: verify_group's lane-derived
-        // constants are recomputed in the body, not held across the loop
-        uint32_t ln = lane_id();
-        asm volatile("" : "+v"(ln));
-        uint64_t doff[4];
-        uint32_t lg[4], tgt[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const bool have = m != 0;
-            const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
-            m = have ? m & (m - 1) : m;
-            tgt[k] = have ? j : 64u;
-            const uint32_t x = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[j]);
-            const uint32_t y = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[64 + j]);
-            const uint32_t z = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[128 + j]);
-            doff[k] = have ? (((uint64_t)y << 32) | x) : 0u;
-            lg[k] = have ? z : 0u;
-        }
-        uint32_t v2 = 0, c2 = 0;
-        verify_group<4, true>(p.base, doff, lg, tgt, ln, v2, c2, [] {});
-        r = (ln == tgt[0] || ln == tgt[1] || ln == tgt[2] || ln == tgt[3]) ? (v2 | (c2 << 8)) : r;
-    }
-}
-
-// Split-role verify at 8 waves/SIMD (verify_small = 10): the layout of
-// l4csum_split_kernel — block b owns the 16 descriptors [q*Q + 16b, +16) of
-// each quarter q; wave k walks its own group of each quarter that holds a
-// packet longer than kSmallMax (4 groups a quarter batch apart, as the
-// wave-per-packet kernel's waves would take them); wave 0 then decodes the
-// block's all-small groups a lane per packet.  The descriptors' geometry is
-// parked in LDS across both roles (held in registers, verify_split_kernel
-// spilled 60 B at 8 waves/SIMD).  An all-small batch costs n / 64 lane-waves
-// (and three one-load waves per block), an all-long one the wave kernel's
-// groups, 4 per wave.
-template <int O = 8>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_split2_kernel(
-    VerifyParams p, uint64_t Q) {
-    __shared__ uint32_t s_geo[4][3 * 64];
-    const uint32_t wib = wave_in_block();
-    const uint64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
-    uint64_t m_mine, m_small;
-    {
-        const uint32_t lane = lane_id();
-        const uint32_t qq = wib == 0 ? lane >> 4 : (lane >> 2) & 3u;
-        const uint32_t oo = wib == 0 ? lane & 15u : 4u * wib + (lane & 3u);
-        const uint64_t i = (uint64_t)qq * Q + 16u * blk + oo;
-        const bool live = (wib == 0 || lane < 16u) && 16u * blk < Q && i < p.n;
-        const v4u d = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0u));
-        const uint32_t len = live ? d.z : 0u;
-        const uint64_t gl = __ballot(live && len > kSmallMax);
-        const bool grp_long = ((gl >> (lane & ~3u)) & 0xfu) != 0;
-        const bool own = wib == 0 ? (lane & 15u) < 4u : true;
-        m_mine = __ballot(live && own && grp_long);
-        m_small = __ballot(wib == 0 && live && !grp_long);
-        s_geo[wib][lane] = live ? d.x : 0u;
-        s_geo[wib][64 + lane] = live ? d.y : 0u;
-        s_geo[wib][128 + lane] = len;
-    }
-    uint32_t r = 0;
-    verify_walk_lds(p, m_mine, s_geo[wib], r);
-    if (m_small) {  // wave-uniform; never true on waves 1-3
-        uint32_t lane = lane_id();
-        asm volatile("" : "+v"(lane));
-        const bool small = (m_small >> lane) & 1u;
-        const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) +
-                            (((uint64_t)s_geo[wib][64 + lane] << 32) | s_geo[wib][lane]);
-        uint32_t sv = 0, sc = 0;
-        verify_lane(a, small ? s_geo[wib][128 + lane] : 0u, small, sv, sc);
-        r = small ? (sv | (sc << 8)) : r;
-    }
-    uint32_t lane = lane_id();
-    asm volatile("" : "+v"(lane));
-    if (((m_mine | m_small) >> lane) & 1u) {
-        const uint32_t qq = wib == 0 ? lane >> 4 : (lane >> 2) & 3u;
-        const uint32_t oo = wib == 0 ? lane & 15u : 4u * wib + (lane & 3u);
-        const uint64_t i = (uint64_t)qq * Q + 16u * blk + oo;
-        p.verdict[i] = (uint8_t)r;
-        if (p.l4)
-            p.l4[i] = (uint16_t)(r >> 8);
-    }
-}
-
-template <int O = 0, bool kLds = false>  // kLds: the long lanes' offsets / lengths parked in LDS across the walk
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, O ? O : 8))) void verify_walk_kernel(
-    VerifyParams p) {
-    __shared__ uint32_t s_geo[kLds ? 4 : 1][kLds ? 3 * 64 : 1];
+// Walking verify (verify_small = 8; the default's choice for all-small
+// batches and for the first call on a stream): one stateless launch of n / 64
+// waves whatever the size mix.  Lane l of wave w (of G) owns descriptor
+// ((l >> 2) * G + w) * 4 + (l & 3) — sixteen 4-descriptor groups a sixteenth
+// of the batch apart, so the waves resident at any moment work on one narrow
+// window of the batch.  Packets of <= kSmallMax bytes are decoded in their
+// lane (verify_lane); the wave then walks its longer packets in group order,
+// 4 at a time, through verify_group.  Measured (profiles/r04_walk_verify_ab.json):
+// 1 M x 64 B 0.0157 ms against the compacting path's 0.0174; long packets
+// cost it 7-9 % against the one-shot wave kernel (a wave then lives for 16
+// groups), so the cost model sends long-dominated batches there.
+__global__ __launch_bounds__(256) void verify_walk_kernel(VerifyParams p) {
     const uint32_t lane = lane_id();
     const uint64_t G = (uint64_t)gridDim.x * 4u;
     const uint64_t w = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
@@ -1661,18 +1001,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
     if (__ballot(small))  // wave-uniform
         verify_lane(reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)ohi << 32) | olo), small ? len : 0u, small, rv,
                     rc);
-    // one register across the walk: verdict | L4 result << 8
-    uint32_t r = rv | (rc << 8);
+    uint32_t r = rv | (rc << 8);  // one register across the walk: verdict | L4 result << 8
     uint64_t m = __ballot(live && !small);
-    if constexpr (kLds) {
-        const uint32_t wib = wave_in_block();
-        if (m) {
-            s_geo[wib][lane] = olo;
-            s_geo[wib][64 + lane] = ohi;
-            s_geo[wib][128 + lane] = len;
-        }
-    }
-    while (m) {  // the long packets, 4 at a time in group order (verify_mask)
+    while (m) {  // the long packets, 4 at a time in group order
         // the lane id laundered per iteration: verify_group's lane-derived
         // constants are recomputed in the body, not held across the loop
         uint32_t ln = lane_id();
@@ -1685,21 +1016,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
             const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
             m = have ? m & (m - 1) : m;
             tgt[k] = have ? j : 64u;
-            if constexpr (kLds) {
-                // same-address LDS reads (broadcast), made wave-uniform
-                const uint32_t wib = wave_in_block();
-                const uint32_t x = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[wib][j]);
-                const uint32_t y = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[wib][64 + j]);
-                const uint32_t z = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_geo[wib][128 + j]);
-                doff[k] = have ? (((uint64_t)y << 32) | x) : 0u;
-                lg[k] = have ? z : 0u;
-            } else {
-                doff[k] = have ? (((uint64_t)rdl(ohi, j) << 32) | rdl(olo, j)) : 0u;
-                lg[k] = have ? rdl(len, j) : 0u;
-            }
+            doff[k] = have ? (((uint64_t)rdl(ohi, j) << 32) | rdl(olo, j)) : 0u;
+            lg[k] = have ? rdl(len, j) : 0u;
         }
         uint32_t v2 = 0, c2 = 0;
-        verify_group<4, true>(p.base, doff, lg, tgt, ln, v2, c2, [] {});
+        verify_group<4>(p.base, doff, lg, tgt, ln, v2, c2, [] {});
         r = (ln == tgt[0] || ln == tgt[1] || ln == tgt[2] || ln == tgt[3]) ? (v2 | (c2 << 8)) : r;
     }
     // the index recomputed from a laundered lane id (held across the walk it spilled)
@@ -1711,6 +1032,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
         if (p.l4)
             p.l4[i2] = (uint16_t)(r >> 8);
     }
+    if (p.sample && blockIdx.x == 0 && wave_in_block() == 0)
+        verify_sample(p, l2);
 }
 
 }  // namespace wg
@@ -1721,8 +1044,9 @@ namespace {
 // lists, two counter sets, and the host-mapped sample word read by the next
 // call.  Created on first use, grown (after draining the stream) when a
 // batch needs more entries, never freed (a handful per process).  A stream
-// whose state cannot be made (table full, allocation failure) runs the wave
-// kernel: the same results by another kernel, never a host fallback.
+// whose state cannot be made (table full, allocation failure, or a call
+// under stream capture) runs the stateless walking kernel: the same results
+// by another kernel, never a host fallback.
 struct VerifyState {
     int dev = -1;
     void *stream = nullptr;
@@ -1740,7 +1064,7 @@ std::mutex g_vstate_mu;
 VerifyState *g_vstate[kMaxVerifyStates];
 size_t g_nvstate = 0;
 
-VerifyState *verify_state(void *stream) {
+VerifyState *verify_state(void *stream, bool create) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess)
         return nullptr;
@@ -1748,7 +1072,7 @@ VerifyState *verify_state(void *stream) {
     for (size_t k = 0; k < g_nvstate; k++)
         if (g_vstate[k]->dev == dev && g_vstate[k]->stream == stream)
             return g_vstate[k];
-    if (g_nvstate == kMaxVerifyStates)
+    if (!create || g_nvstate == kMaxVerifyStates)
         return nullptr;
     VerifyState *s = new VerifyState;
     s->dev = dev;
@@ -1834,13 +1158,19 @@ static int verify_compact_launch(VerifyParams p, VerifyState *s, uint64_t est_lo
 
 }  // namespace wg
 
-// verify_small = 7: the compacting path or the wave kernel, from the previous
-// call's sample (smp of 64 spread packets <= 64 B, the others lb bytes in
-// all).  Cost model, measured on MI355X (profiles/r03_verify_*):
-// the wave kernel spends max(0.88 ns, group bytes / 6.5 TB/s) of chip time
-// per 4-packet group whatever sizes the group mixes; the compacting path pays
-// its lane kernel (~7 ps per descriptor + ~8 ps per small packet) and then
-// the long packets' groups at 1.07x the wave kernel's per-group time.
+// verify_small = 7 (default): per call, one of three kernels from the size mix
+// the previous call on this stream sampled (smp of 64 spread packets <= 64 B,
+// the others lb bytes in all):
+//  * no sample yet (the stream's first call), or every sampled packet small:
+//    the walking kernel — one stateless launch within 7-9 % of the best
+//    kernel on any mix, and the fastest on all-small batches;
+//  * otherwise the cheaper of the wave kernel and the compacting path by a
+//    cost model measured on MI355X (profiles/r03_verify_*): the
+//    wave kernel spends max(0.88 ns, group bytes / 6.5 TB/s) of chip time per
+//    4-packet group whatever sizes the group mixes; the compacting path pays
+//    its lane kernel (~7 ps per descriptor + ~8 ps per small packet) and then
+//    the long packets' groups at 1.07x the wave kernel's per-group time.
+// Every kernel gives the same results; the choice only moves time.
 static bool verify_pick_compact(uint64_t n, uint32_t smp, uint32_t lb, uint32_t min_small) {
     if (smp < min_small)
         return false;
@@ -1853,9 +1183,28 @@ static bool verify_pick_compact(uint64_t n, uint32_t smp, uint32_t lb, uint32_t 
     return t_compact < 0.97 * t_wave;
 }
 
-static uint64_t verify_wave_blocks(uint64_t n) {
-    uint64_t blocks = (n + 15) / 16;  // one-shot 4-packet waves
-    return blocks >= 8 ? (blocks + 7) & ~7ull : blocks;
+enum VerifyPath { kPathWave, kPathCompact, kPathWalk };
+
+static int verify_launch_walk(const VerifyParams &p, hipStream_t st) {
+    uint64_t blocks = (p.n + 255) / 256;  // a wave per 64 descriptors
+    if (blocks >= 8)
+        blocks = (blocks + 7) & ~7ull;
+    if (blocks > 0x7fffffffull)
+        return WG_ERR_INVALID;
+    hipLaunchKernelGGL(verify_walk_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p);
+    return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+}
+
+// The wave kernel at its default geometry (one-shot 4-packet waves, 8 waves
+// per SIMD, header bytes in the L4 gather, one 64-B descriptor load per group).
+static int verify_launch_wave(const VerifyParams &p, hipStream_t st) {
+    uint64_t blocks = (p.n + 15) / 16;
+    if (blocks >= 8)
+        blocks = (blocks + 7) & ~7ull;
+    if (blocks > 0x7fffffffull)
+        return WG_ERR_INVALID;
+    hipLaunchKernelGGL(verify_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, p);
+    return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }
 
 extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_desc, uint64_t n,
@@ -1866,146 +1215,44 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
         return WG_ERR_INVALID;
     VerifyParams p{dev_base, dev_desc, dev_verdict, dev_l4, n};
     const Tune t = tune();
-    if (t.verify_small == 10) {  // split roles at 8 waves/SIMD: one stateless launch
-        const uint64_t Q = ((n + 3) / 4 + 15) & ~15ull;  // as l4csum_split_kernel's quarters
-        uint64_t sb = Q / 16;
-        if (sb >= 8)
-            sb = (sb + 7) & ~7ull;
-        if (sb > 0x7fffffffull)
-            return WG_ERR_INVALID;
-        hipStream_t st = static_cast<hipStream_t>(stream);
-        if (t.verify_occ == 8)
-            hipLaunchKernelGGL(verify_split2_kernel<8>, dim3((unsigned)sb), dim3(256), 0, st, p, Q);
-        else
-            hipLaunchKernelGGL(verify_split2_kernel<0>, dim3((unsigned)sb), dim3(256), 0, st, p, Q);
-        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
-    }
-    if (t.verify_small == 9) {  // persistent walking verify: one stateless launch at the resident capacity
-        hipStream_t st = static_cast<hipStream_t>(stream);
-        if (t.verify_occ == 8) {
-            auto k = verify_persist_kernel<8>;
-            hipLaunchKernelGGL(k, dim3((unsigned)persist_grid(n, resident_blocks(k))), dim3(256), 0, st, p);
-        } else {
-            auto k = verify_persist_kernel<0>;
-            hipLaunchKernelGGL(k, dim3((unsigned)persist_grid(n, resident_blocks(k))), dim3(256), 0, st, p);
-        }
-        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
-    }
-    if (t.verify_small == 8) {  // walking verify: one stateless launch of n / 64 waves
-        uint64_t blocks = (n + 255) / 256;
-        if (blocks >= 8)
-            blocks = (blocks + 7) & ~7ull;
-        if (blocks > 0x7fffffffull)
-            return WG_ERR_INVALID;
-        hipStream_t st = static_cast<hipStream_t>(stream);
-        if (t.verify_occ == 8 && t.verify_dm == 2)  // (experiment) geometry parked in LDS
-            hipLaunchKernelGGL((verify_walk_kernel<8, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
-        else if (t.verify_occ == 8)
-            hipLaunchKernelGGL(verify_walk_kernel<8>, dim3((unsigned)blocks), dim3(256), 0, st, p);
-        else
-            hipLaunchKernelGGL(verify_walk_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, st, p);
-        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
-    }
-    if (t.verify_small >= 6) {
-        // 6: the compacting path; 7 (default): the compacting path when the
-        // previous call on this stream sampled >= verify_auto_t small packets
-        // of 64, else the wave kernel (which samples this batch in turn).
-        // Both give the same results; only the kernels differ.
-        hipStream_t st = static_cast<hipStream_t>(stream);
-        if (VerifyState *s = verify_state(stream)) {
-            std::lock_guard<std::mutex> g(s->mu);
-            const uint32_t smp = __atomic_load_n(s->host_sample, __ATOMIC_RELAXED);
-            const uint32_t lb = __atomic_load_n(s->host_sample + 1, __ATOMIC_RELAXED);
-            const bool known = smp <= 64u;
-            if (t.verify_small == 6 || (known && verify_pick_compact(n, smp, lb, t.verify_auto_t))) {
-                const uint64_t est = known ? (n * (64u - smp) + 63u) / 64u : n;
-                const int rc = verify_compact_launch(p, s, est, t.verify_k2min, st);
-                if (rc != WG_ERR_RUNTIME)
-                    return rc;
-            }
-            p.sample = s->dev_sample;
-            hipLaunchKernelGGL((verify_kernel<4, 8, 0, true, false, true>), dim3((unsigned)verify_wave_blocks(n)),
-                               dim3(256), 0, st, p);
-            return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
-        }
-    }
-    if (t.verify_small == 4 || t.verify_small == 5) {
-        hipStream_t st = static_cast<hipStream_t>(stream);
-        uint64_t nl = (n + 255) / 256, nw = (n + 15) / 16;  // lane-role / wave-role blocks
-        if (nl >= 8) nl = (nl + 7) & ~7ull;
-        if (nw >= 8) nw = (nw + 7) & ~7ull;
-        if (nl + nw > 0x7fffffffull)
-            return WG_ERR_INVALID;
-        if (t.verify_small == 4) {
-            hipLaunchKernelGGL(verify_lane_kernel, dim3((unsigned)nl), dim3(256), 0, st, p);
-            if (t.verify_wblk == 16) {
-                uint64_t nw16 = (n + 63) / 64;
-                if (nw16 >= 8) nw16 = (nw16 + 7) & ~7ull;
-                hipLaunchKernelGGL((verify_long_kernel<8, 16>), dim3((unsigned)nw16), dim3(1024), 0, st, p);
-            } else if (t.verify_occ == 8) {
-                hipLaunchKernelGGL(verify_long_kernel<8>, dim3((unsigned)nw), dim3(256), 0, st, p);
-            } else {
-                hipLaunchKernelGGL(verify_long_kernel<0>, dim3((unsigned)nw), dim3(256), 0, st, p);
-            }
-        } else if (t.verify_occ == 8) {
-            hipLaunchKernelGGL(verify_roles_kernel<8>, dim3((unsigned)(nl + nw)), dim3(256), 0, st, p, (uint32_t)nl);
-        } else {
-            hipLaunchKernelGGL(verify_roles_kernel<0>, dim3((unsigned)(nl + nw)), dim3(256), 0, st, p, (uint32_t)nl);
-        }
-        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
-    }
-    if (t.verify_small == 3) {
-        const uint64_t Q = ((n + 3) / 4 + 15) & ~15ull;  // as l4csum_split_kernel's quarters
-        uint64_t sb = Q / 16;
-        if (sb >= 8)
-            sb = (sb + 7) & ~7ull;
-        if (sb > 0x7fffffffull)
-            return WG_ERR_INVALID;
-        if (t.verify_occ == 8)
-            hipLaunchKernelGGL(verify_split_kernel<8>, dim3((unsigned)sb), dim3(256), 0,
-                               static_cast<hipStream_t>(stream), p, Q);
-        else
-            hipLaunchKernelGGL(verify_split_kernel<0>, dim3((unsigned)sb), dim3(256), 0,
-                               static_cast<hipStream_t>(stream), p, Q);
-        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
-    }
-    if (t.verify_small) {
-        const uint64_t per_block = t.verify_small == 2 ? 64u : 256u;  // descriptors per 256-thread block
-        const uint64_t sb = (n + per_block - 1) / per_block;
-        if (sb > 0x7fffffffull)
-            return WG_ERR_INVALID;
-        if (t.verify_small == 2)
-            hipLaunchKernelGGL((verify_small_kernel<4, 4>), dim3((unsigned)sb), dim3(256), 0,
-                               static_cast<hipStream_t>(stream), p);
-        else
-            hipLaunchKernelGGL((verify_small_kernel<4>), dim3((unsigned)sb), dim3(256), 0,
-                               static_cast<hipStream_t>(stream), p);
-        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
-    }
-    const bool pf = t.verify_dm == 2;
-    uint64_t blocks = (n + 15) / 16;
-    if (pf) {
-        blocks = (blocks + t.l4_iters - 1) / t.l4_iters;
-        if (blocks >= 8)
-            blocks &= ~7ull;  // XCD swizzle bijective; the grid-stride loop covers the rest
-    } else if (blocks >= 8) {
-        blocks = (blocks + 7) & ~7ull;  // one iteration per wave: round up
-    }
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const dim3 grid((unsigned)blocks);
-    if (!pf && t.verify_hdr && t.verify_occ == 8)
-        hipLaunchKernelGGL((verify_kernel<4, 8, 0, true>), grid, dim3(256), 0, st, p);
-    else if (!pf && t.verify_hdr)
-        hipLaunchKernelGGL((verify_kernel<4, 0, 0, true>), grid, dim3(256), 0, st, p);
-    else if (pf && t.verify_occ == 6)
-        hipLaunchKernelGGL((verify_kernel<4, 6, 2>), grid, dim3(256), 0, st, p);
-    else if (pf)
-        hipLaunchKernelGGL((verify_kernel<4, 0, 2>), grid, dim3(256), 0, st, p);
-    else if (t.verify_occ == 8)
-        hipLaunchKernelGGL((verify_kernel<4, 8, 0>), grid, dim3(256), 0, st, p);
-    else
-        hipLaunchKernelGGL((verify_kernel<4, 0, 0>), grid, dim3(256), 0, st, p);
-    return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+    if (t.verify_small == 8)  // the walking kernel always
+        return verify_launch_walk(p, st);
+    if (t.verify_small == 6 || t.verify_small == 7) {
+        // Stream capture: the host's choice and the compacting path's
+        // alternating counter sets would be frozen into the graph (a replay
+        // reuses one set without zeroing it), and the per-stream state cannot
+        // be allocated while capturing — so captured calls take a stateless
+        // kernel and leave the sample alone.
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        const bool capturing = hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
+        VerifyState *s = verify_state(stream, !capturing);
+        if (!s)  // capturing before the stream had state, table full, or allocation failure
+            return verify_launch_walk(p, st);
+        std::lock_guard<std::mutex> g(s->mu);
+        const uint32_t smp = __atomic_load_n(s->host_sample, __ATOMIC_RELAXED);
+        const uint32_t lb = __atomic_load_n(s->host_sample + 1, __ATOMIC_RELAXED);
+        const bool known = smp <= 64u;
+        VerifyPath path = kPathCompact;
+        if (t.verify_small == 7)
+            path = !known || smp == 64u ? kPathWalk
+                   : verify_pick_compact(n, smp, lb, t.verify_auto_t) ? kPathCompact
+                                                                       : kPathWave;
+        if (capturing) {
+            path = path == kPathCompact ? kPathWalk : path;
+        } else {
+            p.sample = s->dev_sample;  // this batch's size mix, for the next call's choice
+        }
+        if (path == kPathCompact) {
+            const uint64_t est = known ? (n * (64u - smp) + 63u) / 64u : n;
+            const int rc = verify_compact_launch(p, s, est, t.verify_k2min, st);
+            if (rc != WG_ERR_RUNTIME)
+                return rc;
+            path = kPathWalk;  // no entry lists for this batch: a stateless kernel instead
+        }
+        return path == kPathWalk ? verify_launch_walk(p, st) : verify_launch_wave(p, st);
+    }
+    return verify_launch_wave(p, st);  // verify_small = 0: the wave kernel
 }
 
 extern "C" int wg_verify_uniform(const uint8_t *dev_base, uint64_t total_len, uint32_t segment_size,
@@ -2029,7 +1276,7 @@ extern "C" int wg_verify_uniform(const uint8_t *dev_base, uint64_t total_len, ui
         if (blocks >= 8) blocks = (blocks + 7) & ~7ull;
         if (blocks > 0x7fffffffull)
             return WG_ERR_INVALID;
-        hipLaunchKernelGGL((verify_kernel<4, 8, 0, true, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+        hipLaunchKernelGGL(verify_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, p);
     }
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }

@@ -13,36 +13,23 @@ namespace wg {
 // defaults are the measured best on MI355X.
 struct Tune {
     uint64_t l4_blocks;   // grid cap for the wave-per-packet checksum kernels
-    uint32_t l4_ppw;      // packets per wave iteration (1, 2, 4, 8)
     uint32_t l4_nt;       // 1: non-temporal packet loads
-    uint32_t l4_descv;    // descriptor mode: 0 scalar loads, 1 vector load, 2 vector prefetch of the next iteration
-    uint32_t l4_iters;    // iterations per wave in descriptor mode 2
-    uint32_t l4_small;    // descriptor-batch kernel: 5 split roles (default), 0 wave-per-packet, 1-4 thread-per-packet variants
-    uint32_t l4_small_uniform;  // 1: uniform batches with segment_size <= 64 by the small-packet kernel
-    uint32_t l4_occ;      // waves/SIMD target of the L4 kernels at 4 packets/wave (0 = compiler's choice; 7, 8)
+    uint32_t l4_small;    // descriptor-batch kernel: 5 split roles (default), 0 wave-per-packet
+    uint32_t l4_small_uniform;  // 2: uniform batches with segment_size <= 64 a lane per segment; 0 the wave kernel
     uint64_t gso_blocks;  // grid cap for the GSO split kernel (one block per super-buffer)
     uint32_t gso_waves;   // waves per block (1, 2, 4, 8)
     uint32_t gso_split;   // blocks per super-buffer (grid y)
     uint32_t gso_groups;  // blocks per super-buffer, consecutive in the flat grid (one-shot waves)
     uint32_t gso_spw;     // segments per wave step: 0 one at a time, 1 ping-pong pipeline, 2-4 issued together
     uint32_t encap_spw;   // the same for the encap step's headers-only split
-    uint32_t verify_dm;   // verify kernel descriptor mode: 0 one-shot waves, 2 next-iteration prefetch (l4_iters)
-    uint32_t verify_occ;  // waves/SIMD target of the verify kernel (0 = compiler's choice; 8)
-    uint32_t verify_small;  // 1: verify by the lane-per-descriptor kernel (packets <= 64 B decoded in a lane)
-    uint32_t verify_wblk; // verify_small = 4: waves per block of the wave-role launch (4, 16)
+    uint32_t verify_small;  // 7 per-call choice (default), 0 wave kernel, 6 compacting path, 8 walking kernel
     uint32_t verify_auto_t;  // verify_small = 7: compacting path when >= this many of 64 sampled packets are small
     uint32_t verify_k2min;   // compacting path: minimum blocks of the long kernel
-    uint32_t verify_hdr;  // 1: header bytes ride in the L4 byte gather (no separate header load)
-    uint32_t gro_lds;     // 1: GRO finalize with LDS-staged cooperative header loads
-    uint32_t gro_wide;    // 1: GRO finalize fields written by two wide stores (LDS variant)
-    uint32_t gro_chunks;  // 16-B chunks staged per flow by the LDS variant (4, 5)
-    uint32_t gro_iters;   // gro_lds = 2: groups of 64 flows per wave (1, 2, 4), next descriptors prefetched
     uint32_t host_chunk_mb;  // host-memory pipeline chunk size, MiB
     uint32_t host_d2h;    // host pipeline downloads into pinned memory by a store kernel (bit 1 encap messages, bit 2 decap plaintext)
     uint32_t l4_unroll;   // split kernel: loads in flight per lane on a long packet's rest (4, 8)
     uint64_t l4_coop;     // descriptor batches of n <= l4_coop: a block of l4_coop_waves waves per packet (0: never)
     uint32_t l4_coop_waves;  // waves per packet in that mode (2, 4, 8, 16)
-    uint32_t l4_split_waves;  // split kernel: waves per block, 4 (16 descriptors per wave) or 8 (8 per wave)
     uint32_t aead_k;      // AEAD: consecutive ChaCha20 blocks per lane (1, 2, 3, 4)
     uint32_t aead_flex;   // AEAD: groups of exactly the lanes a packet needs (<= 32), not a power of two
     uint32_t aead_pair;   // AEAD, aead_k = 2, 4: a lane's blocks two at a time, interleaved (1)
