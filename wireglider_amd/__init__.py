@@ -30,6 +30,7 @@ if os.environ.get("WG_LIB"):
 WG_OK = 0
 WG_PKT_V6 = 0x01
 WG_PKT_TCP = 0x02
+WG_PROBE_DEFAULT_POLICY = 0x100  # wg_probe_copy: default cache policy instead of non-temporal
 ABI_VERSION = 1
 
 # Every symbol declared in include/wireglider_amd.h.
@@ -698,12 +699,14 @@ def probe_read(buf, out, kib_per_wave: int = 4, stream=None, run_bytes: int = 0)
                                  run_bytes, _stream_ptr(stream, buf)), "wg_probe_read")
 
 
-def probe_copy(src, dst, kib_per_wave: int = 2, stream=None) -> None:
-    """Launch the copy-roofline probe (dst = src) over device buffers."""
+def probe_copy(src, dst, kib_per_wave: int = 2, stream=None, default_policy: bool = False) -> None:
+    """Launch the copy-roofline probe (dst = src) over device buffers:
+    non-temporal loads and stores, or the default cache policy."""
     n = min(src.numel() * src.element_size(), dst.numel() * dst.element_size())
     with _on(src):
-        _check(lib.wg_probe_copy(src.data_ptr(), dst.data_ptr(), n, kib_per_wave, _stream_ptr(stream, src)),
-               "wg_probe_copy")
+        _check(lib.wg_probe_copy(src.data_ptr(), dst.data_ptr(), n,
+                                 kib_per_wave | (WG_PROBE_DEFAULT_POLICY if default_policy else 0),
+                                 _stream_ptr(stream, src)), "wg_probe_copy")
 
 
 def device_count() -> int:
