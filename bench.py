@@ -109,6 +109,26 @@ class Workload:
     pcie: Optional[dict] = None       # host-memory workloads: PCIe bytes per step {"h2d": B, "d2h": B}
     rw: Optional[tuple] = None        # (read, written) algorithmic bytes per launch, when both directions count
     copy_dst: Optional[object] = None  # read+write workloads: a device buffer the copy probe may overwrite
+    valu_kernel: Optional[str] = None  # VALU-bound workloads: the timed kernel's full symbol (valu_issue check)
+
+
+def aead_kernel_symbol(wga, maxpay: int, dec: bool = False, ver: bool = False, gso: int = 0) -> str:
+    """The demangled symbol of the AEAD kernel launch_aead (csrc/aead.hip)
+    picks for a batch whose largest payload is `maxpay` bytes: K blocks per
+    lane (knob aead_k; 0 = 2 or 3, whichever packs a wave better), a group of
+    exactly the lanes needed (template 0) up to 32, 1 lane (1), else 64."""
+    nblk = (((maxpay + 15) & ~15) + 63) // 64
+    K = wga.tune_get("aead_k")
+    if K == 0:
+        c = nblk + 1
+        l2, l3 = (c + 1) // 2, (c + 2) // 3
+        w2 = 64 // l2 if l2 <= 32 else 0
+        w3 = 64 // l3 if l3 <= 32 else 0
+        K = 3 if 2 * w3 > 3 * w2 else 2
+    lanes = (nblk + 1 + K - 1) // K
+    G = 1 if lanes <= 1 else (0 if lanes <= 32 else 64)
+    b = lambda v: "true" if v else "false"
+    return f"void wg::aead_kernel<{G}, {K}, {b(dec)}, {b(ver)}, {gso}>(wg::AeadParams)"
 
 
 def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workload:
@@ -329,9 +349,10 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
         cfg = {"workload": "aead (SURVEY §8 f4): WireGuard data-message encryption (ChaCha20-Poly1305, "
                            "Peer::encrypt per segment) of 1,048,576 x 1500 B packets per GPU",
                "packets_per_gpu": n, "segment_size": SEG, "message_stride": mseg, "parallelism": f"shard{world}"}
+        ksym = aead_kernel_symbol(wga, SEG)
         return Workload(launch, n, n * SEG, n * SEG + n * mseg + n, cfg, "weak", buf,
-                        "wg::aead_kernel<0,3,false,true> (9-lane groups, VALU-bound: ChaCha20 + Poly1305)", rank * n, sample=sample,
-                        counts=[n] * world, post=post,
+                        f"{ksym} (VALU-bound: ChaCha20 + Poly1305)", rank * n, sample=sample,
+                        counts=[n] * world, post=post, valu_kernel=ksym,
                         metric="device-resident GiB/s of plaintext, WireGuard data-message encryption (SURVEY f4)")
     if name == "config1":
         # tests/test-checksum.cpp:11-17: checksum(create_packet(n), 0) on random
@@ -1017,7 +1038,7 @@ def build_encap(wga, torch, rank: int, world: int, dev, fused: bool = True) -> W
     split_w = n * nseg * ((hdr + 63) // 64 * 64) if fused else n * out_len
     alg = (n * in_len + split_w + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES)
            + n * out_len + n * mbytes + n * (wga.ENCAP_RESULT_BYTES + 8))
-    aead_k = "wg::aead_kernel<0,3,false,true,false,%d>" % (2 if fused else 1)
+    aead_k = aead_kernel_symbol(wga, seg, gso=2 if fused else 1)
     return Workload(launch, n, n * in_len, alg, cfg, "weak", buf,
                     ("wg_encap_batch (3 split kernels, headers only, + 2 scan kernels + %s)" if fused else
                      "wg_gso_split (3 kernels) + wg_encap_encrypt (2 scan kernels + %s)") % aead_k,
@@ -1643,6 +1664,12 @@ def main():
         "post_checks": post,
     }
     valu = load_valu(args.workload)
+    if valu and wl.valu_kernel and valu.get("kernel") != wl.valu_kernel:
+        # the committed instruction count belongs to another kernel: no fraction
+        line["roofline"]["valu_issue_refused"] = (
+            f"profiles/valu_{args.workload}.json counts {valu.get('kernel')!r}, the timed kernel is "
+            f"{wl.valu_kernel!r}")
+        valu = None
     if valu and valu.get("valu_winst_per_launch"):
         # the issue roofline of a VALU-bound kernel (f4): every VALU
         # instruction priced at full rate, so 64-bit multiplies make the true

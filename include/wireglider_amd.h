@@ -464,13 +464,8 @@ int wg_device_count(void);
  *   "host_chunk_mb" host-memory pipeline chunk size in MiB (1 .. 4096)
  *   "host_d2h"   host pipeline downloads into pinned memory by a store
  *                kernel: bit 1 encap messages (default), bit 2 decap plaintext
- *   "aead_k"     AEAD kernels: consecutive ChaCha20 blocks per lane (1-4; 0
- *                = 2 or 3, whichever fills a wave better for the batch)
- *   "aead_pair"  a lane's blocks computed two at a time, interleaved (1),
- *                and with K = 3 the third one up front beside them (2,
- *                default), or one after the other (0)
- *   "aead_flex"  groups of exactly the lanes a packet needs (1, up to 32)
- *                or the next power of two (0)
+ *   "aead_k"     AEAD kernels: consecutive ChaCha20 blocks per lane (2, 3;
+ *                0 = 2 or 3, whichever fills a wave better for the batch)
  *   "gso_ablate" GSO A/B variants: 1 = non-temporal payload stores, 32 = no
  *                XCD swizzle (both correct); 0 = the default kernel.
  * Thread-safe: each launch reads one consistent snapshot of the knobs. */

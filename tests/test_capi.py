@@ -173,7 +173,8 @@ def test_tune_knobs_validate_and_round_trip():
     assert {"l4_nt", "gso_groups", "verify_small", "l4_small", "host_d2h", "gso_ablate"} <= set(keys)
     # round 4 removed the rejected variants' knobs: no longer accepted
     for gone in ("l4_ppw", "l4_occ", "l4_descv", "l4_iters", "l4_split_waves", "verify_dm", "verify_occ",
-                 "verify_hdr", "verify_wblk", "gro_lds", "gro_wide", "gro_chunks", "gro_iters"):
+                 "verify_hdr", "verify_wblk", "gro_lds", "gro_wide", "gro_chunks", "gro_iters", "aead_pair",
+                 "aead_flex"):
         assert gone not in keys
         with pytest.raises(Exception):
             wga.tune_get(gone)
@@ -184,7 +185,7 @@ def test_tune_knobs_validate_and_round_trip():
     for k, bad in (("l4_small", 1), ("l4_small", 4), ("verify_small", 3), ("l4_small_uniform", 1),
                    ("gso_groups", 0), ("gso_groups", 65),
                    ("gso_waves", 16), ("gso_ablate", 7), ("gso_ablate", 2), ("l4_coop_waves", 3),
-                   ("l4_coop_waves", 32)):
+                   ("l4_coop_waves", 32), ("aead_k", 1), ("aead_k", 4)):
         v = wga.tune_get(k)
         with pytest.raises(Exception):
             wga.tune_set(k, bad)

@@ -29,9 +29,9 @@ def _wga():
 
 @pytest.mark.parametrize("fused", [False, True], ids=["split+encrypt", "encap_batch"])
 @pytest.mark.parametrize("seed", [11, 12])
-@pytest.mark.parametrize("knobs", [{}, {"aead_k": 2, "aead_flex": 0}, {"aead_k": 1}, {"encap_parts": 2},
-                                   {"encap_parts": 3}, {"encap_parts": 8}, {"aead_pair": 2}, {"aead_pair": 1}, {"encap_spw": 4}, {"encap_spw": 0},
-                                   {"aead_pair": 2, "encap_parts": 2}],
+@pytest.mark.parametrize("knobs", [{}, {"aead_k": 2}, {"aead_k": 3}, {"encap_parts": 2},
+                                   {"encap_parts": 3}, {"encap_parts": 8}, {"encap_spw": 4}, {"encap_spw": 0},
+                                   {"aead_k": 2, "encap_parts": 2}],
                          ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()) or "default")
 def test_encap_matches_oracle(gpu, seed, knobs, fused):
     import torch

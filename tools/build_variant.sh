@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build the library from csrc/ with some files taken from a git revision, into
 # tools/exp/variant_<name>/libwireglider_amd.so (for tools/ab_builds.sh).
-# usage: tools/build_variant.sh <name> <rev> <csrc file>...
+# usage: [EXTRA_FLAGS=-D...] tools/build_variant.sh <name> <rev> <csrc file>...
 set -eu
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; REV=$2; shift 2
@@ -11,7 +11,7 @@ for f in "$@"; do git -C "$ROOT" show "$REV:wireglider_amd/csrc/$f" > "$SRC/$f";
 objs=()
 for s in "$SRC"/*.hip "$SRC"/*.cpp; do
   o=$SRC/$(basename "$s").o
-  /opt/rocm/bin/hipcc -O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wno-unused-function -I"$ROOT/include" -I"$SRC" \
+  /opt/rocm/bin/hipcc -O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wno-unused-function ${EXTRA_FLAGS:-} -I"$ROOT/include" -I"$SRC" \
     -x hip -c "$s" -o "$o" &
   objs+=("$o")
 done

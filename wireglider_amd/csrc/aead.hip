@@ -7,25 +7,23 @@
 //          (worker/encap.cpp:136-141; counter = encrypt_nonce++ per call);
 //   decap: every message of a UDP GRO batch (worker/decap_ref.cpp:78-86).
 //
-// Layout: a group of G lanes per packet (the smallest power of two that holds
-// its blocks; G = 64 in passes for packets past 64 K blocks), K consecutive
+// Layout: a group of lanes per packet (exactly the lanes its blocks need, up
+// to 32; 64 lanes in passes for packets past 96 blocks), K consecutive
 // ChaCha20 blocks per lane (knob aead_k; by default 2 or 3 per batch, see
-// launch_aead): block counter c is lane
-// c / K's.  Counter 0 (group lane 0's first block) is the Poly1305 key; the
-// lane writing it also writes the DataHeader and handles the length block;
-// counter c >= 1 is the keystream for the 64 bytes [64(c-1), 64c) of the
-// padded payload, XORed and stored.  Poly1305 runs in the lanes too: each
-// lane Horner-evaluates its (up to) 4K 16-B ciphertext blocks with r,
-// multiplies the result by r^(blocks after it) — a suffix product of
-// r^(n_j) over the later lanes, log2(G) cross-lane steps — and the group sums
-// the products (normalised 26-bit limbs, so 32 of them fit a dword) before
-// one multiplication by r (the length block comes last), the reduction mod
-// 2^130 - 5 and + s.  The per-lane fixed costs (powers of r, the scan, the
-// term) are paid once per K blocks, so larger K means fewer multiplications
-// per byte, against registers.  Groups are exactly the lanes a packet needs
-// (aead_flex; the scan and sums then run by down-shift trees), and a lane's
-// blocks are computed two at a time with their quarter rounds interleaved
-// (aead_pair): a 1,500-B packet takes K = 3 in 9 lanes, 7 packets per wave.
+// launch_aead): block counter c is lane c / K's.  Counter 0 (group lane 0's
+// first block) is the Poly1305 key; the lane writing it also writes the
+// DataHeader and handles the length block; counter c >= 1 is the keystream
+// for the 64 bytes [64(c-1), 64c) of the padded payload, XORed and stored.
+// Poly1305 runs in the lanes too: each lane Horner-evaluates its (up to) 4K
+// 16-B ciphertext blocks with r, multiplies the result by r^(blocks after
+// it) — a suffix product of r^(n_j) over the later lanes, log2(lanes)
+// cross-lane steps — and the group sums the products (normalised 26-bit
+// limbs, so 32 of them fit a dword) before one multiplication by r (the
+// length block comes last), the reduction mod 2^130 - 5 and + s.  The
+// per-lane fixed costs (powers of r, the scan, the term) are paid once per K
+// blocks.  A lane's blocks are computed two at a time with their quarter
+// rounds interleaved, and K = 3's third beside them: a 1,500-B packet takes
+// K = 3 in 9 lanes, 7 packets per wave.
 // ChaCha20 and Poly1305 are integer-VALU work (~1,000 and ~200
 // instructions per 64-B block lane), so this kernel is bound by VALU issue,
 // not HBM.
@@ -663,8 +661,11 @@ constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/prot
 // are (the headers-only split writes exactly those bytes), every later
 // block from the input itself, where plaintext byte q >= hdr_len of segment
 // s is input byte s * gso + q — one source per block, no merge.
-template <int G, int K, bool kDec, int kP = 0, bool kVer = false, int kGso = 0>  // kP: 1 pairs; 2 + K = 3's third block up front
-__global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
+#ifndef WG_AEAD_MIN_WAVES
+#define WG_AEAD_MIN_WAVES 1  // waves per SIMD the register allocation must allow (A/B builds: -D)
+#endif
+template <int G, int K, bool kDec, bool kVer = false, int kGso = 0>
+__global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams p) {
     constexpr bool kFlex = G == 0;
     const uint32_t GG = kFlex ? p.grp : (uint32_t)G;  // lanes per packet
     const uint32_t kPer = kFlex ? 64u / GG : 64u / (uint32_t)(G ? G : 1);  // packets per wave
@@ -744,16 +745,17 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
 
     // Each lane's first block of pass 0 (counter g*K) up front: group lane
     // 0's is block 0, the Poly1305 key (r, s), which every lane needs first.
-    // kPair (K = 2 or 4, one pass): the lane's blocks two at a time, each
-    // pair interleaved (chacha20_block2); the first pair up front
-    constexpr bool kPair = kP && K >= 2 && G < 64;
-    // kP = 2, K = 3, one pass: the lane's third block computed up front too,
-    // so its quarter rounds sit in the same straight-line code as the first
-    // two blocks' XOR / store / Poly1305 chains (dependent multiply-adds).
-    // 141 VGPRs, 3 waves/SIMD, and still faster: the waves wait on dependent
-    // VALU issue, not on memory (forcing 4 waves/SIMD spills and loses half
-    // the gain; profiles/r03_aead_tri_ab.json)
-    constexpr bool kTri = kP == 2 && K == 3 && G < 64;
+    // One pass (G < 64): the lane's blocks two at a time, each pair
+    // interleaved (chacha20_block2), the first pair up front (8 independent
+    // columns per step: -8 %, profiles/r02_aead_pair_ab.json)
+    constexpr bool kPair = K >= 2 && G < 64;
+    // K = 3, one pass: the lane's third block computed up front too, so its
+    // quarter rounds sit in the same straight-line code as the first two
+    // blocks' XOR / store / Poly1305 chains (dependent multiply-adds).
+    // 3 waves/SIMD, and still faster: the waves wait on dependent VALU
+    // issue, not on memory (forcing 4 waves/SIMD spills and loses half the
+    // gain; encrypt -6.5 %, encap -4 %, profiles/r03_aead_tri_ab.json)
+    constexpr bool kTri = K == 3 && G < 64;
     uint32_t ks[16], ks1[16], ks2[kTri ? 16 : 1];
     {
         const ChaPre pc = chacha_pre(p.key, n0, n1, n2);
@@ -1165,40 +1167,16 @@ static AeadKey key_words(const uint8_t key[32]) {
 template <int G, int K, bool kDec>
 static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
     if constexpr (!kDec) {
-        if (p.eres) {  // encap: GSO segments (with the pair interleave where it applies)
-            // the third block up front too (aead_pair = 2): encap 19.33 ->
-            // 18.55 ms (profiles/r03_aead_tri_ab.json)
-            constexpr int kPg = K >= 2 && G < 64 ? 1 : 0;
-            if (p.gmode == 2 && kPg && tune().aead_pair == 2)
-                hipLaunchKernelGGL((aead_kernel<G, K, false, 2, false, 2>), dim3((unsigned)blocks), dim3(256), 0,
-                                   st, p);
-            else if (p.gmode == 2)
-                hipLaunchKernelGGL((aead_kernel<G, K, false, kPg, false, 2>), dim3((unsigned)blocks), dim3(256), 0,
-                                   st, p);
+        if (p.eres) {  // encap: GSO segments
+            if (p.gmode == 2)
+                hipLaunchKernelGGL((aead_kernel<G, K, false, false, 2>), dim3((unsigned)blocks), dim3(256), 0, st, p);
             else
-                hipLaunchKernelGGL((aead_kernel<G, K, false, kPg, false, 1>), dim3((unsigned)blocks), dim3(256), 0,
-                                   st, p);
+                hipLaunchKernelGGL((aead_kernel<G, K, false, false, 1>), dim3((unsigned)blocks), dim3(256), 0, st, p);
             return;
         }
-    }
-    if constexpr (kDec) {
-        if (p.verdict) {  // decrypt + verify (always with the pair interleave where it applies)
-            constexpr int kPv = K >= 2 && G < 64 ? 1 : 0;
-            if (kPv && tune().aead_pair == 2)
-                hipLaunchKernelGGL((aead_kernel<G, K, true, 2, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
-            else
-                hipLaunchKernelGGL((aead_kernel<G, K, true, kPv, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
-            return;
-        }
-    }
-    if constexpr (K >= 2 && G < 64) {
-        const uint32_t pair = tune().aead_pair;
-        if (pair == 2) {  // encrypt 1.343 -> 1.256 ms, decrypt 1.356 -> 1.316 ms (profiles/r03_aead_tri_*)
-            hipLaunchKernelGGL((aead_kernel<G, K, kDec, 2>), dim3((unsigned)blocks), dim3(256), 0, st, p);
-            return;
-        }
-        if (pair) {
-            hipLaunchKernelGGL((aead_kernel<G, K, kDec, 1>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+    } else {
+        if (p.verdict) {  // decrypt + verify
+            hipLaunchKernelGGL((aead_kernel<G, K, true, true>), dim3((unsigned)blocks), dim3(256), 0, st, p);
             return;
         }
     }
@@ -1207,25 +1185,20 @@ static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
 
 template <int K, bool kDec>
 static void launch_k(const AeadParams &p, uint32_t G, uint64_t blocks, hipStream_t st) {
-    switch (G) {
-    case 0: launch_gk<0, K, kDec>(p, blocks, st); break;
-    case 1: launch_gk<1, K, kDec>(p, blocks, st); break;
-    case 2: launch_gk<2, K, kDec>(p, blocks, st); break;
-    case 4: launch_gk<4, K, kDec>(p, blocks, st); break;
-    case 8: launch_gk<8, K, kDec>(p, blocks, st); break;
-    case 16: launch_gk<16, K, kDec>(p, blocks, st); break;
-    case 32: launch_gk<32, K, kDec>(p, blocks, st); break;
-    default: launch_gk<64, K, kDec>(p, blocks, st); break;
-    }
+    if (G == 0)
+        launch_gk<0, K, kDec>(p, blocks, st);
+    else if (G == 1)
+        launch_gk<1, K, kDec>(p, blocks, st);
+    else
+        launch_gk<64, K, kDec>(p, blocks, st);
 }
 
 template <bool kDec>
 static int launch_aead(AeadParams &p, uint32_t maxpay, hipStream_t st) {
     // counters per packet: the key block + the padded payload's 64-B blocks;
     // K (knob aead_k) consecutive blocks per lane; a group of exactly the
-    // lanes needed (aead_flex, up to 32: 64 / lanes packets per wave), else
-    // the smallest power-of-two group (64 lanes and several passes past 64 K
-    // blocks)
+    // lanes needed (up to 32: 64 / lanes packets per wave), else 64 lanes in
+    // several passes
     const uint32_t nblk = (((maxpay + 15u) & ~15u) + 63u) / 64u;
     const Tune t = tune();
     uint32_t K = t.aead_k;
@@ -1240,26 +1213,19 @@ static int launch_aead(AeadParams &p, uint32_t maxpay, hipStream_t st) {
         K = 2u * w3 > 3u * w2 ? 3u : 2u;  // w3 / 3 > w2 / 2
     }
     const uint32_t lanes = (nblk + 1u + K - 1u) / K;
-    uint32_t G = 1;
-    while (G < lanes && G < 64u) G <<= 1;
-    uint32_t per_wave = 64u / G;
-    if (t.aead_flex && lanes <= 32u && lanes != G) {
-        p.grp = lanes;
-        per_wave = 64u / lanes;
-        G = 0;
-    }
+    uint32_t G = lanes <= 1u ? 1u : lanes <= 32u ? 0u : 64u;
+    const uint32_t per_wave = G ? 64u / G : 64u / lanes;
+    p.grp = lanes;
     const uint64_t per_block = 4u * per_wave;  // packets per 256-thread block
     uint64_t blocks = (p.n + per_block - 1) / per_block;
     if (blocks >= 8)
         blocks = (blocks + 7) & ~7ull;  // XCD swizzle bijective; surplus waves have no live packet
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
-    switch (K) {
-    case 1: launch_k<1, kDec>(p, G, blocks, st); break;
-    case 2: launch_k<2, kDec>(p, G, blocks, st); break;
-    case 3: launch_k<3, kDec>(p, G, blocks, st); break;
-    default: launch_k<4, kDec>(p, G, blocks, st); break;
-    }
+    if (K == 2)
+        launch_k<2, kDec>(p, G, blocks, st);
+    else
+        launch_k<3, kDec>(p, G, blocks, st);
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }
 

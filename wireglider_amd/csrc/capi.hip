@@ -29,7 +29,7 @@ struct Knob {
 
 static const uint64_t kL4Small[] = {0, 5}, kL4SU[] = {0, 2}, kVSmall[] = {0, 6, 7, 8},
                       kWaves[] = {1, 2, 4, 8}, kAbl[] = {0, 1, 32},
-                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {0, 1, 2, 3, 4}, kParts[] = {1, 2, 3, 4, 8};
+                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {0, 2, 3}, kParts[] = {1, 2, 3, 4, 8};
 #define WG_N(a) (sizeof(a) / sizeof(a[0]))
 static const Knob kKnobs[] = {
     {"l4_blocks", &Tune::l4_blocks, nullptr, 1, 1u << 20, nullptr, 0},
@@ -52,8 +52,6 @@ static const Knob kKnobs[] = {
     {"l4_coop", &Tune::l4_coop, nullptr, 0, 1u << 20, nullptr, 0},
     {"l4_coop_waves", nullptr, &Tune::l4_coop_waves, 0, 0, kCoopW, WG_N(kCoopW)},
     {"aead_k", nullptr, &Tune::aead_k, 0, 0, kAeadK, WG_N(kAeadK)},
-    {"aead_pair", nullptr, &Tune::aead_pair, 0, 2, nullptr, 0},
-    {"aead_flex", nullptr, &Tune::aead_flex, 0, 1, nullptr, 0},
     {"encap_parts", nullptr, &Tune::encap_parts, 0, 0, kParts, WG_N(kParts)},
 };
 #undef WG_N
@@ -156,12 +154,6 @@ static Tune &tune_storage() {
         // K = 2 in 16-lane groups 1.506 (profiles/r02_aead_flex_ab.json), the
         // interleave -8 % (profiles/r02_aead_pair_ab.json)
         x.aead_k = 0;
-        // 2: a lane's third block (K = 3) computed up front with the pair
-        // too (3 waves/SIMD): encrypt -6.5 %, encap -4 %, decrypt and the
-        // fused decrypt + verify -3-4 % (profiles/r03_aead_tri_ab.json,
-        // profiles/r03_aead_tri_decrypt.txt)
-        x.aead_pair = 2;
-        x.aead_flex = 1;
         x.encap_parts = 1;
         // environment overrides: WG_<KNOB> (upper case), same accepted values
         // as wg_tune_set; anything else is ignored
