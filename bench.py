@@ -1395,6 +1395,26 @@ def load_valu(workload: str):
         return None
 
 
+def valu_issue(valu, kernel: Optional[str], kern_ms: float, workload: str) -> dict:
+    """The VALU issue roofline of a VALU-bound kernel (f4) from its committed
+    instruction count, as roofline fields: {"valu_issue": ...}, or
+    {"valu_issue_refused": why} when the profile counts another kernel than
+    the timed one, or {} without a profile.  Every instruction is priced at
+    one wave64 issue per 2 cycles of a SIMD (MI355X_MICROARCH.md), so
+    multi-cycle operations make the true bound tighter than this fraction."""
+    if not valu or not valu.get("valu_winst_per_launch"):
+        return {}
+    if kernel and valu.get("kernel") != kernel:
+        return {"valu_issue_refused": f"profiles/valu_{workload}.json counts {valu.get('kernel')!r}, "
+                                      f"the timed kernel is {kernel!r}"}
+    ach = valu["valu_winst_per_launch"] / (kern_ms * 1e-3)
+    return {"valu_issue": {
+        "bound": "valu", "achieved": round(ach / 1e12, 4), "peak": round(VALU_PEAK_WINST / 1e12, 4),
+        "unit": "T wave64-instructions/s", "frac": round(ach / VALU_PEAK_WINST, 4),
+        "instructions_per_launch": valu["valu_winst_per_launch"],
+        "source": f"profiles/valu_{workload}.json (rocprofv3 SQ_INSTS_VALU, {valu.get('kernel')})"}}
+
+
 def post_checks(torch, wga, wl: Workload, world: int, dev, no_post: bool = False):
     """Outside the timed region: verify pass, result hash, RCCL gather."""
     from wireglider_amd import dist as wdist
@@ -1605,7 +1625,8 @@ def main():
     post = post_checks(torch, wga, wl, world, dev, args.no_post)
     meta = {"metric": wl.metric or "device-resident GiB/s, L4 checksum over packet batch; 1/2/4/8 MI355X",
             "pcie": pcie, "rw": wl.rw,
-            "unit": wl.unit, "scaling": wl.scaling, "config": wl.cfg, "kernel": wl.kernel, "alg_bytes": wl.alg_bytes}
+            "unit": wl.unit, "scaling": wl.scaling, "config": wl.cfg, "kernel": wl.kernel, "alg_bytes": wl.alg_bytes,
+            "valu_kernel": wl.valu_kernel}
     del wl
     torch.cuda.empty_cache()
     strong = None if args.no_strong else strong_scaling(torch, wga, args, rank, world, dev)
@@ -1663,23 +1684,7 @@ def main():
         },
         "post_checks": post,
     }
-    valu = load_valu(args.workload)
-    if valu and wl.valu_kernel and valu.get("kernel") != wl.valu_kernel:
-        # the committed instruction count belongs to another kernel: no fraction
-        line["roofline"]["valu_issue_refused"] = (
-            f"profiles/valu_{args.workload}.json counts {valu.get('kernel')!r}, the timed kernel is "
-            f"{wl.valu_kernel!r}")
-        valu = None
-    if valu and valu.get("valu_winst_per_launch"):
-        # the issue roofline of a VALU-bound kernel (f4): every VALU
-        # instruction priced at full rate, so 64-bit multiplies make the true
-        # bound tighter than this fraction suggests
-        ach = valu["valu_winst_per_launch"] / (kern_ms * 1e-3)
-        line["roofline"]["valu_issue"] = {
-            "bound": "valu", "achieved": round(ach / 1e12, 4), "peak": round(VALU_PEAK_WINST / 1e12, 4),
-            "unit": "T wave64-instructions/s", "frac": round(ach / VALU_PEAK_WINST, 4),
-            "instructions_per_launch": valu["valu_winst_per_launch"],
-            "source": f"profiles/valu_{args.workload}.json (rocprofv3 SQ_INSTS_VALU, {valu.get('kernel')})"}
+    line["roofline"].update(valu_issue(load_valu(args.workload), meta["valu_kernel"], kern_ms, args.workload))
     if meta["pcie"] is not None:
         # the device roofline does not apply to a host-memory pipeline
         line["roofline_device"] = line["roofline"]

@@ -215,3 +215,21 @@ def test_tune_environment_overrides():
     assert (nt, groups, vs) == (0, 5, 8)
     assert abl == 0  # WG_GSO_ABLATE=2 is not an accepted value: ignored
     assert small == 5  # 3 is not an accepted value: default kept
+
+
+def test_bench_valu_issue_checks_kernel_symbol():
+    """bench.py prices the AEAD line against a committed VALU instruction
+    count only when that profile counted the kernel the line times: the
+    symbol launch_aead picks (aead_kernel_symbol mirrors its K / group rule)."""
+    import bench
+    import wireglider_amd as wga
+
+    assert bench.aead_kernel_symbol(wga, 1500) == "void wg::aead_kernel<0, 3, false, false, 0>(wg::AeadParams)"
+    assert bench.aead_kernel_symbol(wga, 64) == "void wg::aead_kernel<1, 2, false, false, 0>(wg::AeadParams)"
+    assert bench.aead_kernel_symbol(wga, 9000, True, True).startswith("void wg::aead_kernel<64, 2, true, true, 0>")
+    assert bench.aead_kernel_symbol(wga, 1500, gso=2) == "void wg::aead_kernel<0, 3, false, false, 2>(wg::AeadParams)"
+    prof = {"kernel": "void wg::aead_kernel<0, 3, false, true>(wg::AeadParams)", "valu_winst_per_launch": 8e8}
+    ok = bench.valu_issue(dict(prof, kernel="K"), "K", 1.0, "aead")
+    assert ok["valu_issue"]["frac"] == round(8e8 / 1e-3 / bench.VALU_PEAK_WINST, 4)
+    assert "valu_issue_refused" in bench.valu_issue(prof, "K", 1.0, "aead")
+    assert bench.valu_issue(None, "K", 1.0, "aead") == {}

@@ -7,7 +7,7 @@ OUT=$1; R=$2; A=$3; B=$4; shift 4
 for r in $(seq "$R"); do
   for W in "$@"; do
     for L in "$A" "$B"; do
-      WG_LIB=$L timeout -k 10 300 python3 bench.py --workload "$W" --steps 30 --no-cpu-baseline --no-strong --no-post 2>/dev/null | \
+      WG_LIB=$L timeout -k 10 300 python3 bench.py --workload "$W" --steps 30 --no-cpu-baseline --no-strong --no-post 2>>"$OUT.err" | \
         python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'lib': sys.argv[1], 'workload': sys.argv[2], 'kernel_ms': d['roofline']['kernel_ms_avg'], 'frac': d['roofline']['frac']}))" "$L" "$W" >> "$OUT" || exit 1
     done
   done
