@@ -33,6 +33,10 @@
 #include "wg_internal.hpp"
 #include "wireglider_amd.h"
 
+#ifndef WG_P32_CARRY_LAST
+#define WG_P32_CARRY_LAST 0  // A/B builds: -DWG_P32_CARRY_LAST=1
+#endif
+
 namespace wg {
 
 // ---------------------------------------------------------------------------
@@ -312,6 +316,17 @@ __device__ __forceinline__ P32 p32_step(const P32 &x, uint32_t m0, uint32_t m1, 
     const uint32_t t2 = __builtin_addc(x.h[2], m2, c, &c);
     const uint32_t t3 = __builtin_addc(x.h[3], m3, c, &c);
     const uint32_t t4 = x.h[4] + 1u + c;  // + 2^128: the block's pad bit
+#if WG_P32_CARRY_LAST
+    // the four columns as independent multiply-add chains, the carries
+    // propagated after them (a shorter dependency path, three more adds)
+    const uint64_t d0 = mad64(t3, sr[1], mad64(t2, sr[2], mad64(t1, sr[3], (uint64_t)t0 * r[0])));
+    const uint64_t e1 = mad64(t4, sr[1], mad64(t3, sr[2], mad64(t2, sr[3], mad64(t1, r[0], (uint64_t)t0 * r[1]))));
+    const uint64_t e2 = mad64(t4, sr[2], mad64(t3, sr[3], mad64(t2, r[0], mad64(t1, r[1], (uint64_t)t0 * r[2]))));
+    const uint64_t e3 = mad64(t4, sr[3], mad64(t3, r[0], mad64(t2, r[1], mad64(t1, r[2], (uint64_t)t0 * r[3]))));
+    const uint64_t d1 = e1 + (d0 >> 32);
+    const uint64_t d2 = e2 + (d1 >> 32);
+    const uint64_t d3 = e3 + (d2 >> 32);
+#else
     const uint64_t d0 = mad64(t3, sr[1], mad64(t2, sr[2], mad64(t1, sr[3], (uint64_t)t0 * r[0])));
     const uint64_t d1 =
         mad64(t4, sr[1], mad64(t3, sr[2], mad64(t2, sr[3], mad64(t1, r[0], mad64(t0, r[1], d0 >> 32)))));
@@ -319,6 +334,7 @@ __device__ __forceinline__ P32 p32_step(const P32 &x, uint32_t m0, uint32_t m1, 
         mad64(t4, sr[2], mad64(t3, sr[3], mad64(t2, r[0], mad64(t1, r[1], mad64(t0, r[2], d1 >> 32)))));
     const uint64_t d3 =
         mad64(t4, sr[3], mad64(t3, r[0], mad64(t2, r[1], mad64(t1, r[2], mad64(t0, r[3], d2 >> 32)))));
+#endif
     const uint32_t h4 = t4 * r[0] + (uint32_t)(d3 >> 32);
     const uint32_t cc = (h4 >> 2) + (h4 & ~3u);  // 5 * (h4 >> 2): 2^130 == 5
     P32 o;
@@ -686,6 +702,10 @@ __global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams
     uintptr_t hsrc = 0;  // kGso == 2: the segment slot, holding plaintext [0, hl)
     uint32_t hl = 0;     // kGso == 2: hdr_len rounded up to whole 64-B blocks (0: passthrough)
     uint64_t gctr = 0;
+    // encrypt: the end of the contiguous source region holding the packet's
+    // plaintext (blocks at or past hl for kGso == 2): a partial last block
+    // whose 64-B window ends inside it is loaded whole and masked
+    uintptr_t send = 0;
     if constexpr (kGso) {
         sb = ii / p.gm;
         gs = (uint32_t)(ii - sb * p.gm);
@@ -701,9 +721,12 @@ __global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams
             hsrc = reinterpret_cast<uintptr_t>(p.in) + gd.out_offset + so;
             gsrc = reinterpret_cast<uintptr_t>(p.gin) + gd.in_offset +
                    (gr.passthrough ? so : (uint64_t)gs * (S - gr.hdr_len));
+            send = reinterpret_cast<uintptr_t>(p.gin) + gd.in_offset + gd.in_len;
         } else {
             gsrc = (gr.passthrough ? reinterpret_cast<uintptr_t>(p.gin) + gd.in_offset
                                    : reinterpret_cast<uintptr_t>(p.in) + gd.out_offset) + so;
+            send = gr.passthrough ? reinterpret_cast<uintptr_t>(p.gin) + gd.in_offset + gd.in_len
+                                  : reinterpret_cast<uintptr_t>(p.in) + gd.out_offset + gr.out_len;
         }
         gstride = 32u + ((S + 15u) & ~15u);
         gdst = reinterpret_cast<uintptr_t>(p.out) + p.msg_off[sb] + (uint64_t)gs * gstride;
@@ -720,6 +743,8 @@ __global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams
         plen = len;
         pad = (len + 15u) & ~15u;
         src = kGso ? gsrc : reinterpret_cast<uintptr_t>(p.in) + off;
+        if constexpr (!kGso)
+            send = reinterpret_cast<uintptr_t>(p.in) + p.total_len;
         dst = kGso ? gdst : reinterpret_cast<uintptr_t>(p.out) + ii * (32ull + ((p.seg + 15u) & ~15u));
         if (counter >= kRejectAfterMessages)  // proto.cpp:560-562: EncryptError::NoSession
             st = -1;
@@ -867,8 +892,14 @@ __global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams
             // below hl from the segment slot
             const uintptr_t bsrc = (kGso == 2 && boff < hl ? hsrc : src) + boff;
             const uintptr_t bdst = kDec ? dst + boff : dst + 16 + boff;
+            // encrypt: a packet's last block whose 64-B window lies inside
+            // the source region takes the whole-block path too, masked to its
+            // payload bytes (ciphertext stores and Poly1305 steps only below
+            // pad, both whole 16-B chunks): the general path then runs only
+            // for windows at a region's end
+            const bool tail = !kDec && has && nin < 64u && !(kGso == 2 && boff < hl) && bsrc + 64u <= send;
             uint32_t W[16];
-            if (nin == 64u) {
+            if (nin == 64u || tail) {
                 // A whole block inside the payload (every block of a packet
                 // but its last): four 16-B loads at the source address as it
                 // is (gfx950 global loads take any alignment; all 64 bytes
@@ -882,6 +913,13 @@ __global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams
 #pragma unroll
                     for (uint32_t e = 0; e < 4; e++) W[4 * q + e] = v[e];
                 }
+                // wave-uniform: some lane holds a packet's last block here
+                const bool anyt = !kDec && __ballot(tail) != 0;
+                if (anyt) {
+#pragma unroll
+                    for (int m = 0; m < 16; m++)
+                        W[m] = keep_below(W[m], (uint32_t)m, nin);  // padding plaintext is zero (proto.cpp:568-572)
+                }
 #pragma unroll
                 for (int m = 0; m < 16; m++) {
                     if constexpr (!kDec)
@@ -890,12 +928,25 @@ __global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams
                         kb[m] ^= W[m];  // plaintext
                 }
                 const uint32_t *o = kDec ? kb : W;
+                if (anyt) {
+                    const uint32_t nqc = nct / 16u;  // ciphertext chunks below pad
 #pragma unroll
-                for (uint32_t q = 0; q < 4; q++)
-                    st16(bdst + 16u * q, v4u{o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]});
+                    for (uint32_t q = 0; q < 4; q++) {
+                        if (q < nqc)
+                            st16(bdst + 16u * q, v4u{o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]});
+                        const P32 t = p32_step(x, W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3], rw, srw);
 #pragma unroll
-                for (uint32_t q = 0; q < 4; q++)
-                    x = p32_step(x, W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3], rw, srw);
+                        for (int k = 0; k < 5; k++)
+                            x.h[k] = q < nqc ? t.h[k] : x.h[k];
+                    }
+                } else {
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; q++)
+                        st16(bdst + 16u * q, v4u{o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]});
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; q++)
+                        x = p32_step(x, W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3], rw, srw);
+                }
             } else if (has) {
                 // zero past the payload
                 load64(bsrc, nin, W);
