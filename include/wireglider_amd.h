@@ -466,6 +466,9 @@ int wg_device_count(void);
  *                kernel: bit 1 encap messages (default), bit 2 decap plaintext
  *   "aead_k"     AEAD kernels: consecutive ChaCha20 blocks per lane (2, 3;
  *                0 = 2 or 3, whichever fills a wave better for the batch)
+ *   "aead_stage" AEAD encrypt: each wave assembles its messages in LDS and
+ *                writes them out in whole lines (1, default) or every lane
+ *                stores its own blocks (0)
  *   "gso_ablate" GSO A/B variants: 1 = non-temporal payload stores, 32 = no
  *                XCD swizzle (both correct); 0 = the default kernel.
  * Thread-safe: each launch reads one consistent snapshot of the knobs. */

@@ -44,15 +44,18 @@ ENC_CASES = [(1460, 1460 * 40 + 777), (1460, 1460 * 3), (64, 64 * 300 + 1), (1, 
              (32768, 32768 * 2 + 1)]
 
 
-@pytest.fixture(params=[0, 2, 3], ids=lambda k: f"aead_k={k}")
+@pytest.fixture(params=[(0, 1), (2, 1), (3, 1), (0, 0), (2, 0)], ids=lambda kp: f"aead_k={kp[0]},stage={kp[1]}")
 def aead_k(request):
     """Every lane-blocking variant (consecutive ChaCha20 blocks per lane: 2,
-    3 or chosen per batch): a speed knob that must not change any byte."""
+    3 or chosen per batch) with encrypt's messages staged in LDS or stored
+    from the lanes: speed knobs that must not change any byte."""
     wga = _wga()
-    saved = wga.tune_get("aead_k")
-    wga.tune_set("aead_k", request.param)
+    saved = {k: wga.tune_get(k) for k in ("aead_k", "aead_stage")}
+    wga.tune_set("aead_k", request.param[0])
+    wga.tune_set("aead_stage", request.param[1])
     yield request.param
-    wga.tune_set("aead_k", saved)
+    for k, v in saved.items():
+        wga.tune_set(k, v)
 
 
 @pytest.mark.parametrize("seg,total", ENC_CASES)

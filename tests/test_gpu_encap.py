@@ -29,7 +29,7 @@ def _wga():
 
 @pytest.mark.parametrize("fused", [False, True], ids=["split+encrypt", "encap_batch"])
 @pytest.mark.parametrize("seed", [11, 12])
-@pytest.mark.parametrize("knobs", [{}, {"aead_k": 2}, {"aead_k": 3}, {"encap_parts": 2},
+@pytest.mark.parametrize("knobs", [{}, {"aead_k": 2}, {"aead_k": 3}, {"aead_stage": 0}, {"encap_parts": 2},
                                    {"encap_parts": 3}, {"encap_parts": 8}, {"encap_spw": 4}, {"encap_spw": 0},
                                    {"aead_k": 2, "encap_parts": 2}],
                          ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()) or "default")

@@ -592,6 +592,8 @@ struct AeadParams {
                                  // payload from `gin` (wg_encap_batch)
     const uint64_t *ctr_base;    // kGso, nullable: messages of earlier chunks, added to counter0
                                  // (the host path's chained chunks)
+    uint32_t lstride;            // kStage: bytes per message slot in LDS (32 + pad16(seg))
+    uint32_t lds_wave;           // kStage: LDS bytes per wave (packets per wave x lstride)
 };
 
 // The decap verify gates (wg_verify_desc, SURVEY §8 f1: evaluate_packet,
@@ -680,8 +682,17 @@ constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/prot
 #ifndef WG_AEAD_MIN_WAVES
 #define WG_AEAD_MIN_WAVES 1  // waves per SIMD the register allocation must allow (A/B builds: -D)
 #endif
-template <int G, int K, bool kDec, bool kVer = false, int kGso = 0>
+// kStage (encrypt, groups of exactly the lanes needed): every message is
+// assembled in the wave's LDS slot (header, ciphertext blocks, tag) and then
+// written out slot by slot with consecutive lanes on consecutive 16-B chunks,
+// so each store instruction covers whole lines: written straight from the
+// lanes, a block's 64 B straddle two 64-B sectors (the ciphertext starts 16 B
+// into the message) that are completed at different times, and the memory
+// wrote ~1.48x the message bytes (profiles/pmc_aead.json).
+template <int G, int K, bool kDec, bool kVer = false, int kGso = 0, bool kStage = false>
 __global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams p) {
+    static_assert(!kStage || (!kDec && G == 0), "staged messages: encrypt, exact-size groups");
+    extern __shared__ v4u aead_lds[];
     constexpr bool kFlex = G == 0;
     const uint32_t GG = kFlex ? p.grp : (uint32_t)G;  // lanes per packet
     const uint32_t kPer = kFlex ? 64u / GG : 64u / (uint32_t)(G ? G : 1);  // packets per wave
@@ -767,6 +778,8 @@ __global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams
     }
     const uint32_t n0 = 0, n1 = (uint32_t)counter, n2 = (uint32_t)(counter >> 32);  // nonce: 0^4 || le64(counter)
     const bool act = live && st == 0;
+    // kStage: this packet's message slot in LDS (16-B units)
+    const uint32_t lslot = kStage ? (wave_in_block() * p.lds_wave + slot * p.lstride) / 16u : 0u;
 
     // Each lane's first block of pass 0 (counter g*K) up front: group lane
     // 0's is block 0, the Poly1305 key (r, s), which every lane needs first.
@@ -932,8 +945,13 @@ __global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams
                     const uint32_t nqc = nct / 16u;  // ciphertext chunks below pad
 #pragma unroll
                     for (uint32_t q = 0; q < 4; q++) {
-                        if (q < nqc)
-                            st16(bdst + 16u * q, v4u{o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]});
+                        if (q < nqc) {
+                            const v4u v{o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]};
+                            if constexpr (kStage)
+                                aead_lds[lslot + (16u + boff) / 16u + q] = v;
+                            else
+                                st16(bdst + 16u * q, v);
+                        }
                         const P32 t = p32_step(x, W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3], rw, srw);
 #pragma unroll
                         for (int k = 0; k < 5; k++)
@@ -941,8 +959,13 @@ __global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams
                     }
                 } else {
 #pragma unroll
-                    for (uint32_t q = 0; q < 4; q++)
-                        st16(bdst + 16u * q, v4u{o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]});
+                    for (uint32_t q = 0; q < 4; q++) {
+                        const v4u v{o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]};
+                        if constexpr (kStage)
+                            aead_lds[lslot + (16u + boff) / 16u + q] = v;
+                        else
+                            st16(bdst + 16u * q, v);
+                    }
 #pragma unroll
                     for (uint32_t q = 0; q < 4; q++)
                         x = p32_step(x, W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3], rw, srw);
@@ -965,7 +988,14 @@ __global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams
                 }
                 // decrypt stores the plaintext now; a bad tag zeroes it below
                 // (the final bytes are libsodium's either way)
-                store_n(bdst, kDec ? kb : W, kDec ? nin : nct);
+                if constexpr (kStage) {
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; q++)
+                        if (q < nqc)
+                            aead_lds[lslot + (16u + boff) / 16u + q] = v4u{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]};
+                } else {
+                    store_n(bdst, kDec ? kb : W, kDec ? nin : nct);
+                }
 #pragma unroll
                 for (uint32_t q = 0; q < 4; q++) {
                     const P32 t = p32_step(x, W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3], rw, srw);
@@ -1053,8 +1083,15 @@ __global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams
     if constexpr (!kDec) {
         if (g == 0u && live) {
             if (act) {
-                st16(dst, v4u{4u, p.receiver, n1, n2});  // DataHeader (proto.cpp:563-566)
-                st16(dst + 16 + pad, v4u{tagw[0], tagw[1], tagw[2], tagw[3]});
+                const v4u hdr{4u, p.receiver, n1, n2};  // DataHeader (proto.cpp:563-566)
+                const v4u tag{tagw[0], tagw[1], tagw[2], tagw[3]};
+                if constexpr (kStage) {
+                    aead_lds[lslot] = hdr;
+                    aead_lds[lslot + 1u + pad / 16u] = tag;
+                } else {
+                    st16(dst, hdr);
+                    st16(dst + 16 + pad, tag);
+                }
             }
             if constexpr (kGso) {
                 if (gs == 0u)
@@ -1069,6 +1106,25 @@ __global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams
                     p.eres[sb].msg_bytes = gs * gstride;
             } else if (p.status) {
                 p.status[ii] = st;
+            }
+        }
+        if constexpr (kStage) {
+            // the wave's messages, slot by slot: consecutive lanes on
+            // consecutive 16-B chunks of one message (refused / empty slots
+            // write nothing, as unstaged)
+            const uint32_t mch = act ? (32u + pad) / 16u : 0u;  // the message's 16-B chunks
+            const uint32_t dlo = (uint32_t)dst, dhi = (uint32_t)(dst >> 32);
+            const uint32_t wl = wave_in_block() * p.lds_wave / 16u;
+            for (uint32_t s = 0; s < kPer; s++) {  // wave-uniform
+                const int src_lane = (int)(s * GG);
+                const uint32_t n16 = (uint32_t)__builtin_amdgcn_readlane((int)mch, src_lane);
+                if (n16 == 0u)
+                    continue;
+                const uintptr_t base = (uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)dlo, src_lane) |
+                                       ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)dhi, src_lane) << 32);
+                const uint32_t ls = wl + s * p.lstride / 16u;
+                for (uint32_t t = lane; t < n16; t += 64u)
+                    st16(base + 16u * t, aead_lds[ls + t]);
             }
         }
     } else {
@@ -1215,9 +1271,29 @@ static AeadKey key_words(const uint8_t key[32]) {
     return k;
 }
 
+// LDS per block of the staged encrypt kernel: at most this, so three blocks
+// (12 waves) still fit a CU's 160 KiB; larger messages per wave are stored
+// straight from the lanes
+constexpr uint32_t kStageMaxBlockLds = 53248;
+
 template <int G, int K, bool kDec>
 static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
     if constexpr (!kDec) {
+        if constexpr (G == 0) {
+            const uint32_t shm = 4u * p.lds_wave;
+            if (p.lds_wave && shm <= kStageMaxBlockLds) {
+                if (!p.eres)
+                    hipLaunchKernelGGL((aead_kernel<0, K, false, false, 0, true>), dim3((unsigned)blocks), dim3(256),
+                                       shm, st, p);
+                else if (p.gmode == 2)
+                    hipLaunchKernelGGL((aead_kernel<0, K, false, false, 2, true>), dim3((unsigned)blocks), dim3(256),
+                                       shm, st, p);
+                else
+                    hipLaunchKernelGGL((aead_kernel<0, K, false, false, 1, true>), dim3((unsigned)blocks), dim3(256),
+                                       shm, st, p);
+                return;
+            }
+        }
         if (p.eres) {  // encap: GSO segments
             if (p.gmode == 2)
                 hipLaunchKernelGGL((aead_kernel<G, K, false, false, 2>), dim3((unsigned)blocks), dim3(256), 0, st, p);
@@ -1267,6 +1343,9 @@ static int launch_aead(AeadParams &p, uint32_t maxpay, hipStream_t st) {
     uint32_t G = lanes <= 1u ? 1u : lanes <= 32u ? 0u : 64u;
     const uint32_t per_wave = G ? 64u / G : 64u / lanes;
     p.grp = lanes;
+    // staged messages (encrypt, exact-size groups): one LDS slot per packet
+    p.lstride = 32u + ((p.seg + 15u) & ~15u);
+    p.lds_wave = (!kDec && G == 0 && t.aead_stage) ? per_wave * p.lstride : 0u;
     const uint64_t per_block = 4u * per_wave;  // packets per 256-thread block
     uint64_t blocks = (p.n + per_block - 1) / per_block;
     if (blocks >= 8)

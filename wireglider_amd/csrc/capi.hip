@@ -52,6 +52,7 @@ static const Knob kKnobs[] = {
     {"l4_coop", &Tune::l4_coop, nullptr, 0, 1u << 20, nullptr, 0},
     {"l4_coop_waves", nullptr, &Tune::l4_coop_waves, 0, 0, kCoopW, WG_N(kCoopW)},
     {"aead_k", nullptr, &Tune::aead_k, 0, 0, kAeadK, WG_N(kAeadK)},
+    {"aead_stage", nullptr, &Tune::aead_stage, 0, 1, nullptr, 0},
     {"encap_parts", nullptr, &Tune::encap_parts, 0, 0, kParts, WG_N(kParts)},
 };
 #undef WG_N
@@ -154,6 +155,7 @@ static Tune &tune_storage() {
         // K = 2 in 16-lane groups 1.506 (profiles/r02_aead_flex_ab.json), the
         // interleave -8 % (profiles/r02_aead_pair_ab.json)
         x.aead_k = 0;
+        x.aead_stage = 1;
         x.encap_parts = 1;
         // environment overrides: WG_<KNOB> (upper case), same accepted values
         // as wg_tune_set; anything else is ignored

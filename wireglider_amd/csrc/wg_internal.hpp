@@ -31,6 +31,7 @@ struct Tune {
     uint64_t l4_coop;     // descriptor batches of n <= l4_coop: a block of l4_coop_waves waves per packet (0: never)
     uint32_t l4_coop_waves;  // waves per packet in that mode (2, 4, 8, 16)
     uint32_t aead_k;      // AEAD: consecutive ChaCha20 blocks per lane (0 = 2 or 3 per batch, 2, 3)
+    uint32_t aead_stage;  // AEAD encrypt: messages assembled in LDS, written out in whole lines (1)
     uint32_t encap_parts; // wg_encap_batch: slices split on a side stream under the previous slice's AEAD (1 = off)
     uint32_t gso_ablate;  // GSO A/B variants (1 non-temporal stores, 32 no XCD swizzle; both correct)
 };
