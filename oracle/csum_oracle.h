@@ -9,13 +9,17 @@
  * paths relative to the reference root) that it restates.  Pinning: the
  * byte-sum/fold arithmetic is pinned against golden vectors produced by
  * compiling the reference's own test oracle (tests/checksum_tests.hpp:11-48)
- * in place (see oracle/Makefile, tests/golden/).  checksum.cpp and
- * worker/offload.cpp need boost.endian and the un-vendored fastcsum library,
- * neither of which is in the image, so they are unbuildable here; the L4 and
- * GSO-split restatements are pinned by the reference tests' own assertions
- * (tests/test-checksum.cpp:53-82 verify-to-zero, tests/test-offload.cpp:21-171
- * segment geometry) and by an independent RFC 768/793 textbook
- * implementation in tests/.  See DESIGN.md §Oracle.
+ * in place (see oracle/Makefile, tests/golden/).  calc_l4_checksum is pinned
+ * against the reference's own checksum.cpp:8-36, compiled unchanged where it
+ * lies against this repository's drop-in header (its only dependency that is
+ * not in the image is the header's boost/fastcsum include; the drop-in header
+ * stands in its place as a caller's would) — tests/golden/l4/.
+ * worker/offload.cpp needs boost.endian and the un-vendored fastcsum library
+ * directly, so it is unbuildable here; the GSO-split restatement is pinned by
+ * the reference tests' own assertions (tests/test-offload.cpp:21-171 segment
+ * geometry, tests/test-checksum.cpp:53-82 verify-to-zero) and by an
+ * independent RFC 768/793 textbook implementation in tests/.  See DESIGN.md
+ * §3.
  */
 #ifndef WG_CSUM_ORACLE_H
 #define WG_CSUM_ORACLE_H

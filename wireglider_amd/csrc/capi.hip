@@ -155,6 +155,9 @@ static Tune &tune_storage() {
         // K = 2 in 16-lane groups 1.506 (profiles/r02_aead_flex_ab.json), the
         // interleave -8 % (profiles/r02_aead_pair_ab.json)
         x.aead_k = 0;
+        // encrypt: messages assembled in LDS, written in whole lines: writes
+        // 2.53 -> 1.61 GB per 1 M x 1500 B (= the message bytes), encrypt
+        // -1.0 %, encap -2.9 % (profiles/r04_aead_stage/)
         x.aead_stage = 1;
         x.encap_parts = 1;
         // environment overrides: WG_<KNOB> (upper case), same accepted values
