@@ -1171,6 +1171,11 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
     host, gpu_out, kind = sample_fn(npk)
     cores = oracle.host_cores()
     threads = cores["threads"]
+    # worker t on the t-th quietest CPU of the mask, one per physical core
+    # (oracle/orc_pin.h reads ORC_CPUS at the oracle's first threaded call)
+    quiet = oracle.quiet_cpus(threads) if os.environ.get("ORC_PIN", "1") != "0" else None
+    if quiet:
+        os.environ["ORC_CPUS"] = ",".join(map(str, quiet["cpus"]))
     one_scale = 1.0  # the 1-core leg runs on 1/one_scale of the sample
     extra = {}
     if kind[0] == "uniform":
@@ -1326,8 +1331,14 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
     parity = gpu_out is not None and bool(np.array_equal(exp, gpu_out))
     scale, unit = (1e-6, "Mflows/s") if kind[0] == "gro" else (2.0**-30, "GiB/s")
     run_all()  # first touch / warm-up, untimed
+    thr0 = oracle.cgroup_throttling()
     all_s = _spread(_rep_rates(run_all, nbytes, seconds, reps), scale)
+    thr1 = oracle.cgroup_throttling()
     one_s = _spread(_rep_rates(run_one, nbytes * one_scale, seconds / 2, reps), scale)
+    if thr0 and thr1:
+        # CPU-quota throttling while the all-core repetitions ran (a share of
+        # 16 CPUs leaves no room for a 17th busy thread)
+        all_s["cgroup_throttled"] = {k: thr1[k] - thr0[k] for k in thr0}
     try:
         cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except Exception:
@@ -1351,12 +1362,14 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
         "spread": all_s,
         "spread_1core": one_s,
         "cpu_model": cpu_model,
-        "host_cores": cores,
+        "host_cores": dict(cores, pinned_cpus=quiet["cpus"] if quiet else None,
+                           pinned_cpus_busy_before=quiet["busy"] if quiet else None),
         "sample": f"first {npk} units of the same batch, oracle/csum_oracle.c "
                   f"({what}; {nofold} for spans >= 256 B), {threads} pthreads "
                   f"(sched_getaffinity {cores['affinity']}, cgroup quota {cores['cgroup_quota_cpus']}); "
                   f"value = median of {reps - 1} repetitions of >= {seconds:.1f} s after a dropped first one, "
-                  f"1 core: the same of >= {seconds / 2:.1f} s; worker t pinned to CPU t of the affinity mask; "
+                  f"1 core: the same of >= {seconds / 2:.1f} s; worker t pinned to the t-th least busy CPU of the "
+                  f"affinity mask, one per physical core (host_cores.pinned_cpus); "
                   f"bit-exact vs GPU: {parity}",
         "parity_with_gpu": parity,
         **extra,

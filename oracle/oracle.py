@@ -140,6 +140,72 @@ def host_cores() -> dict:
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
+def _cpu_busy(cpus: list, interval: float = 0.3) -> dict:
+    """Busy fraction of each CPU in `cpus` over `interval` s (/proc/stat)."""
+    import time
+
+    def snap():
+        out = {}
+        for line in Path("/proc/stat").read_text().splitlines():
+            if line.startswith("cpu") and line[3:4].isdigit():
+                f = line.split()
+                v = [int(x) for x in f[1:9]]
+                out[int(f[0][3:])] = (sum(v), v[3] + v[4])  # total, idle + iowait
+        return out
+
+    a = snap()
+    time.sleep(interval)
+    b = snap()
+    res = {}
+    for c in cpus:
+        if c in a and c in b:
+            dt = b[c][0] - a[c][0]
+            res[c] = 1.0 - (b[c][1] - a[c][1]) / dt if dt > 0 else 1.0
+    return res
+
+
+def _core_of(c: int):
+    base = Path(f"/sys/devices/system/cpu/cpu{c}/topology")
+    try:
+        return (int((base / "physical_package_id").read_text()), int((base / "core_id").read_text()))
+    except Exception:
+        return (0, c)
+
+
+def quiet_cpus(n: int) -> dict:
+    """The n least busy CPUs of the affinity mask, one per physical core
+    while there are enough cores (a CPU share of a shared host: the workers
+    go where the neighbours are not).  Returns {"cpus": [...], "busy": mean
+    busy fraction of the chosen CPUs before the run}."""
+    cpus = sorted(os.sched_getaffinity(0))
+    busy = _cpu_busy(cpus)
+    order = sorted(cpus, key=lambda c: (busy.get(c, 1.0), c))
+    chosen, cores = [], set()
+    for c in order:
+        k = _core_of(c)
+        if k not in cores:
+            chosen.append(c)
+            cores.add(k)
+        if len(chosen) == n:
+            break
+    for c in order:  # fewer cores than n: fill with the quietest remaining CPUs
+        if len(chosen) == n:
+            break
+        if c not in chosen:
+            chosen.append(c)
+    return {"cpus": chosen, "busy": round(sum(busy.get(c, 1.0) for c in chosen) / max(1, len(chosen)), 4)}
+
+
+def cgroup_throttling() -> dict | None:
+    """cgroup v2 cpu.stat throttling counters (nr_throttled, throttled_usec),
+    or None when not visible."""
+    try:
+        kv = dict(line.split() for line in Path("/sys/fs/cgroup/cpu.stat").read_text().splitlines())
+        return {"nr_throttled": int(kv.get("nr_throttled", 0)), "throttled_usec": int(kv.get("throttled_usec", 0))}
+    except Exception:
+        return None
+
+
 def default_threads() -> int:
     return host_cores()["threads"]
 

@@ -1,12 +1,13 @@
 /*
  * orc_pin.h — TEST INFRASTRUCTURE ONLY (bench.py's cpu_baseline leg).
  *
- * Worker thread t of a timed CPU run is pinned to the t-th CPU of the
- * process's affinity mask, so a 16-thread run on a 16-CPU share of a large
- * host keeps one worker per CPU instead of migrating between them (VERDICT
- * r03: the CPU baseline moved 15-25 % between repetitions).  ORC_PIN=0 in the
- * environment turns it off.  Must be included before any system header that
- * reads _GNU_SOURCE.
+ * Worker thread t of a timed CPU run is pinned to the t-th CPU of
+ * ORC_CPUS (a comma-separated list: bench.py passes the least busy CPUs of
+ * the mask, one per physical core) or else of the process's affinity mask,
+ * so a 16-thread run on a 16-CPU share of a large host keeps one worker per
+ * CPU instead of migrating between them (the CPU baseline moved
+ * 15-25 % between repetitions).  ORC_PIN=0 in the environment turns it off.
+ * Must be included before any system header that reads _GNU_SOURCE.
  */
 #ifndef WG_ORC_PIN_H
 #define WG_ORC_PIN_H
@@ -27,6 +28,20 @@ static void orc_pin_init(void) {
     orc_pin_n = 0;
     if (e && e[0] == '0')
         return;
+    const char *l = getenv("ORC_CPUS");
+    if (l && *l) {
+        while (*l && orc_pin_n < 1024) {
+            char *end = NULL;
+            const long c = strtol(l, &end, 10);
+            if (end == l)
+                break;
+            if (c >= 0 && c < CPU_SETSIZE)
+                orc_pin_cpus[orc_pin_n++] = (int)c;
+            l = *end == ',' ? end + 1 : end;
+        }
+        if (orc_pin_n > 0)
+            return;
+    }
     cpu_set_t set;
     CPU_ZERO(&set);
     if (sched_getaffinity(0, sizeof set, &set) != 0)
