@@ -127,8 +127,12 @@ def aead_kernel_symbol(wga, maxpay: int, dec: bool = False, ver: bool = False, g
         K = 3 if 2 * w3 > 3 * w2 else 2
     lanes = (nblk + 1 + K - 1) // K
     G = 1 if lanes <= 1 else (0 if lanes <= 32 else 64)
+    # encrypt with exact-size groups: messages staged in LDS when a block's
+    # slots fit kStageMaxBlockLds (aead.hip launch_gk)
+    lds_block = 4 * (64 // lanes) * (32 + ((maxpay + 15) & ~15)) if G == 0 else 0
+    stage = not dec and G == 0 and wga.tune_get("aead_stage") == 1 and lds_block <= 53248
     b = lambda v: "true" if v else "false"
-    return f"void wg::aead_kernel<{G}, {K}, {b(dec)}, {b(ver)}, {gso}>(wg::AeadParams)"
+    return f"void wg::aead_kernel<{G}, {K}, {b(dec)}, {b(ver)}, {gso}, {b(stage)}>(wg::AeadParams)"
 
 
 def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workload:
