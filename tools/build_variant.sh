@@ -11,7 +11,9 @@ for f in "$@"; do git -C "$ROOT" show "$REV:wireglider_amd/csrc/$f" > "$SRC/$f";
 objs=()
 for s in "$SRC"/*.hip "$SRC"/*.cpp; do
   o=$SRC/$(basename "$s").o
-  /opt/rocm/bin/hipcc -O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wno-unused-function ${EXTRA_FLAGS:-} -I"$ROOT/include" -I"$SRC" \
+  FF=""
+  [ "$(basename "$s")" = aead.hip ] && FF="-mllvm -amdgpu-sched-strategy=max-ilp"  # wireglider_amd/_build.py FILE_FLAGS
+  /opt/rocm/bin/hipcc -O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wno-unused-function ${EXTRA_FLAGS:-} $FF -I"$ROOT/include" -I"$SRC" \
     -x hip -c "$s" -o "$o" &
   objs+=("$o")
 done

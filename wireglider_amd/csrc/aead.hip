@@ -33,9 +33,6 @@
 #include "wg_internal.hpp"
 #include "wireglider_amd.h"
 
-#ifndef WG_P32_CARRY_LAST
-#define WG_P32_CARRY_LAST 0  // A/B builds: -DWG_P32_CARRY_LAST=1
-#endif
 
 namespace wg {
 
@@ -316,17 +313,6 @@ __device__ __forceinline__ P32 p32_step(const P32 &x, uint32_t m0, uint32_t m1, 
     const uint32_t t2 = __builtin_addc(x.h[2], m2, c, &c);
     const uint32_t t3 = __builtin_addc(x.h[3], m3, c, &c);
     const uint32_t t4 = x.h[4] + 1u + c;  // + 2^128: the block's pad bit
-#if WG_P32_CARRY_LAST
-    // the four columns as independent multiply-add chains, the carries
-    // propagated after them (a shorter dependency path, three more adds)
-    const uint64_t d0 = mad64(t3, sr[1], mad64(t2, sr[2], mad64(t1, sr[3], (uint64_t)t0 * r[0])));
-    const uint64_t e1 = mad64(t4, sr[1], mad64(t3, sr[2], mad64(t2, sr[3], mad64(t1, r[0], (uint64_t)t0 * r[1]))));
-    const uint64_t e2 = mad64(t4, sr[2], mad64(t3, sr[3], mad64(t2, r[0], mad64(t1, r[1], (uint64_t)t0 * r[2]))));
-    const uint64_t e3 = mad64(t4, sr[3], mad64(t3, r[0], mad64(t2, r[1], mad64(t1, r[2], (uint64_t)t0 * r[3]))));
-    const uint64_t d1 = e1 + (d0 >> 32);
-    const uint64_t d2 = e2 + (d1 >> 32);
-    const uint64_t d3 = e3 + (d2 >> 32);
-#else
     const uint64_t d0 = mad64(t3, sr[1], mad64(t2, sr[2], mad64(t1, sr[3], (uint64_t)t0 * r[0])));
     const uint64_t d1 =
         mad64(t4, sr[1], mad64(t3, sr[2], mad64(t2, sr[3], mad64(t1, r[0], mad64(t0, r[1], d0 >> 32)))));
@@ -334,7 +320,6 @@ __device__ __forceinline__ P32 p32_step(const P32 &x, uint32_t m0, uint32_t m1, 
         mad64(t4, sr[2], mad64(t3, sr[3], mad64(t2, r[0], mad64(t1, r[1], mad64(t0, r[2], d1 >> 32)))));
     const uint64_t d3 =
         mad64(t4, sr[3], mad64(t3, r[0], mad64(t2, r[1], mad64(t1, r[2], mad64(t0, r[3], d2 >> 32)))));
-#endif
     const uint32_t h4 = t4 * r[0] + (uint32_t)(d3 >> 32);
     const uint32_t cc = (h4 >> 2) + (h4 & ~3u);  // 5 * (h4 >> 2): 2^130 == 5
     P32 o;
@@ -679,9 +664,6 @@ constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/prot
 // are (the headers-only split writes exactly those bytes), every later
 // block from the input itself, where plaintext byte q >= hdr_len of segment
 // s is input byte s * gso + q — one source per block, no merge.
-#ifndef WG_AEAD_MIN_WAVES
-#define WG_AEAD_MIN_WAVES 1  // waves per SIMD the register allocation must allow (A/B builds: -D)
-#endif
 // kStage (encrypt, groups of exactly the lanes needed): every message is
 // assembled in the wave's LDS slot (header, ciphertext blocks, tag) and then
 // written out slot by slot with consecutive lanes on consecutive 16-B chunks,
@@ -690,7 +672,7 @@ constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/prot
 // into the message) that are completed at different times, and the memory
 // wrote ~1.48x the message bytes (profiles/pmc_aead.json).
 template <int G, int K, bool kDec, bool kVer = false, int kGso = 0, bool kStage = false>
-__global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams p) {
+__global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     static_assert(!kStage || (!kDec && G == 0), "staged messages: encrypt, exact-size groups");
     extern __shared__ v4u aead_lds[];
     constexpr bool kFlex = G == 0;
@@ -795,15 +777,13 @@ __global__ __launch_bounds__(256, WG_AEAD_MIN_WAVES) void aead_kernel(AeadParams
     // gain; encrypt -6.5 %, encap -4 %, profiles/r03_aead_tri_ab.json)
     constexpr bool kTri = K == 3 && G < 64;
     uint32_t ks[16], ks1[16], ks2[kTri ? 16 : 1];
-    {
-        const ChaPre pc = chacha_pre(p.key, n0, n1, n2);
-        if constexpr (kPair)
-            chacha20_block2_pre(p.key, g * (uint32_t)K, n0, n1, n2, pc, ks, ks1);
-        else
-            chacha20_block_pre(p.key, g * (uint32_t)K, n0, n1, n2, pc, ks);
-        if constexpr (kTri)
-            chacha20_block_pre(p.key, g * (uint32_t)K + 2u, n0, n1, n2, pc, ks2);
-    }
+    const ChaPre pc = chacha_pre(p.key, n0, n1, n2);
+    if constexpr (kPair)
+        chacha20_block2_pre(p.key, g * (uint32_t)K, n0, n1, n2, pc, ks, ks1);
+    else
+        chacha20_block_pre(p.key, g * (uint32_t)K, n0, n1, n2, pc, ks);
+    if constexpr (kTri)
+        chacha20_block_pre(p.key, g * (uint32_t)K + 2u, n0, n1, n2, pc, ks2);
     const uint32_t base_lane = kFlex ? slot * GG : lane & ~(uint32_t)(G - 1);
     uint32_t rw[4], sw[4];
 #pragma unroll
