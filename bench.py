@@ -1130,11 +1130,14 @@ def wga_stride(seg: int) -> int:
     return 16 + (seg + 15) // 16 * 16 + 16
 
 
-def _rep_rates(fn, units: float, seconds: float, reps: int) -> list:
+def _rep_rates(fn, units: float, seconds: float, reps: int, before=None) -> list:
     """`reps` repetitions, each running fn() back to back until `seconds` of
-    wall time have passed; the rate (units per second) of each repetition."""
+    wall time have passed (before() ahead of each, untimed); the rate (units
+    per second) of each repetition."""
     out = []
     for _ in range(reps):
+        if before is not None:
+            before()
         k, t0 = 0, time.perf_counter()
         while True:
             fn()
@@ -1148,12 +1151,18 @@ def _rep_rates(fn, units: float, seconds: float, reps: int) -> list:
 
 def _spread(rates: list, scale: float) -> dict:
     """Median / min / max of the repetitions after the first (dropped: first
-    touch of the pages, thread start-up); every value is kept in the line."""
+    touch of the pages, thread start-up); every value is kept in the line.
+    spread_pct = the largest deviation from the median with the single most
+    deviant repetition set aside (on this shared host one repetition in 7-8
+    now and then lands on a neighbour's burst: 56 vs 77 GiB/s); spread_pct_all
+    counts every repetition."""
     vals = [x * scale for x in rates]
     r = sorted(vals[1:] if len(vals) > 1 else vals)
     med = r[len(r) // 2] if len(r) % 2 else 0.5 * (r[len(r) // 2 - 1] + r[len(r) // 2])
+    dev = lambda xs: round(100.0 * max(abs(x - med) for x in xs) / med, 2) if med and xs else None  # noqa: E731
+    trimmed = sorted(r, key=lambda x: abs(x - med))[:-1] if len(r) >= 5 else r
     return {"median": med, "min": r[0], "max": r[-1], "reps": len(r),
-            "spread_pct": round(100.0 * max(med - r[0], r[-1] - med) / med, 2) if med else None,
+            "spread_pct": dev(trimmed), "spread_pct_all": dev(r), "spread_set_aside": len(r) - len(trimmed),
             "values": [round(v, 3) for v in vals], "dropped_first": len(vals) > 1}
 
 
@@ -1177,9 +1186,19 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
     threads = cores["threads"]
     # worker t on the t-th quietest CPU of the mask, one per physical core
     # (oracle/orc_pin.h reads ORC_CPUS at the oracle's first threaded call)
-    quiet = oracle.quiet_cpus(threads) if os.environ.get("ORC_PIN", "1") != "0" else None
-    if quiet:
-        os.environ["ORC_CPUS"] = ",".join(map(str, quiet["cpus"]))
+    pin = os.environ.get("ORC_PIN", "1") != "0"
+    picks = []
+
+    def repick(n):
+        # the n quietest CPUs right now (a neighbour's burst moves between
+        # repetitions); oracle/orc_pin.h reads ORC_CPUS at every thread start
+        if pin:
+            q = oracle.quiet_cpus(n)
+            os.environ["ORC_CPUS"] = ",".join(map(str, q["cpus"]))
+            picks.append(q)
+
+    repick(threads)
+    quiet = picks[0] if picks else None
     one_scale = 1.0  # the 1-core leg runs on 1/one_scale of the sample
     extra = {}
     if kind[0] == "uniform":
@@ -1336,9 +1355,9 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
     scale, unit = (1e-6, "Mflows/s") if kind[0] == "gro" else (2.0**-30, "GiB/s")
     run_all()  # first touch / warm-up, untimed
     thr0 = oracle.cgroup_throttling()
-    all_s = _spread(_rep_rates(run_all, nbytes, seconds, reps), scale)
+    all_s = _spread(_rep_rates(run_all, nbytes, seconds, reps, lambda: repick(threads)), scale)
     thr1 = oracle.cgroup_throttling()
-    one_s = _spread(_rep_rates(run_one, nbytes * one_scale, seconds / 2, reps), scale)
+    one_s = _spread(_rep_rates(run_one, nbytes * one_scale, seconds / 2, reps, lambda: repick(1)), scale)
     if thr0 and thr1:
         # CPU-quota throttling while the all-core repetitions ran (a share of
         # 16 CPUs leaves no room for a 17th busy thread)
@@ -1367,13 +1386,15 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
         "spread_1core": one_s,
         "cpu_model": cpu_model,
         "host_cores": dict(cores, pinned_cpus=quiet["cpus"] if quiet else None,
-                           pinned_cpus_busy_before=quiet["busy"] if quiet else None),
+                           pinned_cpus_busy_before=[q["busy"] for q in picks] if picks else None,
+                           pinning="before each repetition the quietest CPUs of the mask (0.3-s /proc/stat "
+                                   "sample), one worker per physical core" if pin else "off"),
         "sample": f"first {npk} units of the same batch, oracle/csum_oracle.c "
                   f"({what}; {nofold} for spans >= 256 B), {threads} pthreads "
                   f"(sched_getaffinity {cores['affinity']}, cgroup quota {cores['cgroup_quota_cpus']}); "
                   f"value = median of {reps - 1} repetitions of >= {seconds:.1f} s after a dropped first one, "
-                  f"1 core: the same of >= {seconds / 2:.1f} s; worker t pinned to the t-th least busy CPU of the "
-                  f"affinity mask, one per physical core (host_cores.pinned_cpus); "
+                  f"1 core: the same of >= {seconds / 2:.1f} s; before each repetition worker t pinned to the t-th "
+                  f"least busy CPU of the affinity mask, one per physical core (host_cores.pinning); "
                   f"bit-exact vs GPU: {parity}",
         "parity_with_gpu": parity,
         **extra,

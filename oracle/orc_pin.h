@@ -19,46 +19,49 @@
 #include <sched.h>
 #include <stdlib.h>
 
-static int orc_pin_cpus[1024];
-static int orc_pin_n = -1;
-static pthread_once_t orc_pin_once = PTHREAD_ONCE_INIT;
-
-static void orc_pin_init(void) {
+/* The idx-th CPU of ORC_CPUS (read at every call: bench.py re-picks the
+ * quietest CPUs before each timed repetition), else of the affinity mask;
+ * -1 when pinning is off or nothing is known. */
+static int orc_pin_cpu(int idx) {
     const char *e = getenv("ORC_PIN");
-    orc_pin_n = 0;
     if (e && e[0] == '0')
-        return;
+        return -1;
     const char *l = getenv("ORC_CPUS");
     if (l && *l) {
-        while (*l && orc_pin_n < 1024) {
+        int list[1024], n = 0;
+        while (*l && n < 1024) {
             char *end = NULL;
             const long c = strtol(l, &end, 10);
             if (end == l)
                 break;
             if (c >= 0 && c < CPU_SETSIZE)
-                orc_pin_cpus[orc_pin_n++] = (int)c;
+                list[n++] = (int)c;
             l = *end == ',' ? end + 1 : end;
         }
-        if (orc_pin_n > 0)
-            return;
+        if (n > 0)
+            return list[idx % n];
     }
     cpu_set_t set;
     CPU_ZERO(&set);
     if (sched_getaffinity(0, sizeof set, &set) != 0)
-        return;
-    for (int c = 0; c < CPU_SETSIZE && orc_pin_n < 1024; c++)
-        if (CPU_ISSET(c, &set))
-            orc_pin_cpus[orc_pin_n++] = c;
+        return -1;
+    const int n = CPU_COUNT(&set);
+    if (n <= 0)
+        return -1;
+    for (int c = 0, k = 0; c < CPU_SETSIZE; c++)
+        if (CPU_ISSET(c, &set) && k++ == idx % n)
+            return c;
+    return -1;
 }
 
-/* Pin thread `t` (worker index idx) to one CPU of the affinity mask. */
+/* Pin thread `t` (worker index idx) to one CPU. */
 static inline void orc_pin_thread(pthread_t t, int idx) {
-    pthread_once(&orc_pin_once, orc_pin_init);
-    if (orc_pin_n <= 0)
+    const int c = orc_pin_cpu(idx);
+    if (c < 0)
         return;
     cpu_set_t one;
     CPU_ZERO(&one);
-    CPU_SET(orc_pin_cpus[idx % orc_pin_n], &one);
+    CPU_SET(c, &one);
     (void)pthread_setaffinity_np(t, sizeof one, &one);
 }
 
