@@ -11,7 +11,11 @@ the segment / size / capacity bounds (no messages).
 fused=True runs the same step through wg_encap_batch (the headers-only split
 + the AEAD reading payload from the input): its messages, counters, result
 records, GSO results and input prefix zeroing must equal the two-call path's,
-and the segment headers it leaves in `out` the split's."""
+and the segment headers it leaves in `out` the split's.  With encap_synth=1
+the AEAD builds the headers (fields, IPv4 and L4 checksums) of the
+super-buffers it encrypts whose header fits one 64-B block, and the split
+skips those: the same comparisons pin every synthesized header byte and the
+messages encrypted over it."""
 import numpy as np
 import pytest
 
@@ -31,7 +35,9 @@ def _wga():
 @pytest.mark.parametrize("seed", [11, 12])
 @pytest.mark.parametrize("knobs", [{}, {"aead_k": 2}, {"aead_k": 3}, {"aead_stage": 0}, {"encap_parts": 2},
                                    {"encap_parts": 3}, {"encap_parts": 8}, {"encap_spw": 4}, {"encap_spw": 0},
-                                   {"aead_k": 2, "encap_parts": 2}],
+                                   {"aead_k": 2, "encap_parts": 2}, {"encap_synth": 1},
+                                   {"encap_synth": 1, "aead_k": 2}, {"encap_synth": 1, "encap_parts": 3},
+                                   {"encap_synth": 1, "aead_stage": 0}],
                          ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()) or "default")
 def test_encap_matches_oracle(gpu, seed, knobs, fused):
     import torch
@@ -66,6 +72,10 @@ def test_encap_matches_oracle(gpu, seed, knobs, fused):
     d_in_f = d_in.clone()  # the fused call's own copy (the split zeroes prefix fields in place)
     d_res = wga.gso_split(d_in, d_desc, d_out)
     max_seg, max_size, cap = 48, 9100, 48 * (32 + 9104)
+    if knobs.get("encap_synth"):
+        # header synthesis runs with the staged AEAD (segments up to ~6 KB):
+        # super-buffers of larger segments get no messages and keep the split
+        max_size = 1600
     cap_small = 7000  # some super-buffers' messages will not fit: nmsg 0
     msg_off = np.arange(n, dtype=np.int64) * cap
     msgs = torch.full((n * cap + 64,), 0xEE, dtype=torch.uint8, device=gpu)
@@ -126,14 +136,16 @@ def test_encap_matches_oracle(gpu, seed, knobs, fused):
     assert int(total.cpu()[0]) == n_msgs and n_msgs > 50
 
 
-@pytest.mark.parametrize("fused", [False, True], ids=["split+encrypt", "encap_batch"])
-def test_encap_reject_after_messages(gpu, fused):
+@pytest.mark.parametrize("fused,synth", [(False, 0), (True, 0), (True, 1)],
+                         ids=["split+encrypt", "encap_batch", "encap_batch-synth"])
+def test_encap_reject_after_messages(gpu, fused, synth):
     """Counters crossing RejectAfterMessages inside a super-buffer: the
     reference's encrypt refuses every counter >= it (proto.cpp:560-562) but
     still advances encrypt_nonce, and the encap worker advances its outbuf
     over accepted messages only (worker/encap.cpp:138-140): super-buffer 0 is
     all accepted, super-buffer 1 keeps its first 2 messages, super-buffer 2
-    none; nmsg / counter0 / the total count every segment."""
+    none; nmsg / counter0 / the total count every segment.  Refused segments
+    still get their headers (synth: built and checksummed by the AEAD)."""
     import torch
 
     import pktbuild
@@ -161,8 +173,20 @@ def test_encap_reject_after_messages(gpu, fused):
     msgs = torch.full((n * cap,), 0xEE, dtype=torch.uint8, device=gpu)
     d_res = wga.gso_split(d_in.clone(), d_desc, d_out)
     if fused:
-        eres, total = wga.encap_batch(d_in.clone(), d_desc, torch.zeros_like(d_out), torch.zeros_like(d_res), key, 7,
-                                      c0, msg_off, cap, 8, 200, msgs)
+        saved = wga.tune_get("encap_synth")
+        wga.tune_set("encap_synth", synth)
+        d_hdr = torch.zeros_like(d_out)
+        try:
+            eres, total = wga.encap_batch(d_in.clone(), d_desc, d_hdr, torch.zeros_like(d_res), key, 7, c0, msg_off,
+                                          cap, 8, 200, msgs)
+            torch.cuda.synchronize()
+        finally:
+            wga.tune_set("encap_synth", saved)
+        g_hdr, g_seg = d_hdr.cpu().numpy(), d_out.cpu().numpy()
+        for i in range(n):
+            for so in range(0, 5 * 140, 140):
+                o = i * cap + so
+                np.testing.assert_array_equal(g_hdr[o:o + 40], g_seg[o:o + 40], err_msg=f"{i} {so}")
     else:
         eres, total = wga.encap_encrypt(d_in, d_out, d_desc, d_res, key, 7, c0, msg_off, cap, 8, 200, msgs)
     torch.cuda.synchronize()

@@ -579,6 +579,7 @@ struct AeadParams {
                                  // (the host path's chained chunks)
     uint32_t lstride;            // kStage: bytes per message slot in LDS (32 + pad16(seg))
     uint32_t lds_wave;           // kStage: LDS bytes per wave (packets per wave x lstride)
+    uint32_t synth;              // kGso == 2: eligible segments' headers built here (kSyn; encap_synth)
 };
 
 // The decap verify gates (wg_verify_desc, SURVEY §8 f1: evaluate_packet,
@@ -636,6 +637,84 @@ __device__ __forceinline__ HdrGate hdr_gate(const uint32_t R[16], uint32_t len) 
 
 constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/proto/proto.hpp:36
 
+// ---------------------------------------------------------------------------
+// Encap header synthesis (wg_encap_batch, knob encap_synth).  A split
+// segment's first 64 bytes are built in the lane that encrypts them, from the
+// tun super-buffer itself: its prefix (ip_sum and the L4 checksum field zeroed
+// by the split's finalize pass, worker/offload.cpp:145-149) with the
+// segment's fields (:168-199), then the payload.  The L4 checksum needs the
+// whole segment's words, which the group's lanes sum as they encrypt their
+// blocks; block 0 is encrypted with the field as it stands before the
+// checksum is written, and at the end its two ciphertext bytes and the MAC
+// are corrected (Poly1305 is linear in each 16-B block).  So the split pass
+// only plans and finalizes these super-buffers: no per-segment wave, no
+// payload read besides the encryption's own.  Eligible: hdr_len <= 64,
+// csum_start a multiple of 4, the checksum field 2-B aligned (every IPv4 /
+// IPv6 TCP or UDP header); other super-buffers keep the split's segments.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+struct SynSeg {
+    uintptr_t tpl;  // the super-buffer (its prefix is every segment's header template)
+    uint32_t cs, l4off, hdr, gso, idx;
+    bool tcp, v6, last;
+};
+
+// Segment q's plaintext [0, 64) — the header with every field but the L4
+// checksum, which holds pv (the bytes there before it is written), then the
+// payload — built and stored at hdst (the segment slot, where the
+// headers-only split would have written it; the encryption reads it back
+// from there like any split header).  rest: the L4 sum's terms other than
+// the segment's own words from its block 0 on — pseudo-header addresses,
+// protocol, L4 length, and 32 * 0xFFFF minus block 0's words below
+// csum_start (the lanes sum whole blocks; subtracting x mod 0xFFFF is adding
+// 0xFFFF - x).  Every dword by its static index (a run-time index puts the
+// array in scratch).
+__device__ __forceinline__ void syn_block0(const SynSeg &q, uintptr_t psrc, uintptr_t hdst, uint32_t pktlen,
+                                           uint32_t &rest, uint32_t &pv) {
+    const uint32_t nin = pktlen < 64u ? pktlen : 64u;
+    uint32_t T[16], M[16];
+    load64(q.tpl, q.hdr, T);  // the template, zero past the header (split super-buffers hold >= hdr bytes)
+    load64(psrc, nin, M);     // payload byte j of the segment at psrc + j (j >= hdr)
+    const uint32_t cw = q.cs >> 2, fw = q.l4off >> 2;
+    const uint32_t l4len = bswap16((pktlen - q.cs) & 0xffffu);
+    uint32_t ips = 0, ps = 0, p = 0;
+#pragma unroll
+    for (uint32_t m = 0; m < 16; m++) {
+        const uint32_t k = q.hdr > 4u * m ? (q.hdr - 4u * m < 4u ? q.hdr - 4u * m : 4u) : 0u;  // template bytes
+        const uint32_t mk = k >= 4u ? ~0u : (1u << (8u * k)) - 1u;
+        uint32_t w = T[m] | (M[m] & ~mk);
+        if (m == 0u && !q.v6)
+            w = (w & 0xffffu) | (bswap16(pktlen & 0xffffu) << 16);  // ip_len (offload.cpp:183)
+        if (m == 1u) {
+            if (!q.v6)
+                w = (w & 0xffff0000u) | bswap16((bswap16(w & 0xffffu) + q.idx) & 0xffffu);  // ip_id (:178-182)
+            else
+                w = (w & 0xffff0000u) | l4len;  // ip6_plen (:170-172)
+        }
+        if (m >= 5u) {  // the L4 header starts at dword cw >= 5
+            if (q.tcp && m == cw + 1u)
+                w = bswap32(bswap32(w) + q.gso * q.idx);  // seq (:192), seq0 read after the :149 zeroing
+            if (q.tcp && m == cw + 3u && !q.last)
+                w &= ~0x0900u;  // FIN / PSH on the last segment only (:193-195)
+            if (!q.tcp && m == cw + 1u)
+                w = (w & 0xffff0000u) | l4len;  // udp len (:199)
+        }
+        M[m] = w;
+        const uint32_t h = hsum32(w);
+        ips += m < cw ? h : 0u;                                                // [0, cs), ip_sum zero
+        ps += (q.v6 ? (m >= 2u && m < 10u) : (m == 3u || m == 4u)) ? h : 0u;  // addresses
+        p = m == fw ? w : p;
+    }
+    const uint32_t ipcs = ~fold16_32(ips) & 0xffffu;
+    if (!q.v6)
+        M[2] = (M[2] & 0xffffu) | (ipcs << 16);  // ip_sum, native order (:184-186); the template's was zeroed (:147)
+    store_n(hdst, M, nin);
+    pv = (p >> (8u * (q.l4off & 2u))) & 0xffffu;
+    const uint32_t hw = ips + (q.v6 ? 0u : ipcs);  // block 0's words below csum_start, as stored
+    rest = ps + ((q.tcp ? 6u : 17u) << 8) + l4len + (32u * 0xffffu - hw);
+}
+
 // kDec = false: encrypt packet i (bytes [i*seg, +len) of `in`) into the data
 // message at out + i*stride, stride = 16 + pad16(seg) + 16.
 // kDec = true: decrypt message i (bytes [i*seg, +len) of `in`) into
@@ -671,9 +750,11 @@ constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/prot
 // lanes, a block's 64 B straddle two 64-B sectors (the ciphertext starts 16 B
 // into the message) that are completed at different times, and the memory
 // wrote ~1.48x the message bytes (profiles/pmc_aead.json).
-template <int G, int K, bool kDec, bool kVer = false, int kGso = 0, bool kStage = false>
+template <int G, int K, bool kDec, bool kVer = false, int kGso = 0, bool kStage = false, bool kSyn = false>
 __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     static_assert(!kStage || (!kDec && G == 0), "staged messages: encrypt, exact-size groups");
+    static_assert(!kSyn || (kStage && kGso == 2 && K >= 2), "header synthesis: wg_encap_batch with staged messages, "
+                                                             "block 0 in group lane 0");
     extern __shared__ v4u aead_lds[];
     constexpr bool kFlex = G == 0;
     const uint32_t GG = kFlex ? p.grp : (uint32_t)G;  // lanes per packet
@@ -699,6 +780,10 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     // plaintext (blocks at or past hl for kGso == 2): a partial last block
     // whose 64-B window ends inside it is loaded whole and masked
     uintptr_t send = 0;
+    // kSyn: this segment's header is built here (syn_block0) when eligible
+    bool syn = false;
+    uint32_t syn_l4 = 0;  // the checksum field's offset
+    uint32_t syn_rp = 0;  // the rest of the L4 sum folded to 16 bits | the field's bytes before << 16
     if constexpr (kGso) {
         sb = ii / p.gm;
         gs = (uint32_t)(ii - sb * p.gm);
@@ -715,6 +800,28 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             gsrc = reinterpret_cast<uintptr_t>(p.gin) + gd.in_offset +
                    (gr.passthrough ? so : (uint64_t)gs * (S - gr.hdr_len));
             send = reinterpret_cast<uintptr_t>(p.gin) + gd.in_offset + gd.in_len;
+            if constexpr (kSyn) {
+                // in group lane 0, before the keystream (few registers live
+                // here); the lane reads block 0 back from the slot later
+                const uint32_t cs = gd.vnet.csum_start, l4 = cs + gd.vnet.csum_offset;
+                syn = live && !gr.passthrough && syn_eligible(gr.hdr_len, cs, l4);
+                syn_l4 = l4;
+                if (syn && g == 0u) {
+                    SynSeg sq;
+                    sq.tpl = reinterpret_cast<uintptr_t>(p.gin) + gd.in_offset;
+                    sq.cs = cs;
+                    sq.l4off = l4;
+                    sq.hdr = gr.hdr_len;
+                    sq.gso = S - gr.hdr_len;
+                    sq.idx = gs;
+                    sq.tcp = gd.vnet.gso_type == 1u || gd.vnet.gso_type == 4u;  // unmasked (:151): TCP|ECN is fixed up as UDP
+                    sq.v6 = gr.isv6;
+                    sq.last = gs + 1u == er.nmsg;
+                    uint32_t rest, pv;
+                    syn_block0(sq, gsrc, hsrc, len, rest, pv);
+                    syn_rp = fold16_32(rest) | (pv << 16);
+                }
+            }
         } else {
             gsrc = (gr.passthrough ? reinterpret_cast<uintptr_t>(p.gin) + gd.in_offset
                                    : reinterpret_cast<uintptr_t>(p.in) + gd.out_offset) + so;
@@ -807,6 +914,7 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     L5 F = l5_one();
     L5 acc = l5_zero();
     uint32_t vsum = 0;                          // kVer: this lane's plaintext word sum
+    uint32_t psum = 0;  // kSyn: the segment's words from block 0 on (this lane's blocks)
     HdrGate gate{0u, 0u, 20u, 0u, 0u, false};   // kVer: set in the lane holding payload block 0
     for (uint32_t pp = passes; pp-- > 0;) {
         const uint32_t cf = pp * kPass + g * (uint32_t)K;  // this lane's first counter
@@ -913,6 +1021,10 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                     for (int m = 0; m < 16; m++)
                         W[m] = keep_below(W[m], (uint32_t)m, nin);  // padding plaintext is zero (proto.cpp:568-572)
                 }
+                if constexpr (kSyn) {
+#pragma unroll
+                    for (int m = 0; m < 16; m++) psum += hsum32(W[m]);  // the segment's L4 words
+                }
 #pragma unroll
                 for (int m = 0; m < 16; m++) {
                     if constexpr (!kDec)
@@ -953,6 +1065,10 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             } else if (has) {
                 // zero past the payload
                 load64(bsrc, nin, W);
+                if constexpr (kSyn) {
+#pragma unroll
+                    for (int m = 0; m < 16; m++) psum += hsum32(W[m]);  // the segment's L4 words
+                }
                 const uint32_t nqc = nct / 16u;  // whole 16-B Poly1305 chunks in the block (nct is a multiple of 16)
 #pragma unroll
                 for (int m = 0; m < 16; m++) {
@@ -1034,6 +1150,69 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
         // once to the group's sum
         if (nq)
             acc = l5_add(acc, l5_mul(p32_to_l5(x), EF));
+        if constexpr (kSyn) {
+            // a refused message (counter exhausted) encrypts nothing, but
+            // its segment's header still needs the checksum: its lanes sum
+            // their blocks' plaintext here (wave-uniform test, rare)
+            if (__ballot(syn && !act) != 0ull && syn && !act) {
+                for (uint32_t j = 0; j < (uint32_t)K; j++) {
+                    const uint32_t c = g * (uint32_t)K + j, d = c - 1u;
+                    if (c >= 1u && d < nblk) {
+                        const uint32_t boff = 64u * d;
+                        uint32_t W[16];
+                        load64((boff < hl ? hsrc : src) + boff, plen - boff < 64u ? plen - boff : 64u, W);
+#pragma unroll
+                        for (int m = 0; m < 16; m++) psum += hsum32(W[m]);
+                    }
+                }
+            }
+            // the segment's L4 word total into group lane 0 (down-shift tree)
+            uint32_t L = psum;
+            for (uint32_t o = 1; o < GG; o <<= 1) {  // wave-uniform trip count
+                const uint32_t t = grp_down_rt(L, lane, g, GG, o);
+                if (g + o < GG)
+                    L += t;
+            }
+            if (syn && g == 0u) {
+                const uint32_t l4cs = ~fold16_32(fold16_32(L) + (syn_rp & 0xffffu)) & 0xffffu;  // stored native (offload.cpp:202-204)
+                // block 0 was encrypted with syn_pv at the field: its two
+                // ciphertext bytes in the staged message, then the MAC
+                uint16_t *lb = reinterpret_cast<uint16_t *>(aead_lds);
+                const uint32_t hw = (lslot * 16u + 16u + syn_l4) >> 1;
+                const uint32_t oc = lb[hw];
+                const uint32_t nc = (oc ^ (syn_rp >> 16) ^ l4cs) & 0xffffu;
+                lb[hw] = (uint16_t)nc;
+                st8b(hsrc + syn_l4, l4cs);  // and the segment's header in the slot
+                st8b(hsrc + syn_l4 + 1u, l4cs >> 8);
+                // its 16-B block (the lane's chunk l4off / 16) changes by
+                // (nc - oc) * 256^(l4off % 16): add that times its weight mod p
+                const uint32_t pb = syn_l4 & 15u;
+                const bool up = nc >= oc;
+                const uint32_t dv = (up ? nc - oc : oc - nc) << (8u * (pb & 3u));
+                const uint32_t wq = pb >> 2;
+                L5 dl = l5_from_words(wq == 0u ? dv : 0u, wq == 1u ? dv : 0u, wq == 2u ? dv : 0u, wq == 3u ? dv : 0u, 0u);
+                if (!up) {  // -x == 2p - x (mod p); every limb of 2p exceeds x's
+                    const uint32_t tp[5] = {0x7fffff6u, 0x7fffffeu, 0x7fffffeu, 0x7fffffeu, 0x7fffffeu};
+#pragma unroll
+                    for (int k = 0; k < 5; k++) dl.v[k] = tp[k] - dl.v[k];
+                }
+                // weight: r^(nq - k) in this lane's Horner sum (chunk k =
+                // l4off / 16 of block 0, which opens group lane 0's blocks;
+                // 1 <= k <= 3, nq <= 4K, so e <= 11)
+                const uint32_t e = nq - (syn_l4 >> 4);
+                // r rebuilt from its words (live for the Horner steps anyway):
+                // r itself would stay live across every block
+                uint32_t q0 = rw[0], q1 = rw[1], q2 = rw[2], q3 = rw[3];
+                asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
+                const L5 r = l5_from_words(q0, q1, q2, q3, 0u);
+                const L5 r2 = l5_mul(r, r), r4 = l5_mul(r2, r2);
+                const L5 WA = l5_sel(e >= 8u, l5_mul(r4, r4), l5_sel(e >= 4u, r4, l5_one()));
+                const uint32_t eb = e & 3u;
+                const L5 wb = l5_sel(eb >= 2u, r2, l5_sel(eb == 1u, r, l5_one()));
+                const L5 synw = l5_mul(WA, l5_sel(eb == 3u, l5_mul(wb, r), wb));
+                acc = l5_add(acc, l5_mul(l5_mul(dl, synw), EF));
+            }
+        }
     }
     // the length block: le64(0) || le64(pad / payload length), times r
     const uint32_t mlen = kDec ? plen : pad;  // AEAD ct length (encrypt: the padded plaintext)
@@ -1206,15 +1385,8 @@ __global__ __launch_bounds__(1024) void encap_scan_local(EncapScan q) {
     if (i < q.n) {
         const wg_gso_result r = q.gres[i];
         const uint32_t S = r.segment_size;
-        if (r.status == 0 && S && r.out_len) {
-            const uint64_t ns = (r.out_len + S - 1) / S;
-            const uint64_t last = r.out_len - (ns - 1) * S;
-            const uint64_t b = (ns - 1) * (32ull + ((S + 15u) & ~15u)) + 32ull + ((last + 15u) & ~15ull);
-            if (ns <= q.max_segments && S <= q.max_segment_size && b <= q.msg_cap) {
-                nm = (uint32_t)ns;
-                bytes = (uint32_t)b;
-            }
-        }
+        if (r.status == 0)
+            nm = encap_fit(r.out_len, S, q.max_segments, q.max_segment_size, q.msg_cap, bytes);
         q.eres[i].nmsg = nm;
         q.eres[i].msg_bytes = bytes;
         q.eres[i].counter0 = 0;
@@ -1265,6 +1437,9 @@ static void launch_gk(const AeadParams &p, uint64_t blocks, hipStream_t st) {
                 if (!p.eres)
                     hipLaunchKernelGGL((aead_kernel<0, K, false, false, 0, true>), dim3((unsigned)blocks), dim3(256),
                                        shm, st, p);
+                else if (p.gmode == 2 && p.synth)
+                    hipLaunchKernelGGL((aead_kernel<0, K, false, false, 2, true, true>), dim3((unsigned)blocks),
+                                       dim3(256), shm, st, p);
                 else if (p.gmode == 2)
                     hipLaunchKernelGGL((aead_kernel<0, K, false, false, 2, true>), dim3((unsigned)blocks), dim3(256),
                                        shm, st, p);
@@ -1300,14 +1475,16 @@ static void launch_k(const AeadParams &p, uint32_t G, uint64_t blocks, hipStream
         launch_gk<64, K, kDec>(p, blocks, st);
 }
 
-template <bool kDec>
-static int launch_aead(AeadParams &p, uint32_t maxpay, hipStream_t st) {
-    // counters per packet: the key block + the padded payload's 64-B blocks;
-    // K (knob aead_k) consecutive blocks per lane; a group of exactly the
-    // lanes needed (up to 32: 64 / lanes packets per wave), else 64 lanes in
-    // several passes
+// Launch geometry for payloads up to maxpay bytes: counters per packet are
+// the key block + the padded payload's 64-B blocks; K (knob aead_k)
+// consecutive blocks per lane; a group of exactly the lanes needed (up to
+// 32: 64 / lanes packets per wave), else 64 lanes in several passes
+struct AeadGeom {
+    uint32_t K, lanes, G, per_wave, lstride, lds_wave;
+    bool staged;  // the kStage kernel runs (encrypt)
+};
+static AeadGeom aead_geom(uint32_t maxpay, uint32_t seg, bool dec, const Tune &t) {
     const uint32_t nblk = (((maxpay + 15u) & ~15u) + 63u) / 64u;
-    const Tune t = tune();
     uint32_t K = t.aead_k;
     if (K == 0) {
         // auto: K = 2 or 3, whichever moves more packets per unit of lane
@@ -1319,13 +1496,27 @@ static int launch_aead(AeadParams &p, uint32_t maxpay, hipStream_t st) {
         const uint32_t w2 = l2 <= 32u ? 64u / l2 : 0u, w3 = l3 <= 32u ? 64u / l3 : 0u;
         K = 2u * w3 > 3u * w2 ? 3u : 2u;  // w3 / 3 > w2 / 2
     }
-    const uint32_t lanes = (nblk + 1u + K - 1u) / K;
-    uint32_t G = lanes <= 1u ? 1u : lanes <= 32u ? 0u : 64u;
-    const uint32_t per_wave = G ? 64u / G : 64u / lanes;
-    p.grp = lanes;
+    AeadGeom a;
+    a.K = K;
+    a.lanes = (nblk + 1u + K - 1u) / K;
+    a.G = a.lanes <= 1u ? 1u : a.lanes <= 32u ? 0u : 64u;
+    a.per_wave = a.G ? 64u / a.G : 64u / a.lanes;
     // staged messages (encrypt, exact-size groups): one LDS slot per packet
-    p.lstride = 32u + ((p.seg + 15u) & ~15u);
-    p.lds_wave = (!kDec && G == 0 && t.aead_stage) ? per_wave * p.lstride : 0u;
+    a.lstride = 32u + ((seg + 15u) & ~15u);
+    a.lds_wave = (!dec && a.G == 0 && t.aead_stage) ? a.per_wave * a.lstride : 0u;
+    a.staged = a.lds_wave && 4u * a.lds_wave <= kStageMaxBlockLds;
+    return a;
+}
+
+template <bool kDec>
+static int launch_aead(AeadParams &p, uint32_t maxpay, hipStream_t st, const Tune &t) {
+    const AeadGeom a = aead_geom(maxpay, p.seg, kDec, t);
+    const uint32_t K = a.K, G = a.G, per_wave = a.per_wave;
+    p.grp = a.lanes;
+    p.lstride = a.lstride;
+    p.lds_wave = a.lds_wave;
+    if (p.synth && !a.staged)
+        return WG_ERR_INVALID;  // internal: synthesis was decided from the same geometry
     const uint64_t per_block = 4u * per_wave;  // packets per 256-thread block
     uint64_t blocks = (p.n + per_block - 1) / per_block;
     if (blocks >= 8)
@@ -1358,7 +1549,7 @@ extern "C" int wg_aead_encrypt_batch(const uint8_t *dev_in, uint64_t total_len, 
     p.receiver = receiver_index;
     p.counter0 = counter0;
     p.key = key_words(key);
-    return launch_aead<false>(p, segment_size, static_cast<hipStream_t>(stream));
+    return launch_aead<false>(p, segment_size, static_cast<hipStream_t>(stream), tune());
 }
 
 extern "C" int wg_aead_decrypt_batch(const uint8_t *dev_in, uint64_t total_len, uint32_t segment_size,
@@ -1377,7 +1568,7 @@ extern "C" int wg_aead_decrypt_batch(const uint8_t *dev_in, uint64_t total_len, 
     p.n = (total_len + segment_size - 1) / segment_size;
     p.seg = segment_size;
     p.key = key_words(key);
-    return launch_aead<true>(p, segment_size > 32u ? segment_size - 32u : 0u, static_cast<hipStream_t>(stream));
+    return launch_aead<true>(p, segment_size > 32u ? segment_size - 32u : 0u, static_cast<hipStream_t>(stream), tune());
 }
 
 
@@ -1400,7 +1591,7 @@ extern "C" int wg_aead_decrypt_verify_batch(const uint8_t *dev_in, uint64_t tota
     p.n = (total_len + segment_size - 1) / segment_size;
     p.seg = segment_size;
     p.key = key_words(key);
-    return launch_aead<true>(p, segment_size > 32u ? segment_size - 32u : 0u, static_cast<hipStream_t>(stream));
+    return launch_aead<true>(p, segment_size > 32u ? segment_size - 32u : 0u, static_cast<hipStream_t>(stream), tune());
 }
 
 // the encap scans + the AEAD over GSO output (gmode 1: whole segments in
@@ -1409,7 +1600,8 @@ static int encap_launch(const uint8_t *dev_in, const uint8_t *dev_seg, const wg_
                         const wg_gso_result *dev_gso_res, uint64_t n, const uint8_t key[32], uint32_t receiver_index,
                         uint64_t counter0, const uint64_t *dev_msg_offset, uint32_t msg_cap, uint32_t max_segments,
                         uint32_t max_segment_size, uint8_t *dev_msgs, wg_encap_result *dev_res, uint32_t *dev_work,
-                        uint64_t *dev_total, uint32_t gmode, const uint64_t *dev_base, hipStream_t st) {
+                        uint64_t *dev_total, uint32_t gmode, const uint64_t *dev_base, hipStream_t st,
+                        const Tune &t, bool synth) {
     EncapScan q{dev_gso_res, dev_res, dev_work, dev_total, n, msg_cap, max_segments, max_segment_size, dev_base};
     const uint32_t nb = (uint32_t)((n + 1023) / 1024);
     hipLaunchKernelGGL(encap_scan_local, dim3(nb), dim3(1024), 0, st, q);
@@ -1435,7 +1627,8 @@ static int encap_launch(const uint8_t *dev_in, const uint8_t *dev_seg, const wg_
     p.gm = max_segments;
     p.gmode = gmode;
     p.ctr_base = dev_base;
-    return launch_aead<false>(p, max_segment_size, st);
+    p.synth = synth ? 1u : 0u;
+    return launch_aead<false>(p, max_segment_size, st, t);
 }
 
 // the arguments both encap entry points share
@@ -1470,7 +1663,7 @@ extern "C" int wg_encap_encrypt(const uint8_t *dev_in, const uint8_t *dev_seg, c
         return WG_OK;
     return encap_launch(dev_in, dev_seg, dev_desc, dev_gso_res, n, key, receiver_index, counter0, dev_msg_offset,
                         msg_cap, max_segments, max_segment_size, dev_msgs, dev_res, dev_work, dev_total, 1u,
-                        nullptr, static_cast<hipStream_t>(stream));
+                        nullptr, static_cast<hipStream_t>(stream), tune(), false);
 }
 
 namespace wg {
@@ -1512,14 +1705,20 @@ int encap_batch_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n,
         return WG_ERR_INVALID;
     if (!n)
         return WG_OK;
-    const uint32_t parts = tune().encap_parts;
+    // one knob snapshot for the split and the AEAD: header synthesis
+    // (encap_synth) needs the staged kernel, and the split must skip exactly
+    // the super-buffers the AEAD synthesizes
+    const Tune t = tune();
+    const bool synth = t.encap_synth && aead_geom(max_segment_size, max_segment_size, false, t).staged;
+    const EncapFit fit{msg_cap, max_segments, max_segment_size};
+    const uint32_t parts = t.encap_parts;
     if (parts <= 1 || n < 2ull * parts) {
-        const int rc = gso_split_launch(dev_in, dev_desc, n, dev_out, dev_gso_res, true, st);
+        const int rc = gso_split_launch(dev_in, dev_desc, n, dev_out, dev_gso_res, true, st, synth ? &fit : nullptr);
         if (rc != WG_OK)
             return rc;
         return encap_launch(dev_in, dev_out, dev_desc, dev_gso_res, n, key, receiver_index, counter0, dev_msg_offset,
                             msg_cap, max_segments, max_segment_size, dev_msgs, dev_res, dev_work, dev_total, 2u,
-                            dev_base, st);
+                            dev_base, st, t, synth);
     }
     // Pipelined: the batch in `parts` slices of super-buffers; slice k's
     // headers-only split runs on a side stream while slice k-1's scans and
@@ -1544,7 +1743,8 @@ int encap_batch_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n,
         return WG_ERR_RUNTIME;
     for (uint32_t k = 0; k < parts; k++) {
         const uint64_t i0 = n * k / parts, cnt = n * (k + 1) / parts - i0;
-        rc = gso_split_launch(dev_in, dev_desc + i0, cnt, dev_out, dev_gso_res + i0, true, e.side);
+        rc = gso_split_launch(dev_in, dev_desc + i0, cnt, dev_out, dev_gso_res + i0, true, e.side,
+                              synth ? &fit : nullptr);
         if (rc != WG_OK)
             return rc;
         if (hipEventRecord(e.split_done[k], e.side) != hipSuccess ||
@@ -1552,7 +1752,7 @@ int encap_batch_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n,
             return WG_ERR_RUNTIME;
         rc = encap_launch(dev_in, dev_out, dev_desc + i0, dev_gso_res + i0, cnt, key, receiver_index, counter0,
                           dev_msg_offset + i0, msg_cap, max_segments, max_segment_size, dev_msgs, dev_res + i0,
-                          dev_work, k + 1 == parts ? dev_total : ctr + k + 1, 2u, ctr + k, st);
+                          dev_work, k + 1 == parts ? dev_total : ctr + k + 1, 2u, ctr + k, st, t, synth);
         if (rc != WG_OK)
             return rc;
     }

@@ -54,6 +54,7 @@ static const Knob kKnobs[] = {
     {"aead_k", nullptr, &Tune::aead_k, 0, 0, kAeadK, WG_N(kAeadK)},
     {"aead_stage", nullptr, &Tune::aead_stage, 0, 1, nullptr, 0},
     {"encap_parts", nullptr, &Tune::encap_parts, 0, 0, kParts, WG_N(kParts)},
+    {"encap_synth", nullptr, &Tune::encap_synth, 0, 1, nullptr, 0},
 };
 #undef WG_N
 
@@ -160,6 +161,7 @@ static Tune &tune_storage() {
         // -1.0 %, encap -2.9 % (profiles/r04_aead_stage/)
         x.aead_stage = 1;
         x.encap_parts = 1;
+        x.encap_synth = 0;
         // environment overrides: WG_<KNOB> (upper case), same accepted values
         // as wg_tune_set; anything else is ignored
         for (const Knob &k : kKnobs) {

@@ -413,6 +413,15 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
         const uint32_t kind = (pr.w[1] >> 16) & 0xffu, nseg = pr.w[2] >> 16;
         if (!(kind & kPlanSplit) || gw * kStep >= nseg)
             continue;  // passthrough / error (in-place work: gso_finalize_kernel) or no segment for this slot
+        if constexpr (Abl & kHdrOnly) {
+            if (p.synth && syn_eligible(pr.w[0] & 0xffffu, pr.w[0] >> 16, pr.w[1] & 0xffffu)) {
+                const uint32_t H = pr.w[0] & 0xffffu, gso = pr.w[2] & 0xffffu;
+                uint32_t bytes;
+                if (encap_fit((uint64_t)(dr.w[4] - H) + (uint64_t)nseg * H, H + gso, p.fit_segs, p.fit_size,
+                              p.fit_cap, bytes))
+                    continue;  // wg_encap_batch's AEAD writes these headers itself
+            }
+        }
         const uint64_t in_off = (uint64_t)dr.w[0] | ((uint64_t)dr.w[1] << 32);
         const uint64_t out_off = (uint64_t)dr.w[2] | ((uint64_t)dr.w[3] << 32);
         const uint32_t in_len = dr.w[4];
@@ -664,11 +673,13 @@ static void launch_split(const GsoParams &p, dim3 g, uint32_t waves, hipStream_t
 
 namespace wg {
 // plan -> split -> finalize for n super-buffers (wg_gso_split; hdr_only:
-// wg_encap_batch's headers-only split)
+// wg_encap_batch's headers-only split, synth: without the super-buffers
+// whose headers its AEAD synthesizes)
 int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
-                     wg_gso_result *dev_res, bool hdr_only, hipStream_t st) {
+                     wg_gso_result *dev_res, bool hdr_only, hipStream_t st, const EncapFit *synth) {
     const Tune t = tune();
-    GsoParams p{dev_in, dev_desc, n, dev_out, dev_res, t.gso_groups};
+    GsoParams p{dev_in, dev_desc, n, dev_out, dev_res, t.gso_groups, hdr_only && synth ? 1u : 0u,
+                synth ? synth->msg_cap : 0u, synth ? synth->max_segments : 0u, synth ? synth->max_segment_size : 0u};
     // 1. plans (into dev_res), thread per super-buffer
     const uint64_t pb = (n + kPlanBlock - 1) / kPlanBlock;
     if (pb > 0x7fffffffull)

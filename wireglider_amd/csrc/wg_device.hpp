@@ -164,6 +164,38 @@ __device__ __forceinline__ void bst8(rsrc_t r, uint32_t off, uint32_t b) {
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)b, r, off, 0, 0);
 }
 
+// A PacketBatch of out_len bytes in segments of S: its encap messages and
+// their bytes, or 0 / 0 when a bound is exceeded (more than max_segments
+// segments, segments over max_segment_size, messages over msg_cap bytes).
+// The encap counter scan (aead.hip encap_scan_local) and the headers-only
+// split's synthesis skip (gso.hip) agree through this one function.
+__device__ __forceinline__ uint32_t encap_fit(uint64_t out_len, uint32_t S, uint32_t max_segments,
+                                             uint32_t max_segment_size, uint32_t msg_cap, uint32_t &bytes) {
+    bytes = 0;
+    if (!S || !out_len)
+        return 0;
+    const uint64_t ns = (out_len + S - 1) / S;
+    const uint64_t last = out_len - (ns - 1) * S;
+    const uint64_t b = (ns - 1) * (32ull + ((S + 15u) & ~15u)) + 32ull + ((last + 15u) & ~15ull);
+    if (ns > max_segments || S > max_segment_size || b > msg_cap)
+        return 0;
+    bytes = (uint32_t)b;
+    return (uint32_t)ns;
+}
+
+// wg_encap_batch header synthesis (knob encap_synth, aead.hip): a split
+// super-buffer whose segments' headers the AEAD builds itself — the header in
+// one 64-B block, the L4 sum starting on a dword (the lanes' word sums then
+// pair as the checksum does), the checksum field 2-B aligned, csum_start past
+// the 20-B IPv4 header (the classification guarantees it for split plans; the
+// MAC correction assumes the field lies past the block's first 16 bytes).
+// The headers-only split skips exactly these (gso.hip), the AEAD builds
+// exactly these.
+__device__ __forceinline__ bool syn_eligible(uint32_t hdr_len, uint32_t cs, uint32_t l4off) {
+    return hdr_len <= 64u && cs >= 20u && (cs & 3u) == 0u && (l4off & 1u) == 0u && l4off + 2u <= hdr_len &&
+           cs + 8u <= hdr_len;
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;

@@ -29,6 +29,10 @@ struct GsoParams {
     uint8_t *out;
     wg_gso_result *res;
     uint32_t groups;  // blocks per super-buffer (flat grid: block u -> super-buffer u / groups)
+    // headers-only split of wg_encap_batch with header synthesis: skip the
+    // super-buffers whose segments the AEAD encrypts (encap_fit) and builds
+    // (syn_eligible); every other one is split as usual
+    uint32_t synth, fit_cap, fit_segs, fit_size;
 };
 
 struct Ctx {

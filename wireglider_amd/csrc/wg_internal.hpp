@@ -33,6 +33,7 @@ struct Tune {
     uint32_t aead_k;      // AEAD: consecutive ChaCha20 blocks per lane (0 = 2 or 3 per batch, 2, 3)
     uint32_t aead_stage;  // AEAD encrypt: messages assembled in LDS, written out in whole lines (1)
     uint32_t encap_parts; // wg_encap_batch: slices split on a side stream under the previous slice's AEAD (1 = off)
+    uint32_t encap_synth; // wg_encap_batch: the AEAD builds eligible segments' headers, the split skips them
     uint32_t gso_ablate;  // GSO A/B variants (1 non-temporal stores, 32 no XCD swizzle; both correct)
 };
 
@@ -46,9 +47,15 @@ Tune tune();
 bool debug_sync(hipStream_t st, const char *kernel);
 
 // wg_gso_split's three launches (gso.hip); hdr_only = wg_encap_batch's
-// headers-only split (segment headers written, payload left in the input).
+// headers-only split (segment headers written, payload left in the input);
+// synth (non-null): its super-buffers that pass syn_eligible and whose
+// messages fit these bounds (encap_fit) are not split at all (the encap
+// AEAD writes their headers).
+struct EncapFit {
+    uint32_t msg_cap, max_segments, max_segment_size;
+};
 int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
-                     wg_gso_result *dev_res, bool hdr_only, hipStream_t st);
+                     wg_gso_result *dev_res, bool hdr_only, hipStream_t st, const EncapFit *synth = nullptr);
 
 // wg_encap_batch with a device-resident counter base (aead.hip): counters
 // start at counter0 + *dev_base (nullable: 0) and *dev_total gets *dev_base +
