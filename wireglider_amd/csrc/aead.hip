@@ -594,6 +594,8 @@ struct HdrGate {
 };
 
 __device__ __forceinline__ uint32_t hsum32(uint32_t w) { return (w & 0xffffu) + (w >> 16); }
+// acc + both 16-bit halves of w in one instruction (v_sad_u16 against zero)
+__device__ __forceinline__ uint32_t hacc(uint32_t acc, uint32_t w) { return __builtin_amdgcn_sad_u16(w, 0u, acc); }
 
 __device__ __forceinline__ HdrGate hdr_gate(const uint32_t R[16], uint32_t len) {
     HdrGate h{0u, 0u, 20u, 0u, 0u, false};
@@ -656,6 +658,7 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 
 struct SynSeg {
     uintptr_t tpl;  // the super-buffer (its prefix is every segment's header template)
+    uint32_t tlen;  // its length
     uint32_t cs, l4off, hdr, gso, idx;
     bool tcp, v6, last;
 };
@@ -674,8 +677,22 @@ __device__ __forceinline__ void syn_block0(const SynSeg &q, uintptr_t psrc, uint
                                            uint32_t &rest, uint32_t &pv) {
     const uint32_t nin = pktlen < 64u ? pktlen : 64u;
     uint32_t T[16], M[16];
-    load64(q.tpl, q.hdr, T);  // the template, zero past the header (split super-buffers hold >= hdr bytes)
-    load64(psrc, nin, M);     // payload byte j of the segment at psrc + j (j >= hdr)
+    if (nin == 64u && q.tlen >= 64u) {
+        // both 64-B windows inside the super-buffer: four 16-B loads each at
+        // the addresses as they are (the usual case)
+#pragma unroll
+        for (uint32_t c = 0; c < 4; c++) {
+            const v4u t = ld16(q.tpl + 16u * c), v = ld16(psrc + 16u * c);
+#pragma unroll
+            for (uint32_t e = 0; e < 4; e++) {
+                T[4 * c + e] = t[e];
+                M[4 * c + e] = v[e];
+            }
+        }
+    } else {
+        load64(q.tpl, q.hdr, T);  // the template (split super-buffers hold >= hdr bytes)
+        load64(psrc, nin, M);     // payload byte j of the segment at psrc + j (j >= hdr), zero past nin
+    }
     const uint32_t cw = q.cs >> 2, fw = q.l4off >> 2;
     const uint32_t l4len = bswap16((pktlen - q.cs) & 0xffffu);
     uint32_t ips = 0, ps = 0, p = 0;
@@ -683,7 +700,7 @@ __device__ __forceinline__ void syn_block0(const SynSeg &q, uintptr_t psrc, uint
     for (uint32_t m = 0; m < 16; m++) {
         const uint32_t k = q.hdr > 4u * m ? (q.hdr - 4u * m < 4u ? q.hdr - 4u * m : 4u) : 0u;  // template bytes
         const uint32_t mk = k >= 4u ? ~0u : (1u << (8u * k)) - 1u;
-        uint32_t w = T[m] | (M[m] & ~mk);
+        uint32_t w = (T[m] & mk) | (M[m] & ~mk);
         if (m == 0u && !q.v6)
             w = (w & 0xffffu) | (bswap16(pktlen & 0xffffu) << 16);  // ip_len (offload.cpp:183)
         if (m == 1u) {
@@ -701,15 +718,21 @@ __device__ __forceinline__ void syn_block0(const SynSeg &q, uintptr_t psrc, uint
                 w = (w & 0xffff0000u) | l4len;  // udp len (:199)
         }
         M[m] = w;
-        const uint32_t h = hsum32(w);
-        ips += m < cw ? h : 0u;                                                // [0, cs), ip_sum zero
-        ps += (q.v6 ? (m >= 2u && m < 10u) : (m == 3u || m == 4u)) ? h : 0u;  // addresses
+        if (m < 15u)
+            ips = m < cw ? hacc(ips, w) : ips;  // [0, cs), ip_sum zero (cw <= 14)
+        if (m >= 2u && m < 10u)
+            ps = (q.v6 || m == 3u || m == 4u) ? hacc(ps, w) : ps;  // addresses: v6 8-39, v4 12-19
         p = m == fw ? w : p;
     }
     const uint32_t ipcs = ~fold16_32(ips) & 0xffffu;
     if (!q.v6)
         M[2] = (M[2] & 0xffffu) | (ipcs << 16);  // ip_sum, native order (:184-186); the template's was zeroed (:147)
-    store_n(hdst, M, nin);
+    if (nin == 64u) {
+#pragma unroll
+        for (uint32_t c = 0; c < 4; c++) st16(hdst + 16u * c, v4u{M[4 * c], M[4 * c + 1], M[4 * c + 2], M[4 * c + 3]});
+    } else {
+        store_n(hdst, M, nin);
+    }
     pv = (p >> (8u * (q.l4off & 2u))) & 0xffffu;
     const uint32_t hw = ips + (q.v6 ? 0u : ipcs);  // block 0's words below csum_start, as stored
     rest = ps + ((q.tcp ? 6u : 17u) << 8) + l4len + (32u * 0xffffu - hw);
@@ -809,6 +832,7 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                 if (syn && g == 0u) {
                     SynSeg sq;
                     sq.tpl = reinterpret_cast<uintptr_t>(p.gin) + gd.in_offset;
+                    sq.tlen = gd.in_len;
                     sq.cs = cs;
                     sq.l4off = l4;
                     sq.hdr = gr.hdr_len;
@@ -930,6 +954,7 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             nq = hi > lo ? ((64u * hi < pad ? 64u * hi : pad) - 64u * lo) / 16u : 0u;
         }
         L5 S;
+        L5 synw;  // kSyn: r^(nq - k), the weight of chunk k = l4off / 16 (the checksum's) in group lane 0's sum
         {
             // r^nq = r^(4a) r^b from r, r^2 and r^4, r^8 (K >= 2), r^12, r^16
             // (K = 4); limb-wise selects (a select between whole L5 values
@@ -951,6 +976,15 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             const L5 rb = l5_sel(b >= 2u, r2, l5_sel(b == 1u, r, l5_one()));
             const L5 QB = l5_sel(b == 3u, l5_mul(rb, r), rb);  // r^3 = r^2 r
             S = l5_sel(b == 0u, QA, l5_sel(a4 == 0u, QB, l5_mul(QA, QB)));
+            if constexpr (kSyn) {
+                // chunk k opens group lane 0's Horner sum at block 0 (1 <= k
+                // <= 3, nq <= 4K: e <= 11)
+                const uint32_t e = syn && g == 0u && nq > syn_l4 / 16u ? nq - syn_l4 / 16u : 0u;
+                const L5 WA = l5_sel(e >= 8u, l5_mul(r4, r4), l5_sel(e >= 4u, r4, l5_one()));
+                const uint32_t eb = e & 3u;
+                const L5 wb = l5_sel(eb >= 2u, r2, l5_sel(eb == 1u, r, l5_one()));
+                synw = l5_mul(WA, l5_sel(eb == 3u, l5_mul(wb, r), wb));
+            }
         }
         L5 E;
         if constexpr (kFlex) {
@@ -972,6 +1006,16 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
         }
         // the later passes' blocks (F == 1 with one pass: wave-uniform test)
         const L5 EF = passes > 1 ? l5_mul(E, F) : E;
+        if constexpr (kSyn) {
+            // the L4 checksum field's weight, times EF, parked in the message
+            // slot's header / tag positions (written only at the end) until
+            // the checksum is known: no registers held across the blocks
+            const L5 w = l5_mul(synw, EF);
+            if (syn && g == 0u) {
+                aead_lds[lslot] = v4u{w.v[0], w.v[1], w.v[2], w.v[3]};
+                reinterpret_cast<uint32_t *>(aead_lds)[4u * (lslot + 1u + pad / 16u)] = w.v[4];
+            }
+        }
         if (passes > 1 && pp > 0) {
             // F *= product of the whole pass (group lane 0 holds S over lanes >= 0)
             L5 Sall;
@@ -1023,7 +1067,7 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                 }
                 if constexpr (kSyn) {
 #pragma unroll
-                    for (int m = 0; m < 16; m++) psum += hsum32(W[m]);  // the segment's L4 words
+                    for (int m = 0; m < 16; m++) psum = hacc(psum, W[m]);  // the segment's L4 words
                 }
 #pragma unroll
                 for (int m = 0; m < 16; m++) {
@@ -1067,7 +1111,7 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                 load64(bsrc, nin, W);
                 if constexpr (kSyn) {
 #pragma unroll
-                    for (int m = 0; m < 16; m++) psum += hsum32(W[m]);  // the segment's L4 words
+                    for (int m = 0; m < 16; m++) psum = hacc(psum, W[m]);  // the segment's L4 words
                 }
                 const uint32_t nqc = nct / 16u;  // whole 16-B Poly1305 chunks in the block (nct is a multiple of 16)
 #pragma unroll
@@ -1104,7 +1148,7 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                 // the plaintext's words; the first 64 bytes decide the gates
                 if (has) {
 #pragma unroll
-                    for (int m = 0; m < 16; m++) vsum += hsum32(kb[m]);
+                    for (int m = 0; m < 16; m++) vsum = hacc(vsum, kb[m]);
                     if (d == 0u)
                         gate = hdr_gate(kb, plen);
                 }
@@ -1162,7 +1206,7 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                         uint32_t W[16];
                         load64((boff < hl ? hsrc : src) + boff, plen - boff < 64u ? plen - boff : 64u, W);
 #pragma unroll
-                        for (int m = 0; m < 16; m++) psum += hsum32(W[m]);
+                        for (int m = 0; m < 16; m++) psum = hacc(psum, W[m]);
                     }
                 }
             }
@@ -1196,21 +1240,11 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
 #pragma unroll
                     for (int k = 0; k < 5; k++) dl.v[k] = tp[k] - dl.v[k];
                 }
-                // weight: r^(nq - k) in this lane's Horner sum (chunk k =
-                // l4off / 16 of block 0, which opens group lane 0's blocks;
-                // 1 <= k <= 3, nq <= 4K, so e <= 11)
-                const uint32_t e = nq - (syn_l4 >> 4);
-                // r rebuilt from its words (live for the Horner steps anyway):
-                // r itself would stay live across every block
-                uint32_t q0 = rw[0], q1 = rw[1], q2 = rw[2], q3 = rw[3];
-                asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
-                const L5 r = l5_from_words(q0, q1, q2, q3, 0u);
-                const L5 r2 = l5_mul(r, r), r4 = l5_mul(r2, r2);
-                const L5 WA = l5_sel(e >= 8u, l5_mul(r4, r4), l5_sel(e >= 4u, r4, l5_one()));
-                const uint32_t eb = e & 3u;
-                const L5 wb = l5_sel(eb >= 2u, r2, l5_sel(eb == 1u, r, l5_one()));
-                const L5 synw = l5_mul(WA, l5_sel(eb == 3u, l5_mul(wb, r), wb));
-                acc = l5_add(acc, l5_mul(l5_mul(dl, synw), EF));
+                // its weight r^(nq - k) * EF, parked in the slot by the S step
+                const uint32_t *lw = reinterpret_cast<const uint32_t *>(aead_lds);
+                const v4u w4 = aead_lds[lslot];
+                const L5 synw{{w4[0], w4[1], w4[2], w4[3], lw[4u * (lslot + 1u + pad / 16u)]}};
+                acc = l5_add(acc, l5_mul(dl, synw));
             }
         }
     }
@@ -1713,7 +1747,10 @@ int encap_batch_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n,
     const EncapFit fit{msg_cap, max_segments, max_segment_size};
     const uint32_t parts = t.encap_parts;
     if (parts <= 1 || n < 2ull * parts) {
-        const int rc = gso_split_launch(dev_in, dev_desc, n, dev_out, dev_gso_res, true, st, synth ? &fit : nullptr);
+        // the split's list of super-buffers left to it lives in dev_work,
+        // which the scans only use after the split
+        const int rc = gso_split_launch(dev_in, dev_desc, n, dev_out, dev_gso_res, true, st, synth ? &fit : nullptr,
+                                        dev_work);
         if (rc != WG_OK)
             return rc;
         return encap_launch(dev_in, dev_out, dev_desc, dev_gso_res, n, key, receiver_index, counter0, dev_msg_offset,

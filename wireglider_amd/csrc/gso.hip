@@ -396,11 +396,12 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
     const uint32_t lane = lane_id();
     const uint32_t G = p.groups;
     const uint32_t gstride = gridDim.y * G * W * kStep;
-    const uint64_t units = p.n * G;
+    const uint64_t units = (p.list ? sload(p.list) : p.n) * G;
     const uint64_t u0 = (Abl & kAblNoSwizzle) ? blockIdx.x : xcd_swizzle(blockIdx.x, gridDim.x);
     for (uint64_t u = u0; u < units; u += gridDim.x) {
-        const uint64_t b = G == 1 ? u : u / G;
-        const uint32_t gw = (blockIdx.y * G + (uint32_t)(u - b * G)) * W + wave_in_block();  // segment slot
+        const uint64_t ub = G == 1 ? u : u / G;
+        const uint64_t b = p.list ? sload(p.list + 1 + ub) : ub;
+        const uint32_t gw = (blockIdx.y * G + (uint32_t)(u - ub * G)) * W + wave_in_block();  // segment slot
         // plan and descriptor as raw dwords: one s_load each (16-bit struct
         // fields would become dependent vector loads), unpacked by shifts
         const DescRaw dr = sload(reinterpret_cast<const DescRaw *>(p.desc + b));  // first 20 B of the 40-B descriptor
@@ -594,6 +595,23 @@ __global__ __launch_bounds__(kPlanBlock) void gso_plan_kernel(GsoParams p) {
         pl.flags13 = (uint8_t)(-cl.status);
     }
     reinterpret_cast<GsoPlan *>(p.res)[b] = pl;
+    if (p.list) {
+        // still split here unless wg_encap_batch's AEAD synthesizes it
+        uint32_t bytes;
+        const bool split =
+            !cl.pass && !(p.synth && syn_eligible(c.hdr_len, c.cs, c.l4off) &&
+                          encap_fit((uint64_t)(dsc.in_len - c.hdr_len) + (uint64_t)c.nseg * c.hdr_len,
+                                    c.hdr_len + c.gso, p.fit_segs, p.fit_size, p.fit_cap, bytes));
+        const uint64_t m = __ballot(split);  // the wave's active threads
+        if (split) {
+            const uint32_t lane = lane_id(), lead = (uint32_t)__builtin_ctzll(m);
+            uint32_t base = 0;
+            if (lane == lead)
+                base = atomicAdd(p.list, (uint32_t)__builtin_popcountll(m));
+            base = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead << 2), (int)base);
+            p.list[1u + base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull))] = (uint32_t)b;
+        }
+    }
 }
 
 // Finalize (same stream, after the split kernel), thread per super-buffer
@@ -676,10 +694,22 @@ namespace wg {
 // wg_encap_batch's headers-only split, synth: without the super-buffers
 // whose headers its AEAD synthesizes)
 int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
-                     wg_gso_result *dev_res, bool hdr_only, hipStream_t st, const EncapFit *synth) {
+                     wg_gso_result *dev_res, bool hdr_only, hipStream_t st, const EncapFit *synth, uint32_t *list) {
     const Tune t = tune();
-    GsoParams p{dev_in, dev_desc, n, dev_out, dev_res, t.gso_groups, hdr_only && synth ? 1u : 0u,
-                synth ? synth->msg_cap : 0u, synth ? synth->max_segments : 0u, synth ? synth->max_segment_size : 0u};
+    const bool syn = hdr_only && synth;
+    GsoParams p{dev_in,
+                dev_desc,
+                n,
+                dev_out,
+                dev_res,
+                t.gso_groups,
+                syn ? 1u : 0u,
+                syn ? synth->msg_cap : 0u,
+                syn ? synth->max_segments : 0u,
+                syn ? synth->max_segment_size : 0u,
+                syn ? list : nullptr};
+    if (p.list && hipMemsetAsync(p.list, 0, sizeof(uint32_t), st) != hipSuccess)
+        return WG_ERR_RUNTIME;
     // 1. plans (into dev_res), thread per super-buffer
     const uint64_t pb = (n + kPlanBlock - 1) / kPlanBlock;
     if (pb > 0x7fffffffull)
@@ -689,7 +719,9 @@ int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, u
         return WG_ERR_LAUNCH;
     // 2. the split
     const uint64_t units = n * t.gso_groups;
-    uint64_t blocks = units < t.gso_blocks ? units : t.gso_blocks;
+    // list mode: a fixed grid walks the listed super-buffers (usually few)
+    const uint64_t cap = p.list ? 4096u : t.gso_blocks;
+    uint64_t blocks = units < cap ? units : cap;
     if (blocks >= 8)
         blocks &= ~7ull;  // the XCD swizzle wants a multiple of 8 (the grid-stride loop covers the rest)
     const dim3 g((unsigned)blocks, t.gso_split);

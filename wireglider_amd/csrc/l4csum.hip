@@ -303,14 +303,12 @@ __global__ __launch_bounds__(256) void l4csum_uniform_small_kernel(L4Params p) {
 //    machinery; small packets among long ones ride along in their issue
 //    phase at next to no cost (config 4's mixed batch measured +2.5 % when
 //    they went to the lane role instead).
-//  * LANE role (wave b % 4 of block b, so these long-lived waves spread over
-//    the four SIMDs): the block's all-small groups, a lane per packet,
+//  * LANE role (wave 0): the block's all-small groups, a lane per packet,
 //    summed from its 5 aligned chunks (4 KiB of loads in flight per wave).
-// The lane-role wave loads the block's 64 descriptors (lane l = descriptor
-// (l >> 4) * Q + 16b + (l & 15); its own groups are lanes whose (l & 15) / 4
-// is its wave index), the other waves their 16: every descriptor read once
-// from HBM.  An all-small batch keeps a lane per packet (the other waves
-// leave after one descriptor load),
+// Wave 0 loads the block's 64 descriptors (lane l = descriptor
+// (l >> 4) * Q + 16b + (l & 15); its own groups are lanes with (l & 15) < 4),
+// waves 1-3 their 16: every descriptor read once from HBM.  An all-small
+// batch keeps a lane per packet (waves 1-3 leave after one descriptor load),
 // an all-long one keeps the short 16-packet waves with every descriptor in
 // one vector load.  One launch, no host knowledge of the mix.
 template <int kKind, bool kNT, int U = 4>  // U: loads in flight per lane on a long packet's rest
@@ -320,16 +318,11 @@ __global__ __launch_bounds__(256) void l4csum_split_kernel(L4Params p) {
     const uint32_t wib = wave_in_block();
     const uint64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
     const uint64_t Q = p.quarter;
-    // the lane-role wave rotates with the block (block b: wave b % 4), so the
-    // long-lived lane-role waves of an all-small batch spread over the four
-    // SIMDs instead of filling SIMD 0 while waves 1-3 leave at once
-    const uint32_t lw = (uint32_t)(blockIdx.x & 3u);
-    const bool lrole = wib == lw;
     // lane -> (quarter, offset in the block's 16 of that quarter)
-    const uint32_t qq = lrole ? lane >> 4 : (lane >> 2) & 3u;
-    const uint32_t oo = lrole ? lane & 15u : 4u * wib + (lane & 3u);
+    const uint32_t qq = wib == 0 ? lane >> 4 : (lane >> 2) & 3u;
+    const uint32_t oo = wib == 0 ? lane & 15u : 4u * wib + (lane & 3u);
     const uint64_t i = (uint64_t)qq * Q + 16u * blk + oo;
-    const bool live = (lrole || lane < 16u) && 16u * blk < Q && i < p.n;
+    const bool live = (wib == 0 || lane < 16u) && 16u * blk < Q && i < p.n;
     const v4u d = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : p.n - 1));
     const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32);
     const uintptr_t a = reinterpret_cast<uintptr_t>(p.base) + (live ? off : 0u);
@@ -340,15 +333,15 @@ __global__ __launch_bounds__(256) void l4csum_split_kernel(L4Params p) {
     const uint64_t gl = __ballot(live && len > kSmallMax);
     const bool grp_long = ((gl >> (lane & ~3u)) & 0xfu) != 0;
     // ---- wave role: this wave's groups that hold a long packet
-    const bool own = lrole ? ((lane & 15u) >> 2) == lw : true;
+    const bool own = wib == 0 ? (lane & 15u) < 4u : true;
     const bool mine = live && own && grp_long;
     uint32_t res = 0;
     wave_long<kL4, kNT, 4, U>(__ballot(mine), a, len, cs, fl, p.base, lane, res);
     if (mine)
         p.out[i] = (uint16_t)res;
-    // ---- lane role (wave lw): the block's all-small groups
-    const bool small = lrole && live && !grp_long;
-    if (__ballot(small)) {  // wave-uniform; never true on the other waves
+    // ---- lane role (wave 0): the block's all-small groups
+    const bool small = wib == 0 && live && !grp_long;
+    if (__ballot(small)) {  // wave-uniform; never true on waves 1-3
         v4u W[5];
         lane_chunks(a, len, small && len, W);
         const uint32_t t = lane_sum<kL4>(W, a, small ? len : 0u, cs, fl);

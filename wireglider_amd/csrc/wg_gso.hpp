@@ -33,6 +33,10 @@ struct GsoParams {
     // super-buffers whose segments the AEAD encrypts (encap_fit) and builds
     // (syn_eligible); every other one is split as usual
     uint32_t synth, fit_cap, fit_segs, fit_size;
+    // nullable: the plan kernel lists the super-buffers still to split here
+    // ([0] count, then indices) and the split kernel walks that list (synth
+    // with nearly every super-buffer synthesized: no wave per skipped one)
+    uint32_t *list;
 };
 
 struct Ctx {

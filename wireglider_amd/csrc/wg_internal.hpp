@@ -50,12 +50,14 @@ bool debug_sync(hipStream_t st, const char *kernel);
 // headers-only split (segment headers written, payload left in the input);
 // synth (non-null): its super-buffers that pass syn_eligible and whose
 // messages fit these bounds (encap_fit) are not split at all (the encap
-// AEAD writes their headers).
+// AEAD writes their headers); list (nullable, 4 * (n + 1) bytes of device
+// scratch): the plan kernel lists the rest and the split walks only those.
 struct EncapFit {
     uint32_t msg_cap, max_segments, max_segment_size;
 };
 int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
-                     wg_gso_result *dev_res, bool hdr_only, hipStream_t st, const EncapFit *synth = nullptr);
+                     wg_gso_result *dev_res, bool hdr_only, hipStream_t st, const EncapFit *synth = nullptr,
+                     uint32_t *list = nullptr);
 
 // wg_encap_batch with a device-resident counter base (aead.hip): counters
 // start at counter0 + *dev_base (nullable: 0) and *dev_total gets *dev_base +
