@@ -131,8 +131,10 @@ def aead_kernel_symbol(wga, maxpay: int, dec: bool = False, ver: bool = False, g
     # slots fit kStageMaxBlockLds (aead.hip launch_gk)
     lds_block = 4 * (64 // lanes) * (32 + ((maxpay + 15) & ~15)) if G == 0 else 0
     stage = not dec and G == 0 and wga.tune_get("aead_stage") == 1 and lds_block <= 53248
+    # wg_encap_batch with the staged kernel: header synthesis (knob encap_synth)
+    syn = gso == 2 and stage and wga.tune_get("encap_synth") == 1
     b = lambda v: "true" if v else "false"
-    return f"void wg::aead_kernel<{G}, {K}, {b(dec)}, {b(ver)}, {gso}, {b(stage)}>(wg::AeadParams)"
+    return f"void wg::aead_kernel<{G}, {K}, {b(dec)}, {b(ver)}, {gso}, {b(stage)}, {b(syn)}>(wg::AeadParams)"
 
 
 def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workload:
@@ -1044,7 +1046,10 @@ def build_encap(wga, torch, rank: int, world: int, dev, fused: bool = True) -> W
            + n * out_len + n * mbytes + n * (wga.ENCAP_RESULT_BYTES + 8))
     aead_k = aead_kernel_symbol(wga, seg, gso=2 if fused else 1)
     return Workload(launch, n, n * in_len, alg, cfg, "weak", buf,
-                    ("wg_encap_batch (3 split kernels, headers only, + 2 scan kernels + %s)" if fused else
+                    ("wg_encap_batch (plan + finalize kernels, the headers-only split walking the list of "
+                     "super-buffers left to it (none here: the AEAD synthesizes every segment header), "
+                     "2 scan kernels + %s)" if fused and "true>(" in aead_k else
+                     "wg_encap_batch (3 split kernels, headers only, + 2 scan kernels + %s)" if fused else
                      "wg_gso_split (3 kernels) + wg_encap_encrypt (2 scan kernels + %s)") % aead_k,
                     rank * n, sample=sample, counts=[n] * world, post=post, copy_dst=msgs,
                     metric="device-resident GiB/s of tun input, GSO split + data-message encryption (encap worker)")

@@ -471,8 +471,8 @@ int wg_device_count(void);
  *                stores its own blocks (0)
  *   "encap_synth" wg_encap_batch: the AEAD builds the headers of segments
  *                whose header fits one 64-B block itself (fields, IPv4 and L4
- *                checksums) and the split skips those super-buffers (1), or
- *                every segment header comes from the split (0)
+ *                checksums) and the split skips those super-buffers (1,
+ *                default), or every segment header comes from the split (0)
  *   "gso_ablate" GSO A/B variants: 1 = non-temporal payload stores, 32 = no
  *                XCD swizzle (both correct); 0 = the default kernel.
  * Thread-safe: each launch reads one consistent snapshot of the knobs. */

@@ -224,19 +224,27 @@ def test_bench_valu_issue_checks_kernel_symbol():
     import bench
     import wireglider_amd as wga
 
-    assert bench.aead_kernel_symbol(wga, 1500) == "void wg::aead_kernel<0, 3, false, false, 0, true>(wg::AeadParams)"
-    assert bench.aead_kernel_symbol(wga, 64) == "void wg::aead_kernel<1, 2, false, false, 0, false>(wg::AeadParams)"
-    assert bench.aead_kernel_symbol(wga, 9000, True, True).startswith("void wg::aead_kernel<64, 2, true, true, 0, false>")
+    assert bench.aead_kernel_symbol(wga, 1500) == \
+        "void wg::aead_kernel<0, 3, false, false, 0, true, false>(wg::AeadParams)"
+    assert bench.aead_kernel_symbol(wga, 64) == "void wg::aead_kernel<1, 2, false, false, 0, false, false>(wg::AeadParams)"
+    assert bench.aead_kernel_symbol(wga, 9000, True, True).startswith("void wg::aead_kernel<64, 2, true, true, 0, false,")
+    # wg_encap_batch: the header-synthesizing instantiation (encap_synth = 1, the default)
     assert bench.aead_kernel_symbol(wga, 1500, gso=2) == \
-        "void wg::aead_kernel<0, 3, false, false, 2, true>(wg::AeadParams)"
+        "void wg::aead_kernel<0, 3, false, false, 2, true, true>(wg::AeadParams)"
+    assert bench.aead_kernel_symbol(wga, 1500, gso=1).endswith("1, true, false>(wg::AeadParams)")
     # exact-size groups always fit: 32 lanes, 2 packets per wave, 4 x 2 x (32 + 6,080) B
-    assert bench.aead_kernel_symbol(wga, 6070).endswith("false, false, 0, true>(wg::AeadParams)")
-    saved = wga.tune_get("aead_stage")
+    assert bench.aead_kernel_symbol(wga, 6070).endswith("false, false, 0, true, false>(wg::AeadParams)")
+    saved = {k: wga.tune_get(k) for k in ("aead_stage", "encap_synth")}
     try:
         wga.tune_set("aead_stage", 0)
-        assert bench.aead_kernel_symbol(wga, 1500).endswith("0, false>(wg::AeadParams)")
+        assert bench.aead_kernel_symbol(wga, 1500).endswith("0, false, false>(wg::AeadParams)")
+        assert bench.aead_kernel_symbol(wga, 1500, gso=2).endswith("2, false, false>(wg::AeadParams)")
+        wga.tune_set("aead_stage", 1)
+        wga.tune_set("encap_synth", 0)
+        assert bench.aead_kernel_symbol(wga, 1500, gso=2).endswith("2, true, false>(wg::AeadParams)")
     finally:
-        wga.tune_set("aead_stage", saved)
+        for k, v in saved.items():
+            wga.tune_set(k, v)
     prof = {"kernel": "void wg::aead_kernel<0, 3, false, true>(wg::AeadParams)", "valu_winst_per_launch": 8e8}
     ok = bench.valu_issue(dict(prof, kernel="K"), "K", 1.0, "aead")
     assert ok["valu_issue"]["frac"] == round(8e8 / 1e-3 / bench.VALU_PEAK_WINST, 4)

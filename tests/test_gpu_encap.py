@@ -37,7 +37,7 @@ def _wga():
                                    {"encap_parts": 3}, {"encap_parts": 8}, {"encap_spw": 4}, {"encap_spw": 0},
                                    {"aead_k": 2, "encap_parts": 2}, {"encap_synth": 1},
                                    {"encap_synth": 1, "aead_k": 2}, {"encap_synth": 1, "encap_parts": 3},
-                                   {"encap_synth": 1, "aead_stage": 0}],
+                                   {"encap_synth": 1, "aead_stage": 0}, {"encap_synth": 0}],
                          ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()) or "default")
 def test_encap_matches_oracle(gpu, seed, knobs, fused):
     import torch
@@ -72,7 +72,7 @@ def test_encap_matches_oracle(gpu, seed, knobs, fused):
     d_in_f = d_in.clone()  # the fused call's own copy (the split zeroes prefix fields in place)
     d_res = wga.gso_split(d_in, d_desc, d_out)
     max_seg, max_size, cap = 48, 9100, 48 * (32 + 9104)
-    if knobs.get("encap_synth"):
+    if "encap_synth" in knobs:
         # header synthesis runs with the staged AEAD (segments up to ~6 KB):
         # super-buffers of larger segments get no messages and keep the split
         max_size = 1600

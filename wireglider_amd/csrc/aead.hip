@@ -663,18 +663,24 @@ struct SynSeg {
     bool tcp, v6, last;
 };
 
-// Segment q's plaintext [0, 64) — the header with every field but the L4
-// checksum, which holds pv (the bytes there before it is written), then the
-// payload — built and stored at hdst (the segment slot, where the
-// headers-only split would have written it; the encryption reads it back
-// from there like any split header).  rest: the L4 sum's terms other than
-// the segment's own words from its block 0 on — pseudo-header addresses,
-// protocol, L4 length, and 32 * 0xFFFF minus block 0's words below
-// csum_start (the lanes sum whole blocks; subtracting x mod 0xFFFF is adding
-// 0xFFFF - x).  Every dword by its static index (a run-time index puts the
-// array in scratch).
+// Segment q's plaintext [0, 64) — the template's header with the segment's
+// fields, then the payload — stored at hdst (the segment slot, where the
+// headers-only split would have written it; the encryption reads block 0
+// back from there like any split header, so its lanes' word sums cover the
+// header as stored).  The IP fields sit at fixed dwords and are set in
+// registers; the L4 fields (TCP seq / flags, UDP length) sit at run-time
+// offsets and are stored over the written block byte by byte (selecting
+// dwords by a run-time index costs a select chain per dword).  rest: the L4
+// sum's terms other than the segment's words from block 0 on — pseudo-header
+// addresses, protocol, L4 length, and 32 * 0xFFFF minus block 0's words below
+// csum_start (subtracting x mod 0xFFFF is adding 0xFFFF - x), plus pv, the
+// two bytes at the checksum field once every field is set (the reference
+// sums them, then overwrites them, :202-204): the field is stored as zero
+// here (pv only differs from zero when the field overlaps the TCP seq or the
+// UDP length), so the encryption needs no register for pv and the end just
+// writes the checksum over a zero field.
 __device__ __forceinline__ void syn_block0(const SynSeg &q, uintptr_t psrc, uintptr_t hdst, uint32_t pktlen,
-                                           uint32_t &rest, uint32_t &pv) {
+                                           uint32_t &rest) {
     const uint32_t nin = pktlen < 64u ? pktlen : 64u;
     uint32_t T[16], M[16];
     if (nin == 64u && q.tlen >= 64u) {
@@ -690,17 +696,17 @@ __device__ __forceinline__ void syn_block0(const SynSeg &q, uintptr_t psrc, uint
             }
         }
     } else {
+        // a real branch, taken only for short segments / super-buffers
+        asm volatile("" ::: "memory");
         load64(q.tpl, q.hdr, T);  // the template (split super-buffers hold >= hdr bytes)
         load64(psrc, nin, M);     // payload byte j of the segment at psrc + j (j >= hdr), zero past nin
     }
-    const uint32_t cw = q.cs >> 2, fw = q.l4off >> 2;
+    const uint32_t hw4 = q.hdr >> 2, cw = q.cs >> 2;  // both multiples of 4 (syn_eligible)
     const uint32_t l4len = bswap16((pktlen - q.cs) & 0xffffu);
-    uint32_t ips = 0, ps = 0, p = 0;
+    uint32_t ips = 0, ps = 0;
 #pragma unroll
     for (uint32_t m = 0; m < 16; m++) {
-        const uint32_t k = q.hdr > 4u * m ? (q.hdr - 4u * m < 4u ? q.hdr - 4u * m : 4u) : 0u;  // template bytes
-        const uint32_t mk = k >= 4u ? ~0u : (1u << (8u * k)) - 1u;
-        uint32_t w = (T[m] & mk) | (M[m] & ~mk);
+        uint32_t w = m < hw4 ? T[m] : M[m];
         if (m == 0u && !q.v6)
             w = (w & 0xffffu) | (bswap16(pktlen & 0xffffu) << 16);  // ip_len (offload.cpp:183)
         if (m == 1u) {
@@ -709,20 +715,11 @@ __device__ __forceinline__ void syn_block0(const SynSeg &q, uintptr_t psrc, uint
             else
                 w = (w & 0xffff0000u) | l4len;  // ip6_plen (:170-172)
         }
-        if (m >= 5u) {  // the L4 header starts at dword cw >= 5
-            if (q.tcp && m == cw + 1u)
-                w = bswap32(bswap32(w) + q.gso * q.idx);  // seq (:192), seq0 read after the :149 zeroing
-            if (q.tcp && m == cw + 3u && !q.last)
-                w &= ~0x0900u;  // FIN / PSH on the last segment only (:193-195)
-            if (!q.tcp && m == cw + 1u)
-                w = (w & 0xffff0000u) | l4len;  // udp len (:199)
-        }
         M[m] = w;
         if (m < 15u)
             ips = m < cw ? hacc(ips, w) : ips;  // [0, cs), ip_sum zero (cw <= 14)
         if (m >= 2u && m < 10u)
             ps = (q.v6 || m == 3u || m == 4u) ? hacc(ps, w) : ps;  // addresses: v6 8-39, v4 12-19
-        p = m == fw ? w : p;
     }
     const uint32_t ipcs = ~fold16_32(ips) & 0xffffu;
     if (!q.v6)
@@ -733,9 +730,30 @@ __device__ __forceinline__ void syn_block0(const SynSeg &q, uintptr_t psrc, uint
     } else {
         store_n(hdst, M, nin);
     }
-    pv = (p >> (8u * (q.l4off & 2u))) & 0xffffu;
+    const uintptr_t l4 = hdst + q.cs, t4 = q.tpl + q.cs;
+    const uint32_t f0 = q.l4off - q.cs - 4u, f1 = f0 + 1u;  // the field's bytes from L4 byte 4 (wrap: none)
+    uint32_t pv;
+    if (q.tcp) {
+        // seq (:192; seq0 read after the :149 zeroing) and FIN / PSH on the
+        // last segment only (:193-195)
+        const uint32_t s0 = (ld8(t4 + 4) << 24) | (ld8(t4 + 5) << 16) | (ld8(t4 + 6) << 8) | ld8(t4 + 7);
+        const uint32_t sq = s0 + q.gso * q.idx;
+        st8b(l4 + 4, sq >> 24);
+        st8b(l4 + 5, sq >> 16);
+        st8b(l4 + 6, sq >> 8);
+        st8b(l4 + 7, sq);
+        if (!q.last)
+            st8b(l4 + 13, ld8(t4 + 13) & ~0x09u);  // (a flags byte inside the field is zero already)
+        pv = (f0 < 4u ? (sq >> (24u - 8u * f0)) & 0xffu : 0u) | ((f1 < 4u ? (sq >> (24u - 8u * f1)) & 0xffu : 0u) << 8);
+    } else {
+        st8b(l4 + 4, l4len);  // udp len (:199)
+        st8b(l4 + 5, l4len >> 8);
+        pv = (f0 < 2u ? (l4len >> (8u * f0)) & 0xffu : 0u) | ((f1 < 2u ? (l4len >> (8u * f1)) & 0xffu : 0u) << 8);
+    }
+    st8b(hdst + q.l4off, 0u);  // the field zero until the checksum is written
+    st8b(hdst + q.l4off + 1u, 0u);
     const uint32_t hw = ips + (q.v6 ? 0u : ipcs);  // block 0's words below csum_start, as stored
-    rest = ps + ((q.tcp ? 6u : 17u) << 8) + l4len + (32u * 0xffffu - hw);
+    rest = ps + ((q.tcp ? 6u : 17u) << 8) + l4len + pv + (32u * 0xffffu - hw);
 }
 
 // kDec = false: encrypt packet i (bytes [i*seg, +len) of `in`) into the data
@@ -805,8 +823,8 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
     uintptr_t send = 0;
     // kSyn: this segment's header is built here (syn_block0) when eligible
     bool syn = false;
-    uint32_t syn_l4 = 0;  // the checksum field's offset
-    uint32_t syn_rp = 0;  // the rest of the L4 sum folded to 16 bits | the field's bytes before << 16
+    // the rest of the L4 sum folded to 16 bits | the checksum field's offset << 16
+    uint32_t syn_rl = 0;
     if constexpr (kGso) {
         sb = ii / p.gm;
         gs = (uint32_t)(ii - sb * p.gm);
@@ -828,7 +846,7 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                 // here); the lane reads block 0 back from the slot later
                 const uint32_t cs = gd.vnet.csum_start, l4 = cs + gd.vnet.csum_offset;
                 syn = live && !gr.passthrough && syn_eligible(gr.hdr_len, cs, l4);
-                syn_l4 = l4;
+                syn_rl = l4 << 16;
                 if (syn && g == 0u) {
                     SynSeg sq;
                     sq.tpl = reinterpret_cast<uintptr_t>(p.gin) + gd.in_offset;
@@ -841,9 +859,9 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                     sq.tcp = gd.vnet.gso_type == 1u || gd.vnet.gso_type == 4u;  // unmasked (:151): TCP|ECN is fixed up as UDP
                     sq.v6 = gr.isv6;
                     sq.last = gs + 1u == er.nmsg;
-                    uint32_t rest, pv;
-                    syn_block0(sq, gsrc, hsrc, len, rest, pv);
-                    syn_rp = fold16_32(rest) | (pv << 16);
+                    uint32_t rest;
+                    syn_block0(sq, gsrc, hsrc, len, rest);
+                    syn_rl |= fold16_32(rest);
                 }
             }
         } else {
@@ -974,16 +992,17 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                 }
             }
             const L5 rb = l5_sel(b >= 2u, r2, l5_sel(b == 1u, r, l5_one()));
-            const L5 QB = l5_sel(b == 3u, l5_mul(rb, r), rb);  // r^3 = r^2 r
+            const L5 r3 = l5_mul(r2, r);
+            const L5 QB = l5_sel(b == 3u, r3, rb);
             S = l5_sel(b == 0u, QA, l5_sel(a4 == 0u, QB, l5_mul(QA, QB)));
             if constexpr (kSyn) {
                 // chunk k opens group lane 0's Horner sum at block 0 (1 <= k
-                // <= 3, nq <= 4K: e <= 11)
-                const uint32_t e = syn && g == 0u && nq > syn_l4 / 16u ? nq - syn_l4 / 16u : 0u;
-                const L5 WA = l5_sel(e >= 8u, l5_mul(r4, r4), l5_sel(e >= 4u, r4, l5_one()));
+                // <= 3; lane 0's first counter is the key: nq <= 4(K - 1),
+                // e <= 7)
+                const uint32_t e = syn && g == 0u && nq > (syn_rl >> 20) ? nq - (syn_rl >> 20) : 0u;
                 const uint32_t eb = e & 3u;
-                const L5 wb = l5_sel(eb >= 2u, r2, l5_sel(eb == 1u, r, l5_one()));
-                synw = l5_mul(WA, l5_sel(eb == 3u, l5_mul(wb, r), wb));
+                const L5 WB = l5_sel(eb == 3u, r3, l5_sel(eb == 2u, r2, l5_sel(eb == 1u, r, l5_one())));
+                synw = l5_mul(l5_sel(e >= 4u, r4, l5_one()), WB);
             }
         }
         L5 E;
@@ -1210,21 +1229,42 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                     }
                 }
             }
-            // the segment's L4 word total into group lane 0 (down-shift tree)
-            uint32_t L = psum;
-            for (uint32_t o = 1; o < GG; o <<= 1) {  // wave-uniform trip count
-                const uint32_t t = grp_down_rt(L, lane, g, GG, o);
-                if (g + o < GG)
-                    L += t;
+        }
+    }
+    // the length block: le64(0) || le64(pad / payload length), times r
+    const uint32_t mlen = kDec ? plen : pad;  // AEAD ct length (encrypt: the padded plaintext)
+    const L5 lenblk = l5_from_words(0u, 0u, mlen, 0u, 1u);
+    if (g == 0u && act)
+        acc = l5_add(acc, lenblk);
+    // group sum, times r (every term's last factor), every lane finishes
+    L5 tot;
+    if constexpr (kFlex) {
+        // reduction tree by down-shifts (lane g sums [g, g + 2^k)), then the
+        // group's first lane broadcasts: any group size
+        L5 a = l5_norm(acc);
+        uint32_t L = psum;  // kSyn: the segment's L4 words, summed along
+        for (uint32_t o = 1; o < GG; o <<= 1) {
+            const L5 t = l5_down_rt(a, lane, g, GG, o);
+            uint32_t tl = 0;
+            if constexpr (kSyn)
+                tl = grp_down_rt(L, lane, g, GG, o);
+            if (g + o < GG) {
+                a = l5_add(a, t);
+                L += tl;
             }
+        }
+        if constexpr (kSyn) {
+            // group lane 0 now holds the segment's L4 word total: the
+            // checksum, and the MAC's correction added to the group's sum
             if (syn && g == 0u) {
-                const uint32_t l4cs = ~fold16_32(fold16_32(L) + (syn_rp & 0xffffu)) & 0xffffu;  // stored native (offload.cpp:202-204)
-                // block 0 was encrypted with syn_pv at the field: its two
+                const uint32_t l4cs = ~fold16_32(fold16_32(L) + (syn_rl & 0xffffu)) & 0xffffu;  // stored native (offload.cpp:202-204)
+                // block 0 was encrypted with a zero field: its two
                 // ciphertext bytes in the staged message, then the MAC
                 uint16_t *lb = reinterpret_cast<uint16_t *>(aead_lds);
+                const uint32_t syn_l4 = syn_rl >> 16;
                 const uint32_t hw = (lslot * 16u + 16u + syn_l4) >> 1;
                 const uint32_t oc = lb[hw];
-                const uint32_t nc = (oc ^ (syn_rp >> 16) ^ l4cs) & 0xffffu;
+                const uint32_t nc = (oc ^ l4cs) & 0xffffu;
                 lb[hw] = (uint16_t)nc;
                 st8b(hsrc + syn_l4, l4cs);  // and the segment's header in the slot
                 st8b(hsrc + syn_l4 + 1u, l4cs >> 8);
@@ -1244,25 +1284,8 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                 const uint32_t *lw = reinterpret_cast<const uint32_t *>(aead_lds);
                 const v4u w4 = aead_lds[lslot];
                 const L5 synw{{w4[0], w4[1], w4[2], w4[3], lw[4u * (lslot + 1u + pad / 16u)]}};
-                acc = l5_add(acc, l5_mul(dl, synw));
+                a = l5_add(a, l5_mul(dl, synw));
             }
-        }
-    }
-    // the length block: le64(0) || le64(pad / payload length), times r
-    const uint32_t mlen = kDec ? plen : pad;  // AEAD ct length (encrypt: the padded plaintext)
-    const L5 lenblk = l5_from_words(0u, 0u, mlen, 0u, 1u);
-    if (g == 0u && act)
-        acc = l5_add(acc, lenblk);
-    // group sum, times r (every term's last factor), every lane finishes
-    L5 tot;
-    if constexpr (kFlex) {
-        // reduction tree by down-shifts (lane g sums [g, g + 2^k)), then the
-        // group's first lane broadcasts: any group size
-        L5 a = l5_norm(acc);
-        for (uint32_t o = 1; o < GG; o <<= 1) {
-            const L5 t = l5_down_rt(a, lane, g, GG, o);
-            if (g + o < GG)
-                a = l5_add(a, t);
         }
 #pragma unroll
         for (int k = 0; k < 5; k++)

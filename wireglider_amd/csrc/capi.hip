@@ -161,7 +161,10 @@ static Tune &tune_storage() {
         // -1.0 %, encap -2.9 % (profiles/r04_aead_stage/)
         x.aead_stage = 1;
         x.encap_parts = 1;
-        x.encap_synth = 0;
+        // wg_encap_batch: the AEAD builds the segment headers, the split only
+        // plans: config 3's super-buffers 16.99 -> 14.96 ms
+        // (profiles/r04_encap_synth/)
+        x.encap_synth = 1;
         // environment overrides: WG_<KNOB> (upper case), same accepted values
         // as wg_tune_set; anything else is ignored
         for (const Knob &k : kKnobs) {

@@ -185,15 +185,15 @@ __device__ __forceinline__ uint32_t encap_fit(uint64_t out_len, uint32_t S, uint
 
 // wg_encap_batch header synthesis (knob encap_synth, aead.hip): a split
 // super-buffer whose segments' headers the AEAD builds itself — the header in
-// one 64-B block, the L4 sum starting on a dword (the lanes' word sums then
-// pair as the checksum does), the checksum field 2-B aligned, csum_start past
+// whole dwords of one 64-B block (every TCP / UDP header is), the L4 sum
+// starting on a dword (the lanes' word sums then pair as the checksum does), the checksum field 2-B aligned, csum_start past
 // the 20-B IPv4 header (the classification guarantees it for split plans; the
 // MAC correction assumes the field lies past the block's first 16 bytes).
 // The headers-only split skips exactly these (gso.hip), the AEAD builds
 // exactly these.
 __device__ __forceinline__ bool syn_eligible(uint32_t hdr_len, uint32_t cs, uint32_t l4off) {
-    return hdr_len <= 64u && cs >= 20u && (cs & 3u) == 0u && (l4off & 1u) == 0u && l4off + 2u <= hdr_len &&
-           cs + 8u <= hdr_len;
+    return hdr_len <= 64u && (hdr_len & 3u) == 0u && cs >= 20u && (cs & 3u) == 0u && (l4off & 1u) == 0u &&
+           l4off + 2u <= hdr_len && cs + 8u <= hdr_len;
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
