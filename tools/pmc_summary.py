@@ -42,6 +42,7 @@ STEP_KERNELS = {
     "verify1500u": ["verify_"],
     "gro": ["gro_finalize"],
     "aead": ["aead_kernel"],
+    "encap": ["gso_plan_kernel", "gso_split_kernel", "gso_finalize_kernel", "encap_scan", "aead_kernel"],
 }
 
 
