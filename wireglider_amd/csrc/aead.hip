@@ -593,7 +593,6 @@ struct HdrGate {
     bool l4;
 };
 
-__device__ __forceinline__ uint32_t hsum32(uint32_t w) { return (w & 0xffffu) + (w >> 16); }
 // acc + both 16-bit halves of w in one instruction (v_sad_u16 against zero)
 __device__ __forceinline__ uint32_t hacc(uint32_t acc, uint32_t w) { return __builtin_amdgcn_sad_u16(w, 0u, acc); }
 
@@ -608,7 +607,7 @@ __device__ __forceinline__ HdrGate hdr_gate(const uint32_t R[16], uint32_t len) 
     bool ip_ok = false;
     if (len >= h.ihs && len <= 65535u) {  // evaluator.hpp:118-121
         if (!v6) {
-            const uint32_t hs = hsum32(R[0]) + hsum32(R[1]) + hsum32(R[2]) + hsum32(R[3]) + hsum32(R[4]);
+            const uint32_t hs = hacc(hacc(hacc(hacc(hacc(0u, R[0]), R[1]), R[2]), R[3]), R[4]);
             ip_ok = (b0 & 0xfu) == 5u &&                      // ip_hl, evaluator.cpp:19
                     len == bswap16(R[0] >> 16) &&              // ip_len, :21
                     (bswap16(R[1] >> 16) & ~0x4000u) == 0 &&  // ip_off & ~IP_DF, :24
@@ -631,8 +630,8 @@ __device__ __forceinline__ HdrGate hdr_gate(const uint32_t R[16], uint32_t len) 
     }
 #pragma unroll
     for (uint32_t m = 0; m < 10; m++) {
-        h.hsum += 4u * m < h.ihs ? hsum32(R[m]) : 0u;
-        h.asum += (v6 ? (m >= 2u && m < 10u) : (m == 3u || m == 4u)) ? hsum32(R[m]) : 0u;  // v6 8-39, v4 12-19
+        h.hsum = 4u * m < h.ihs ? hacc(h.hsum, R[m]) : h.hsum;
+        h.asum = (v6 ? (m >= 2u && m < 10u) : (m == 3u || m == 4u)) ? hacc(h.asum, R[m]) : h.asum;  // v6 8-39, v4 12-19
     }
     return h;
 }

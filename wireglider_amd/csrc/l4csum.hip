@@ -164,7 +164,8 @@ __global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSmallMax = 64;  // bytes: five aligned 16-B chunks at any alignment
 
-__device__ __forceinline__ uint32_t half_sum(uint32_t w) { return (w & 0xffffu) + (w >> 16); }
+// acc + both 16-bit halves of w in one instruction (v_sad_u16 against zero)
+__device__ __forceinline__ uint32_t hacc(uint32_t acc, uint32_t w) { return __builtin_amdgcn_sad_u16(w, 0u, acc); }
 
 // Packet-relative dword m (bytes 4m .. 4m+3 of the packet): keep the bytes
 // at positions < lim / >= lo.
@@ -217,10 +218,12 @@ __device__ __forceinline__ uint32_t lane_sum(const v4u W[5], uintptr_t a, uint32
         const uint32_t lo = q4 == 0 ? Wd[m] : q4 == 1 ? Wd[m + 1] : q4 == 2 ? Wd[m + 2] : Wd[m + 3];
         const uint32_t hi = q4 == 0 ? Wd[m + 1] : q4 == 1 ? Wd[m + 2] : q4 == 2 ? Wd[m + 3] : Wd[m + 4];
         const uint32_t r = bytes_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, len);
-        sr += half_sum(bytes_from(r, m, o0));
+        sr = hacc(sr, bytes_from(r, m, o0));
         if (kL4) {
-            const bool in_addr = v6 ? (m >= 2u && m < 10u) : (m == 3u || m == 4u);  // v6 8-39, v4 12-19
-            sq += in_addr ? half_sum(r) : 0u;
+            if (m == 3u || m == 4u)  // v6 8-39, v4 12-19
+                sq = hacc(sq, r);
+            else if (m >= 2u && m < 10u)
+                sq = v6 ? hacc(sq, r) : sq;
         }
     }
     sr = fold16_32(sr);
@@ -789,8 +792,7 @@ __device__ __forceinline__ void verify_lane_decode(const v4u W[5], uintptr_t a, 
         uint32_t proto = 0;
         if (len >= ihs) {  // evaluator.hpp:118-121 (len <= 64 here)
             if (!v6) {
-                const uint32_t hs = half_sum(R[0]) + half_sum(R[1]) + half_sum(R[2]) + half_sum(R[3]) +
-                                    half_sum(R[4]);
+                const uint32_t hs = hacc(hacc(hacc(hacc(hacc(0u, R[0]), R[1]), R[2]), R[3]), R[4]);
                 ip_ok = (b0 & 0xfu) == 5u &&                                  // ip_hl, evaluator.cpp:19
                         len == bswap16(R[0] >> 16) &&                          // ip_len, :21
                         (bswap16(R[1] >> 16) & ~0x4000u) == 0 &&              // ip_off & ~IP_DF, :24
@@ -813,13 +815,12 @@ __device__ __forceinline__ void verify_lane_decode(const v4u W[5], uintptr_t a, 
             }
         }
         if (l4) {  // calc_l4_checksum(pkt, isv6, istcp, ihs), checksum.cpp:8-36
+            // the addresses (v6 bytes 8-39, v4 12-19) and the L4 bytes from
+            // ihs (40 / 20) are each dword from 2 (v6) / 3 (v4) on, once
             uint32_t sum = (proto << 8) + bswap16((len - ihs) & 0xffffu);
+            sum = v6 ? hacc(sum, R[2]) : sum;
 #pragma unroll
-            for (uint32_t m = 2; m < 16; m++) {
-                const bool in_l4 = 4u * m >= ihs;
-                const bool in_addr = v6 ? m < 10u : (m == 3u || m == 4u);  // v6 bytes 8-39, v4 12-19
-                sum += (in_l4 ? half_sum(R[m]) : 0u) + (in_addr ? half_sum(R[m]) : 0u);
-            }
+            for (uint32_t m = 3; m < 16; m++) sum = hacc(sum, R[m]);
             c = ~fold16_32(sum) & 0xffffu;
             if (c == 0)
                 v |= WG_VERDICT_L4_OK;
