@@ -321,8 +321,7 @@ static void aead_parallel(aead_job proto, uint64_t n, int threads) {
         if (threads == 1)
             aead_job_run(&jobs[t]);
         else {
-            pthread_create(&tid[t], NULL, aead_job_run, &jobs[t]);
-            orc_pin_thread(tid[t], t);
+            orc_spawn(&tid[t], t, aead_job_run, &jobs[t]);
         }
     }
     if (threads > 1)

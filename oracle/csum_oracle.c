@@ -340,8 +340,7 @@ static void run_parallel(job_t proto, uint64_t n, int threads) {
         jobs[t] = proto;
         jobs[t].lo = n * (uint64_t)t / (uint64_t)threads;
         jobs[t].hi = n * (uint64_t)(t + 1) / (uint64_t)threads;
-        pthread_create(&tids[t], NULL, job_thread, &jobs[t]);
-        orc_pin_thread(tids[t], t);
+        orc_spawn(&tids[t], t, job_thread, &jobs[t]);
     }
     for (int t = 0; t < threads; t++)
         pthread_join(tids[t], NULL);

@@ -75,8 +75,9 @@ int oss_wg_encrypt_batch(const uint8_t key[32], uint32_t rx, uint64_t c0, const 
                         n * (uint64_t)(t + 1) / (uint64_t)threads, 0};
         if (threads == 1)
             run(&jobs[t]);
-        else
-            pthread_create(&tid[t], NULL, run, &jobs[t]), orc_pin_thread(tid[t], t);
+        else {
+            orc_spawn(&tid[t], t, run, &jobs[t]);
+        }
     }
     int rc = 0;
     for (int t = 0; t < threads; t++) {
@@ -147,8 +148,9 @@ int oss_wg_decrypt_batch(const uint8_t key[32], const uint8_t *in, uint64_t tota
                          n * (uint64_t)(t + 1) / (uint64_t)threads, 0};
         if (threads == 1)
             drun(&jobs[t]);
-        else
-            pthread_create(&tid[t], NULL, drun, &jobs[t]), orc_pin_thread(tid[t], t);
+        else {
+            orc_spawn(&tid[t], t, drun, &jobs[t]);
+        }
     }
     int rc = 0;
     for (int t = 0; t < threads; t++) {
