@@ -1040,11 +1040,15 @@ def build_encap(wga, torch, rank: int, world: int, dev, fused: bool = True) -> W
            "entry": "wg_encap_batch" if fused else "wg_gso_split + wg_encap_encrypt"}
     # the split reads the input and writes the segments (fused: only each
     # segment's header block, pad64(hdr) bytes); the AEAD reads every
-    # segment's plaintext once and writes the messages
+    # segment's plaintext once and writes the messages (synthesis: the AEAD
+    # is the only reader of the input and writes the header blocks itself)
     split_w = n * nseg * ((hdr + 63) // 64 * 64) if fused else n * out_len
-    alg = (n * in_len + split_w + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES)
-           + n * out_len + n * mbytes + n * (wga.ENCAP_RESULT_BYTES + 8))
     aead_k = aead_kernel_symbol(wga, seg, gso=2 if fused else 1)
+    # with header synthesis (the AEAD builds the headers while it encrypts)
+    # the input is read once: no separate pass of the segments
+    synth = fused and "true>(" in aead_k
+    alg = (n * in_len + split_w + n * (wga.GSO_DESC_BYTES + wga.GSO_RESULT_BYTES)
+           + (0 if synth else n * out_len) + n * mbytes + n * (wga.ENCAP_RESULT_BYTES + 8))
     return Workload(launch, n, n * in_len, alg, cfg, "weak", buf,
                     ("wg_encap_batch (plan + finalize kernels, the headers-only split walking the list of "
                      "super-buffers left to it (none here: the AEAD synthesizes every segment header), "

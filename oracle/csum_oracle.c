@@ -14,6 +14,7 @@
 #include <pthread.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 /* ------------------------------------------------------------------------ */
 /* Scalar arithmetic                                                        */
@@ -314,12 +315,68 @@ static void run_job(job_t *j) {
     }
 }
 
-static void *job_thread(void *arg) {
-    run_job((job_t *)arg);
+#define ORC_MAX_THREADS 256
+
+/* Persistent worker pool for the timed parallel runs (bench.py's CPU
+ * baseline calls the same function back to back for seconds; a 64-B verify or
+ * GRO call is ~1 ms of work, and creating + pinning + joining 16 threads per
+ * call put the neighbours' scheduling noise into every repetition).  Workers
+ * are created pinned (orc_spawn) and kept; a new thread count or a new
+ * ORC_CPUS list (bench.py re-picks the quietest CPUs before each repetition)
+ * rebuilds the pool.  Calls are serialised by pool_mu: the oracle is driven
+ * from one thread. */
+static struct {
+    pthread_mutex_t mu;
+    pthread_cond_t go, done;
+    pthread_t tid[ORC_MAX_THREADS];
+    job_t *jobs;
+    int threads;
+    unsigned long gen;   /* bumped per call (and to stop the workers: stop = 1) */
+    int pending, stop;
+    char cpus[4096];     /* the ORC_CPUS the workers were pinned under */
+    pid_t pid;           /* the process that made them (a forked child has none) */
+} pool = {.mu = PTHREAD_MUTEX_INITIALIZER, .go = PTHREAD_COND_INITIALIZER, .done = PTHREAD_COND_INITIALIZER};
+static pthread_mutex_t pool_mu = PTHREAD_MUTEX_INITIALIZER;
+
+typedef struct {
+    int idx;
+    unsigned long seen;  /* pool.gen when the worker was made: it runs the calls after that */
+} worker_arg;
+static worker_arg pool_args[ORC_MAX_THREADS];
+
+static void *pool_worker(void *arg) {
+    const int idx = ((worker_arg *)arg)->idx;
+    unsigned long seen = ((worker_arg *)arg)->seen;
+    pthread_mutex_lock(&pool.mu);
+    for (;;) {
+        while (pool.gen == seen && !pool.stop)
+            pthread_cond_wait(&pool.go, &pool.mu);
+        if (pool.stop)
+            break;
+        seen = pool.gen;
+        job_t *j = &pool.jobs[idx];
+        pthread_mutex_unlock(&pool.mu);
+        run_job(j);
+        pthread_mutex_lock(&pool.mu);
+        if (--pool.pending == 0)
+            pthread_cond_signal(&pool.done);
+    }
+    pthread_mutex_unlock(&pool.mu);
     return NULL;
 }
 
-#define ORC_MAX_THREADS 256
+static void pool_stop(void) {
+    if (!pool.threads)
+        return;
+    pthread_mutex_lock(&pool.mu);
+    pool.stop = 1;
+    pthread_cond_broadcast(&pool.go);
+    pthread_mutex_unlock(&pool.mu);
+    for (int t = 0; t < pool.threads; t++)
+        pthread_join(pool.tid[t], NULL);
+    pool.threads = 0;
+    pool.stop = 0;
+}
 
 static void run_parallel(job_t proto, uint64_t n, int threads) {
     if (threads < 1)
@@ -334,16 +391,49 @@ static void run_parallel(job_t proto, uint64_t n, int threads) {
         run_job(&proto);
         return;
     }
-    pthread_t tids[ORC_MAX_THREADS];
     job_t jobs[ORC_MAX_THREADS];
     for (int t = 0; t < threads; t++) {
         jobs[t] = proto;
         jobs[t].lo = n * (uint64_t)t / (uint64_t)threads;
         jobs[t].hi = n * (uint64_t)(t + 1) / (uint64_t)threads;
-        orc_spawn(&tids[t], t, job_thread, &jobs[t]);
     }
-    for (int t = 0; t < threads; t++)
-        pthread_join(tids[t], NULL);
+    pthread_mutex_lock(&pool_mu);
+    if (pool.threads && pool.pid != getpid())
+        pool.threads = 0;  /* forked: the parent's workers do not exist here */
+    const char *cpus = getenv("ORC_CPUS");
+    if (!cpus)
+        cpus = "";
+    if (pool.threads != threads || strncmp(pool.cpus, cpus, sizeof pool.cpus) != 0) {
+        pool_stop();
+        strncpy(pool.cpus, cpus, sizeof pool.cpus - 1);
+        pool.cpus[sizeof pool.cpus - 1] = 0;
+        int made = 0;
+        for (int t = 0; t < threads; t++) {
+            pool_args[t].idx = t;
+            pool_args[t].seen = pool.gen;
+            if (orc_spawn(&pool.tid[t], t, pool_worker, &pool_args[t]) != 0)
+                break;
+            made++;
+        }
+        pool.threads = made;
+        pool.pid = getpid();
+        if (made != threads) {  /* no pool: run here */
+            pool_stop();
+            pthread_mutex_unlock(&pool_mu);
+            for (int t = 0; t < threads; t++)
+                run_job(&jobs[t]);
+            return;
+        }
+    }
+    pthread_mutex_lock(&pool.mu);
+    pool.jobs = jobs;
+    pool.pending = threads;
+    pool.gen++;
+    pthread_cond_broadcast(&pool.go);
+    while (pool.pending)
+        pthread_cond_wait(&pool.done, &pool.mu);
+    pthread_mutex_unlock(&pool.mu);
+    pthread_mutex_unlock(&pool_mu);
 }
 
 void orc_l4_uniform(const uint8_t *base, uint64_t total_len, uint32_t segment_size,
