@@ -640,18 +640,21 @@ constexpr uint64_t kRejectAfterMessages = ~0ull - (1ull << 13);  // include/prot
 
 // ---------------------------------------------------------------------------
 // Encap header synthesis (wg_encap_batch, knob encap_synth).  A split
-// segment's first 64 bytes are built in the lane that encrypts them, from the
-// tun super-buffer itself: its prefix (ip_sum and the L4 checksum field zeroed
-// by the split's finalize pass, worker/offload.cpp:145-149) with the
-// segment's fields (:168-199), then the payload.  The L4 checksum needs the
-// whole segment's words, which the group's lanes sum as they encrypt their
-// blocks; block 0 is encrypted with the field as it stands before the
-// checksum is written, and at the end its two ciphertext bytes and the MAC
-// are corrected (Poly1305 is linear in each 16-B block).  So the split pass
-// only plans and finalizes these super-buffers: no per-segment wave, no
-// payload read besides the encryption's own.  Eligible: hdr_len <= 64,
-// csum_start a multiple of 4, the checksum field 2-B aligned (every IPv4 /
-// IPv6 TCP or UDP header); other super-buffers keep the split's segments.
+// segment's first 64 bytes are built by its group's lane 0 before the
+// keystream, from the tun super-buffer itself: its prefix (ip_sum and the L4
+// checksum field zeroed by the split's finalize pass,
+// worker/offload.cpp:145-149) with the segment's fields (:168-199), then the
+// payload, stored where the headers-only split would have written them.  The
+// L4 checksum needs the whole segment's words, which the group's lanes sum
+// as they encrypt their blocks (the totals ride along in the tag's group
+// reduction); block 0 is encrypted with the field at zero, and at the end its
+// two ciphertext bytes and the MAC are corrected (Poly1305 is linear in each
+// 16-B block).  So the split pass only plans and finalizes these
+// super-buffers: no per-segment wave, no payload read besides the
+// encryption's own.  Eligible (syn_eligible, wg_device.hpp): the header in
+// whole dwords of one 64-B block, csum_start a multiple of 4, the checksum
+// field 2-B aligned — every plain IPv4 / IPv6 TCP or UDP header; other
+// super-buffers keep the split's segments.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
