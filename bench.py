@@ -1056,6 +1056,7 @@ def build_encap(wga, torch, rank: int, world: int, dev, fused: bool = True) -> W
                      "wg_encap_batch (3 split kernels, headers only, + 2 scan kernels + %s)" if fused else
                      "wg_gso_split (3 kernels) + wg_encap_encrypt (2 scan kernels + %s)") % aead_k,
                     rank * n, sample=sample, counts=[n] * world, post=post, copy_dst=msgs,
+                    valu_kernel=aead_k if synth else None,
                     metric="device-resident GiB/s of tun input, GSO split + data-message encryption (encap worker)")
 
 
