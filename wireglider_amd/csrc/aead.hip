@@ -1333,16 +1333,28 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             const uint32_t mch = act ? (32u + pad) / 16u : 0u;  // the message's 16-B chunks
             const uint32_t dlo = (uint32_t)dst, dhi = (uint32_t)(dst >> 32);
             const uint32_t wl = wave_in_block() * p.lds_wave / 16u;
-            for (uint32_t s = 0; s < kPer; s++) {  // wave-uniform
-                const int src_lane = (int)(s * GG);
-                const uint32_t n16 = (uint32_t)__builtin_amdgcn_readlane((int)mch, src_lane);
-                if (n16 == 0u)
-                    continue;
-                const uintptr_t base = (uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)dlo, src_lane) |
-                                       ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)dhi, src_lane) << 32);
-                const uint32_t ls = wl + s * p.lstride / 16u;
-                for (uint32_t t = lane; t < n16; t += 64u)
-                    st16(base + 16u * t, aead_lds[ls + t]);
+            const uint32_t l16 = p.lstride / 16u;
+            // every slot a full-size message and the wave's messages back to
+            // back in memory as they are in LDS (consecutive packets; a
+            // super-buffer's segments): one flat copy of the whole run
+            const uintptr_t base0 = (uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)dlo, 0) |
+                                    ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)dhi, 0) << 32);
+            const bool off = g == 0u && slot < kPer && (mch != l16 || dst != base0 + (uint64_t)slot * p.lstride);
+            if (__ballot(off) == 0ull) {
+                for (uint32_t t = lane; t < kPer * l16; t += 64u)
+                    st16(base0 + 16u * t, aead_lds[wl + t]);
+            } else {
+                for (uint32_t s = 0; s < kPer; s++) {  // wave-uniform
+                    const int src_lane = (int)(s * GG);
+                    const uint32_t n16 = (uint32_t)__builtin_amdgcn_readlane((int)mch, src_lane);
+                    if (n16 == 0u)
+                        continue;
+                    const uintptr_t base = (uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)dlo, src_lane) |
+                                           ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)dhi, src_lane) << 32);
+                    const uint32_t ls = wl + s * l16;
+                    for (uint32_t t = lane; t < n16; t += 64u)
+                        st16(base + 16u * t, aead_lds[ls + t]);
+                }
             }
         }
     } else {
