@@ -446,10 +446,11 @@ __device__ __forceinline__ void poly_finish(L5 h, const uint32_t s[4], uint32_t 
 static __device__ v4u g_aead_zero16;
 
 __device__ __forceinline__ uint32_t keep_below(uint32_t w, uint32_t m, uint32_t lim) {
-    // bytes of dword m below lim, clamped to 0..4; the mask by a 64-bit
-    // shift so 4 bytes need no special case (branch-free)
-    const uint32_t k = lim > 4u * m ? (lim - 4u * m < 4u ? lim - 4u * m : 4u) : 0u;
-    return w & (uint32_t)((1ull << (8u * k)) - 1ull);
+    // bytes of dword m below lim: all of them, none, or the low lim % 4 of
+    // the one dword lim falls in (m is a compile-time index at every call:
+    // two compares against constants and one mask shared by the dwords)
+    const uint32_t part = (1u << (8u * (lim & 3u))) - 1u;
+    return lim >= 4u * m + 4u ? w : (lim > 4u * m ? w & part : 0u);
 }
 
 // The 64 bytes at a (of which the first `n` belong to the packet, n may be
