@@ -302,12 +302,14 @@ __global__ __launch_bounds__(256) void l4csum_uniform_small_kernel(L4Params p) {
 // wave-per-packet kernel's grid-stride iterations (consecutive packets per
 // wave measured 3-4 % slower).
 //  * WAVE role (every wave): every packet of its groups that hold a packet
-//    longer than kSmallMax, 2 at a time through the wave-per-packet
-//    machinery (4 at a time held 94 VGPRs, 5 waves per SIMD; 2 hold 74, 6:
-//    config 4's 64-B sub-batch -11.5 %, config 4 +0.7 %, config 5 -0.3 %,
-//    profiles/r04_q2_ab.txt); small packets among long ones ride along in
-//    their issue phase at next to no cost (config 4's mixed batch measured
-//    +2.5 % when they went to the lane role instead).
+//    longer than kSmallMax, one at a time through the wave-per-packet
+//    machinery.  The long-packet path sets the kernel's register budget and
+//    so the lane role's occupancy: 4 at a time held 94 VGPRs (5 waves per
+//    SIMD), 2 held 74 (6), 1 holds 64 (8) — config 4's 64-B sub-batch 64 ->
+//    56 -> 51 us, config 4 +0.7 % and +0.9 %, config 5 -0.3 % and 0 %
+//    (profiles/r04_q2_ab.txt, r04_q1_ab.txt).  Small packets among long ones
+//    ride along in their issue phase at next to no cost (config 4's mixed
+//    batch measured +2.5 % when they went to the lane role instead).
 //  * LANE role (wave 0): the block's all-small groups, a lane per packet,
 //    summed from its 5 aligned chunks (4 KiB of loads in flight per wave).
 // Wave 0 loads the block's 64 descriptors (lane l = descriptor
@@ -341,7 +343,7 @@ __global__ __launch_bounds__(256) void l4csum_split_kernel(L4Params p) {
     const bool own = wib == 0 ? (lane & 15u) < 4u : true;
     const bool mine = live && own && grp_long;
     uint32_t res = 0;
-    wave_long<kL4, kNT, 2, U>(__ballot(mine), a, len, cs, fl, p.base, lane, res);
+    wave_long<kL4, kNT, 1, U>(__ballot(mine), a, len, cs, fl, p.base, lane, res);
     if (mine)
         p.out[i] = (uint16_t)res;
     // ---- lane role (wave 0): the block's all-small groups
