@@ -79,6 +79,9 @@ def parse():
     ap.add_argument("--no-post", action="store_true",
                     help="skip the workload's own post-checks (PMC passes: only the step's launches of its kernels)")
     ap.add_argument("--no-strong", action="store_true", help="skip the config 5 strong-scaling companion")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="create the process group (WG_DIST_BACKEND, default nccl = RCCL) even at world size 1, "
+                         "so every collective of the multi-GPU path runs (the RCCL path checked on one GPU)")
     ap.add_argument("--cpu-seconds", type=float, default=2.0,
                     help="wall seconds of each CPU baseline repetition on all cores (half on one core); 8 repetitions each, the first dropped")
     ap.add_argument("--settle-seconds", type=float, default=0.3,
@@ -1140,10 +1143,10 @@ def wga_stride(seg: int) -> int:
     return 16 + (seg + 15) // 16 * 16 + 16
 
 
-def _rep_rates(fn, units: float, seconds: float, reps: int, before=None) -> list:
+def _rep_rates(fn, units: float, seconds: float, reps: int, before=None, after=None) -> list:
     """`reps` repetitions, each running fn() back to back until `seconds` of
-    wall time have passed (before() ahead of each, untimed); the rate (units
-    per second) of each repetition."""
+    wall time have passed (before() ahead of each and after() behind each,
+    untimed); the rate (units per second) of each repetition."""
     out = []
     for _ in range(reps):
         if before is not None:
@@ -1156,7 +1159,22 @@ def _rep_rates(fn, units: float, seconds: float, reps: int, before=None) -> list
             if t >= seconds:
                 break
         out.append(units * k / t)
+        if after is not None:
+            after()
     return out
+
+
+def _cpu_freqs_khz(cpus) -> list | None:
+    """scaling_cur_freq (kHz) of each CPU, or None where the host does not
+    expose it (read right after a repetition: the clock the pinned worker ran
+    at, to within the governor's sampling)."""
+    out = []
+    for c in cpus:
+        try:
+            out.append(int(Path(f"/sys/devices/system/cpu/cpu{c}/cpufreq/scaling_cur_freq").read_text()))
+        except Exception:
+            out.append(None)
+    return out if any(x is not None for x in out) else None
 
 
 def _spread(rates: list, scale: float) -> dict:
@@ -1194,20 +1212,29 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
     host, gpu_out, kind = sample_fn(npk)
     cores = oracle.host_cores()
     threads = cores["threads"]
-    # worker t on the t-th quietest CPU of the mask, one per physical core
-    # (oracle/orc_pin.h reads ORC_CPUS at the oracle's first threaded call)
+    # worker t on the t-th quietest CPU of the mask, one per physical core,
+    # picked ONCE per leg and kept for all its repetitions (re-picking before
+    # every repetition put the 1-core leg on cores of different speed:
+    # bimodal values in round 4); oracle/orc_pin.h reads ORC_CPUS at every
+    # thread start
     pin = os.environ.get("ORC_PIN", "1") != "0"
     picks = []
 
-    def repick(n):
-        # the n quietest CPUs right now (a neighbour's burst moves between
-        # repetitions); oracle/orc_pin.h reads ORC_CPUS at every thread start
+    def pick(n):
         if pin:
             q = oracle.quiet_cpus(n)
             os.environ["ORC_CPUS"] = ",".join(map(str, q["cpus"]))
             picks.append(q)
+            return q["cpus"]
+        return None
 
-    repick(threads)
+    reps_log = {"all": [], "one": []}
+
+    def logger(leg, cpus):
+        # each repetition's CPUs and their clock right after it
+        return lambda: reps_log[leg].append({"cpus": cpus, "cur_freq_khz": _cpu_freqs_khz(cpus) if cpus else None})
+
+    cpus_all = pick(threads)
     quiet = picks[0] if picks else None
     one_scale = 1.0  # the 1-core leg runs on 1/one_scale of the sample
     extra = {}
@@ -1365,9 +1392,13 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
     scale, unit = (1e-6, "Mflows/s") if kind[0] == "gro" else (2.0**-30, "GiB/s")
     run_all()  # first touch / warm-up, untimed
     thr0 = oracle.cgroup_throttling()
-    all_s = _spread(_rep_rates(run_all, nbytes, seconds, reps, lambda: repick(threads)), scale)
+    all_s = _spread(_rep_rates(run_all, nbytes, seconds, reps, after=logger("all", cpus_all)), scale)
     thr1 = oracle.cgroup_throttling()
-    one_s = _spread(_rep_rates(run_one, nbytes * one_scale, seconds / 2, reps, lambda: repick(1)), scale)
+    cpus_one = pick(1)
+    run_one()  # the 1-core leg's first touch on its CPU, untimed
+    one_s = _spread(_rep_rates(run_one, nbytes * one_scale, seconds / 2, reps, after=logger("one", cpus_one)), scale)
+    all_s["repetitions"] = reps_log["all"]
+    one_s["repetitions"] = reps_log["one"]
     if thr0 and thr1:
         # CPU-quota throttling while the all-core repetitions ran (a share of
         # 16 CPUs leaves no room for a 17th busy thread)
@@ -1396,15 +1427,17 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
         "spread_1core": one_s,
         "cpu_model": cpu_model,
         "host_cores": dict(cores, pinned_cpus=quiet["cpus"] if quiet else None,
+                           pinned_cpu_1core=cpus_one[0] if cpus_one else None,
                            pinned_cpus_busy_before=[q["busy"] for q in picks] if picks else None,
-                           pinning="before each repetition the quietest CPUs of the mask (0.3-s /proc/stat "
-                                   "sample), one worker per physical core" if pin else "off"),
+                           pinning="per leg, once before its repetitions: the quietest CPUs of the mask (0.3-s "
+                                   "/proc/stat sample), one worker per physical core, kept for every repetition "
+                                   "of the leg" if pin else "off"),
         "sample": f"first {npk} units of the same batch, oracle/csum_oracle.c "
                   f"({what}; {nofold} for spans >= 256 B), {threads} pthreads "
                   f"(sched_getaffinity {cores['affinity']}, cgroup quota {cores['cgroup_quota_cpus']}); "
                   f"value = median of {reps - 1} repetitions of >= {seconds:.1f} s after a dropped first one, "
-                  f"1 core: the same of >= {seconds / 2:.1f} s; before each repetition worker t pinned to the t-th "
-                  f"least busy CPU of the affinity mask, one per physical core (host_cores.pinning); "
+                  f"1 core: the same of >= {seconds / 2:.1f} s; worker t pinned to the t-th least busy CPU of the "
+                  f"affinity mask, one per physical core, picked once per leg (host_cores.pinning); "
                   f"bit-exact vs GPU: {parity}",
         "parity_with_gpu": parity,
         **extra,
@@ -1485,9 +1518,9 @@ def post_checks(torch, wga, wl: Workload, world: int, dev, no_post: bool = False
     wga.store_l4csum(wl.buf, wl.desc, wl.out)
     ver = wga.calc_l4_checksum_desc(wl.buf, wl.desc)
     bad = torch.count_nonzero(ver.to(torch.int32)).to(torch.int64).reshape(1)
-    if world > 1:
-        import torch.distributed as dist
+    import torch.distributed as dist
 
+    if dist.is_initialized():
         dist.all_reduce(bad, op=dist.ReduceOp.SUM)
     info["verify_nonzero"] = int(bad.item())
     return info
@@ -1528,7 +1561,7 @@ def time_steps(torch, wl: Workload, args, world: int, dev) -> dict:
     from wireglider_amd import dist as wdist
 
     def barrier():
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -1617,7 +1650,17 @@ def main():
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 or args.force_dist:
+        if world == 1:  # no launcher: a one-rank group on 127.0.0.1
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                import socket
+
+                with socket.socket() as so:
+                    so.bind(("127.0.0.1", 0))
+                    os.environ["MASTER_PORT"] = str(so.getsockname()[1])
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -1625,9 +1668,10 @@ def main():
         got = dist.get_world_size()
     else:
         got = 1
+    grouped = dist.is_initialized()
     if got != args.gpus:
         print(f"bench.py: process group has {got} rank(s) but --gpus {args.gpus}", file=sys.stderr)
-        if world > 1:
+        if grouped:
             dist.destroy_process_group()
         sys.exit(3)
 
@@ -1694,7 +1738,7 @@ def main():
         "dtype": "u8",
         "data": "synthetic (device-generated, seeded; BASELINE config shapes)",
         "config": meta["config"],
-        "distributed": {"backend": backend if world > 1 else None, "world_size": got,
+        "distributed": {"backend": dist.get_backend() if grouped else None, "world_size": got,
                         "kernel_ms_per_rank": t["kern_ms_per_rank"], "wall_s_per_rank": t["wall_s_per_rank"],
                         # the whole job against R x HBM peak (algorithmic
                         # bytes of every rank / the slowest rank's kernel time)
@@ -1743,7 +1787,7 @@ def main():
     if rank == 0:
         line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 

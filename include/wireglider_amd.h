@@ -31,7 +31,10 @@
 extern "C" {
 #endif
 
-#define WG_ABI_VERSION 1
+/* ABI history: 1 = rounds 1-3; 2 = round 4's knob set (removed knob names
+ * and values are WG_ERR_INVALID from wg_tune_set, their WG_* environment
+ * overrides ignored). */
+#define WG_ABI_VERSION 2
 
 /* Return codes. */
 #define WG_OK 0
@@ -306,7 +309,13 @@ int wg_encap_encrypt(const uint8_t *dev_in, const uint8_t *dev_seg, const wg_gso
  * and dev_in's zeroed prefix fields are exactly what the two calls give;
  * dev_out holds the segment headers only.  dev_out must be sized as for
  * wg_gso_split (the headers sit at the segments' offsets).  Arguments and
- * bounds as for the two calls. */
+ * bounds as for the two calls.
+ * max_segment_size also picks the AEAD kernel: for 129 <= max_segment_size
+ * <= 6,080 the messages are staged in LDS and (knob encap_synth) the AEAD
+ * builds the segment headers itself; outside that range every header comes
+ * from the headers-only split and lanes store their own blocks — the same
+ * bytes, about 12 % slower on config 3's super-buffers.
+ * Pass the batch's real largest segment size, not a jumbo bound. */
 int wg_encap_batch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, uint8_t *dev_out,
                    wg_gso_result *dev_gso_res, const uint8_t key[32], uint32_t receiver_index, uint64_t counter0,
                    const uint64_t *dev_msg_offset, uint32_t msg_cap, uint32_t max_segments, uint32_t max_segment_size,
@@ -472,7 +481,9 @@ int wg_device_count(void);
  *   "encap_synth" wg_encap_batch: the AEAD builds the headers of segments
  *                whose header fits one 64-B block itself (fields, IPv4 and L4
  *                checksums) and the split skips those super-buffers (1,
- *                default), or every segment header comes from the split (0)
+ *                default; needs the staged kernel, i.e. the call's
+ *                max_segment_size in [129, 6080]), or every segment header
+ *                comes from the split (0)
  *   "gso_ablate" GSO A/B variants: 1 = non-temporal payload stores, 32 = no
  *                XCD swizzle (both correct); 0 = the default kernel.
  * Thread-safe: each launch reads one consistent snapshot of the knobs. */

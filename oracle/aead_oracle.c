@@ -314,17 +314,18 @@ static void aead_parallel(aead_job proto, uint64_t n, int threads) {
     if ((uint64_t)threads > n) threads = n ? (int)n : 1;
     pthread_t tid[256];
     aead_job jobs[256];
+    const int spawn = threads > 1 || orc_pin_single();
     for (int t = 0; t < threads; t++) {
         jobs[t] = proto;
         jobs[t].lo = n * (uint64_t)t / (uint64_t)threads;
         jobs[t].hi = n * (uint64_t)(t + 1) / (uint64_t)threads;
-        if (threads == 1)
+        if (!spawn)
             aead_job_run(&jobs[t]);
         else {
             orc_spawn(&tid[t], t, aead_job_run, &jobs[t]);
         }
     }
-    if (threads > 1)
+    if (spawn)
         for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
 }
 

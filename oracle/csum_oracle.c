@@ -385,7 +385,7 @@ static void run_parallel(job_t proto, uint64_t n, int threads) {
         threads = ORC_MAX_THREADS;
     if ((uint64_t)threads > n)
         threads = n ? (int)n : 1;
-    if (threads == 1) {
+    if (threads == 1 && !orc_pin_single()) {
         proto.lo = 0;
         proto.hi = n;
         run_job(&proto);

@@ -68,12 +68,13 @@ int oss_wg_encrypt_batch(const uint8_t key[32], uint32_t rx, uint64_t c0, const 
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
     if ((uint64_t)threads > n) threads = n ? (int)n : 1;
+    const int spawn = threads > 1 || orc_pin_single();
     pthread_t tid[256];
     job jobs[256];
     for (int t = 0; t < threads; t++) {
         jobs[t] = (job){key, rx, c0, in, total, seg, out, n * (uint64_t)t / (uint64_t)threads,
                         n * (uint64_t)(t + 1) / (uint64_t)threads, 0};
-        if (threads == 1)
+        if (!spawn)
             run(&jobs[t]);
         else {
             orc_spawn(&tid[t], t, run, &jobs[t]);
@@ -81,7 +82,7 @@ int oss_wg_encrypt_batch(const uint8_t key[32], uint32_t rx, uint64_t c0, const 
     }
     int rc = 0;
     for (int t = 0; t < threads; t++) {
-        if (threads > 1)
+        if (spawn)
             pthread_join(tid[t], NULL);
         rc |= jobs[t].rc;
     }
@@ -141,12 +142,13 @@ int oss_wg_decrypt_batch(const uint8_t key[32], const uint8_t *in, uint64_t tota
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
     if ((uint64_t)threads > n) threads = n ? (int)n : 1;
+    const int spawn = threads > 1 || orc_pin_single();
     pthread_t tid[256];
     djob jobs[256];
     for (int t = 0; t < threads; t++) {
         jobs[t] = (djob){key, in, total, seg, out, status, n * (uint64_t)t / (uint64_t)threads,
                          n * (uint64_t)(t + 1) / (uint64_t)threads, 0};
-        if (threads == 1)
+        if (!spawn)
             drun(&jobs[t]);
         else {
             orc_spawn(&tid[t], t, drun, &jobs[t]);
@@ -154,7 +156,7 @@ int oss_wg_decrypt_batch(const uint8_t key[32], const uint8_t *in, uint64_t tota
     }
     int rc = 0;
     for (int t = 0; t < threads; t++) {
-        if (threads > 1)
+        if (spawn)
             pthread_join(tid[t], NULL);
         rc |= jobs[t].rc;
     }

@@ -54,6 +54,17 @@ static int orc_pin_cpu(int idx) {
     return -1;
 }
 
+/* A one-thread timed run goes to a pinned worker too when bench.py names
+ * the CPUs (ORC_CPUS set, pinning on): run on the calling thread it could
+ * migrate between cores of different speed from repetition to repetition
+ * (round 4's bimodal 1-core leg).  Without ORC_CPUS (tests) one thread runs
+ * on the caller. */
+static inline int orc_pin_single(void) {
+    const char *e = getenv("ORC_PIN");
+    const char *l = getenv("ORC_CPUS");
+    return !(e && e[0] == '0') && l && *l;
+}
+
 /* Start worker idx on its CPU.  The CPU is set in the creation attributes,
  * never on the running thread by its handle: a worker that has already
  * finished carries TID 0 in its handle, and sched_setaffinity(0) pins the

@@ -11,6 +11,8 @@
 // usage: ref_l4 <packets.bin> <desc.bin> <out.u16>
 //   desc.bin: wg_pkt_desc records {u64 offset, u32 len, u16 csum_start, u8 flags, u8 reserved}
 #include <cstdint>
+#include <cstring>
+#include <span>
 #include <cstdio>
 #include <vector>
 

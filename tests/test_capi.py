@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_and_device_count():
     import wireglider_amd as wga
 
-    assert wga.lib.wg_abi_version() == 1
+    assert wga.lib.wg_abi_version() == wga.ABI_VERSION == 2
     assert wga.lib.wg_strerror(-1) == b"invalid argument"
     assert wga.device_count() >= 0
 

@@ -91,3 +91,27 @@ def test_percall_latency_host(tmp_path):
     r = subprocess.run([str(exe), "20000"], capture_output=True, text=True, timeout=120, env=env, check=True)
     lat = json.loads(r.stdout)
     assert lat["ns_per_call_1500B"] < 5000
+
+
+def test_percall_threads_count_and_scale(tmp_path):
+    """Worker threads calling the drop-in at once (one per tun queue,
+    wireglider.cpp:117-151): every call is counted exactly once in the
+    per-thread placement slots, exited threads included, and the results
+    agree across threads.  The per-call time at 8 threads stays near the
+    1-thread figure (no shared counter line; the box measures 1 vs 16)."""
+    import json
+
+    exe = _build(tmp_path, "percall_latency")
+    env = {k: v for k, v in os.environ.items() if k != "WG_PERCALL"}
+    reps = 20000
+    threads = [1, 8]
+    r = subprocess.run([str(exe), str(reps)] + [str(t) for t in threads], capture_output=True, text=True,
+                       timeout=300, env=env, check=True)
+    lat = json.loads(r.stdout)
+    per_thread = 3 * (1 + reps // 10 + reps)
+    assert lat["percall_stats"] == {"gpu": 0, "fallback": 0, "host": sum(threads) * per_thread}
+    for t in threads:
+        assert lat[f"threads_{t}"]["results_agree"]
+        assert lat[f"threads_{t}"]["results"] == lat["threads_1"]["results"]
+    # loose on a shared CI container; the tight bound is the GPU box's figure
+    assert lat["threads_8"]["ns_per_call_1500B"] < 4 * lat["threads_1"]["ns_per_call_1500B"] + 200

@@ -134,3 +134,36 @@ def test_bench_two_ranks_on_one_gpu(gpu, tmp_path):
     assert s4["result_hash"] == CONFIG4_HASH
     assert sum(s4["packets_per_rank"]) == 1 << 22
     assert max(s4["bytes_per_rank"]) - min(s4["bytes_per_rank"]) <= 9000
+
+
+def test_bench_rccl_one_rank(gpu, tmp_path):
+    """The RCCL branch of the multi-GPU path, on one GPU:
+    bench.py under torch.distributed.run --nproc-per-node=1 with
+    --force-dist and WG_DIST_BACKEND=nccl creates the process group with
+    init_process_group("nccl", device_id=...) and runs every collective the
+    8-GPU run uses on device tensors — the uint8 all_gather of the results
+    (gather_results), the int64 all_reduce of the hashes (allreduce_hash)
+    and of the verify count, the float64 max (max_over_ranks) and all_gather
+    (all_gather_floats), barriers — and still reproduces the N = 1 hashes."""
+    import socket
+
+    env = dict(os.environ)
+    env["WG_DIST_BACKEND"] = "nccl"
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                        "--master-addr", "127.0.0.1", f"--master-port={port}", str(ROOT / "bench.py"),
+                        "--gpus", "1", "--force-dist", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+                        "--settle-seconds", "0.05"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    print("rccl_one_rank", json.dumps({k: line[k] for k in ("distributed", "post_checks", "value")}))
+    assert line["distributed"]["backend"] == "nccl" and line["distributed"]["world_size"] == 1
+    assert line["n_gpus"] == 1 and len(line["distributed"]["kernel_ms_per_rank"]) == 1
+    assert line["post_checks"]["verify_nonzero"] == 0
+    assert line["post_checks"]["gathered_results"] == 1 << 20
+    assert line["strong_scaling"]["result_hash"] == CONFIG5_HASH
+    assert line["strong_scaling_config4"]["result_hash"] == CONFIG4_HASH

@@ -302,7 +302,7 @@ def test_host_path_keeps_current_device(gpu):
 @pytest.mark.gpu
 def test_pipeline_build_failure(gpu):
     """A pipeline whose build fails part-way (the third event creation, forced
-    by the WG_TEST_PIPE_FAIL hook, as under resource exhaustion) returns an
+    by the WG_INTERNAL_TEST_FAULT_INJECT_PIPE hook, as under resource exhaustion) returns an
     error and leaves nothing half-built: the thread's next call builds the
     pipeline again and its results are bit-exact (a failed build
     had left the device marked, so later calls ran with null streams and
@@ -325,7 +325,7 @@ def test_pipeline_build_failure(gpu):
         "    print('FIRST failed:', e)\n"
         "out = wga.calc_l4_checksum_host(buf.tobytes(), 1500, False, False, 20)\n"
         "print('SECOND', bool(np.array_equal(out, oracle.l4_uniform(buf, 1500, 20, 0))))\n")
-    env = dict(os.environ, WG_TEST_PIPE_FAIL="3")
+    env = dict(os.environ, WG_INTERNAL_TEST_FAULT_INJECT_PIPE="3")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "FIRST failed" in r.stdout and "HIP runtime failure" in r.stdout, r.stdout

@@ -31,7 +31,7 @@ WG_OK = 0
 WG_PKT_V6 = 0x01
 WG_PKT_TCP = 0x02
 WG_PROBE_DEFAULT_POLICY = 0x100  # wg_probe_copy: default cache policy instead of non-temporal
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # Every symbol declared in include/wireglider_amd.h.
 EXPORTED_SYMBOLS = (

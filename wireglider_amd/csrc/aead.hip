@@ -1284,6 +1284,9 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
                     for (int k = 0; k < 5; k++) dl.v[k] = tp[k] - dl.v[k];
                 }
                 // its weight r^(nq - k) * EF, parked in the slot by the S step
+                // (and the slot's ciphertext written by the group's lanes):
+                // an explicit wave-scope LDS handoff, not LDS issue order
+                wave_lds_handoff();
                 const uint32_t *lw = reinterpret_cast<const uint32_t *>(aead_lds);
                 const v4u w4 = aead_lds[lslot];
                 const L5 synw{{w4[0], w4[1], w4[2], w4[3], lw[4u * (lslot + 1u + pad / 16u)]}};
@@ -1328,6 +1331,9 @@ __global__ __launch_bounds__(256) void aead_kernel(AeadParams p) {
             }
         }
         if constexpr (kStage) {
+            // every lane's blocks, headers and tags are in the slots: the
+            // copy-out reads what other lanes of the wave wrote
+            wave_lds_handoff();
             // the wave's messages, slot by slot: consecutive lanes on
             // consecutive 16-B chunks of one message (refused / empty slots
             // write nothing, as unstaged)

@@ -13,9 +13,17 @@
 // which is the same checksum by construction (tests/test_dropin_host.py).
 // wg_percall_stats counts which placement answered, so a test can tell a GPU
 // answer from a fallback although both give the same checksum.
+//
+// The counts are per thread: the reference calls this from one worker thread
+// per tun queue (wireglider.cpp:117-151), and a process-wide atomic would
+// move one cache line between those cores on every call.  Each thread owns a
+// cache-line-sized slot (written only by that thread, plain relaxed stores);
+// wg_percall_stats sums the live slots plus what exited threads left behind.
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "wireglider/checksum.hpp"
 
@@ -23,9 +31,55 @@ namespace wireglider {
 
 namespace {
 
-// Who answered each call (wg_percall_stats): the GPU round trip, the host
-// after a failed GPU round trip, or the host by placement.
-std::atomic<uint64_t> g_gpu{0}, g_fallback{0}, g_host{0};
+struct alignas(64) Slot {
+    // who answered: the GPU round trip, the host after a failed GPU round
+    // trip, the host by placement
+    std::atomic<uint64_t> gpu{0}, fallback{0}, host{0};
+};
+
+struct Registry {
+    std::mutex mu;
+    std::vector<Slot *> live;
+    uint64_t gone[3] = {0, 0, 0};  // exited threads' counts
+};
+
+Registry &registry() {
+    static Registry *r = new Registry;  // never destroyed: threads may exit after static destruction
+    return *r;
+}
+
+// The calling thread's slot, registered on its first call and folded into
+// `gone` when the thread exits.
+struct SlotOwner {
+    Slot slot;
+    SlotOwner() {
+        Registry &r = registry();
+        std::lock_guard<std::mutex> g(r.mu);
+        r.live.push_back(&slot);
+    }
+    ~SlotOwner() {
+        Registry &r = registry();
+        std::lock_guard<std::mutex> g(r.mu);
+        r.gone[0] += slot.gpu.load(std::memory_order_relaxed);
+        r.gone[1] += slot.fallback.load(std::memory_order_relaxed);
+        r.gone[2] += slot.host.load(std::memory_order_relaxed);
+        for (auto it = r.live.begin(); it != r.live.end(); ++it)
+            if (*it == &slot) {
+                r.live.erase(it);
+                break;
+            }
+    }
+};
+
+inline Slot &my_slot() {
+    thread_local SlotOwner owner;
+    return owner.slot;
+}
+
+// Owner-only increment: a load and a store, no locked read-modify-write.
+inline void bump(std::atomic<uint64_t> &c) {
+    c.store(c.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
+}
 
 bool percall_gpu() {
     static const bool on = [] {
@@ -38,17 +92,18 @@ bool percall_gpu() {
 }  // namespace
 
 uint16_t calc_l4_checksum(std::span<const uint8_t> ippkt, bool isv6, bool istcp, uint16_t csum_start) {
+    Slot &s = my_slot();
     if (percall_gpu() && !ippkt.empty()) {
         uint16_t out = 0;
         const int rc = wg_l4csum_uniform_host(ippkt.data(), ippkt.size(), static_cast<uint32_t>(ippkt.size()),
                                               csum_start, (isv6 ? WG_PKT_V6 : 0u) | (istcp ? WG_PKT_TCP : 0u), &out);
         if (rc == WG_OK) {
-            g_gpu.fetch_add(1, std::memory_order_relaxed);
+            bump(s.gpu);
             return out;
         }
-        g_fallback.fetch_add(1, std::memory_order_relaxed);
+        bump(s.fallback);
     } else {
-        g_host.fetch_add(1, std::memory_order_relaxed);
+        bump(s.host);
     }
     return host::calc_l4_checksum(ippkt, isv6, istcp, csum_start);
 }
@@ -56,8 +111,22 @@ uint16_t calc_l4_checksum(std::span<const uint8_t> ippkt, bool isv6, bool istcp,
 }  // namespace wireglider
 
 extern "C" int wg_percall_stats(uint64_t *gpu_answered, uint64_t *host_fallback, uint64_t *host_answered) {
-    if (gpu_answered) *gpu_answered = wireglider::g_gpu.load();
-    if (host_fallback) *host_fallback = wireglider::g_fallback.load();
-    if (host_answered) *host_answered = wireglider::g_host.load();
+    using namespace wireglider;
+    Registry &r = registry();
+    uint64_t t[3];
+    {
+        std::lock_guard<std::mutex> g(r.mu);
+        t[0] = r.gone[0];
+        t[1] = r.gone[1];
+        t[2] = r.gone[2];
+        for (const Slot *s : r.live) {
+            t[0] += s->gpu.load(std::memory_order_relaxed);
+            t[1] += s->fallback.load(std::memory_order_relaxed);
+            t[2] += s->host.load(std::memory_order_relaxed);
+        }
+    }
+    if (gpu_answered) *gpu_answered = t[0];
+    if (host_fallback) *host_fallback = t[1];
+    if (host_answered) *host_answered = t[2];
     return WG_OK;
 }

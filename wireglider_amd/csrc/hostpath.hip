@@ -123,11 +123,11 @@ int pipe_init(Pipe &c) {
     c.release();  // first use on this thread, or the thread switched devices (current device kept)
     static std::once_flag once;
     std::call_once(once, [] { std::atexit([] { g_exiting.store(true); }); });
-    // Test hook (WG_TEST_PIPE_FAIL=k, read once): the process's first
+    // Test hook (WG_INTERNAL_TEST_FAULT_INJECT_PIPE=k, read once): the process's first
     // pipeline build fails at its k-th event creation, as under resource
     // exhaustion (tests/test_gpu_hostpath.py::test_pipeline_build_failure).
     static std::atomic<int> fail_at{[] {
-        const char *v = std::getenv("WG_TEST_PIPE_FAIL");
+        const char *v = std::getenv("WG_INTERNAL_TEST_FAULT_INJECT_PIPE");
         return v && *v ? std::atoi(v) : 0;
     }()};
     int nev = 0;

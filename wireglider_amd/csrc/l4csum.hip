@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
 #include <mutex>
 
 #include "wg_device.hpp"
@@ -917,8 +918,19 @@ __global__ __launch_bounds__(256) void verify_compact_lane_kernel(VerifyParams p
             // cap from the blocks per shard) when its counter started at 0,
             // which stream order guarantees (captured calls never come here);
             // the bound keeps a broken protocol from writing past the list.
-            if (s_base + pre + r < c.cap)
+            if (s_base + pre + r < c.cap) {
                 c.ent[sh * c.cap + s_base + pre + r] = v4u{dv.x, dv.y, len, (uint32_t)i};
+            } else {
+                // never under the protocol; if it ever happens the packet
+                // gets a defined verdict (0: not verified -> dropped, as a
+                // failed gate), never a stale one, and the host is told
+                // through the mapped sample area (word 2) on its next call
+                p.verdict[i] = 0;
+                if (p.l4)
+                    p.l4[i] = 0xffffu;
+                if (p.sample)
+                    __hip_atomic_store(p.sample + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
     }
     if (small) {
@@ -1046,22 +1058,26 @@ __global__ __launch_bounds__(256) void verify_walk_kernel(VerifyParams p) {
 namespace {
 
 // Per (device, stream) scratch of the compacting verify path: the entry
-// lists, two counter sets, and the host-mapped sample word read by the next
-// call.  Created on first use, grown (after draining the stream) when a
-// batch needs more entries, never freed (a handful per process).  A stream
-// whose state cannot be made (table full, allocation failure, or a call
-// under stream capture) runs the stateless walking kernel: the same results
-// by another kernel, never a host fallback.
+// lists, two counter sets, and the host-mapped sample words read by the next
+// call.  Created right AFTER a stream's first call has launched its (stateless)
+// kernel, so that call waits on no allocation; grown (after draining the
+// stream) when a batch needs more entries, never freed (a handful per
+// process).  A stream whose state cannot be made (table full, allocation
+// failure, or a call under stream capture) runs the stateless walking kernel:
+// the same results by another kernel, never a host fallback.
 struct VerifyState {
     int dev = -1;
     void *stream = nullptr;
     std::mutex mu;
-    uint32_t *host_sample = nullptr;  // hipHostMalloc'd, mapped
+    uint32_t *host_sample = nullptr;  // hipHostMalloc'd, mapped: [0] small count, [1] long bytes, [2] overflow flag
     uint32_t *dev_sample = nullptr;
     uint32_t *ctr = nullptr;          // 2 sets x kVShards x kVCtrStride words
+    bool ctr_zeroed = false;          // zeroed on the stream by the first compacting call
     wg::v4u *ent = nullptr;
     uint64_t cap = 0;                 // entries per shard
     uint32_t parity = 0;
+    int last_pick = -1;               // the path the previous call's sample priced (VerifyPath), -1 none
+    bool overflow_reported = false;
 };
 constexpr uint32_t kSampleUnknown = 0xffffffffu;
 constexpr size_t kMaxVerifyStates = 64;
@@ -1069,6 +1085,9 @@ std::mutex g_vstate_mu;
 VerifyState *g_vstate[kMaxVerifyStates];
 size_t g_nvstate = 0;
 
+// The (current device, stream)'s state, or nullptr; with create, made when
+// absent (nullptr when the table is full or an allocation fails).  No device
+// work is queued or waited for here.
 VerifyState *verify_state(void *stream, bool create) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess)
@@ -1088,8 +1107,7 @@ VerifyState *verify_state(void *stream, bool create) {
         return nullptr;
     }
     if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void **>(&s->ctr), 2u * wg::kVShards * wg::kVCtrStride * 4u) != hipSuccess ||
-        hipMemset(s->ctr, 0, 2u * wg::kVShards * wg::kVCtrStride * 4u) != hipSuccess) {
+        hipMalloc(reinterpret_cast<void **>(&s->ctr), 2u * wg::kVShards * wg::kVCtrStride * 4u) != hipSuccess) {
         (void)hipHostFree(h);
         if (s->ctr)
             (void)hipFree(s->ctr);
@@ -1100,6 +1118,7 @@ VerifyState *verify_state(void *stream, bool create) {
     s->dev_sample = static_cast<uint32_t *>(d);
     __atomic_store_n(s->host_sample, kSampleUnknown, __ATOMIC_RELAXED);
     __atomic_store_n(s->host_sample + 1, 0u, __ATOMIC_RELAXED);
+    __atomic_store_n(s->host_sample + 2, 0u, __ATOMIC_RELAXED);
     g_vstate[g_nvstate++] = s;
     return s;
 }
@@ -1138,6 +1157,11 @@ static int verify_compact_launch(VerifyParams p, VerifyState *s, uint64_t est_lo
     const uint64_t cap = per_block * ((nl + kVShards - 1) / kVShards);
     if (nl > 0x7fffffffull || p.n >= (1ull << 32) || !verify_reserve(s, cap, st))
         return WG_ERR_RUNTIME;  // the caller runs the wave kernel instead
+    if (!s->ctr_zeroed) {  // the stream's first compacting call: both counter sets, in stream order
+        if (hipMemsetAsync(s->ctr, 0, 2u * kVShards * kVCtrStride * 4u, st) != hipSuccess)
+            return WG_ERR_RUNTIME;
+        s->ctr_zeroed = true;
+    }
     VerifyCompact c{s->ent, s->cap, s->ctr + s->parity * kVShards * kVCtrStride,
                     s->ctr + (s->parity ^ 1u) * kVShards * kVCtrStride};
     s->parity ^= 1u;
@@ -1163,18 +1187,26 @@ static int verify_compact_launch(VerifyParams p, VerifyState *s, uint64_t est_lo
 
 }  // namespace wg
 
-// verify_small = 7 (default): per call, one of three kernels from the size mix
-// the previous call on this stream sampled (smp of 64 spread packets <= 64 B,
-// the others lb bytes in all):
-//  * no sample yet (the stream's first call), or every sampled packet small:
-//    the walking kernel — one stateless launch within 7-9 % of the best
-//    kernel on any mix, and the fastest on all-small batches;
-//  * otherwise the cheaper of the wave kernel and the compacting path by a
-//    cost model measured on MI355X (profiles/r03_verify_*): the
-//    wave kernel spends max(0.88 ns, group bytes / 6.5 TB/s) of chip time per
-//    4-packet group whatever sizes the group mixes; the compacting path pays
-//    its lane kernel (~7 ps per descriptor + ~8 ps per small packet) and then
-//    the long packets' groups at 1.07x the wave kernel's per-group time.
+// verify_small = 7 (default): per call, one of three kernels from the size
+// mixes the previous calls on this stream sampled (smp of 64 spread packets
+// <= 64 B, the others lb bytes in all):
+//  * the stream's first call: the walking kernel, launched before the
+//    stream's state exists (the state is made after the launch, so the first
+//    call waits on no allocation and writes no sample);
+//  * each later sample prices a kernel: the walking kernel when the sample
+//    is unknown or all small (one stateless launch within 7-9 % of the best
+//    kernel on any mix, and the fastest on all-small batches), otherwise the
+//    cheaper of the wave kernel and the compacting path by a cost model
+//    measured on MI355X (profiles/r03_verify_*): the wave kernel
+//    spends max(0.88 ns, group bytes / 6.5 TB/s) of chip time per 4-packet
+//    group whatever sizes the group mixes; the compacting path pays its lane
+//    kernel (~7 ps per descriptor + ~8 ps per small packet) and then the long
+//    packets' groups at 1.07x the wave kernel's per-group time;
+//  * a kernel other than the walking one runs only when the last TWO
+//    samples priced it: a worker that alternates ACK-sized and MTU-sized
+//    batches gets the walking kernel (at most 7-9 % over the best on its long
+//    batches) instead of a kernel priced for the other shape (the wave kernel
+//    on a 64-B batch is ~14x the walking kernel).
 // Every kernel gives the same results; the choice only moves time.
 static bool verify_pick_compact(uint64_t n, uint32_t smp, uint32_t lb, uint32_t min_small) {
     if (smp < min_small)
@@ -1231,18 +1263,34 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
         // kernel and leave the sample alone.
         hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
         const bool capturing = hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
-        VerifyState *s = verify_state(stream, !capturing);
-        if (!s)  // capturing before the stream had state, table full, or allocation failure
-            return verify_launch_walk(p, st);
+        VerifyState *s = verify_state(stream, false);
+        if (!s) {
+            // the stream's first call (or capturing before it had state, or
+            // the table is full): the stateless kernel goes out first, the
+            // state is made behind it for the next call
+            const int rc = verify_launch_walk(p, st);
+            if (!capturing)
+                (void)verify_state(stream, true);
+            return rc;
+        }
         std::lock_guard<std::mutex> g(s->mu);
         const uint32_t smp = __atomic_load_n(s->host_sample, __ATOMIC_RELAXED);
         const uint32_t lb = __atomic_load_n(s->host_sample + 1, __ATOMIC_RELAXED);
+        if (__atomic_load_n(s->host_sample + 2, __ATOMIC_RELAXED) && !s->overflow_reported) {
+            s->overflow_reported = true;
+            std::fprintf(stderr, "wireglider_amd: wg_verify_desc entry list overflow on a stream "
+                                 "(stream-order protocol broken?); affected packets got verdict 0\n");
+        }
         const bool known = smp <= 64u;
         VerifyPath path = kPathCompact;
-        if (t.verify_small == 7)
-            path = !known || smp == 64u ? kPathWalk
-                   : verify_pick_compact(n, smp, lb, t.verify_auto_t) ? kPathCompact
-                                                                       : kPathWave;
+        if (t.verify_small == 7) {
+            const VerifyPath priced = !known || smp == 64u ? kPathWalk
+                                      : verify_pick_compact(n, smp, lb, t.verify_auto_t) ? kPathCompact
+                                                                                          : kPathWave;
+            path = (int)priced == s->last_pick ? priced : kPathWalk;
+            if (!capturing)
+                s->last_pick = (int)priced;
+        }
         if (capturing) {
             path = path == kPathCompact ? kPathWalk : path;
         } else {

@@ -95,6 +95,15 @@ __device__ __forceinline__ uint32_t group_sum_u32(uint32_t v) {
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
+// Cross-lane LDS handoff within one wave: every LDS write this wave issued
+// before is visible to its reads after (release / acquire at wavefront scope
+// around a scheduling barrier), instead of relying on LDS issue order.
+__device__ __forceinline__ void wave_lds_handoff() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Wave index within the grid, provably uniform to the compiler.
 __device__ __forceinline__ uint32_t wave_in_block() {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));

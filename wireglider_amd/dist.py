@@ -10,6 +10,9 @@ data path.  Collectives are used only around it:
     for the bit-exact check against a reference hash;
   - max_over_ranks(): the max of a timing value (bench.py).
 Shards are balanced by BYTES, not packet counts (config 4-style mixes).
+Every helper runs its collective whenever a process group exists, even of
+one rank (bench.py --force-dist: the RCCL code path exercised on a one-GPU
+box); without a group they return the local answer.
 """
 from __future__ import annotations
 
@@ -98,7 +101,7 @@ def allreduce_hash(local_hash: int, group=None, device=None) -> int:
     import torch.distributed as dist
 
     h = int(local_hash)
-    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+    if not dist.is_initialized():
         return h % HASH_MOD
     t = torch.tensor([h & 0x7FFFFFFF, h >> 31], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
@@ -114,7 +117,7 @@ def gather_results(local, counts: Sequence[int], group=None):
     import torch
     import torch.distributed as dist
 
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not dist.is_initialized():
         return local.clone()
     mx = max(counts)
     buf = torch.zeros(2 * mx, dtype=torch.uint8, device=local.device)
@@ -128,7 +131,7 @@ def max_over_ranks(x: float, device=None, group=None) -> float:
     import torch
     import torch.distributed as dist
 
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not dist.is_initialized():
         return float(x)
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
@@ -142,7 +145,7 @@ def all_gather_floats(values: Sequence[float], device=None, group=None) -> list[
     import torch
     import torch.distributed as dist
 
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not dist.is_initialized():
         return [list(map(float, values))]
     if dist.get_backend(group) == "gloo":
         device = "cpu"
