@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round 5: the row-order GSO tile kernel — parity (test_gpu_gso.py, every
+# variant incl. gso_rows) then an in-process A/B on config 3 / 3udp; the
+# verify first call with the per-device pool.
+set -uo pipefail
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}"
+cd "$ROOT"
+TAG=$1
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_gso.py -x -q --timeout 300 --timeout-method thread \
+  > "$OUT/pytest_gso.txt" 2>&1 || { tail -40 "$OUT/pytest_gso.txt"; exit 1; }
+tail -1 "$OUT/pytest_gso.txt"
+timeout -k 10 300 python3 -u tools/ab.py config3 gso_rows=0 gso_rows=1 gso_rows=1,gso_tile_u=2 gso_rows=1,gso_tile_u=4 \
+  > "$OUT/ab_config3.json" 2>&1 || { tail "$OUT/ab_config3.json"; exit 1; }
+cat "$OUT/ab_config3.json"
+timeout -k 10 300 python3 -u tools/ab.py config3udp gso_rows=0 gso_rows=1 > "$OUT/ab_config3udp.json" 2>&1 || { tail "$OUT/ab_config3udp.json"; exit 1; }
+cat "$OUT/ab_config3udp.json"
+timeout -k 10 200 python3 -u tools/verify_first_call.py > "$OUT/first_call.json" 2> "$OUT/first_call.err" || { tail "$OUT/first_call.err"; exit 1; }
+cut -c1-400 "$OUT/first_call.json"
+echo "session $TAG done"

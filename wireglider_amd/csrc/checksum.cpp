@@ -48,8 +48,13 @@ Registry &registry() {
     return *r;
 }
 
-// The calling thread's slot, registered on its first call and folded into
-// `gone` when the thread exits.
+// The calling thread's slot: a trivially initialised thread-local pointer
+// (initial-exec TLS: one load, no guard, no __tls_get_addr call per call),
+// set on the thread's first call by registering a slot whose owner folds it
+// into `gone` when the thread exits.
+struct SlotOwner;
+__attribute__((tls_model("initial-exec"))) thread_local Slot *t_slot = nullptr;
+
 struct SlotOwner {
     Slot slot;
     SlotOwner() {
@@ -58,6 +63,7 @@ struct SlotOwner {
         r.live.push_back(&slot);
     }
     ~SlotOwner() {
+        t_slot = nullptr;
         Registry &r = registry();
         std::lock_guard<std::mutex> g(r.mu);
         r.gone[0] += slot.gpu.load(std::memory_order_relaxed);
@@ -71,9 +77,17 @@ struct SlotOwner {
     }
 };
 
-inline Slot &my_slot() {
+__attribute__((noinline)) Slot *register_slot() {
     thread_local SlotOwner owner;
-    return owner.slot;
+    t_slot = &owner.slot;
+    return t_slot;
+}
+
+inline Slot &my_slot() {
+    Slot *s = t_slot;
+    if (__builtin_expect(s == nullptr, 0))
+        s = register_slot();
+    return *s;
 }
 
 // Owner-only increment: a load and a store, no locked read-modify-write.

@@ -505,6 +505,310 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Row-order tile kernel (knob gso_rows = 1).  The output of one super-buffer
+// is cut into TILES of K whole segments (K * (hdr_len + gso) bytes, at most
+// the block's capacity of 64 W U 16-B chunks); a 64W-thread block streams a
+// tile in address order — lane t of the block owns output chunks t, t + 64W,
+// ..., so each load / store instruction of the block covers 64W consecutive
+// destination chunks (the copy shape measured at 6.5 TB/s),
+// instead of one wave per segment.  Segments never straddle tiles, so each
+// segment's checksum is completed inside its block:
+//   1. every lane issues its U chunk loads: ONE 16-B load per destination-
+//      aligned chunk from its (unaligned) source — a chunk's payload bytes
+//      all belong to one segment s and sit at in + (chunk - s * hdr_len);
+//   2. while they are in flight, the waves build each segment's header in an
+//      LDS image (fields as the reference writes them, offload.cpp:168-200,
+//      L4 checksum still zero), placed at the segment's 16-B phase so the
+//      chunk overlapping it reads the image with one aligned ds_read_b128;
+//   3. each chunk's payload bytes are summed (byte masks only where a chunk
+//      touches a header or the tile edge) and reduced per segment: a wave
+//      row of 64 chunks spans at most two segments when segments exceed 1 KiB
+//      (two DPP reductions), otherwise per-lane LDS adds;
+//   4. one thread per segment finishes its L4 checksum into the image
+//      (offload.cpp:202-204); 5. chunks are merged with the images and stored
+//      whole — headers included, no byte stores — except the tile's two edge
+//      chunks, shared with the neighbouring tiles, stored byte by byte.
+// Super-buffers the tile shape cannot take (gso < 16, headers over 128 B, a
+// segment over the tile capacity) run the segment-per-wave code in the same
+// kernel.  Results are bit-identical to gso_split_kernel's (tests).
+constexpr uint32_t kTileKMax = 32;   // segments per tile (LDS images)
+constexpr uint32_t kImgBytes = 144;  // a header image: <= 128 B at any 16-B phase
+
+// 16-bit byte mask of chunk bytes [lo, hi), each clamped to [0, 16]
+__device__ __forceinline__ uint32_t bmask16(int lo, int hi) {
+    lo = lo < 0 ? 0 : (lo > 16 ? 16 : lo);
+    hi = hi < 0 ? 0 : (hi > 16 ? 16 : hi);
+    return hi > lo ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
+}
+
+// dword d's byte mask (0xFF per selected byte) from a 16-bit chunk byte mask
+__device__ __forceinline__ uint32_t bexpand(uint32_t m16, int d) {
+    const uint32_t n = (m16 >> (4 * d)) & 15u;
+    const uint32_t x = (n * 0x00204081u) & 0x01010101u;  // bit b -> byte b's lsb
+    return (x << 8) - x;
+}
+
+__device__ __forceinline__ uint32_t v4get(const v4u &v, int d) {
+    return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+}
+
+// v's bytes moved down by d (0..15): byte k of the result is byte k + d of v
+__device__ __forceinline__ v4u shr_bytes(v4u v, uint32_t d) {
+    const uint32_t dq = d >> 2, db = d & 3u;
+    const uint32_t a0 = dq == 0 ? v.x : dq == 1 ? v.y : dq == 2 ? v.z : v.w;
+    const uint32_t a1 = dq == 0 ? v.y : dq == 1 ? v.z : dq == 2 ? v.w : 0u;
+    const uint32_t a2 = dq == 0 ? v.z : dq == 1 ? v.w : 0u;
+    const uint32_t a3 = dq == 0 ? v.w : 0u;
+    return v4u{__builtin_amdgcn_alignbyte(a1, a0, db), __builtin_amdgcn_alignbyte(a2, a1, db),
+               __builtin_amdgcn_alignbyte(a3, a2, db), __builtin_amdgcn_alignbyte(0u, a3, db)};
+}
+
+// Per-segment header fields (offload.cpp:168-200): IPv4 total length / id /
+// header checksum, TCP seq + flags or UDP length.
+struct SegFields {
+    uint32_t pktlen, ipcs, seq, flags;
+};
+__device__ __forceinline__ SegFields seg_fields(const Ctx &c, uint32_t i) {
+    SegFields f;
+    const uint32_t off = i * c.gso;
+    const uint32_t datalen = c.rest - off < c.gso ? c.rest - off : c.gso;
+    f.pktlen = c.hdr_len + datalen;
+    f.ipcs = c.v6 ? 0u : ~fold16_32(c.ip_base + bswap16(f.pktlen & 0xffffu) + bswap16((c.id0 + i) & 0xffffu)) & 0xffffu;
+    f.seq = c.seq0 + c.gso * i;
+    f.flags = i + 1 == c.nseg ? c.flags13 : (c.flags13 & ~0x09u);  // FIN/PSH only on the last segment
+    return f;
+}
+
+template <int W, int U>
+__global__ __launch_bounds__(64 * W) void gso_tile_kernel(GsoParams p) {
+    constexpr uint32_t kThreads = 64u * W;
+    constexpr uint32_t kCap = 16u * kThreads * U;  // tile capacity, bytes
+    __shared__ uint32_t s_img[kTileKMax * kImgBytes / 4];
+    __shared__ uint32_t s_sum[kTileKMax];
+    uint8_t *img8 = reinterpret_cast<uint8_t *>(s_img);
+    const uint32_t t = threadIdx.x, lane = lane_id(), wv = wave_in_block();
+    if (t < kTileKMax)
+        s_sum[t] = 0;
+    __syncthreads();
+    const uint32_t T = p.tiles;
+    const uint64_t units = p.n * T;
+    for (uint64_t u = xcd_swizzle(blockIdx.x, gridDim.x); u < units; u += gridDim.x) {
+        const uint64_t b = u / T;
+        const uint32_t jt = (uint32_t)(u - b * T);
+        const bool more_units = u + gridDim.x < units;
+        const DescRaw dr = sload(reinterpret_cast<const DescRaw *>(p.desc + b));
+        const PlanRaw pr = sload(reinterpret_cast<const PlanRaw *>(p.res) + b);
+        asm volatile("" ::"s"(pr.w[0]), "s"(pr.w[1]), "s"(pr.w[2]), "s"(pr.w[3]), "s"(pr.w[4]), "s"(pr.w[5]),
+                     "s"(dr.w[0]), "s"(dr.w[1]), "s"(dr.w[2]), "s"(dr.w[3]), "s"(dr.w[4]));
+        const uint32_t kind = (pr.w[1] >> 16) & 0xffu, nseg = pr.w[2] >> 16;
+        if (!(kind & kPlanSplit))
+            continue;  // passthrough / error / in place: gso_finalize_kernel
+        const uint64_t in_off = (uint64_t)dr.w[0] | ((uint64_t)dr.w[1] << 32);
+        const uint64_t out_off = (uint64_t)dr.w[2] | ((uint64_t)dr.w[3] << 32);
+        Ctx c;
+        c.in = reinterpret_cast<uintptr_t>(p.in) + in_off;
+        c.in_len = dr.w[4];
+        c.hdr_len = pr.w[0] & 0xffffu;
+        c.cs = pr.w[0] >> 16;
+        c.l4off = pr.w[1] & 0xffffu;
+        c.gso = pr.w[2] & 0xffffu;
+        c.nseg = nseg;
+        c.rest = c.in_len - c.hdr_len;
+        c.v6 = kind & kPlanV6;
+        c.tcp = kind & kPlanTcp;
+        c.id0 = pr.w[3] & 0xffffu;
+        c.seq0 = pr.w[5];
+        c.ip_base = pr.w[3] >> 16;
+        c.l4h_base = pr.w[4] & 0xffffu;
+        c.ps_sum = pr.w[4] >> 16;
+        c.flags13 = pr.w[1] >> 24;
+        const uintptr_t out_base = reinterpret_cast<uintptr_t>(p.out) + out_off;
+        const uint32_t H = c.hdr_len, S = H + c.gso;
+        // the prefix bytes this lane builds headers from, and their field codes
+        c.hb0 = ld8(c.in + (lane < H ? lane : 0u));
+        c.hb1 = ld8(c.in + (lane + 64 < H ? lane + 64 : 0u));
+        c.hc0 = hdr_code(c, lane);
+        c.hc1 = hdr_code(c, lane + 64);
+        if (!(c.gso >= 16u && H <= 128u && S + 30u <= kCap)) {
+            // not tileable: segment per wave (segments jt * W + wave, stride T * W)
+            for (uint32_t i = jt * W + wv; i < c.nseg; i += T * W) {
+                SegFront f;
+                seg_issue<0>(c, out_base, i, lane, f);
+                seg_finish<0>(c, out_base, f, lane);
+            }
+            continue;
+        }
+        uint32_t K = (kCap - 30u) / S;
+        K = K < kTileKMax ? K : kTileKMax;
+        const uint32_t ntiles = (c.nseg + K - 1u) / K;
+        const uint32_t out_len = c.rest + c.nseg * H;
+        const float rS = 1.0f / (float)S;
+        const uint32_t proto = (c.tcp ? 6u : 17u) << 8;
+        for (uint32_t tile = jt; tile < ntiles; tile += T) {
+            const uint32_t seg0 = tile * K;
+            const uint32_t Kt = c.nseg - seg0 < K ? c.nseg - seg0 : K;
+            const uint32_t tstart = seg0 * S;
+            const uint32_t tend = seg0 + Kt == c.nseg ? out_len : tstart + Kt * S;
+            const uintptr_t A0 = (out_base + tstart) & ~(uintptr_t)15;
+            const int q0 = (int)tstart - (int)((out_base + tstart) & 15u);  // chunk 0, relative to out_base
+            const uint32_t nch = (uint32_t)((((out_base + tend + 15u) & ~(uintptr_t)15) - A0) >> 4);
+            // chunk geometry: segment (tile-local) of its first tile byte
+            auto seg_of = [&](int q) -> uint32_t {
+                const uint32_t dq = q > (int)tstart ? (uint32_t)q - tstart : 0u;
+                uint32_t li = (uint32_t)((float)dq * rS);
+                li = li * S > dq ? li - 1u : ((li + 1u) * S <= dq ? li + 1u : li);
+                return li < Kt ? li : Kt - 1u;
+            };
+            // 1. loads
+            v4u v[U];
+            uint32_t sh[U];
+#pragma unroll
+            for (int k = 0; k < U; k++) {
+                const uint32_t ck = (uint32_t)k * kThreads + t;
+                const int q = q0 + 16 * (int)ck;
+                const uint32_t li = seg_of(q);
+                const uint32_t i = seg0 + li;
+                const int g = (int)(tstart + li * S);
+                const uint32_t dl = c.rest - i * c.gso < c.gso ? c.rest - i * c.gso : c.gso;
+                const bool has = ck < nch && g + (int)H - q < 16 && g + (int)(H + dl) - q > 0;
+                uint32_t x = (uint32_t)(q - (int)(i * H));  // source offset of chunk byte 0 (payload bytes)
+                uint32_t d = 0;
+                if (x + 16u > c.in_len) {  // the last segment's end: load the input's last 16 B, shift below
+                    d = x + 16u - c.in_len;
+                    x = c.in_len - 16u;
+                }
+                sh[k] = has ? d : 0u;
+                v[k] = ld16(c.in + (has ? x : 0u));
+            }
+            // 2. header images, L4 checksum field zero (waves round-robin over the tile's segments)
+            for (uint32_t li = wv; li < Kt; li += W) {
+                const uint32_t i = seg0 + li;
+                const SegFields f = seg_fields(c, i);
+                uint32_t tbl = 0;
+                tbl = (uint32_t)wg_writelane_i32((int)f.pktlen, kFldPkt, (int)tbl);
+                tbl = (uint32_t)wg_writelane_i32((int)(c.id0 + i), kFldId, (int)tbl);
+                tbl = (uint32_t)wg_writelane_i32((int)f.ipcs, kFldIpcs, (int)tbl);
+                tbl = (uint32_t)wg_writelane_i32(0, kFldL4cs, (int)tbl);
+                tbl = (uint32_t)wg_writelane_i32((int)f.seq, kFldSeq, (int)tbl);
+                tbl = (uint32_t)wg_writelane_i32((int)(f.pktlen - c.cs), kFldUlen, (int)tbl);
+                tbl = (uint32_t)wg_writelane_i32((int)f.flags, kFldFlags, (int)tbl);
+                const uint32_t base = li * kImgBytes + (uint32_t)((out_base + tstart + li * S) & 15u);
+                const uint32_t r0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((c.hc0 & 7u) << 2), (int)tbl);
+                const uint32_t b0 = (c.hc0 & 7u) ? (r0 >> (c.hc0 >> 8)) & 0xffu : c.hb0;
+                if (lane < H)
+                    img8[base + lane] = (uint8_t)b0;
+                if (H > 64) {
+                    const uint32_t r1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((c.hc1 & 7u) << 2), (int)tbl);
+                    const uint32_t b1 = (c.hc1 & 7u) ? (r1 >> (c.hc1 >> 8)) & 0xffu : c.hb1;
+                    if (lane + 64 < H)
+                        img8[base + lane + 64] = (uint8_t)b1;
+                }
+            }
+            // 3. payload sums per segment
+#pragma unroll
+            for (int k = 0; k < U; k++) {
+                if (__ballot(sh[k] != 0u))
+                    v[k] = sh[k] ? shr_bytes(v[k], sh[k]) : v[k];
+                const uint32_t ck = (uint32_t)k * kThreads + t;
+                const int q = q0 + 16 * (int)ck;
+                const uint32_t li = seg_of(q);
+                const uint32_t i = seg0 + li;
+                const int g = (int)(tstart + li * S);
+                const uint32_t dl = c.rest - i * c.gso < c.gso ? c.rest - i * c.gso : c.gso;
+                const uint32_t pm = ck < nch ? bmask16(g + (int)H - q, g + (int)(H + dl) - q) : 0u;
+                Acc acc;
+                if (pm == 0xffffu) {
+                    acc.add4(v[k]);
+                } else {
+#pragma unroll
+                    for (int d = 0; d < 4; d++) acc.add(v4get(v[k], d) & bexpand(pm, d));
+                }
+                const uint32_t ps = fold16(acc.value());
+                const uint32_t kf = (uint32_t)__builtin_amdgcn_readfirstlane((int)li);
+                const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)li, 63);
+                if (kf == kl) {
+                    const uint32_t s0 = wave_sum_u32(ps);
+                    if (lane == 0)
+                        atomicAdd(&s_sum[kf], s0);
+                } else if (kl == kf + 1u) {
+                    const uint32_t s0 = wave_sum_u32(li == kf ? ps : 0u);
+                    const uint32_t s1 = wave_sum_u32(li == kf ? 0u : ps);
+                    if (lane == 0) {
+                        atomicAdd(&s_sum[kf], s0);
+                        atomicAdd(&s_sum[kl], s1);
+                    }
+                } else {
+                    atomicAdd(&s_sum[li], ps);
+                }
+            }
+            __syncthreads();
+            // 4. the L4 checksums (offload.cpp:202-204: native order, UDP 0 stays 0)
+            if (t < Kt) {
+                const uint32_t li = t, i = seg0 + li;
+                const SegFields f = seg_fields(c, i);
+                const uint32_t gs = tstart + li * S;
+                uint32_t lp = fold16_32(s_sum[li]);
+                s_sum[li] = 0;  // for the block's next tile (behind the barrier below)
+                if ((out_base + gs + c.cs) & 1u)  // summed in absolute pairing; the L4 region pairs from gs + cs
+                    lp = bswap16(lp);
+                uint32_t l4h = c.l4h_base;
+                if (c.tcp)
+                    l4h += bswap16(f.seq >> 16) + bswap16(f.seq & 0xffffu) + (f.flags << 8);
+                else
+                    l4h += bswap16((f.pktlen - c.cs) & 0xffffu);
+                const uint32_t T4 = lp + l4h + c.ps_sum + proto + bswap16((f.pktlen - c.cs) & 0xffffu);
+                const uint32_t l4cs = ~fold16_32(T4) & 0xffffu;
+                const uint32_t base = li * kImgBytes + (uint32_t)((out_base + gs) & 15u);
+                img8[base + c.l4off] = (uint8_t)l4cs;
+                img8[base + c.l4off + 1u] = (uint8_t)(l4cs >> 8);
+            }
+            __syncthreads();
+            // 5. merge the headers, store
+#pragma unroll
+            for (int k = 0; k < U; k++) {
+                const uint32_t ck = (uint32_t)k * kThreads + t;
+                if (ck >= nch)
+                    continue;
+                const int q = q0 + 16 * (int)ck;
+                const uint32_t li = seg_of(q);
+                const uint32_t i = seg0 + li;
+                const int g = (int)(tstart + li * S);
+                const uint32_t dl = c.rest - i * c.gso < c.gso ? c.rest - i * c.gso : c.gso;
+                const uint32_t pm = bmask16(g + (int)H - q, g + (int)(H + dl) - q);
+                uint32_t hm = bmask16(g - q, g + (int)H - q);
+                uint32_t lh = li;
+                if (hm == 0u && li + 1u < Kt) {
+                    hm = bmask16(g + (int)S - q, g + (int)(S + H) - q);
+                    lh = li + 1u;
+                }
+                const uintptr_t A = A0 + 16u * ck;
+                v4u o = v[k];
+                if (hm) {
+                    const uintptr_t gh = out_base + tstart + lh * S;
+                    const uint32_t off = lh * kImgBytes + (uint32_t)(A - (gh & ~(uintptr_t)15));
+                    const v4u im = *reinterpret_cast<const v4u *>(img8 + off);
+                    o = v4u{(v[k].x & bexpand(pm, 0)) | (im.x & bexpand(hm, 0)),
+                            (v[k].y & bexpand(pm, 1)) | (im.y & bexpand(hm, 1)),
+                            (v[k].z & bexpand(pm, 2)) | (im.z & bexpand(hm, 2)),
+                            (v[k].w & bexpand(pm, 3)) | (im.w & bexpand(hm, 3))};
+                }
+                const uint32_t own = bmask16((int)tstart - q, (int)tend - q);
+                if (own == 0xffffu) {
+                    *reinterpret_cast<__attribute__((address_space(1))) v4u *>(A) = o;
+                } else {
+#pragma unroll
+                    for (int jb = 0; jb < 16; jb++)
+                        if ((own >> jb) & 1u)
+                            st8(A + jb, v4get(o, jb >> 2) >> (8 * (jb & 3)));
+                }
+            }
+            if (tile + T < ntiles || more_units)
+                __syncthreads();  // the images / sums are rewritten by the next tile
+        }
+    }
+}
+
 // Plan pass, ONE THREAD per super-buffer: classification (:48-134), the
 // per-super-buffer fields (IPv4 id, TCP seq read after the :145-149 zeroing)
 // and the invariant header sums into the GsoPlan.  This is scalar,
@@ -707,7 +1011,8 @@ int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, u
                 syn ? synth->msg_cap : 0u,
                 syn ? synth->max_segments : 0u,
                 syn ? synth->max_segment_size : 0u,
-                syn ? list : nullptr};
+                syn ? list : nullptr,
+                t.gso_tiles};
     if (p.list && hipMemsetAsync(p.list, 0, sizeof(uint32_t), st) != hipSuccess)
         return WG_ERR_RUNTIME;
     // 1. plans (into dev_res), thread per super-buffer
@@ -718,6 +1023,24 @@ int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, u
     if (!debug_sync(st, "gso_plan_kernel"))
         return WG_ERR_LAUNCH;
     // 2. the split
+    if (!hdr_only && t.gso_rows && t.gso_ablate == 0) {
+        // the row-order tile kernel: gso_tiles blocks per super-buffer
+        uint64_t blocks = n * t.gso_tiles;
+        blocks = blocks < t.gso_blocks ? blocks : t.gso_blocks;
+        if (blocks >= 8)
+            blocks = (blocks + 7) & ~7ull;  // the XCD swizzle wants a multiple of 8 (extra blocks find no unit)
+        switch (t.gso_tile_u) {
+        case 2: hipLaunchKernelGGL((gso_tile_kernel<4, 2>), dim3((unsigned)blocks), dim3(256), 0, st, p); break;
+        case 4: hipLaunchKernelGGL((gso_tile_kernel<4, 4>), dim3((unsigned)blocks), dim3(256), 0, st, p); break;
+        default: hipLaunchKernelGGL((gso_tile_kernel<4, 3>), dim3((unsigned)blocks), dim3(256), 0, st, p); break;
+        }
+        if (hipGetLastError() != hipSuccess || !debug_sync(st, "gso_tile_kernel"))
+            return WG_ERR_LAUNCH;
+        hipLaunchKernelGGL(gso_finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
+        if (!debug_sync(st, "gso_finalize_kernel"))
+            return WG_ERR_LAUNCH;
+        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
+    }
     const uint64_t units = n * t.gso_groups;
     // list mode: a fixed grid walks the listed super-buffers (usually few)
     const uint64_t cap = p.list ? 4096u : t.gso_blocks;

@@ -1059,19 +1059,22 @@ namespace {
 
 // Per (device, stream) scratch of the compacting verify path: the entry
 // lists, two counter sets, and the host-mapped sample words read by the next
-// call.  Created right AFTER a stream's first call has launched its (stateless)
-// kernel, so that call waits on no allocation; grown (after draining the
-// stream) when a batch needs more entries, never freed (a handful per
-// process).  A stream whose state cannot be made (table full, allocation
-// failure, or a call under stream capture) runs the stateless walking kernel:
-// the same results by another kernel, never a host fallback.
+// call.  The sample words and counter sets of every stream on a device come
+// from one pool allocated once per device — right AFTER the device's first
+// verify call has launched its (stateless) kernel — so a stream's state is a
+// table entry and a later stream's first call allocates nothing.  Entry lists
+// are per stream, allocated when the compacting path first runs there and
+// grown (after draining the stream) when a batch needs more; never freed (a
+// handful per process).  A stream whose state cannot be made (table full,
+// allocation failure, or a call under stream capture) runs the stateless
+// walking kernel: the same results by another kernel, never a host fallback.
 struct VerifyState {
     int dev = -1;
     void *stream = nullptr;
     std::mutex mu;
-    uint32_t *host_sample = nullptr;  // hipHostMalloc'd, mapped: [0] small count, [1] long bytes, [2] overflow flag
+    uint32_t *host_sample = nullptr;  // host-mapped (pool): [0] small count, [1] long bytes, [2] overflow flag
     uint32_t *dev_sample = nullptr;
-    uint32_t *ctr = nullptr;          // 2 sets x kVShards x kVCtrStride words
+    uint32_t *ctr = nullptr;          // 2 sets x kVShards x kVCtrStride words (pool)
     bool ctr_zeroed = false;          // zeroed on the stream by the first compacting call
     wg::v4u *ent = nullptr;
     uint64_t cap = 0;                 // entries per shard
@@ -1080,10 +1083,45 @@ struct VerifyState {
     bool overflow_reported = false;
 };
 constexpr uint32_t kSampleUnknown = 0xffffffffu;
-constexpr size_t kMaxVerifyStates = 64;
+constexpr size_t kMaxVerifyStates = 64;  // streams, over all devices
+constexpr size_t kSampleWords = 16;      // 64 B per stream in the mapped pool
+constexpr size_t kCtrWords = 2u * wg::kVShards * wg::kVCtrStride;
+struct VerifyPool {
+    int dev = -1;
+    uint32_t *host = nullptr, *devp = nullptr;  // kMaxVerifyStates x kSampleWords, mapped
+    uint32_t *ctr = nullptr;                    // kMaxVerifyStates x kCtrWords
+    size_t used = 0;
+};
+constexpr size_t kMaxVerifyDevices = 64;
 std::mutex g_vstate_mu;
 VerifyState *g_vstate[kMaxVerifyStates];
 size_t g_nvstate = 0;
+VerifyPool g_vpool[kMaxVerifyDevices];
+size_t g_nvpool = 0;
+
+// The device's pool (caller holds g_vstate_mu), made on first use; nullptr
+// when an allocation fails (then the walking kernel serves that device).
+VerifyPool *verify_pool(int dev) {
+    for (size_t k = 0; k < g_nvpool; k++)
+        if (g_vpool[k].dev == dev)
+            return g_vpool[k].host ? &g_vpool[k] : nullptr;
+    if (g_nvpool == kMaxVerifyDevices)
+        return nullptr;
+    VerifyPool &p = g_vpool[g_nvpool++];
+    p.dev = dev;  // a failed allocation is remembered: never retried per call
+    void *h = nullptr, *d = nullptr, *c = nullptr;
+    if (hipHostMalloc(&h, kMaxVerifyStates * kSampleWords * 4u, hipHostMallocMapped | hipHostMallocCoherent) !=
+        hipSuccess)
+        return nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || hipMalloc(&c, kMaxVerifyStates * kCtrWords * 4u) != hipSuccess) {
+        (void)hipHostFree(h);
+        return nullptr;
+    }
+    p.host = static_cast<uint32_t *>(h);
+    p.devp = static_cast<uint32_t *>(d);
+    p.ctr = static_cast<uint32_t *>(c);
+    return &p;
+}
 
 // The (current device, stream)'s state, or nullptr; with create, made when
 // absent (nullptr when the table is full or an allocation fails).  No device
@@ -1098,24 +1136,16 @@ VerifyState *verify_state(void *stream, bool create) {
             return g_vstate[k];
     if (!create || g_nvstate == kMaxVerifyStates)
         return nullptr;
+    VerifyPool *pool = verify_pool(dev);
+    if (!pool || pool->used == kMaxVerifyStates)
+        return nullptr;
+    const size_t slot = pool->used++;
     VerifyState *s = new VerifyState;
     s->dev = dev;
     s->stream = stream;
-    void *h = nullptr, *d = nullptr;
-    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
-        delete s;
-        return nullptr;
-    }
-    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void **>(&s->ctr), 2u * wg::kVShards * wg::kVCtrStride * 4u) != hipSuccess) {
-        (void)hipHostFree(h);
-        if (s->ctr)
-            (void)hipFree(s->ctr);
-        delete s;
-        return nullptr;
-    }
-    s->host_sample = static_cast<uint32_t *>(h);
-    s->dev_sample = static_cast<uint32_t *>(d);
+    s->host_sample = pool->host + slot * kSampleWords;
+    s->dev_sample = pool->devp + slot * kSampleWords;
+    s->ctr = pool->ctr + slot * kCtrWords;
     __atomic_store_n(s->host_sample, kSampleUnknown, __ATOMIC_RELAXED);
     __atomic_store_n(s->host_sample + 1, 0u, __ATOMIC_RELAXED);
     __atomic_store_n(s->host_sample + 2, 0u, __ATOMIC_RELAXED);
