@@ -580,6 +580,48 @@ __device__ __forceinline__ SegFields seg_fields(const Ctx &c, uint32_t i) {
     return f;
 }
 
+// One segment by one wave, one chunk per lane at a time and every header
+// byte by the general field lookup: the tile kernel's path for the
+// super-buffers tiles cannot take (gso < 16, headers over 128 B, segments
+// over a tile), kept light so it does not set the tile path's registers.
+__device__ __forceinline__ void seg_simple(const Ctx &c, uintptr_t out_base, uint32_t i, uint32_t lane) {
+    const SegGeom g = seg_geom(c, out_base, i);
+    Acc acc;
+    for (uint32_t k = lane; k < g.nint; k += 64) {
+        const v4u v = ld16(g.base + 16u * k);
+        *reinterpret_cast<__attribute__((address_space(1))) v4u *>(g.c0 + 16u * k) = v;
+        acc.add4(v);
+    }
+    const uint32_t eo = edge_off(g, lane);
+    if (eo != kNoEdge) {
+        const uint32_t b = ld8(g.sa + eo);
+        st8(g.oa + eo, b);
+        acc.add(b << (8u * (((uint32_t)g.oa + eo) & 1u)));
+    }
+    const SegFields f = seg_fields(c, i);
+    uint32_t l4h = c.l4h_base;
+    if (c.tcp)
+        l4h += bswap16(f.seq >> 16) + bswap16(f.seq & 0xffffu) + (f.flags << 8);
+    else
+        l4h += bswap16((f.pktlen - c.cs) & 0xffffu);
+    uint32_t lp = fold16(acc.value());
+    if ((g.seg + c.cs) & 1u)
+        lp = bswap16(lp);
+    uint32_t T = wave_sum_u32(lp) + l4h + c.ps_sum;
+    T += ((c.tcp ? 6u : 17u) << 8) + bswap16((f.pktlen - c.cs) & 0xffffu);
+    HdrVals hv;
+    hv.v[0] = 0;
+    hv.v[kFldPkt] = f.pktlen;
+    hv.v[kFldId] = c.id0 + i;
+    hv.v[kFldIpcs] = f.ipcs;
+    hv.v[kFldL4cs] = ~fold16_32(T) & 0xffffu;
+    hv.v[kFldSeq] = f.seq;
+    hv.v[kFldUlen] = f.pktlen - c.cs;
+    hv.v[kFldFlags] = f.flags;
+    for (uint32_t j = lane; j < c.hdr_len; j += 64)
+        st8(g.seg + j, hdr_byte_slow(hv, hdr_code(c, j), ld8(c.in + j)));
+}
+
 template <int W, int U>
 __global__ __launch_bounds__(64 * W) void gso_tile_kernel(GsoParams p) {
     constexpr uint32_t kThreads = 64u * W;
@@ -632,11 +674,8 @@ __global__ __launch_bounds__(64 * W) void gso_tile_kernel(GsoParams p) {
         c.hc1 = hdr_code(c, lane + 64);
         if (!(c.gso >= 16u && H <= 128u && S + 30u <= kCap)) {
             // not tileable: segment per wave (segments jt * W + wave, stride T * W)
-            for (uint32_t i = jt * W + wv; i < c.nseg; i += T * W) {
-                SegFront f;
-                seg_issue<0>(c, out_base, i, lane, f);
-                seg_finish<0>(c, out_base, f, lane);
-            }
+            for (uint32_t i = jt * W + wv; i < c.nseg; i += T * W)
+                seg_simple(c, out_base, i, lane);
             continue;
         }
         uint32_t K = (kCap - 30u) / S;
