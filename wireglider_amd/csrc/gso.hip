@@ -699,9 +699,10 @@ __global__ __launch_bounds__(64 * W) void gso_tile_kernel(GsoParams p) {
                 li = li * S > dq ? li - 1u : ((li + 1u) * S <= dq ? li + 1u : li);
                 return li < Kt ? li : Kt - 1u;
             };
-            // 1. loads
+            // 1. loads, and each chunk's geometry once: its segment (tile-local),
+            // payload / header byte masks, source shift
             v4u v[U];
-            uint32_t sh[U];
+            uint32_t mk[U], ax[U];  // mk: payload mask | header mask << 16; ax: shift | next-header bit 4 | li << 8
 #pragma unroll
             for (int k = 0; k < U; k++) {
                 const uint32_t ck = (uint32_t)k * kThreads + t;
@@ -710,15 +711,22 @@ __global__ __launch_bounds__(64 * W) void gso_tile_kernel(GsoParams p) {
                 const uint32_t i = seg0 + li;
                 const int g = (int)(tstart + li * S);
                 const uint32_t dl = c.rest - i * c.gso < c.gso ? c.rest - i * c.gso : c.gso;
-                const bool has = ck < nch && g + (int)H - q < 16 && g + (int)(H + dl) - q > 0;
+                const bool live = ck < nch;
+                const uint32_t pm = live ? bmask16(g + (int)H - q, g + (int)(H + dl) - q) : 0u;
+                uint32_t hm = bmask16(g - q, g + (int)H - q), nx = 0;
+                if (hm == 0u && li + 1u < Kt) {
+                    hm = bmask16(g + (int)S - q, g + (int)(S + H) - q);
+                    nx = hm ? 16u : 0u;
+                }
                 uint32_t x = (uint32_t)(q - (int)(i * H));  // source offset of chunk byte 0 (payload bytes)
                 uint32_t d = 0;
                 if (x + 16u > c.in_len) {  // the last segment's end: load the input's last 16 B, shift below
                     d = x + 16u - c.in_len;
                     x = c.in_len - 16u;
                 }
-                sh[k] = has ? d : 0u;
-                v[k] = ld16(c.in + (has ? x : 0u));
+                mk[k] = pm | ((live ? hm : 0u) << 16);
+                ax[k] = (pm ? d : 0u) | nx | (li << 8);
+                v[k] = ld16(c.in + (pm ? x : 0u));
             }
             // 2. header images, L4 checksum field zero (waves round-robin over the tile's segments)
             for (uint32_t li = wv; li < Kt; li += W) {
@@ -747,21 +755,16 @@ __global__ __launch_bounds__(64 * W) void gso_tile_kernel(GsoParams p) {
             // 3. payload sums per segment
 #pragma unroll
             for (int k = 0; k < U; k++) {
-                if (__ballot(sh[k] != 0u))
-                    v[k] = sh[k] ? shr_bytes(v[k], sh[k]) : v[k];
-                const uint32_t ck = (uint32_t)k * kThreads + t;
-                const int q = q0 + 16 * (int)ck;
-                const uint32_t li = seg_of(q);
-                const uint32_t i = seg0 + li;
-                const int g = (int)(tstart + li * S);
-                const uint32_t dl = c.rest - i * c.gso < c.gso ? c.rest - i * c.gso : c.gso;
-                const uint32_t pm = ck < nch ? bmask16(g + (int)H - q, g + (int)(H + dl) - q) : 0u;
+                const uint32_t d = ax[k] & 15u;
+                if (__ballot(d != 0u))
+                    v[k] = d ? shr_bytes(v[k], d) : v[k];
+                const uint32_t pm = mk[k] & 0xffffu, li = (ax[k] >> 8) & 0xffu;
                 Acc acc;
                 if (pm == 0xffffu) {
                     acc.add4(v[k]);
                 } else {
 #pragma unroll
-                    for (int d = 0; d < 4; d++) acc.add(v4get(v[k], d) & bexpand(pm, d));
+                    for (int dd = 0; dd < 4; dd++) acc.add(v4get(v[k], dd) & bexpand(pm, dd));
                 }
                 const uint32_t ps = fold16(acc.value());
                 const uint32_t kf = (uint32_t)__builtin_amdgcn_readfirstlane((int)li);
@@ -809,21 +812,11 @@ __global__ __launch_bounds__(64 * W) void gso_tile_kernel(GsoParams p) {
                 const uint32_t ck = (uint32_t)k * kThreads + t;
                 if (ck >= nch)
                     continue;
-                const int q = q0 + 16 * (int)ck;
-                const uint32_t li = seg_of(q);
-                const uint32_t i = seg0 + li;
-                const int g = (int)(tstart + li * S);
-                const uint32_t dl = c.rest - i * c.gso < c.gso ? c.rest - i * c.gso : c.gso;
-                const uint32_t pm = bmask16(g + (int)H - q, g + (int)(H + dl) - q);
-                uint32_t hm = bmask16(g - q, g + (int)H - q);
-                uint32_t lh = li;
-                if (hm == 0u && li + 1u < Kt) {
-                    hm = bmask16(g + (int)S - q, g + (int)(S + H) - q);
-                    lh = li + 1u;
-                }
+                const uint32_t pm = mk[k] & 0xffffu, hm = mk[k] >> 16;
                 const uintptr_t A = A0 + 16u * ck;
                 v4u o = v[k];
                 if (hm) {
+                    const uint32_t lh = ((ax[k] >> 8) & 0xffu) + ((ax[k] >> 4) & 1u);
                     const uintptr_t gh = out_base + tstart + lh * S;
                     const uint32_t off = lh * kImgBytes + (uint32_t)(A - (gh & ~(uintptr_t)15));
                     const v4u im = *reinterpret_cast<const v4u *>(img8 + off);
@@ -832,7 +825,9 @@ __global__ __launch_bounds__(64 * W) void gso_tile_kernel(GsoParams p) {
                             (v[k].z & bexpand(pm, 2)) | (im.z & bexpand(hm, 2)),
                             (v[k].w & bexpand(pm, 3)) | (im.w & bexpand(hm, 3))};
                 }
-                const uint32_t own = bmask16((int)tstart - q, (int)tend - q);
+                // every tile byte is header or payload: a chunk is whole unless it
+                // holds a tile edge
+                const uint32_t own = pm | hm;
                 if (own == 0xffffu) {
                     *reinterpret_cast<__attribute__((address_space(1))) v4u *>(A) = o;
                 } else {
