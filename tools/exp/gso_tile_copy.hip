@@ -1,0 +1,90 @@
+// Experiment (not built into the library): the copy ceiling of the row-order
+// tile kernel's access shape (gso.hip gso_tile_kernel) on BASELINE config 3
+// (262,144 x 65,535 B super-buffers at stride 65,536 -> 45 x 1,500 B
+// segments at stride 73,216).  A 256-thread block per tile of K = 8 segments
+// (12,000 B), lane t owning chunks t, t + 256, ... (U per lane): every output
+// chunk ONE unaligned 16-B load from its payload source, stored whole; the
+// header bytes carry whatever that load returned (no headers, no sums).
+//   T<U, NT>: U chunks per lane (2, 3 -> K = 5 / 8 segments per tile), NT bit 1
+//   non-temporal loads, bit 2 non-temporal stores.
+// Prints one JSON line per variant: ms per launch and read + write TB/s.
+// usage: gso_tile_copy [iters]
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) v4u g_v4u;
+typedef __attribute__((address_space(1))) const v4u gc_v4u;
+
+constexpr unsigned N = 1u << 18, IN_STRIDE = 65536, OUT_STRIDE = 73216, IN_LEN = 65535, H = 40, G = 1460;
+constexpr unsigned S = H + G, NSEG = (IN_LEN - H + G - 1) / G, OUT_LEN = IN_LEN - H + NSEG * H;
+
+template <int U, int NT>
+__global__ __launch_bounds__(256) void tile_copy(const unsigned char *in, unsigned char *out, unsigned tiles) {
+    constexpr unsigned K = (16u * 256u * U - 30u) / S;
+    const unsigned ntiles = (NSEG + K - 1) / K;
+    unsigned b = blockIdx.x;
+    if (!(gridDim.x & 7u)) b = (b & 7u) * (gridDim.x >> 3) + (b >> 3);
+    const unsigned sb = b / tiles, tile = b % tiles;
+    if (sb >= N || tile >= ntiles) return;
+    const uintptr_t src = (uintptr_t)in + (uintptr_t)sb * IN_STRIDE, dst = (uintptr_t)out + (uintptr_t)sb * OUT_STRIDE;
+    const unsigned seg0 = tile * K, Kt = NSEG - seg0 < K ? NSEG - seg0 : K;
+    const unsigned tstart = seg0 * S, tend = seg0 + Kt == NSEG ? OUT_LEN : tstart + Kt * S;
+    const unsigned c0 = tstart & ~15u, nch = ((tend + 15u) & ~15u) / 16u - c0 / 16u;
+    v4u v[U];
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+        const unsigned ck = k * 256u + threadIdx.x;
+        const unsigned q = c0 + 16u * (ck < nch ? ck : nch - 1u);
+        const unsigned i = q / S;
+        unsigned x = q - i * H;
+        if (x + 16u > IN_LEN) x = IN_LEN - 16u;
+        if (NT & 1) v[k] = __builtin_nontemporal_load(reinterpret_cast<gc_v4u *>(src + x));
+        else v[k] = *reinterpret_cast<gc_v4u *>(src + x);
+    }
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+        const unsigned ck = k * 256u + threadIdx.x;
+        if (ck >= nch) continue;
+        g_v4u *p = reinterpret_cast<g_v4u *>(dst + c0 + 16u * ck);
+        if (NT & 2) __builtin_nontemporal_store(v[k], p);
+        else *p = v[k];
+    }
+}
+
+int main(int argc, char **argv) {
+    const int iters = argc > 1 ? atoi(argv[1]) : 20;
+    unsigned char *in, *out;
+    hipMalloc(&in, (size_t)N * IN_STRIDE);
+    hipMalloc(&out, (size_t)N * OUT_STRIDE);
+    hipMemset(in, 1, (size_t)N * IN_STRIDE);
+    hipMemset(out, 0, (size_t)N * OUT_STRIDE);
+    const double alg = (double)N * (IN_LEN + OUT_LEN);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    auto run = [&](auto kern, unsigned tiles, const char *name) {
+        const unsigned grid = N * tiles;
+        for (int w = 0; w < 3; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, in, out, tiles);
+        hipEventRecord(e0);
+        for (int w = 0; w < iters; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, in, out, tiles);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        printf("{\"variant\": \"%s\", \"ms\": %.4f, \"TBps\": %.3f}\n", name, ms / iters, alg / (ms / iters * 1e-3) / 1e12);
+    };
+    for (int rep = 0; rep < 2; rep++) {
+        run(tile_copy<3, 0>, 6, "U3 default policy");
+        run(tile_copy<3, 1>, 6, "U3 nt loads");
+        run(tile_copy<3, 2>, 6, "U3 nt stores");
+        run(tile_copy<3, 3>, 6, "U3 nt both");
+        run(tile_copy<2, 0>, 9, "U2 default policy");
+        run(tile_copy<4, 0>, 5, "U4 default policy");
+    }
+    printf("{\"err\": \"%s\"}\n", hipGetErrorString(hipGetLastError()));
+    return 0;
+}

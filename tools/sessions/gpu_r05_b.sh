@@ -19,4 +19,6 @@ timeout -k 10 300 python3 -u tools/ab.py config3udp gso_rows=0 gso_rows=1 > "$OU
 cat "$OUT/ab_config3udp.json"
 timeout -k 10 200 python3 -u tools/verify_first_call.py > "$OUT/first_call.json" 2> "$OUT/first_call.err" || { tail "$OUT/first_call.err"; exit 1; }
 cut -c1-400 "$OUT/first_call.json"
+timeout -k 10 120 tools/exp/bin/gso_tile_copy 20 > "$OUT/tile_copy.jsonl" 2>&1 || { tail "$OUT/tile_copy.jsonl"; exit 1; }
+cat "$OUT/tile_copy.jsonl"
 echo "session $TAG done"
