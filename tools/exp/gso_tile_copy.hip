@@ -55,6 +55,28 @@ __global__ __launch_bounds__(256) void tile_copy(const unsigned char *in, unsign
     }
 }
 
+// Row windows (round 2's R0): a block of B threads per B x 16-B output window
+// of the super-buffer (segments straddle windows), one chunk per thread.
+template <int B, int NT>
+__global__ __launch_bounds__(B) void row_copy(const unsigned char *in, unsigned char *out, unsigned rows) {
+    unsigned b = blockIdx.x;
+    if (!(gridDim.x & 7u)) b = (b & 7u) * (gridDim.x >> 3) + (b >> 3);
+    const unsigned sb = b / rows, row = b % rows;
+    if (sb >= N) return;
+    const uintptr_t src = (uintptr_t)in + (uintptr_t)sb * IN_STRIDE, dst = (uintptr_t)out + (uintptr_t)sb * OUT_STRIDE;
+    const unsigned o = (row * B + threadIdx.x) * 16u;
+    if (o >= OUT_LEN) return;
+    const unsigned i = o / S;
+    unsigned x = o - i * H;
+    if (x + 16u > IN_LEN) x = IN_LEN - 16u;
+    v4u v;
+    if (NT & 1) v = __builtin_nontemporal_load(reinterpret_cast<gc_v4u *>(src + x));
+    else v = *reinterpret_cast<gc_v4u *>(src + x);
+    g_v4u *p = reinterpret_cast<g_v4u *>(dst + o);
+    if (NT & 2) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 int main(int argc, char **argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 20;
     unsigned char *in, *out;
@@ -77,7 +99,24 @@ int main(int argc, char **argv) {
         hipEventElapsedTime(&ms, e0, e1);
         printf("{\"variant\": \"%s\", \"ms\": %.4f, \"TBps\": %.3f}\n", name, ms / iters, alg / (ms / iters * 1e-3) / 1e12);
     };
+    auto runrow = [&](auto kern, unsigned B, const char *name) {
+        const unsigned rows = (OUT_LEN + 16 * B - 1) / (16 * B);
+        const unsigned grid = ((N * rows + 7) / 8) * 8;
+        for (int w = 0; w < 3; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(B), 0, 0, in, out, rows);
+        hipEventRecord(e0);
+        for (int w = 0; w < iters; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(B), 0, 0, in, out, rows);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        printf("{\"variant\": \"%s\", \"ms\": %.4f, \"TBps\": %.3f}\n", name, ms / iters, alg / (ms / iters * 1e-3) / 1e12);
+    };
     for (int rep = 0; rep < 2; rep++) {
+        runrow(row_copy<256, 0>, 256, "R0 rows 4 KiB blocks default");
+        runrow(row_copy<256, 3>, 256, "R0 rows 4 KiB blocks nt both");
+        runrow(row_copy<128, 3>, 128, "R0 rows 2 KiB blocks nt both");
+        runrow(row_copy<512, 3>, 512, "R0 rows 8 KiB blocks nt both");
+        runrow(row_copy<64, 3>, 64, "R0 rows 1 KiB blocks nt both");
         run(tile_copy<3, 0>, 6, "U3 default policy");
         run(tile_copy<3, 1>, 6, "U3 nt loads");
         run(tile_copy<3, 2>, 6, "U3 nt stores");
