@@ -14,6 +14,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) v4u g_v4u;
@@ -55,6 +56,37 @@ __global__ __launch_bounds__(256) void tile_copy(const unsigned char *in, unsign
     }
 }
 
+// Segment tiles with ONE chunk per lane: a block of B threads per tile of K
+// whole segments (K = (16 B - 30) / S).  E bit: chunks in the tile's first /
+// last 128-B line stored with the default policy (the neighbouring tiles'
+// bytes share those lines), the rest non-temporal.
+template <int B, int NT, int E>
+__global__ __launch_bounds__(B) void tile1_copy(const unsigned char *in, unsigned char *out, unsigned tiles) {
+    constexpr unsigned K = (16u * B - 30u) / S;
+    const unsigned ntiles = (NSEG + K - 1) / K;
+    unsigned b = blockIdx.x;
+    if (!(gridDim.x & 7u)) b = (b & 7u) * (gridDim.x >> 3) + (b >> 3);
+    const unsigned sb = b / tiles, tile = b % tiles;
+    if (sb >= N || tile >= ntiles) return;
+    const uintptr_t src = (uintptr_t)in + (uintptr_t)sb * IN_STRIDE, dst = (uintptr_t)out + (uintptr_t)sb * OUT_STRIDE;
+    const unsigned seg0 = tile * K, Kt = NSEG - seg0 < K ? NSEG - seg0 : K;
+    const unsigned tstart = seg0 * S, tend = seg0 + Kt == NSEG ? OUT_LEN : tstart + Kt * S;
+    const unsigned c0 = tstart & ~15u, nch = ((tend + 15u) & ~15u) / 16u - c0 / 16u;
+    const unsigned ck = threadIdx.x;
+    if (ck >= nch) return;
+    const unsigned q = c0 + 16u * ck;
+    const unsigned i = q / S;
+    unsigned x = q - i * H;
+    if (x + 16u > IN_LEN) x = IN_LEN - 16u;
+    v4u v;
+    if (NT & 1) v = __builtin_nontemporal_load(reinterpret_cast<gc_v4u *>(src + x));
+    else v = *reinterpret_cast<gc_v4u *>(src + x);
+    g_v4u *p = reinterpret_cast<g_v4u *>(dst + q);
+    const bool edge = E && ((q >> 7) == (tstart >> 7) || (q >> 7) == ((tend - 1u) >> 7));
+    if ((NT & 2) && !edge) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // Row windows (round 2's R0): a block of B threads per B x 16-B output window
 // of the super-buffer (segments straddle windows), one chunk per thread.
 template <int B, int NT>
@@ -88,11 +120,17 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    auto run = [&](auto kern, unsigned tiles, const char *name) {
+    auto run = [&](auto kern, unsigned tiles, const char *name, unsigned bs = 0) {
         const unsigned grid = N * tiles;
-        for (int w = 0; w < 3; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, in, out, tiles);
+        if (!bs) {  // the block size from the variant's name: T1 kernels carry it in their template
+            bs = 256;
+            if (strstr(name, "192 threads")) bs = 192;
+            if (strstr(name, "512 threads")) bs = 512;
+            if (strstr(name, "768 threads")) bs = 768;
+        }
+        for (int w = 0; w < 3; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(bs), 0, 0, in, out, tiles);
         hipEventRecord(e0);
-        for (int w = 0; w < iters; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, in, out, tiles);
+        for (int w = 0; w < iters; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(bs), 0, 0, in, out, tiles);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         float ms;
@@ -112,6 +150,12 @@ int main(int argc, char **argv) {
         printf("{\"variant\": \"%s\", \"ms\": %.4f, \"TBps\": %.3f}\n", name, ms / iters, alg / (ms / iters * 1e-3) / 1e12);
     };
     for (int rep = 0; rep < 2; rep++) {
+        run(tile1_copy<192, 3, 0>, 23, "T1 tiles of 2 segments, 192 threads, 1 chunk each, nt both");
+        run(tile1_copy<192, 3, 1>, 23, "T1 192 threads, nt except the tile-edge lines");
+        run(tile1_copy<192, 0, 0>, 23, "T1 192 threads, default policy");
+        run(tile1_copy<256, 3, 1>, 23, "T1 tiles of 2 segments, 256 threads, nt except edge lines");
+        run(tile1_copy<512, 3, 1>, 9, "T1 tiles of 5 segments, 512 threads, nt except edge lines");
+        run(tile1_copy<768, 3, 1>, 6, "T1 tiles of 8 segments, 768 threads, nt except edge lines");
         runrow(row_copy<256, 0>, 256, "R0 rows 4 KiB blocks default");
         runrow(row_copy<256, 3>, 256, "R0 rows 4 KiB blocks nt both");
         runrow(row_copy<128, 3>, 128, "R0 rows 2 KiB blocks nt both");

@@ -13,9 +13,9 @@ timeout -k 10 120 tools/exp/bin/gso_tile_copy 20 > "$OUT/tile_copy.jsonl" 2>&1 |
 cat "$OUT/tile_copy.jsonl"
 timeout -k 10 300 python3 -u tools/ab.py config3 gso_rows=0 > "$OUT/ab_config3.json" 2>&1 || { tail "$OUT/ab_config3.json"; exit 1; }
 cat "$OUT/ab_config3.json"
-g++ -std=c++20 -O2 -I include tests/cpp/percall_latency.cpp -L wireglider_amd/lib -lwireglider_amd \
-  -Wl,-rpath,"$ROOT/wireglider_amd/lib" -lpthread -o "$OUT/percall_latency" || exit 1
-timeout -k 10 120 env -u WG_PERCALL "$OUT/percall_latency" 200000 1 16 > "$OUT/percall_threads.json" || exit 1
-cat "$OUT/percall_threads.json"
+
+
+
+
 nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null; python3 -c "import os; print(len(os.sched_getaffinity(0)))"
 echo "session $TAG done"
