@@ -32,22 +32,22 @@ def _wga():
                         {"gso_groups": 3, "gso_spw": 1}, {"gso_groups": 2, "gso_spw": 3},
                         {"gso_groups": 1, "gso_spw": 4, "gso_waves": 2},
                         {"gso_rows": 1}, {"gso_rows": 1, "gso_tiles": 1}, {"gso_rows": 1, "gso_tiles": 2},
-                        {"gso_rows": 1, "gso_tiles": 64}, {"gso_rows": 1, "gso_tile_u": 2, "gso_tiles": 3},
-                        {"gso_rows": 1, "gso_tile_u": 4}],
+                        {"gso_rows": 1, "gso_tiles": 64}, {"gso_rows": 1, "gso_tile_waves": 8, "gso_tiles": 3},
+                        {"gso_rows": 1, "gso_tile_waves": 4}, {"gso_rows": 1, "gso_tile_waves": 12, "gso_tiles": 5}],
                 ids=["swizzled", "launch-order", "groups3", "groups12", "groups5x8", "groups3-pairs",
                      "groups2-serial", "groups12x1", "groups7x2", "groups3-pingpong", "groups2-triples",
-                     "groups1x2-quads", "rows", "rows-tiles1", "rows-tiles2", "rows-tiles64", "rows-u2-tiles3",
-                     "rows-u4"])
+                     "groups1x2-quads", "rows", "rows-tiles1", "rows-tiles2", "rows-tiles64", "rows-w8-tiles3",
+                     "rows-w4", "rows-w12-tiles5"])
 def variant(request):
     """Every correct block -> (super-buffer, segment slot) mapping of the GSO
     kernel: one looping block per super-buffer (XCD-swizzled or in launch
     order) and several blocks per super-buffer (flat grid groups); and the
-    row-order tile kernel (gso_rows) with 1, 2, 3, 6 and 64 blocks per
-    super-buffer (blocks looping over tiles, idle blocks) at 2, 3 and 4 chunks
-    per lane."""
+    row-order tile kernel (gso_rows) with 1, 2, 3, 5, 23 (auto) and 64 blocks
+    per super-buffer (blocks looping over tiles, idle blocks) at 3, 4, 8 and
+    12 waves per block."""
     wga = _wga()
     saved = {k: wga.tune_get(k) for k in ("gso_ablate", "gso_groups", "gso_waves", "gso_spw", "gso_rows",
-                                          "gso_tiles", "gso_tile_u")}
+                                          "gso_tiles", "gso_tile_waves")}
     for k, v in request.param.items():
         wga.tune_set(k, v)
     yield request.param

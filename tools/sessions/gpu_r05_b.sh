@@ -12,13 +12,9 @@ export TMPDIR=/tmp
 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_gso.py -x -q --timeout 300 --timeout-method thread \
   > "$OUT/pytest_gso.txt" 2>&1 || { tail -40 "$OUT/pytest_gso.txt"; exit 1; }
 tail -1 "$OUT/pytest_gso.txt"
-timeout -k 10 300 python3 -u tools/ab.py config3 gso_rows=0 gso_rows=1 gso_rows=1,gso_tile_u=2 gso_rows=1,gso_tile_u=4 \
+timeout -k 10 300 python3 -u tools/ab.py config3 gso_rows=0 gso_rows=1 gso_rows=1,gso_tile_waves=4 gso_rows=1,gso_tile_waves=8 gso_rows=1,gso_tile_waves=12 \
   > "$OUT/ab_config3.json" 2>&1 || { tail "$OUT/ab_config3.json"; exit 1; }
 cat "$OUT/ab_config3.json"
 timeout -k 10 300 python3 -u tools/ab.py config3udp gso_rows=0 gso_rows=1 > "$OUT/ab_config3udp.json" 2>&1 || { tail "$OUT/ab_config3udp.json"; exit 1; }
 cat "$OUT/ab_config3udp.json"
-timeout -k 10 200 python3 -u tools/verify_first_call.py > "$OUT/first_call.json" 2> "$OUT/first_call.err" || { tail "$OUT/first_call.err"; exit 1; }
-cut -c1-400 "$OUT/first_call.json"
-timeout -k 10 120 tools/exp/bin/gso_tile_copy 20 > "$OUT/tile_copy.jsonl" 2>&1 || { tail "$OUT/tile_copy.jsonl"; exit 1; }
-cat "$OUT/tile_copy.jsonl"
 echo "session $TAG done"

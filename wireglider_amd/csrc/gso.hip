@@ -507,62 +507,27 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
 
 // ---------------------------------------------------------------------------
 // Row-order tile kernel (knob gso_rows = 1).  The output of one super-buffer
-// is cut into TILES of K whole segments (K * (hdr_len + gso) bytes, at most
-// the block's capacity of 64 W U 16-B chunks); a 64W-thread block streams a
-// tile in address order — lane t of the block owns output chunks t, t + 64W,
-// ..., so each load / store instruction of the block covers 64W consecutive
-// destination chunks (the copy shape measured at 6.5 TB/s),
-// instead of one wave per segment.  Segments never straddle tiles, so each
-// segment's checksum is completed inside its block:
-//   1. every lane issues its U chunk loads: ONE 16-B load per destination-
-//      aligned chunk from its (unaligned) source — a chunk's payload bytes
-//      all belong to one segment s and sit at in + (chunk - s * hdr_len);
-//   2. while they are in flight, the waves build each segment's header in an
-//      LDS image (fields as the reference writes them, offload.cpp:168-200,
-//      L4 checksum still zero), placed at the segment's 16-B phase so the
-//      chunk overlapping it reads the image with one aligned ds_read_b128;
-//   3. each chunk's payload bytes are summed (byte masks only where a chunk
-//      touches a header or the tile edge) and reduced per segment: a wave
-//      row of 64 chunks spans at most two segments when segments exceed 1 KiB
-//      (two DPP reductions), otherwise per-lane LDS adds;
-//   4. one thread per segment finishes its L4 checksum into the image
-//      (offload.cpp:202-204); 5. chunks are merged with the images and stored
-//      whole — headers included, no byte stores — except the tile's two edge
-//      chunks, shared with the neighbouring tiles, stored byte by byte.
+// is cut into TILES of K whole segments (at most 16 * 64W - 30 bytes); a
+// 64W-thread block takes one tile, ONE 16-B output chunk per lane in address
+// order — the copy shape of short row windows, measured at 5.27-5.38 ms for
+// config 3's bytes against 5.55-5.82 for segment-per-wave shapes on the same
+// boxes (profiles/r05_tile/).  Segments never straddle tiles, so every
+// checksum completes inside its block:
+//   1. a lane whose chunk lies inside one segment's payload (16-B aligned,
+//      destination side) loads it with ONE unaligned non-temporal 16-B load
+//      from in + (chunk - s * hdr_len), stores it non-temporally and sums it;
+//   2. the rest of each segment — its header and the <= 15-byte payload head
+//      and tail around the aligned chunks, at most hdr_len + 30 bytes — is a
+//      byte per lane over the block (payload bytes loaded, summed, stored);
+//      per-segment sums meet in LDS (two DPP reductions per wave when a row
+//      of 64 chunks spans two segments);
+//   3. one thread per segment turns its sum into the L4 checksum and the
+//      other per-segment fields (offload.cpp:168-204) into an LDS table;
+//   4. the header bytes, a byte per lane, from the table or the prefix.
 // Super-buffers the tile shape cannot take (gso < 16, headers over 128 B, a
-// segment over the tile capacity) run the segment-per-wave code in the same
-// kernel.  Results are bit-identical to gso_split_kernel's (tests).
-constexpr uint32_t kTileKMax = 32;   // segments per tile (LDS images)
-constexpr uint32_t kImgBytes = 144;  // a header image: <= 128 B at any 16-B phase
-
-// 16-bit byte mask of chunk bytes [lo, hi), each clamped to [0, 16]
-__device__ __forceinline__ uint32_t bmask16(int lo, int hi) {
-    lo = lo < 0 ? 0 : (lo > 16 ? 16 : lo);
-    hi = hi < 0 ? 0 : (hi > 16 ? 16 : hi);
-    return hi > lo ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
-}
-
-// dword d's byte mask (0xFF per selected byte) from a 16-bit chunk byte mask
-__device__ __forceinline__ uint32_t bexpand(uint32_t m16, int d) {
-    const uint32_t n = (m16 >> (4 * d)) & 15u;
-    const uint32_t x = (n * 0x00204081u) & 0x01010101u;  // bit b -> byte b's lsb
-    return (x << 8) - x;
-}
-
-__device__ __forceinline__ uint32_t v4get(const v4u &v, int d) {
-    return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
-}
-
-// v's bytes moved down by d (0..15): byte k of the result is byte k + d of v
-__device__ __forceinline__ v4u shr_bytes(v4u v, uint32_t d) {
-    const uint32_t dq = d >> 2, db = d & 3u;
-    const uint32_t a0 = dq == 0 ? v.x : dq == 1 ? v.y : dq == 2 ? v.z : v.w;
-    const uint32_t a1 = dq == 0 ? v.y : dq == 1 ? v.z : dq == 2 ? v.w : 0u;
-    const uint32_t a2 = dq == 0 ? v.z : dq == 1 ? v.w : 0u;
-    const uint32_t a3 = dq == 0 ? v.w : 0u;
-    return v4u{__builtin_amdgcn_alignbyte(a1, a0, db), __builtin_amdgcn_alignbyte(a2, a1, db),
-               __builtin_amdgcn_alignbyte(a3, a2, db), __builtin_amdgcn_alignbyte(0u, a3, db)};
-}
+// segment over the tile capacity) run a light segment-per-wave loop in the
+// same kernel.  Results are bit-identical to gso_split_kernel's (tests).
+constexpr uint32_t kTileKMax = 32;  // segments per tile (LDS sums / field tables)
 
 // Per-segment header fields (offload.cpp:168-200): IPv4 total length / id /
 // header checksum, TCP seq + flags or UDP length.
@@ -622,13 +587,34 @@ __device__ __forceinline__ void seg_simple(const Ctx &c, uintptr_t out_base, uin
         st8(g.seg + j, hdr_byte_slow(hv, hdr_code(c, j), ld8(c.in + j)));
 }
 
-template <int W, int U>
+// Adds lane value v into s_sum[key]; keys are non-decreasing over the lanes
+// and EXEC is full.  One or two distinct keys (a wave row within one or two
+// segments): DPP sums and one LDS add per key; more: an LDS add per lane.
+__device__ __forceinline__ void keyed_add(uint32_t *s_sum, uint32_t key, uint32_t v, uint32_t lane) {
+    const uint32_t kf = (uint32_t)__builtin_amdgcn_readfirstlane((int)key);
+    const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)key, 63);
+    if (kf == kl) {
+        const uint32_t s0 = wave_sum_u32(v);
+        if (lane == 0 && s0)
+            atomicAdd(&s_sum[kf], s0);
+    } else if (kl == kf + 1u) {
+        const uint32_t s0 = wave_sum_u32(key == kf ? v : 0u);
+        const uint32_t s1 = wave_sum_u32(key == kf ? 0u : v);
+        if (lane == 0) {
+            atomicAdd(&s_sum[kf], s0);
+            atomicAdd(&s_sum[kl], s1);
+        }
+    } else if (v) {
+        atomicAdd(&s_sum[key], v);
+    }
+}
+
+template <int W>
 __global__ __launch_bounds__(64 * W) void gso_tile_kernel(GsoParams p) {
     constexpr uint32_t kThreads = 64u * W;
-    constexpr uint32_t kCap = 16u * kThreads * U;  // tile capacity, bytes
-    __shared__ uint32_t s_img[kTileKMax * kImgBytes / 4];
+    constexpr uint32_t kCap = 16u * kThreads;  // tile capacity, bytes
     __shared__ uint32_t s_sum[kTileKMax];
-    uint8_t *img8 = reinterpret_cast<uint8_t *>(s_img);
+    __shared__ uint32_t s_fld[kTileKMax * 8];
     const uint32_t t = threadIdx.x, lane = lane_id(), wv = wave_in_block();
     if (t < kTileKMax)
         s_sum[t] = 0;
@@ -667,11 +653,6 @@ __global__ __launch_bounds__(64 * W) void gso_tile_kernel(GsoParams p) {
         c.flags13 = pr.w[1] >> 24;
         const uintptr_t out_base = reinterpret_cast<uintptr_t>(p.out) + out_off;
         const uint32_t H = c.hdr_len, S = H + c.gso;
-        // the prefix bytes this lane builds headers from, and their field codes
-        c.hb0 = ld8(c.in + (lane < H ? lane : 0u));
-        c.hb1 = ld8(c.in + (lane + 64 < H ? lane + 64 : 0u));
-        c.hc0 = hdr_code(c, lane);
-        c.hc1 = hdr_code(c, lane + 64);
         if (!(c.gso >= 16u && H <= 128u && S + 30u <= kCap)) {
             // not tileable: segment per wave (segments jt * W + wave, stride T * W)
             for (uint32_t i = jt * W + wv; i < c.nseg; i += T * W)
@@ -682,163 +663,111 @@ __global__ __launch_bounds__(64 * W) void gso_tile_kernel(GsoParams p) {
         K = K < kTileKMax ? K : kTileKMax;
         const uint32_t ntiles = (c.nseg + K - 1u) / K;
         const uint32_t out_len = c.rest + c.nseg * H;
-        const float rS = 1.0f / (float)S;
-        const uint32_t proto = (c.tcp ? 6u : 17u) << 8;
+        const uint32_t RB = H + 30u;  // boundary bytes per segment, at most
+        const float rS = 1.0f / (float)S, rRB = 1.0f / (float)RB, rH = 1.0f / (float)H;
+        const uint32_t omis = (uint32_t)out_base & 15u;  // output address bits below the chunk grid
         for (uint32_t tile = jt; tile < ntiles; tile += T) {
             const uint32_t seg0 = tile * K;
             const uint32_t Kt = c.nseg - seg0 < K ? c.nseg - seg0 : K;
             const uint32_t tstart = seg0 * S;
             const uint32_t tend = seg0 + Kt == c.nseg ? out_len : tstart + Kt * S;
-            const uintptr_t A0 = (out_base + tstart) & ~(uintptr_t)15;
-            const int q0 = (int)tstart - (int)((out_base + tstart) & 15u);  // chunk 0, relative to out_base
-            const uint32_t nch = (uint32_t)((((out_base + tend + 15u) & ~(uintptr_t)15) - A0) >> 4);
-            // chunk geometry: segment (tile-local) of its first tile byte
-            auto seg_of = [&](int q) -> uint32_t {
-                const uint32_t dq = q > (int)tstart ? (uint32_t)q - tstart : 0u;
-                uint32_t li = (uint32_t)((float)dq * rS);
-                li = li * S > dq ? li - 1u : ((li + 1u) * S <= dq ? li + 1u : li);
-                return li < Kt ? li : Kt - 1u;
+            const int q0 = (int)tstart - (int)((omis + tstart) & 15u);  // chunk 0, relative to out_base
+            const uint32_t nch = (uint32_t)(((omis + tend + 15u) & ~15u) - ((omis + tstart) & ~15u)) >> 4;
+            // floor(x / d) for small x by a float reciprocal, corrected by one
+            auto div_small = [](uint32_t x, uint32_t d, float rd) -> uint32_t {
+                uint32_t r = (uint32_t)((float)x * rd);
+                return r * d > x ? r - 1u : ((r + 1u) * d <= x ? r + 1u : r);
             };
-            // 1. loads, and each chunk's geometry once: its segment (tile-local),
-            // payload / header byte masks, source shift
-            v4u v[U];
-            uint32_t mk[U], ax[U];  // mk: payload mask | header mask << 16; ax: shift | next-header bit 4 | li << 8
-#pragma unroll
-            for (int k = 0; k < U; k++) {
-                const uint32_t ck = (uint32_t)k * kThreads + t;
-                const int q = q0 + 16 * (int)ck;
-                const uint32_t li = seg_of(q);
-                const uint32_t i = seg0 + li;
-                const int g = (int)(tstart + li * S);
-                const uint32_t dl = c.rest - i * c.gso < c.gso ? c.rest - i * c.gso : c.gso;
-                const bool live = ck < nch;
-                const uint32_t pm = live ? bmask16(g + (int)H - q, g + (int)(H + dl) - q) : 0u;
-                uint32_t hm = bmask16(g - q, g + (int)H - q), nx = 0;
-                if (hm == 0u && li + 1u < Kt) {
-                    hm = bmask16(g + (int)S - q, g + (int)(S + H) - q);
-                    nx = hm ? 16u : 0u;
+            // segment li's payload [pb, pe) and its aligned chunk span [P0, P1), relative to out_base
+            struct SegSpan {
+                uint32_t g, pe, P0, P1, i;
+            };
+            auto span_of = [&](uint32_t li) -> SegSpan {
+                SegSpan z;
+                z.i = seg0 + li;
+                z.g = tstart + li * S;
+                const uint32_t dl = c.rest - z.i * c.gso < c.gso ? c.rest - z.i * c.gso : c.gso;
+                const uint32_t pb = z.g + H;
+                z.pe = pb + dl;
+                const uint32_t a0 = ((omis + pb + 15u) & ~15u) - omis, a1 = ((omis + z.pe) & ~15u) - omis;
+                z.P0 = a0 < z.pe ? a0 : z.pe;
+                z.P1 = a1 > z.P0 ? a1 : z.P0;
+                return z;
+            };
+            // 1. this lane's chunk, when it is a whole payload chunk
+            const int q = q0 + 16 * (int)t;
+            const uint32_t dq = q > (int)tstart ? (uint32_t)q - tstart : 0u;
+            uint32_t li = div_small(dq, S, rS);
+            li = li < Kt ? li : Kt - 1u;
+            const SegSpan sp = span_of(li);
+            const bool pure = t < nch && q >= (int)sp.P0 && q + 16 <= (int)sp.P1;
+            const v4u v = ld16_nt(c.in + (pure ? (uint32_t)q - sp.i * H : 0u));
+            // 2. the boundary bytes: byte j of segment bl's head [g, P0) then tail [P1, pe)
+            for (uint32_t f0 = 0; f0 < Kt * RB; f0 += kThreads) {
+                const uint32_t f = f0 + t;
+                uint32_t bl = div_small(f, RB, rRB);
+                const bool inb = bl < Kt;
+                bl = inb ? bl : Kt - 1u;
+                const uint32_t j = f - bl * RB;
+                const SegSpan z = span_of(bl);
+                const uint32_t hl = z.P0 - z.g;  // head bytes (header + payload head)
+                const uint32_t pos = j < hl ? z.g + j : z.P1 + (j - hl);
+                const bool pay = inb && pos < z.pe && pos >= z.g + H;
+                const uint32_t bb = pay ? ld8(c.in + pos - z.i * H) : 0u;
+                if (f0 == 0 && pure) {  // the chunk, with the first pass's byte loads in flight
+                    __builtin_nontemporal_store(
+                        v, reinterpret_cast<__attribute__((address_space(1))) v4u *>(out_base + (uint32_t)q));
                 }
-                uint32_t x = (uint32_t)(q - (int)(i * H));  // source offset of chunk byte 0 (payload bytes)
-                uint32_t d = 0;
-                if (x + 16u > c.in_len) {  // the last segment's end: load the input's last 16 B, shift below
-                    d = x + 16u - c.in_len;
-                    x = c.in_len - 16u;
+                if (f0 == 0) {
+                    Acc acc;
+                    if (pure)
+                        acc.add4(v);
+                    keyed_add(s_sum, li, fold16(acc.value()), lane);
                 }
-                mk[k] = pm | ((live ? hm : 0u) << 16);
-                ax[k] = (pm ? d : 0u) | nx | (li << 8);
-                v[k] = ld16(c.in + (pm ? x : 0u));
-            }
-            // 2. header images, L4 checksum field zero (waves round-robin over the tile's segments)
-            for (uint32_t li = wv; li < Kt; li += W) {
-                const uint32_t i = seg0 + li;
-                const SegFields f = seg_fields(c, i);
-                uint32_t tbl = 0;
-                tbl = (uint32_t)wg_writelane_i32((int)f.pktlen, kFldPkt, (int)tbl);
-                tbl = (uint32_t)wg_writelane_i32((int)(c.id0 + i), kFldId, (int)tbl);
-                tbl = (uint32_t)wg_writelane_i32((int)f.ipcs, kFldIpcs, (int)tbl);
-                tbl = (uint32_t)wg_writelane_i32(0, kFldL4cs, (int)tbl);
-                tbl = (uint32_t)wg_writelane_i32((int)f.seq, kFldSeq, (int)tbl);
-                tbl = (uint32_t)wg_writelane_i32((int)(f.pktlen - c.cs), kFldUlen, (int)tbl);
-                tbl = (uint32_t)wg_writelane_i32((int)f.flags, kFldFlags, (int)tbl);
-                const uint32_t base = li * kImgBytes + (uint32_t)((out_base + tstart + li * S) & 15u);
-                const uint32_t r0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((c.hc0 & 7u) << 2), (int)tbl);
-                const uint32_t b0 = (c.hc0 & 7u) ? (r0 >> (c.hc0 >> 8)) & 0xffu : c.hb0;
-                if (lane < H)
-                    img8[base + lane] = (uint8_t)b0;
-                if (H > 64) {
-                    const uint32_t r1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((c.hc1 & 7u) << 2), (int)tbl);
-                    const uint32_t b1 = (c.hc1 & 7u) ? (r1 >> (c.hc1 >> 8)) & 0xffu : c.hb1;
-                    if (lane + 64 < H)
-                        img8[base + lane + 64] = (uint8_t)b1;
-                }
-            }
-            // 3. payload sums per segment
-#pragma unroll
-            for (int k = 0; k < U; k++) {
-                const uint32_t d = ax[k] & 15u;
-                if (__ballot(d != 0u))
-                    v[k] = d ? shr_bytes(v[k], d) : v[k];
-                const uint32_t pm = mk[k] & 0xffffu, li = (ax[k] >> 8) & 0xffu;
-                Acc acc;
-                if (pm == 0xffffu) {
-                    acc.add4(v[k]);
-                } else {
-#pragma unroll
-                    for (int dd = 0; dd < 4; dd++) acc.add(v4get(v[k], dd) & bexpand(pm, dd));
-                }
-                const uint32_t ps = fold16(acc.value());
-                const uint32_t kf = (uint32_t)__builtin_amdgcn_readfirstlane((int)li);
-                const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)li, 63);
-                if (kf == kl) {
-                    const uint32_t s0 = wave_sum_u32(ps);
-                    if (lane == 0)
-                        atomicAdd(&s_sum[kf], s0);
-                } else if (kl == kf + 1u) {
-                    const uint32_t s0 = wave_sum_u32(li == kf ? ps : 0u);
-                    const uint32_t s1 = wave_sum_u32(li == kf ? 0u : ps);
-                    if (lane == 0) {
-                        atomicAdd(&s_sum[kf], s0);
-                        atomicAdd(&s_sum[kl], s1);
-                    }
-                } else {
-                    atomicAdd(&s_sum[li], ps);
-                }
+                if (pay)
+                    st8(out_base + pos, bb);
+                keyed_add(s_sum, bl, bb << (8u * ((omis + pos) & 1u)), lane);
             }
             __syncthreads();
-            // 4. the L4 checksums (offload.cpp:202-204: native order, UDP 0 stays 0)
+            // 3. per segment: the L4 checksum and the other fields (offload.cpp:168-204)
             if (t < Kt) {
-                const uint32_t li = t, i = seg0 + li;
+                const uint32_t i = seg0 + t;
                 const SegFields f = seg_fields(c, i);
-                const uint32_t gs = tstart + li * S;
-                uint32_t lp = fold16_32(s_sum[li]);
-                s_sum[li] = 0;  // for the block's next tile (behind the barrier below)
-                if ((out_base + gs + c.cs) & 1u)  // summed in absolute pairing; the L4 region pairs from gs + cs
+                const uint32_t gs = tstart + t * S;
+                uint32_t lp = fold16_32(s_sum[t]);
+                s_sum[t] = 0;  // for the block's next tile (behind the barrier below)
+                if ((omis + gs + c.cs) & 1u)  // summed in absolute pairing; the L4 region pairs from gs + cs
                     lp = bswap16(lp);
                 uint32_t l4h = c.l4h_base;
                 if (c.tcp)
                     l4h += bswap16(f.seq >> 16) + bswap16(f.seq & 0xffffu) + (f.flags << 8);
                 else
                     l4h += bswap16((f.pktlen - c.cs) & 0xffffu);
-                const uint32_t T4 = lp + l4h + c.ps_sum + proto + bswap16((f.pktlen - c.cs) & 0xffffu);
-                const uint32_t l4cs = ~fold16_32(T4) & 0xffffu;
-                const uint32_t base = li * kImgBytes + (uint32_t)((out_base + gs) & 15u);
-                img8[base + c.l4off] = (uint8_t)l4cs;
-                img8[base + c.l4off + 1u] = (uint8_t)(l4cs >> 8);
+                const uint32_t T4 = lp + l4h + c.ps_sum + ((c.tcp ? 6u : 17u) << 8) + bswap16((f.pktlen - c.cs) & 0xffffu);
+                uint32_t *fl = &s_fld[t * 8u];
+                fl[kFldPkt] = f.pktlen;
+                fl[kFldId] = c.id0 + i;
+                fl[kFldIpcs] = f.ipcs;
+                fl[kFldL4cs] = ~fold16_32(T4) & 0xffffu;
+                fl[kFldSeq] = f.seq;
+                fl[kFldUlen] = f.pktlen - c.cs;
+                fl[kFldFlags] = f.flags;
             }
             __syncthreads();
-            // 5. merge the headers, store
-#pragma unroll
-            for (int k = 0; k < U; k++) {
-                const uint32_t ck = (uint32_t)k * kThreads + t;
-                if (ck >= nch)
-                    continue;
-                const uint32_t pm = mk[k] & 0xffffu, hm = mk[k] >> 16;
-                const uintptr_t A = A0 + 16u * ck;
-                v4u o = v[k];
-                if (hm) {
-                    const uint32_t lh = ((ax[k] >> 8) & 0xffu) + ((ax[k] >> 4) & 1u);
-                    const uintptr_t gh = out_base + tstart + lh * S;
-                    const uint32_t off = lh * kImgBytes + (uint32_t)(A - (gh & ~(uintptr_t)15));
-                    const v4u im = *reinterpret_cast<const v4u *>(img8 + off);
-                    o = v4u{(v[k].x & bexpand(pm, 0)) | (im.x & bexpand(hm, 0)),
-                            (v[k].y & bexpand(pm, 1)) | (im.y & bexpand(hm, 1)),
-                            (v[k].z & bexpand(pm, 2)) | (im.z & bexpand(hm, 2)),
-                            (v[k].w & bexpand(pm, 3)) | (im.w & bexpand(hm, 3))};
-                }
-                // every tile byte is header or payload: a chunk is whole unless it
-                // holds a tile edge
-                const uint32_t own = pm | hm;
-                if (own == 0xffffu) {
-                    *reinterpret_cast<__attribute__((address_space(1))) v4u *>(A) = o;
-                } else {
-#pragma unroll
-                    for (int jb = 0; jb < 16; jb++)
-                        if ((own >> jb) & 1u)
-                            st8(A + jb, v4get(o, jb >> 2) >> (8 * (jb & 3)));
+            // 4. the headers, a byte per lane (the reference's write order, :168-204)
+            for (uint32_t f0 = 0; f0 < Kt * H; f0 += kThreads) {
+                const uint32_t f = f0 + t;
+                const uint32_t hs = div_small(f, H, rH);
+                if (hs < Kt) {
+                    const uint32_t j = f - hs * H;
+                    const uint32_t code = hdr_code(c, j);
+                    const uint32_t tb = ld8(c.in + j);
+                    const uint32_t val = (code & 7u) ? (s_fld[hs * 8u + (code & 7u)] >> (code >> 8)) & 0xffu : tb;
+                    st8(out_base + tstart + hs * S + j, val);
                 }
             }
             if (tile + T < ntiles || more_units)
-                __syncthreads();  // the images / sums are rewritten by the next tile
+                __syncthreads();  // the sums / field tables are rewritten by the next tile
         }
     }
 }
@@ -1059,14 +988,22 @@ int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, u
     // 2. the split
     if (!hdr_only && t.gso_rows && t.gso_ablate == 0) {
         // the row-order tile kernel: gso_tiles blocks per super-buffer
-        uint64_t blocks = n * t.gso_tiles;
+        // blocks per super-buffer: gso_tiles, or (0) the tiles of a 64-KiB
+        // TSO / USO super-buffer at MTU 1500 (45 segments of <= 1,500 B);
+        // other geometries are served all the same (blocks loop over tiles
+        // or find none)
+        const uint32_t tw = t.gso_tile_waves;
+        const uint32_t kseg = (16u * 64u * tw - 30u) / 1500u;
+        p.tiles = t.gso_tiles ? t.gso_tiles : (45u + kseg - 1u) / kseg;
+        uint64_t blocks = n * p.tiles;
         blocks = blocks < t.gso_blocks ? blocks : t.gso_blocks;
         if (blocks >= 8)
             blocks = (blocks + 7) & ~7ull;  // the XCD swizzle wants a multiple of 8 (extra blocks find no unit)
-        switch (t.gso_tile_u) {
-        case 2: hipLaunchKernelGGL((gso_tile_kernel<4, 2>), dim3((unsigned)blocks), dim3(256), 0, st, p); break;
-        case 4: hipLaunchKernelGGL((gso_tile_kernel<4, 4>), dim3((unsigned)blocks), dim3(256), 0, st, p); break;
-        default: hipLaunchKernelGGL((gso_tile_kernel<4, 3>), dim3((unsigned)blocks), dim3(256), 0, st, p); break;
+        switch (t.gso_tile_waves) {
+        case 4: hipLaunchKernelGGL((gso_tile_kernel<4>), dim3((unsigned)blocks), dim3(256), 0, st, p); break;
+        case 8: hipLaunchKernelGGL((gso_tile_kernel<8>), dim3((unsigned)blocks), dim3(512), 0, st, p); break;
+        case 12: hipLaunchKernelGGL((gso_tile_kernel<12>), dim3((unsigned)blocks), dim3(768), 0, st, p); break;
+        default: hipLaunchKernelGGL((gso_tile_kernel<3>), dim3((unsigned)blocks), dim3(192), 0, st, p); break;
         }
         if (hipGetLastError() != hipSuccess || !debug_sync(st, "gso_tile_kernel"))
             return WG_ERR_LAUNCH;
