@@ -99,26 +99,41 @@ template <bool kNT, int U = 4>
 __device__ __forceinline__ uint32_t finish(uint32_t lane, const Front &f) {
     static_assert(U == 4 || U == 8, "loads in flight");
     Acc acc;
-    acc.add4(f.v0);
-    acc.add4(f.v1);
     if (f.nint > 128) {  // long packet (> ~2 KiB): stream the rest, U loads in flight
         const uintptr_t q = f.c0;
         const uint32_t last = f.nint - 1;
         // wave-uniform trip count: every round issues U loads (lanes past the
         // end re-read the last chunk and are masked), so the remainder is one
-        // round trip too
-        for (uint32_t k0 = 128; k0 < f.nint; k0 += 64 * U) {
-            v4u a[U];
+        // round trip too.  The first round goes out BEFORE the issue phase's
+        // chunks are consumed (loads return in order: the adds of v0 / v1 wait
+        // for those alone), so a packet of up to 128 + 64 U chunks costs one
+        // memory round trip, not two.
+        uint32_t k0 = 128;
+        v4u a[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t k = k0 + 64 * u + lane;
+            a[u] = ld16x<kNT>(q + 16ull * (k < last ? k : last));
+        }
+        acc.add4(f.v0);
+        acc.add4(f.v1);
+        for (;;) {
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (k0 + 64 * u + lane < f.nint)
+                    acc.add4(a[u]);
+            k0 += 64 * U;
+            if (k0 >= f.nint)
+                break;
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const uint32_t k = k0 + 64 * u + lane;
                 a[u] = ld16x<kNT>(q + 16ull * (k < last ? k : last));
             }
-#pragma unroll
-            for (int u = 0; u < U; u++)
-                if (k0 + 64 * u + lane < f.nint)
-                    acc.add4(a[u]);
         }
+    } else {
+        acc.add4(f.v0);
+        acc.add4(f.v1);
     }
     if (!f.bt)
         acc.add(f.bv);
