@@ -87,6 +87,73 @@ __global__ __launch_bounds__(B) void tile1_copy(const unsigned char *in, unsigne
     else *p = v;
 }
 
+// The production split's shape (gso.hip gso_split_kernel: 3 blocks of 4 waves
+// per super-buffer, 4 consecutive segments per wave with all their loads in
+// flight, destination-aligned interior chunks, edge and header bytes one per
+// lane), copy only.  P: 0 default policy; 1 non-temporal stores for chunks
+// whose 128-B line lies inside the segment's interior (edge lines default);
+// 2 = 1 + non-temporal loads for those chunks; 3 every chunk non-temporal.
+template <int P>
+__global__ __launch_bounds__(256) void seg_copy(const unsigned char *in, unsigned char *out) {
+    unsigned b = blockIdx.x;
+    if (!(gridDim.x & 7u)) b = (b & 7u) * (gridDim.x >> 3) + (b >> 3);
+    const unsigned sb = b / 3u, grp = b % 3u;
+    if (sb >= N) return;
+    const unsigned lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uintptr_t src = (uintptr_t)in + (uintptr_t)sb * IN_STRIDE, dst = (uintptr_t)out + (uintptr_t)sb * OUT_STRIDE;
+    const unsigned s0 = (grp * 4u + wv) * 4u;
+    v4u lo[4][2];
+    unsigned eb[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const unsigned i = s0 + k < NSEG ? s0 + k : NSEG - 1u;
+        const unsigned dl = IN_LEN - H - i * G < G ? IN_LEN - H - i * G : G;
+        const uintptr_t oa = dst + i * S + H, sa = src + H + i * G;
+        const uintptr_t c0 = (oa + 15u) & ~(uintptr_t)15, c1 = (oa + dl) & ~(uintptr_t)15;
+        const unsigned nint = c1 > c0 ? (unsigned)((c1 - c0) >> 4) : 0u;
+        const uintptr_t base = c0 + (sa - oa);
+        const unsigned last = nint ? nint - 1u : 0u;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const unsigned kk = lane + 64u * h < last ? lane + 64u * h : last;
+            const uintptr_t a = base + 16u * kk;
+            const uintptr_t la = (c0 + 16u * kk) & ~(uintptr_t)127;
+            const bool inner = la >= c0 && la + 128u <= c1;
+            if ((P == 3) || (P == 2 && inner)) lo[k][h] = __builtin_nontemporal_load(reinterpret_cast<gc_v4u *>(a));
+            else lo[k][h] = *reinterpret_cast<gc_v4u *>(a);
+        }
+        const unsigned he = (unsigned)((c0 < oa + dl ? c0 : oa + dl) - oa), ts = (unsigned)((c1 > c0 ? c1 : c0) - oa);
+        const unsigned xt = ts + lane - 16u;
+        const unsigned eo = lane < 16u && lane < he ? lane : (lane >= 16u && lane < 32u && xt < dl ? xt : 0xffffffffu);
+        eb[k] = eo != 0xffffffffu ? *reinterpret_cast<const unsigned char *>(sa + eo) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const unsigned i = s0 + k;
+        if (i >= NSEG) break;
+        const unsigned dl = IN_LEN - H - i * G < G ? IN_LEN - H - i * G : G;
+        const uintptr_t seg = dst + i * S, oa = seg + H;
+        const uintptr_t c0 = (oa + 15u) & ~(uintptr_t)15, c1 = (oa + dl) & ~(uintptr_t)15;
+        const unsigned nint = c1 > c0 ? (unsigned)((c1 - c0) >> 4) : 0u;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const unsigned kk = lane + 64u * h;
+            if (kk < nint) {
+                const uintptr_t a = c0 + 16u * kk;
+                const uintptr_t la = a & ~(uintptr_t)127;
+                const bool inner = la >= c0 && la + 128u <= c1;
+                if (P == 3 || (P >= 1 && inner)) __builtin_nontemporal_store(lo[k][h], reinterpret_cast<g_v4u *>(a));
+                else *reinterpret_cast<g_v4u *>(a) = lo[k][h];
+            }
+        }
+        const unsigned he = (unsigned)((c0 < oa + dl ? c0 : oa + dl) - oa), ts = (unsigned)((c1 > c0 ? c1 : c0) - oa);
+        const unsigned xt = ts + lane - 16u;
+        const unsigned eo = lane < 16u && lane < he ? lane : (lane >= 16u && lane < 32u && xt < dl ? xt : 0xffffffffu);
+        if (eo != 0xffffffffu) *reinterpret_cast<unsigned char *>(oa + eo) = (unsigned char)eb[k];
+        if (lane < H) *reinterpret_cast<unsigned char *>(seg + lane) = *reinterpret_cast<const unsigned char *>(src + lane);
+    }
+}
+
 // Row windows (round 2's R0): a block of B threads per B x 16-B output window
 // of the super-buffer (segments straddle windows), one chunk per thread.
 template <int B, int NT>
@@ -149,7 +216,25 @@ int main(int argc, char **argv) {
         hipEventElapsedTime(&ms, e0, e1);
         printf("{\"variant\": \"%s\", \"ms\": %.4f, \"TBps\": %.3f}\n", name, ms / iters, alg / (ms / iters * 1e-3) / 1e12);
     };
+    auto runseg = [&](auto kern, const char *name) {
+        const unsigned grid = N * 3u;
+        for (int w = 0; w < 3; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, in, out);
+        hipEventRecord(e0);
+        for (int w = 0; w < iters; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, in, out);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        printf("{\"variant\": \"%s\", \"ms\": %.4f, \"TBps\": %.3f}\n", name, ms / iters, alg / (ms / iters * 1e-3) / 1e12);
+    };
+    const bool segs_only = argc > 2;
     for (int rep = 0; rep < 2; rep++) {
+        runseg(seg_copy<0>, "S production shape, default policy");
+        runseg(seg_copy<1>, "S production shape, nt stores on interior lines");
+        runseg(seg_copy<2>, "S production shape, nt loads + stores on interior lines");
+        runseg(seg_copy<3>, "S production shape, every chunk nt");
+        runrow(row_copy<256, 3>, 256, "R0 rows 4 KiB blocks nt both");
+        if (segs_only) continue;
         run(tile1_copy<192, 3, 0>, 23, "T1 tiles of 2 segments, 192 threads, 1 chunk each, nt both");
         run(tile1_copy<192, 3, 1>, 23, "T1 192 threads, nt except the tile-edge lines");
         run(tile1_copy<192, 0, 0>, 23, "T1 192 threads, default policy");
