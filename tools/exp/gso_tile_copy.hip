@@ -93,19 +93,20 @@ __global__ __launch_bounds__(B) void tile1_copy(const unsigned char *in, unsigne
 // lane), copy only.  P: 0 default policy; 1 non-temporal stores for chunks
 // whose 128-B line lies inside the segment's interior (edge lines default);
 // 2 = 1 + non-temporal loads for those chunks; 3 every chunk non-temporal.
-template <int P>
+template <int P, int SPW = 4, int BY = 1>
 __global__ __launch_bounds__(256) void seg_copy(const unsigned char *in, unsigned char *out) {
+    constexpr unsigned GRP = (NSEG + 4 * SPW - 1) / (4 * SPW);  // blocks per super-buffer
     unsigned b = blockIdx.x;
     if (!(gridDim.x & 7u)) b = (b & 7u) * (gridDim.x >> 3) + (b >> 3);
-    const unsigned sb = b / 3u, grp = b % 3u;
+    const unsigned sb = b / GRP, grp = b % GRP;
     if (sb >= N) return;
     const unsigned lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uintptr_t src = (uintptr_t)in + (uintptr_t)sb * IN_STRIDE, dst = (uintptr_t)out + (uintptr_t)sb * OUT_STRIDE;
-    const unsigned s0 = (grp * 4u + wv) * 4u;
-    v4u lo[4][2];
-    unsigned eb[4];
+    const unsigned s0 = (grp * 4u + wv) * SPW;
+    v4u lo[SPW][2];
+    unsigned eb[SPW];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < SPW; k++) {
         const unsigned i = s0 + k < NSEG ? s0 + k : NSEG - 1u;
         const unsigned dl = IN_LEN - H - i * G < G ? IN_LEN - H - i * G : G;
         const uintptr_t oa = dst + i * S + H, sa = src + H + i * G;
@@ -128,7 +129,7 @@ __global__ __launch_bounds__(256) void seg_copy(const unsigned char *in, unsigne
         eb[k] = eo != 0xffffffffu ? *reinterpret_cast<const unsigned char *>(sa + eo) : 0u;
     }
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < SPW; k++) {
         const unsigned i = s0 + k;
         if (i >= NSEG) break;
         const unsigned dl = IN_LEN - H - i * G < G ? IN_LEN - H - i * G : G;
@@ -149,8 +150,8 @@ __global__ __launch_bounds__(256) void seg_copy(const unsigned char *in, unsigne
         const unsigned he = (unsigned)((c0 < oa + dl ? c0 : oa + dl) - oa), ts = (unsigned)((c1 > c0 ? c1 : c0) - oa);
         const unsigned xt = ts + lane - 16u;
         const unsigned eo = lane < 16u && lane < he ? lane : (lane >= 16u && lane < 32u && xt < dl ? xt : 0xffffffffu);
-        if (eo != 0xffffffffu) *reinterpret_cast<unsigned char *>(oa + eo) = (unsigned char)eb[k];
-        if (lane < H) *reinterpret_cast<unsigned char *>(seg + lane) = *reinterpret_cast<const unsigned char *>(src + lane);
+        if (BY && eo != 0xffffffffu) *reinterpret_cast<unsigned char *>(oa + eo) = (unsigned char)eb[k];
+        if (BY && lane < H) *reinterpret_cast<unsigned char *>(seg + lane) = *reinterpret_cast<const unsigned char *>(src + lane);
     }
 }
 
@@ -216,8 +217,8 @@ int main(int argc, char **argv) {
         hipEventElapsedTime(&ms, e0, e1);
         printf("{\"variant\": \"%s\", \"ms\": %.4f, \"TBps\": %.3f}\n", name, ms / iters, alg / (ms / iters * 1e-3) / 1e12);
     };
-    auto runseg = [&](auto kern, const char *name) {
-        const unsigned grid = N * 3u;
+    auto runseg = [&](auto kern, const char *name, unsigned grp = 3) {
+        const unsigned grid = N * grp;
         for (int w = 0; w < 3; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, in, out);
         hipEventRecord(e0);
         for (int w = 0; w < iters; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, in, out);
@@ -233,6 +234,11 @@ int main(int argc, char **argv) {
         runseg(seg_copy<1>, "S production shape, nt stores on interior lines");
         runseg(seg_copy<2>, "S production shape, nt loads + stores on interior lines");
         runseg(seg_copy<3>, "S production shape, every chunk nt");
+        runseg(seg_copy<0, 4, 0>, "S2 no byte stores, default");
+        runseg(seg_copy<3, 4, 0>, "S2 no byte stores, every chunk nt");
+        runseg(seg_copy<0, 1, 1>, "S1 one segment per wave, default", 12);
+        runseg(seg_copy<3, 1, 0>, "S1 one segment per wave, no byte stores, nt", 12);
+        runseg(seg_copy<0, 1, 0>, "S1 one segment per wave, no byte stores, default", 12);
         runrow(row_copy<256, 3>, 256, "R0 rows 4 KiB blocks nt both");
         if (segs_only) continue;
         run(tile1_copy<192, 3, 0>, 23, "T1 tiles of 2 segments, 192 threads, 1 chunk each, nt both");
