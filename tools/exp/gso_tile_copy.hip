@@ -155,6 +155,126 @@ __global__ __launch_bounds__(256) void seg_copy(const unsigned char *in, unsigne
     }
 }
 
+// Row windows with the split's work added level by level (timing only: the
+// header bytes and checksums written are placeholders):
+//   V1  + a per-super-buffer record (scalar load) giving the geometry at run
+//       time, chunk -> segment by a float reciprocal
+//   V2  + each chunk's payload sum (whole chunks: 4 adds; chunks touching a
+//       header or a payload end: byte masks), a two-key DPP reduction per
+//       wave row, one non-returning global atomic per (wave, segment)
+//   V3  + header bytes merged into the header chunks from an LDS image the
+//       wave writes (lane j = byte j), header chunks stored default-policy
+//   V4  + the atomic returns; the segment's last contributor stores the
+//       2-byte checksum field (default policy) and clears its slot
+struct XRec {
+    unsigned hdr, gso, in_len, pad;
+};
+__device__ __forceinline__ unsigned xmask16(int lo, int hi) {
+    lo = lo < 0 ? 0 : (lo > 16 ? 16 : lo);
+    hi = hi < 0 ? 0 : (hi > 16 ? 16 : hi);
+    return hi > lo ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
+}
+__device__ __forceinline__ unsigned xexp(unsigned m16, int d) {
+    const unsigned n = (m16 >> (4 * d)) & 15u, x = (n * 0x00204081u) & 0x01010101u;
+    return (x << 8) - x;
+}
+__device__ __forceinline__ unsigned xwsum(unsigned v) {
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
+    return (unsigned)__builtin_amdgcn_readlane((int)v, 0) + (unsigned)__builtin_amdgcn_readlane((int)v, 16) +
+           (unsigned)__builtin_amdgcn_readlane((int)v, 32) + (unsigned)__builtin_amdgcn_readlane((int)v, 48);
+}
+template <int V>
+__global__ __launch_bounds__(256) void rowk(const unsigned char *in, unsigned char *out, unsigned rows,
+                                            const XRec *recs, unsigned long long *slots) {
+    __shared__ unsigned char img[4][192];
+    unsigned b = blockIdx.x;
+    if (!(gridDim.x & 7u)) b = (b & 7u) * (gridDim.x >> 3) + (b >> 3);
+    const unsigned sb = b / rows, row = b % rows;
+    if (sb >= N) return;
+    const unsigned lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uintptr_t src = (uintptr_t)in + (uintptr_t)sb * IN_STRIDE, dst = (uintptr_t)out + (uintptr_t)sb * OUT_STRIDE;
+    const XRec r = recs[sb];
+    const unsigned h = r.hdr, gso = r.gso, in_len = r.in_len, seg = h + gso;
+    const unsigned nseg = (in_len - h + gso - 1u) / gso, olen = in_len - h + nseg * h;
+    const unsigned o = (row * 256u + threadIdx.x) * 16u;
+    const bool live = o < olen;
+    const unsigned oc = live ? o : olen - 16u;
+    const float rs = 1.0f / (float)seg;
+    unsigned i = (unsigned)((float)oc * rs);
+    i = i * seg > oc ? i - 1u : ((i + 1u) * seg <= oc ? i + 1u : i);
+    const unsigned g = i * seg, dl = in_len - h - i * gso < gso ? in_len - h - i * gso : gso;
+    const int q = (int)oc;
+    const unsigned pm = live ? xmask16((int)(g + h) - q, (int)(g + h + dl) - q) : 0u;
+    unsigned x = oc - i * h;
+    if (x + 16u > in_len) x = in_len - 16u;
+    v4u v = __builtin_nontemporal_load(reinterpret_cast<gc_v4u *>(src + (pm ? x : 0u)));
+    unsigned hm = 0, hseg = i;
+    if (V >= 3) {
+        hm = xmask16((int)g - q, (int)(g + h) - q);
+        if (!hm && i + 1u < nseg) {
+            hm = xmask16((int)(g + seg) - q, (int)(g + seg + h) - q);
+            hseg = i + 1u;
+        }
+        // the wave's header image: the first segment starting in its 1 KiB row
+        const unsigned w0 = row * 4096u + wv * 1024u;
+        const unsigned sh = (w0 + seg - 1u) / seg, hs = sh * seg;
+        if (hs < w0 + 1024u && hs < olen && lane < h)
+            img[wv][(hs & 15u) + lane] = (unsigned char)(lane * 7u + sh);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (hm && live) {
+            const unsigned hs2 = hseg * seg;
+            const unsigned off = (hs2 & 15u) + (o - (hs2 & ~15u)) - (hs2 & 15u);
+            v4u im = *reinterpret_cast<const v4u *>(&img[wv][off < 176u ? off & ~15u : 0u]);
+            v = v4u{(v.x & xexp(pm, 0)) | (im.x & xexp(hm, 0)), (v.y & xexp(pm, 1)) | (im.y & xexp(hm, 1)),
+                    (v.z & xexp(pm, 2)) | (im.z & xexp(hm, 2)), (v.w & xexp(pm, 3)) | (im.w & xexp(hm, 3))};
+        }
+    }
+    if (live) {
+        g_v4u *pp = reinterpret_cast<g_v4u *>(dst + o);
+        if (V >= 3 && hm) *pp = v;
+        else __builtin_nontemporal_store(v, pp);
+    }
+    if (V >= 2) {
+        unsigned lo = 0, hi = 0, c;
+        if (pm == 0xffffu) {
+            lo = __builtin_addc(lo, v.x, 0u, &c); hi += c;
+            lo = __builtin_addc(lo, v.y, 0u, &c); hi += c;
+            lo = __builtin_addc(lo, v.z, 0u, &c); hi += c;
+            lo = __builtin_addc(lo, v.w, 0u, &c); hi += c;
+        } else {
+            lo = __builtin_addc(lo, v.x & xexp(pm, 0), 0u, &c); hi += c;
+            lo = __builtin_addc(lo, v.y & xexp(pm, 1), 0u, &c); hi += c;
+            lo = __builtin_addc(lo, v.z & xexp(pm, 2), 0u, &c); hi += c;
+            lo = __builtin_addc(lo, v.w & xexp(pm, 3), 0u, &c); hi += c;
+        }
+        unsigned t = (lo & 0xffffu) + (lo >> 16) + hi;
+        t = (t & 0xffffu) + (t >> 16);
+        const unsigned kf = (unsigned)__builtin_amdgcn_readfirstlane((int)i);
+        const unsigned kl = (unsigned)__builtin_amdgcn_readlane((int)i, 63);
+        const unsigned s0 = xwsum(i == kf ? t : 0u), s1 = xwsum(i == kf ? 0u : t);
+        if (lane < 2u && (lane == 0u || kl != kf)) {
+            const unsigned k = lane ? kl : kf;
+            unsigned long long *slot = slots + (size_t)sb * 48u + k;
+            const unsigned long long add = (1ull << 48) | (lane ? s1 : s0);
+            if (V >= 4) {
+                const unsigned long long old = atomicAdd(slot, add);
+                if ((old >> 48) == 1ull) {  // placeholder completion rule (2 contributions)
+                    *slot = 0ull;
+                    const unsigned cs = ~(unsigned)((old + add) & 0xffffu) & 0xffffu;
+                    *reinterpret_cast<unsigned short *>(dst + k * seg + 36u) = (unsigned short)cs;
+                }
+            } else {
+                __hip_atomic_fetch_add(slot, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+}
+
 // Row windows (round 2's R0): a block of B threads per B x 16-B output window
 // of the super-buffer (segments straddle windows), one chunk per thread.
 template <int B, int NT>
@@ -228,6 +348,40 @@ int main(int argc, char **argv) {
         hipEventElapsedTime(&ms, e0, e1);
         printf("{\"variant\": \"%s\", \"ms\": %.4f, \"TBps\": %.3f}\n", name, ms / iters, alg / (ms / iters * 1e-3) / 1e12);
     };
+    XRec *recs;
+    unsigned long long *slots;
+    hipMalloc(&recs, (size_t)N * sizeof(XRec));
+    hipMalloc(&slots, (size_t)N * 48 * 8);
+    hipMemset(slots, 0, (size_t)N * 48 * 8);
+    {
+        XRec *hr = (XRec *)malloc((size_t)N * sizeof(XRec));
+        for (unsigned k = 0; k < N; k++) hr[k] = XRec{H, G, IN_LEN, 0};
+        hipMemcpy(recs, hr, (size_t)N * sizeof(XRec), hipMemcpyHostToDevice);
+        free(hr);
+    }
+    auto runv = [&](auto kern, const char *name) {
+        const unsigned rows = (OUT_LEN + 4095) / 4096;
+        const unsigned grid = ((N * rows + 7) / 8) * 8;
+        for (int w = 0; w < 3; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, in, out, rows, recs, slots);
+        hipEventRecord(e0);
+        for (int w = 0; w < iters; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, in, out, rows, recs, slots);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        printf("{\"variant\": \"%s\", \"ms\": %.4f, \"TBps\": %.3f}\n", name, ms / iters, alg / (ms / iters * 1e-3) / 1e12);
+    };
+    if (argc > 2 && !strcmp(argv[2], "rowk")) {
+        for (int rep = 0; rep < 2; rep++) {
+            runrow(row_copy<256, 3>, 256, "R0 rows 4 KiB blocks nt both");
+            runv(rowk<1>, "V1 + record, run-time geometry");
+            runv(rowk<2>, "V2 + chunk sums, two-key reduction, atomics");
+            runv(rowk<3>, "V3 + header merge from a wave LDS image");
+            runv(rowk<4>, "V4 + returning atomics, last contributor stores the checksum");
+        }
+        printf("{\"err\": \"%s\"}\n", hipGetErrorString(hipGetLastError()));
+        return 0;
+    }
     const bool segs_only = argc > 2;
     for (int rep = 0; rep < 2; rep++) {
         runseg(seg_copy<0>, "S production shape, default policy");
