@@ -212,7 +212,7 @@ __global__ __launch_bounds__(256) void rowk(const unsigned char *in, unsigned ch
     if (x + 16u > in_len) x = in_len - 16u;
     v4u v = __builtin_nontemporal_load(reinterpret_cast<gc_v4u *>(src + (pm ? x : 0u)));
     unsigned hm = 0, hseg = i;
-    if (V >= 3) {
+    if (V >= 3 && V <= 4) {
         hm = xmask16((int)g - q, (int)(g + h) - q);
         if (!hm && i + 1u < nseg) {
             hm = xmask16((int)(g + seg) - q, (int)(g + seg + h) - q);
@@ -236,10 +236,17 @@ __global__ __launch_bounds__(256) void rowk(const unsigned char *in, unsigned ch
     }
     if (live) {
         g_v4u *pp = reinterpret_cast<g_v4u *>(dst + o);
-        if (V >= 3 && hm) *pp = v;
+        if (V >= 3 && V <= 4 && hm) *pp = v;
         else __builtin_nontemporal_store(v, pp);
     }
-    if (V >= 2) {
+    if (V == 6) {  // the atomics alone: one non-returning add per (wave, segment), constant values
+        const unsigned kf = (unsigned)__builtin_amdgcn_readfirstlane((int)i);
+        const unsigned kl = (unsigned)__builtin_amdgcn_readlane((int)i, 63);
+        if (lane < 2u && (lane == 0u || kl != kf))
+            __hip_atomic_fetch_add(slots + (size_t)sb * 48u + (lane ? kl : kf), (1ull << 48) | 7ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (V >= 2 && V != 6) {
         unsigned lo = 0, hi = 0, c;
         if (pm == 0xffffu) {
             lo = __builtin_addc(lo, v.x, 0u, &c); hi += c;
@@ -261,7 +268,9 @@ __global__ __launch_bounds__(256) void rowk(const unsigned char *in, unsigned ch
             const unsigned k = lane ? kl : kf;
             unsigned long long *slot = slots + (size_t)sb * 48u + k;
             const unsigned long long add = (1ull << 48) | (lane ? s1 : s0);
-            if (V >= 4) {
+            if (V == 5) {  // the sums and reductions alone: kept in LDS, no atomic
+                reinterpret_cast<unsigned *>(img[wv])[lane] = (unsigned)add;
+            } else if (V >= 4) {
                 const unsigned long long old = atomicAdd(slot, add);
                 if ((old >> 48) == 1ull) {  // placeholder completion rule (2 contributions)
                     *slot = 0ull;
@@ -378,6 +387,8 @@ int main(int argc, char **argv) {
             runv(rowk<2>, "V2 + chunk sums, two-key reduction, atomics");
             runv(rowk<3>, "V3 + header merge from a wave LDS image");
             runv(rowk<4>, "V4 + returning atomics, last contributor stores the checksum");
+            runv(rowk<5>, "V5 = V2 without the atomics (sums to LDS)");
+            runv(rowk<6>, "V6 = V1 + the atomics alone (no sums)");
         }
         printf("{\"err\": \"%s\"}\n", hipGetErrorString(hipGetLastError()));
         return 0;
