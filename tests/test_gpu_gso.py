@@ -30,24 +30,16 @@ def _wga():
                         {"gso_groups": 3, "gso_spw": 2}, {"gso_groups": 2, "gso_spw": 0},
                         {"gso_groups": 12, "gso_waves": 1}, {"gso_groups": 7, "gso_waves": 2},
                         {"gso_groups": 3, "gso_spw": 1}, {"gso_groups": 2, "gso_spw": 3},
-                        {"gso_groups": 1, "gso_spw": 4, "gso_waves": 2},
-                        {"gso_rows": 1}, {"gso_rows": 1, "gso_tiles": 1}, {"gso_rows": 1, "gso_tiles": 2},
-                        {"gso_rows": 1, "gso_tiles": 64}, {"gso_rows": 1, "gso_tile_waves": 8, "gso_tiles": 3},
-                        {"gso_rows": 1, "gso_tile_waves": 4}, {"gso_rows": 1, "gso_tile_waves": 12, "gso_tiles": 5}],
+                        {"gso_groups": 1, "gso_spw": 4, "gso_waves": 2}],
                 ids=["swizzled", "launch-order", "groups3", "groups12", "groups5x8", "groups3-pairs",
                      "groups2-serial", "groups12x1", "groups7x2", "groups3-pingpong", "groups2-triples",
-                     "groups1x2-quads", "rows", "rows-tiles1", "rows-tiles2", "rows-tiles64", "rows-w8-tiles3",
-                     "rows-w4", "rows-w12-tiles5"])
+                     "groups1x2-quads"])
 def variant(request):
     """Every correct block -> (super-buffer, segment slot) mapping of the GSO
     kernel: one looping block per super-buffer (XCD-swizzled or in launch
-    order) and several blocks per super-buffer (flat grid groups); and the
-    row-order tile kernel (gso_rows) with 1, 2, 3, 5, 23 (auto) and 64 blocks
-    per super-buffer (blocks looping over tiles, idle blocks) at 3, 4, 8 and
-    12 waves per block."""
+    order) and several blocks per super-buffer (flat grid groups)."""
     wga = _wga()
-    saved = {k: wga.tune_get(k) for k in ("gso_ablate", "gso_groups", "gso_waves", "gso_spw", "gso_rows",
-                                          "gso_tiles", "gso_tile_waves")}
+    saved = {k: wga.tune_get(k) for k in ("gso_ablate", "gso_groups", "gso_waves", "gso_spw")}
     for k, v in request.param.items():
         wga.tune_set(k, v)
     yield request.param
@@ -221,10 +213,9 @@ def test_geometry_edges(gpu, variant):
     for cs in (508, 600):
         p = _far_csum_start(rng, cs, 5000)
         cases.append((p, dict(flags=1, gso_type=1, gso_size=1000, csum_start=cs, csum_offset=16), None))
-    # the row-order kernel's tile capacity (16 x 256 x U bytes, a segment fits
-    # when hdr_len + gso + 30 <= it): segments at the limit, one past it (the
-    # segment-per-wave path in the same kernel), two and 32+ per tile, and a
-    # header of 128 / 129 bytes (TCP options + IPv4 options)
+    # segments of 8-16 KB (near and past 8,162 / 12,258 / 16,354 B, once a
+    # row-order kernel's tile limits), 16-100-B segments by the hundred, and
+    # headers of 88 / 92 / 128 / 129 bytes (IPv4 options + TCP options)
     for cap in (8192, 12288, 16384):
         for seg in (cap - 30, cap - 29, (cap - 30) // 2, (cap - 30) // 2 + 1):
             p = pktbuild.build(False, True, rng.integers(0, 256, 3 * (seg - 40) + 5, dtype=np.uint8).tobytes(),
@@ -242,7 +233,7 @@ def test_geometry_edges(gpu, variant):
         cs = 20 + ipopt
         pkt[cs + 12] = 15 << 4
         cases.append((bytes(pkt), dict(flags=1, gso_type=1, gso_size=700, csum_start=cs, csum_offset=16), None))
-    for cs in (68, 69):  # csum_start past the IP header: hdr_len 128 (a tile) / 129 (segment per wave)
+    for cs in (68, 69):  # csum_start past the IP header: hdr_len 128 / 129 (the register / general header paths)
         p = _far_csum_start(rng, cs, 9000)
         pkt = bytearray(p)
         pkt[cs + 12] = 15 << 4

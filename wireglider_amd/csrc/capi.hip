@@ -29,7 +29,7 @@ struct Knob {
 
 static const uint64_t kL4Small[] = {0, 5}, kL4SU[] = {0, 2}, kVSmall[] = {0, 6, 7, 8},
                       kWaves[] = {1, 2, 4, 8}, kAbl[] = {0, 1, 32},
-                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {0, 2, 3}, kParts[] = {1, 2, 3, 4, 8}, kTileW[] = {3, 4, 8, 12};
+                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {0, 2, 3}, kParts[] = {1, 2, 3, 4, 8};
 #define WG_N(a) (sizeof(a) / sizeof(a[0]))
 static const Knob kKnobs[] = {
     {"l4_blocks", &Tune::l4_blocks, nullptr, 1, 1u << 20, nullptr, 0},
@@ -55,9 +55,6 @@ static const Knob kKnobs[] = {
     {"aead_stage", nullptr, &Tune::aead_stage, 0, 1, nullptr, 0},
     {"encap_parts", nullptr, &Tune::encap_parts, 0, 0, kParts, WG_N(kParts)},
     {"encap_synth", nullptr, &Tune::encap_synth, 0, 1, nullptr, 0},
-    {"gso_rows", nullptr, &Tune::gso_rows, 0, 1, nullptr, 0},
-    {"gso_tiles", nullptr, &Tune::gso_tiles, 0, 64, nullptr, 0},
-    {"gso_tile_waves", nullptr, &Tune::gso_tile_waves, 0, 0, kTileW, WG_N(kTileW)},
 };
 #undef WG_N
 
@@ -129,9 +126,6 @@ static Tune &tune_storage() {
         x.verify_auto_t = 1;
         x.verify_k2min = 2048;
         x.gso_ablate = 0;
-        x.gso_rows = 0;
-        x.gso_tiles = 0;  // auto: enough blocks for a 64-KiB super-buffer of 1,500-B segments
-        x.gso_tile_waves = 3;
         // host pipeline chunk: 128-512 MiB reach 97-98 % of the raw H2D rate
         // (8 MiB: 70 %, per-chunk overheads; profiles/r02_host_path.json);
         // with both directions in flight 64 MiB: decap 35.2 ms vs 37.3 at

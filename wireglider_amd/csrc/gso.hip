@@ -505,273 +505,6 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
     }
 }
 
-// ---------------------------------------------------------------------------
-// Row-order tile kernel (knob gso_rows = 1).  The output of one super-buffer
-// is cut into TILES of K whole segments (at most 16 * 64W - 30 bytes); a
-// 64W-thread block takes one tile, ONE 16-B output chunk per lane in address
-// order — the copy shape of short row windows, measured at 5.27-5.38 ms for
-// config 3's bytes against 5.55-5.82 for segment-per-wave shapes on the same
-// boxes (profiles/r05_tile/).  Segments never straddle tiles, so every
-// checksum completes inside its block:
-//   1. a lane whose chunk lies inside one segment's payload (16-B aligned,
-//      destination side) loads it with ONE unaligned non-temporal 16-B load
-//      from in + (chunk - s * hdr_len), stores it non-temporally and sums it;
-//   2. the rest of each segment — its header and the <= 15-byte payload head
-//      and tail around the aligned chunks, at most hdr_len + 30 bytes — is a
-//      byte per lane over the block (payload bytes loaded, summed, stored);
-//      per-segment sums meet in LDS (two DPP reductions per wave when a row
-//      of 64 chunks spans two segments);
-//   3. one thread per segment turns its sum into the L4 checksum and the
-//      other per-segment fields (offload.cpp:168-204) into an LDS table;
-//   4. the header bytes, a byte per lane, from the table or the prefix.
-// Super-buffers the tile shape cannot take (gso < 16, headers over 128 B, a
-// segment over the tile capacity) run a light segment-per-wave loop in the
-// same kernel.  Results are bit-identical to gso_split_kernel's (tests).
-constexpr uint32_t kTileKMax = 32;  // segments per tile (LDS sums / field tables)
-
-// Per-segment header fields (offload.cpp:168-200): IPv4 total length / id /
-// header checksum, TCP seq + flags or UDP length.
-struct SegFields {
-    uint32_t pktlen, ipcs, seq, flags;
-};
-__device__ __forceinline__ SegFields seg_fields(const Ctx &c, uint32_t i) {
-    SegFields f;
-    const uint32_t off = i * c.gso;
-    const uint32_t datalen = c.rest - off < c.gso ? c.rest - off : c.gso;
-    f.pktlen = c.hdr_len + datalen;
-    f.ipcs = c.v6 ? 0u : ~fold16_32(c.ip_base + bswap16(f.pktlen & 0xffffu) + bswap16((c.id0 + i) & 0xffffu)) & 0xffffu;
-    f.seq = c.seq0 + c.gso * i;
-    f.flags = i + 1 == c.nseg ? c.flags13 : (c.flags13 & ~0x09u);  // FIN/PSH only on the last segment
-    return f;
-}
-
-// One segment by one wave, one chunk per lane at a time and every header
-// byte by the general field lookup: the tile kernel's path for the
-// super-buffers tiles cannot take (gso < 16, headers over 128 B, segments
-// over a tile), kept light so it does not set the tile path's registers.
-__device__ __forceinline__ void seg_simple(const Ctx &c, uintptr_t out_base, uint32_t i, uint32_t lane) {
-    const SegGeom g = seg_geom(c, out_base, i);
-    Acc acc;
-    for (uint32_t k = lane; k < g.nint; k += 64) {
-        const v4u v = ld16(g.base + 16u * k);
-        *reinterpret_cast<__attribute__((address_space(1))) v4u *>(g.c0 + 16u * k) = v;
-        acc.add4(v);
-    }
-    const uint32_t eo = edge_off(g, lane);
-    if (eo != kNoEdge) {
-        const uint32_t b = ld8(g.sa + eo);
-        st8(g.oa + eo, b);
-        acc.add(b << (8u * (((uint32_t)g.oa + eo) & 1u)));
-    }
-    const SegFields f = seg_fields(c, i);
-    uint32_t l4h = c.l4h_base;
-    if (c.tcp)
-        l4h += bswap16(f.seq >> 16) + bswap16(f.seq & 0xffffu) + (f.flags << 8);
-    else
-        l4h += bswap16((f.pktlen - c.cs) & 0xffffu);
-    uint32_t lp = fold16(acc.value());
-    if ((g.seg + c.cs) & 1u)
-        lp = bswap16(lp);
-    uint32_t T = wave_sum_u32(lp) + l4h + c.ps_sum;
-    T += ((c.tcp ? 6u : 17u) << 8) + bswap16((f.pktlen - c.cs) & 0xffffu);
-    HdrVals hv;
-    hv.v[0] = 0;
-    hv.v[kFldPkt] = f.pktlen;
-    hv.v[kFldId] = c.id0 + i;
-    hv.v[kFldIpcs] = f.ipcs;
-    hv.v[kFldL4cs] = ~fold16_32(T) & 0xffffu;
-    hv.v[kFldSeq] = f.seq;
-    hv.v[kFldUlen] = f.pktlen - c.cs;
-    hv.v[kFldFlags] = f.flags;
-    for (uint32_t j = lane; j < c.hdr_len; j += 64)
-        st8(g.seg + j, hdr_byte_slow(hv, hdr_code(c, j), ld8(c.in + j)));
-}
-
-// Adds lane value v into s_sum[key]; keys are non-decreasing over the lanes
-// and EXEC is full.  One or two distinct keys (a wave row within one or two
-// segments): DPP sums and one LDS add per key; more: an LDS add per lane.
-__device__ __forceinline__ void keyed_add(uint32_t *s_sum, uint32_t key, uint32_t v, uint32_t lane) {
-    const uint32_t kf = (uint32_t)__builtin_amdgcn_readfirstlane((int)key);
-    const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)key, 63);
-    if (kf == kl) {
-        const uint32_t s0 = wave_sum_u32(v);
-        if (lane == 0 && s0)
-            atomicAdd(&s_sum[kf], s0);
-    } else if (kl == kf + 1u) {
-        const uint32_t s0 = wave_sum_u32(key == kf ? v : 0u);
-        const uint32_t s1 = wave_sum_u32(key == kf ? 0u : v);
-        if (lane == 0) {
-            atomicAdd(&s_sum[kf], s0);
-            atomicAdd(&s_sum[kl], s1);
-        }
-    } else if (v) {
-        atomicAdd(&s_sum[key], v);
-    }
-}
-
-template <int W>
-__global__ __launch_bounds__(64 * W) void gso_tile_kernel(GsoParams p) {
-    constexpr uint32_t kThreads = 64u * W;
-    constexpr uint32_t kCap = 16u * kThreads;  // tile capacity, bytes
-    __shared__ uint32_t s_sum[kTileKMax];
-    __shared__ uint32_t s_fld[kTileKMax * 8];
-    const uint32_t t = threadIdx.x, lane = lane_id(), wv = wave_in_block();
-    if (t < kTileKMax)
-        s_sum[t] = 0;
-    __syncthreads();
-    const uint32_t T = p.tiles;
-    const uint64_t units = p.n * T;
-    for (uint64_t u = xcd_swizzle(blockIdx.x, gridDim.x); u < units; u += gridDim.x) {
-        const uint64_t b = u / T;
-        const uint32_t jt = (uint32_t)(u - b * T);
-        const bool more_units = u + gridDim.x < units;
-        const DescRaw dr = sload(reinterpret_cast<const DescRaw *>(p.desc + b));
-        const PlanRaw pr = sload(reinterpret_cast<const PlanRaw *>(p.res) + b);
-        asm volatile("" ::"s"(pr.w[0]), "s"(pr.w[1]), "s"(pr.w[2]), "s"(pr.w[3]), "s"(pr.w[4]), "s"(pr.w[5]),
-                     "s"(dr.w[0]), "s"(dr.w[1]), "s"(dr.w[2]), "s"(dr.w[3]), "s"(dr.w[4]));
-        const uint32_t kind = (pr.w[1] >> 16) & 0xffu, nseg = pr.w[2] >> 16;
-        if (!(kind & kPlanSplit))
-            continue;  // passthrough / error / in place: gso_finalize_kernel
-        const uint64_t in_off = (uint64_t)dr.w[0] | ((uint64_t)dr.w[1] << 32);
-        const uint64_t out_off = (uint64_t)dr.w[2] | ((uint64_t)dr.w[3] << 32);
-        Ctx c;
-        c.in = reinterpret_cast<uintptr_t>(p.in) + in_off;
-        c.in_len = dr.w[4];
-        c.hdr_len = pr.w[0] & 0xffffu;
-        c.cs = pr.w[0] >> 16;
-        c.l4off = pr.w[1] & 0xffffu;
-        c.gso = pr.w[2] & 0xffffu;
-        c.nseg = nseg;
-        c.rest = c.in_len - c.hdr_len;
-        c.v6 = kind & kPlanV6;
-        c.tcp = kind & kPlanTcp;
-        c.id0 = pr.w[3] & 0xffffu;
-        c.seq0 = pr.w[5];
-        c.ip_base = pr.w[3] >> 16;
-        c.l4h_base = pr.w[4] & 0xffffu;
-        c.ps_sum = pr.w[4] >> 16;
-        c.flags13 = pr.w[1] >> 24;
-        const uintptr_t out_base = reinterpret_cast<uintptr_t>(p.out) + out_off;
-        const uint32_t H = c.hdr_len, S = H + c.gso;
-        if (!(c.gso >= 16u && H <= 128u && S + 30u <= kCap)) {
-            // not tileable: segment per wave (segments jt * W + wave, stride T * W)
-            for (uint32_t i = jt * W + wv; i < c.nseg; i += T * W)
-                seg_simple(c, out_base, i, lane);
-            continue;
-        }
-        uint32_t K = (kCap - 30u) / S;
-        K = K < kTileKMax ? K : kTileKMax;
-        const uint32_t ntiles = (c.nseg + K - 1u) / K;
-        const uint32_t out_len = c.rest + c.nseg * H;
-        const uint32_t RB = H + 30u;  // boundary bytes per segment, at most
-        const float rS = 1.0f / (float)S, rRB = 1.0f / (float)RB, rH = 1.0f / (float)H;
-        const uint32_t omis = (uint32_t)out_base & 15u;  // output address bits below the chunk grid
-        for (uint32_t tile = jt; tile < ntiles; tile += T) {
-            const uint32_t seg0 = tile * K;
-            const uint32_t Kt = c.nseg - seg0 < K ? c.nseg - seg0 : K;
-            const uint32_t tstart = seg0 * S;
-            const uint32_t tend = seg0 + Kt == c.nseg ? out_len : tstart + Kt * S;
-            const int q0 = (int)tstart - (int)((omis + tstart) & 15u);  // chunk 0, relative to out_base
-            const uint32_t nch = (uint32_t)(((omis + tend + 15u) & ~15u) - ((omis + tstart) & ~15u)) >> 4;
-            // floor(x / d) for small x by a float reciprocal, corrected by one
-            auto div_small = [](uint32_t x, uint32_t d, float rd) -> uint32_t {
-                uint32_t r = (uint32_t)((float)x * rd);
-                return r * d > x ? r - 1u : ((r + 1u) * d <= x ? r + 1u : r);
-            };
-            // segment li's payload [pb, pe) and its aligned chunk span [P0, P1), relative to out_base
-            struct SegSpan {
-                uint32_t g, pe, P0, P1, i;
-            };
-            auto span_of = [&](uint32_t li) -> SegSpan {
-                SegSpan z;
-                z.i = seg0 + li;
-                z.g = tstart + li * S;
-                const uint32_t dl = c.rest - z.i * c.gso < c.gso ? c.rest - z.i * c.gso : c.gso;
-                const uint32_t pb = z.g + H;
-                z.pe = pb + dl;
-                const uint32_t a0 = ((omis + pb + 15u) & ~15u) - omis, a1 = ((omis + z.pe) & ~15u) - omis;
-                z.P0 = a0 < z.pe ? a0 : z.pe;
-                z.P1 = a1 > z.P0 ? a1 : z.P0;
-                return z;
-            };
-            // 1. this lane's chunk, when it is a whole payload chunk
-            const int q = q0 + 16 * (int)t;
-            const uint32_t dq = q > (int)tstart ? (uint32_t)q - tstart : 0u;
-            uint32_t li = div_small(dq, S, rS);
-            li = li < Kt ? li : Kt - 1u;
-            const SegSpan sp = span_of(li);
-            const bool pure = t < nch && q >= (int)sp.P0 && q + 16 <= (int)sp.P1;
-            const v4u v = ld16_nt(c.in + (pure ? (uint32_t)q - sp.i * H : 0u));
-            // 2. the boundary bytes: byte j of segment bl's head [g, P0) then tail [P1, pe)
-            for (uint32_t f0 = 0; f0 < Kt * RB; f0 += kThreads) {
-                const uint32_t f = f0 + t;
-                uint32_t bl = div_small(f, RB, rRB);
-                const bool inb = bl < Kt;
-                bl = inb ? bl : Kt - 1u;
-                const uint32_t j = f - bl * RB;
-                const SegSpan z = span_of(bl);
-                const uint32_t hl = z.P0 - z.g;  // head bytes (header + payload head)
-                const uint32_t pos = j < hl ? z.g + j : z.P1 + (j - hl);
-                const bool pay = inb && pos < z.pe && pos >= z.g + H;
-                const uint32_t bb = pay ? ld8(c.in + pos - z.i * H) : 0u;
-                if (f0 == 0 && pure) {  // the chunk, with the first pass's byte loads in flight
-                    __builtin_nontemporal_store(
-                        v, reinterpret_cast<__attribute__((address_space(1))) v4u *>(out_base + (uint32_t)q));
-                }
-                if (f0 == 0) {
-                    Acc acc;
-                    if (pure)
-                        acc.add4(v);
-                    keyed_add(s_sum, li, fold16(acc.value()), lane);
-                }
-                if (pay)
-                    st8(out_base + pos, bb);
-                keyed_add(s_sum, bl, bb << (8u * ((omis + pos) & 1u)), lane);
-            }
-            __syncthreads();
-            // 3. per segment: the L4 checksum and the other fields (offload.cpp:168-204)
-            if (t < Kt) {
-                const uint32_t i = seg0 + t;
-                const SegFields f = seg_fields(c, i);
-                const uint32_t gs = tstart + t * S;
-                uint32_t lp = fold16_32(s_sum[t]);
-                s_sum[t] = 0;  // for the block's next tile (behind the barrier below)
-                if ((omis + gs + c.cs) & 1u)  // summed in absolute pairing; the L4 region pairs from gs + cs
-                    lp = bswap16(lp);
-                uint32_t l4h = c.l4h_base;
-                if (c.tcp)
-                    l4h += bswap16(f.seq >> 16) + bswap16(f.seq & 0xffffu) + (f.flags << 8);
-                else
-                    l4h += bswap16((f.pktlen - c.cs) & 0xffffu);
-                const uint32_t T4 = lp + l4h + c.ps_sum + ((c.tcp ? 6u : 17u) << 8) + bswap16((f.pktlen - c.cs) & 0xffffu);
-                uint32_t *fl = &s_fld[t * 8u];
-                fl[kFldPkt] = f.pktlen;
-                fl[kFldId] = c.id0 + i;
-                fl[kFldIpcs] = f.ipcs;
-                fl[kFldL4cs] = ~fold16_32(T4) & 0xffffu;
-                fl[kFldSeq] = f.seq;
-                fl[kFldUlen] = f.pktlen - c.cs;
-                fl[kFldFlags] = f.flags;
-            }
-            __syncthreads();
-            // 4. the headers, a byte per lane (the reference's write order, :168-204)
-            for (uint32_t f0 = 0; f0 < Kt * H; f0 += kThreads) {
-                const uint32_t f = f0 + t;
-                const uint32_t hs = div_small(f, H, rH);
-                if (hs < Kt) {
-                    const uint32_t j = f - hs * H;
-                    const uint32_t code = hdr_code(c, j);
-                    const uint32_t tb = ld8(c.in + j);
-                    const uint32_t val = (code & 7u) ? (s_fld[hs * 8u + (code & 7u)] >> (code >> 8)) & 0xffu : tb;
-                    st8(out_base + tstart + hs * S + j, val);
-                }
-            }
-            if (tile + T < ntiles || more_units)
-                __syncthreads();  // the sums / field tables are rewritten by the next tile
-        }
-    }
-}
-
 // Plan pass, ONE THREAD per super-buffer: classification (:48-134), the
 // per-super-buffer fields (IPv4 id, TCP seq read after the :145-149 zeroing)
 // and the invariant header sums into the GsoPlan.  This is scalar,
@@ -974,8 +707,7 @@ int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, u
                 syn ? synth->msg_cap : 0u,
                 syn ? synth->max_segments : 0u,
                 syn ? synth->max_segment_size : 0u,
-                syn ? list : nullptr,
-                t.gso_tiles};
+                syn ? list : nullptr};
     if (p.list && hipMemsetAsync(p.list, 0, sizeof(uint32_t), st) != hipSuccess)
         return WG_ERR_RUNTIME;
     // 1. plans (into dev_res), thread per super-buffer
@@ -986,32 +718,6 @@ int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, u
     if (!debug_sync(st, "gso_plan_kernel"))
         return WG_ERR_LAUNCH;
     // 2. the split
-    if (!hdr_only && t.gso_rows && t.gso_ablate == 0) {
-        // the row-order tile kernel: gso_tiles blocks per super-buffer
-        // blocks per super-buffer: gso_tiles, or (0) the tiles of a 64-KiB
-        // TSO / USO super-buffer at MTU 1500 (45 segments of <= 1,500 B);
-        // other geometries are served all the same (blocks loop over tiles
-        // or find none)
-        const uint32_t tw = t.gso_tile_waves;
-        const uint32_t kseg = (16u * 64u * tw - 30u) / 1500u;
-        p.tiles = t.gso_tiles ? t.gso_tiles : (45u + kseg - 1u) / kseg;
-        uint64_t blocks = n * p.tiles;
-        blocks = blocks < t.gso_blocks ? blocks : t.gso_blocks;
-        if (blocks >= 8)
-            blocks = (blocks + 7) & ~7ull;  // the XCD swizzle wants a multiple of 8 (extra blocks find no unit)
-        switch (t.gso_tile_waves) {
-        case 4: hipLaunchKernelGGL((gso_tile_kernel<4>), dim3((unsigned)blocks), dim3(256), 0, st, p); break;
-        case 8: hipLaunchKernelGGL((gso_tile_kernel<8>), dim3((unsigned)blocks), dim3(512), 0, st, p); break;
-        case 12: hipLaunchKernelGGL((gso_tile_kernel<12>), dim3((unsigned)blocks), dim3(768), 0, st, p); break;
-        default: hipLaunchKernelGGL((gso_tile_kernel<3>), dim3((unsigned)blocks), dim3(192), 0, st, p); break;
-        }
-        if (hipGetLastError() != hipSuccess || !debug_sync(st, "gso_tile_kernel"))
-            return WG_ERR_LAUNCH;
-        hipLaunchKernelGGL(gso_finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
-        if (!debug_sync(st, "gso_finalize_kernel"))
-            return WG_ERR_LAUNCH;
-        return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
-    }
     const uint64_t units = n * t.gso_groups;
     // list mode: a fixed grid walks the listed super-buffers (usually few)
     const uint64_t cap = p.list ? 4096u : t.gso_blocks;

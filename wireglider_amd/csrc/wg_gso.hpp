@@ -37,7 +37,6 @@ struct GsoParams {
     // ([0] count, then indices) and the split kernel walks that list (synth
     // with nearly every super-buffer synthesized: no wave per skipped one)
     uint32_t *list;
-    uint32_t tiles;  // row-order tile kernel: blocks per super-buffer
 };
 
 struct Ctx {

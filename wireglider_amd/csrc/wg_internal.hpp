@@ -35,9 +35,6 @@ struct Tune {
     uint32_t encap_parts; // wg_encap_batch: slices split on a side stream under the previous slice's AEAD (1 = off)
     uint32_t encap_synth; // wg_encap_batch: the AEAD builds eligible segments' headers, the split skips them
     uint32_t gso_ablate;  // GSO A/B variants (1 non-temporal stores, 32 no XCD swizzle; both correct)
-    uint32_t gso_rows;    // full split: 1 row-order tile kernel, 0 the segment-per-wave kernel
-    uint32_t gso_tiles;   // row-order kernel: blocks per super-buffer (each takes tiles j, j + tiles, ...); 0 auto
-    uint32_t gso_tile_waves;  // row-order kernel: waves per block, one 16-B chunk per lane (3, 4, 8, 12)
 };
 
 // A snapshot of the knobs (copied under the knob mutex: wg_tune_set may run
