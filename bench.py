@@ -1669,6 +1669,17 @@ def main():
     else:
         got = 1
     grouped = dist.is_initialized()
+    if grouped:
+        # The group's first collectives initialise the communicator lazily,
+        # and for the next ~25 ms the device runs this rank's kernels up to
+        # 18 % slower (tools/dist_hiccup_probe.py, profiles/r05_dist_hiccup.json):
+        # do them now, ahead of the workload's build and clock settling, so no
+        # timed region sees it.
+        for _ in range(3):
+            dist.barrier()
+            warm = torch.ones(1, dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+            dist.all_reduce(warm)
+        torch.cuda.synchronize()
     if got != args.gpus:
         print(f"bench.py: process group has {got} rank(s) but --gpus {args.gpus}", file=sys.stderr)
         if grouped:

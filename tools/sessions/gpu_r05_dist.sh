@@ -24,6 +24,7 @@ run tr_gloo WG_DIST_BACKEND=gloo $TR --master-port=$(port) bench.py --gpus 1 --f
 run tr_nccl WG_DIST_BACKEND=nccl $TR --master-port=$(port) bench.py --gpus 1 --force-dist $A
 run plain2 X=1 python3 bench.py $A
 run nccl_direct WG_DIST_BACKEND=nccl python3 bench.py --gpus 1 --force-dist $A
+run tr_nccl2 WG_DIST_BACKEND=nccl $TR --master-port=$(port) bench.py --gpus 1 --force-dist $A
 (cd /tmp && WG_DIST_BACKEND=nccl timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_nccl" -o run --output-format csv -- \
   python3 "$ROOT/bench.py" --gpus 1 --force-dist $A > "$OUT/trace_nccl.json" 2> "$OUT/trace_nccl.err") || { tail "$OUT/trace_nccl.err"; exit 1; }
 find "$OUT/trace_nccl" -name "*kernel_stats.csv" -exec head -8 {} \;
