@@ -249,8 +249,12 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
             # their GPU output and their descriptors rebased to the sample
             k = min(n, 4096)
             gk = gd[:k].copy()
-            return (buf[: k * in_stride].cpu().numpy(), outb[: k * out_stride].cpu().numpy(),
-                    ("gso", gk, k * out_stride))
+            g = outb[: k * out_stride].cpu().numpy().reshape(k, out_stride)
+            # only each super-buffer's PacketBatch [0, out_len) is output; the
+            # rest of its 73,216-B slot is never written by the split (it held
+            # the copy probe's bytes) and stays zero in the oracle's buffer
+            g[:, out_len:] = 0
+            return (buf[: k * in_stride].cpu().numpy(), g.reshape(-1), ("gso", gk, k * out_stride))
 
         proto = ("UDP_L4, IPv4/UDP, 65535 B) -> 45 x 1472 B UDP segments each"
                  if udp else "IPv4/TCP, 65535 B) -> 45 x 1460 B segments each")
