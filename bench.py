@@ -1395,11 +1395,21 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
     parity = gpu_out is not None and bool(np.array_equal(exp, gpu_out))
     scale, unit = (1e-6, "Mflows/s") if kind[0] == "gro" else (2.0**-30, "GiB/s")
     run_all()  # first touch / warm-up, untimed
+    def warm(fn, secs):
+        # untimed runs until the leg's pages have settled where its workers
+        # run (round 5: repetitions still rose 30-60 % over the first
+        # seconds on a 256-CPU host — page placement, not clocks: every
+        # repetition's CPUs held the same scaling_cur_freq)
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < secs:
+            fn()
+
+    warm(run_all, min(seconds, 1.5))
     thr0 = oracle.cgroup_throttling()
     all_s = _spread(_rep_rates(run_all, nbytes, seconds, reps, after=logger("all", cpus_all)), scale)
     thr1 = oracle.cgroup_throttling()
     cpus_one = pick(1)
-    run_one()  # the 1-core leg's first touch on its CPU, untimed
+    warm(run_one, min(seconds, 1.5))  # the 1-core leg's first touch on its CPU, untimed
     one_s = _spread(_rep_rates(run_one, nbytes * one_scale, seconds / 2, reps, after=logger("one", cpus_one)), scale)
     all_s["repetitions"] = reps_log["all"]
     one_s["repetitions"] = reps_log["one"]
@@ -1439,7 +1449,8 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
         "sample": f"first {npk} units of the same batch, oracle/csum_oracle.c "
                   f"({what}; {nofold} for spans >= 256 B), {threads} pthreads "
                   f"(sched_getaffinity {cores['affinity']}, cgroup quota {cores['cgroup_quota_cpus']}); "
-                  f"value = median of {reps - 1} repetitions of >= {seconds:.1f} s after a dropped first one, "
+                  f"value = median of {reps - 1} repetitions of >= {seconds:.1f} s after a dropped first one "
+                  f"(and >= {min(seconds, 1.5):.1f} s of untimed runs per leg), "
                   f"1 core: the same of >= {seconds / 2:.1f} s; worker t pinned to the t-th least busy CPU of the "
                   f"affinity mask, one per physical core, picked once per leg (host_cores.pinning); "
                   f"bit-exact vs GPU: {parity}",
