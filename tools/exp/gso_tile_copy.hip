@@ -346,11 +346,11 @@ int main(int argc, char **argv) {
         hipEventElapsedTime(&ms, e0, e1);
         printf("{\"variant\": \"%s\", \"ms\": %.4f, \"TBps\": %.3f}\n", name, ms / iters, alg / (ms / iters * 1e-3) / 1e12);
     };
-    auto runseg = [&](auto kern, const char *name, unsigned grp = 3) {
+    auto runseg = [&](auto kern, const char *name, unsigned grp = 3, unsigned lds = 0) {
         const unsigned grid = N * grp;
-        for (int w = 0; w < 3; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, in, out);
+        for (int w = 0; w < 3; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, 0, in, out);
         hipEventRecord(e0);
-        for (int w = 0; w < iters; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, in, out);
+        for (int w = 0; w < iters; w++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, 0, in, out);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         float ms;
@@ -389,6 +389,21 @@ int main(int argc, char **argv) {
             runv(rowk<4>, "V4 + returning atomics, last contributor stores the checksum");
             runv(rowk<5>, "V5 = V2 without the atomics (sums to LDS)");
             runv(rowk<6>, "V6 = V1 + the atomics alone (no sums)");
+        }
+        printf("{\"err\": \"%s\"}\n", hipGetErrorString(hipGetLastError()));
+        return 0;
+    }
+    if (argc > 2 && !strcmp(argv[2], "occ")) {  // the split's shape at capped occupancy (dynamic LDS per block)
+        for (int rep = 0; rep < 2; rep++) {
+            runseg(seg_copy<0>, "S production shape, default policy");
+            runseg(seg_copy<0>, "S, 6 blocks per CU (24 KiB LDS each)", 3, 24576);
+            runseg(seg_copy<0>, "S, 5 blocks per CU (30 KiB LDS each)", 3, 30720);
+            runseg(seg_copy<0>, "S, 4 blocks per CU (40 KiB LDS each)", 3, 40960);
+            runseg(seg_copy<0>, "S, 3 blocks per CU (52 KiB LDS each)", 3, 53248);
+            runseg(seg_copy<0, 1, 1>, "S1 one segment per wave, default", 12);
+            runseg(seg_copy<0, 1, 1>, "S1, 5 blocks per CU", 12, 30720);
+            runseg(seg_copy<0, 1, 1>, "S1, 4 blocks per CU", 12, 40960);
+            runrow(row_copy<256, 3>, 256, "R0 rows 4 KiB blocks nt both");
         }
         printf("{\"err\": \"%s\"}\n", hipGetErrorString(hipGetLastError()));
         return 0;
