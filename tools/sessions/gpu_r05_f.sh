@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 120 tools/exp/bin/gso_tile_copy 20 ${PROBE_MODE:-segs} > "$OUT/seg_copy.jsonl" 2>&1 || { tail "$OUT/seg_copy.jsonl"; exit 1; }
 cat "$OUT/seg_copy.jsonl"
-timeout -k 10 300 python3 -u tools/ab.py config3 gso_rows=0 > "$OUT/ab_config3.json" 2>&1 || { tail "$OUT/ab_config3.json"; exit 1; }
+timeout -k 10 300 python3 -u tools/ab.py config3 > "$OUT/ab_config3.json" 2>&1 || { tail "$OUT/ab_config3.json"; exit 1; }
 cat "$OUT/ab_config3.json"
 if [ -n "${AB_R03F:-}" ]; then
   timeout -k 10 900 bash tools/ab_trees.sh "$OUT/ab_r03f.jsonl" 3 config4,config5,config4small tools/exp/r03f_tree . \

@@ -8,8 +8,7 @@ TAG=$1
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 400 python3 -u tools/ab.py config3 gso_rows=0 gso_groups=12,gso_spw=0 gso_groups=12,gso_spw=1 \
-  gso_groups=6,gso_spw=2 gso_groups=48,gso_waves=1,gso_spw=0 gso_groups=24,gso_waves=2,gso_spw=0 gso_groups=6,gso_waves=8,gso_spw=0 \
+timeout -k 10 400 python3 -u tools/ab.py config3 gso_occ=0 gso_occ=3 gso_occ=4 gso_occ=2 gso_occ=3,gso_groups=1 gso_occ=4,gso_spw=3 \
   > "$OUT/ab_config3.json" 2>&1 || { tail "$OUT/ab_config3.json"; exit 1; }
 cat "$OUT/ab_config3.json"
 echo "session $TAG done"
