@@ -55,7 +55,6 @@ static const Knob kKnobs[] = {
     {"aead_stage", nullptr, &Tune::aead_stage, 0, 1, nullptr, 0},
     {"encap_parts", nullptr, &Tune::encap_parts, 0, 0, kParts, WG_N(kParts)},
     {"encap_synth", nullptr, &Tune::encap_synth, 0, 1, nullptr, 0},
-    {"gso_occ", nullptr, &Tune::gso_occ, 0, 8, nullptr, 0},
 };
 #undef WG_N
 
@@ -127,7 +126,6 @@ static Tune &tune_storage() {
         x.verify_auto_t = 1;
         x.verify_k2min = 2048;
         x.gso_ablate = 0;
-        x.gso_occ = 0;
         // host pipeline chunk: 128-512 MiB reach 97-98 % of the raw H2D rate
         // (8 MiB: 70 %, per-chunk overheads; profiles/r02_host_path.json);
         // with both directions in flight 64 MiB: decap 35.2 ms vs 37.3 at

@@ -679,15 +679,13 @@ __global__ __launch_bounds__(256) void gso_finalize_kernel(GsoParams p) {
 
 using namespace wg;
 
-// lds: dynamic LDS per block that only caps the blocks resident per CU
-// (knob gso_occ; the kernel uses none)
 template <int S, int Abl>
-static void launch_split(const GsoParams &p, dim3 g, uint32_t waves, hipStream_t st, uint32_t lds = 0) {
+static void launch_split(const GsoParams &p, dim3 g, uint32_t waves, hipStream_t st) {
     switch (waves) {
-    case 1: hipLaunchKernelGGL((gso_split_kernel<1, S, Abl>), g, dim3(64), lds, st, p); break;
-    case 2: hipLaunchKernelGGL((gso_split_kernel<2, S, Abl>), g, dim3(128), lds, st, p); break;
-    case 8: hipLaunchKernelGGL((gso_split_kernel<8, S, Abl>), g, dim3(512), lds, st, p); break;
-    default: hipLaunchKernelGGL((gso_split_kernel<4, S, Abl>), g, dim3(256), lds, st, p); break;
+    case 1: hipLaunchKernelGGL((gso_split_kernel<1, S, Abl>), g, dim3(64), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((gso_split_kernel<2, S, Abl>), g, dim3(128), 0, st, p); break;
+    case 8: hipLaunchKernelGGL((gso_split_kernel<8, S, Abl>), g, dim3(512), 0, st, p); break;
+    default: hipLaunchKernelGGL((gso_split_kernel<4, S, Abl>), g, dim3(256), 0, st, p); break;
     }
 }
 
@@ -740,15 +738,12 @@ int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, u
         case 1: launch_split<0, 1>(p, g, 4, st); break;
         case 32: launch_split<0, 32>(p, g, 4, st); break;
         default:
-            // gso_occ: at most that many blocks per CU (160 KiB of LDS per CU
-            // shared out; 512-B allocation granules)
-            const uint32_t lds = t.gso_occ ? ((160u * 1024u / t.gso_occ) & ~511u) : 0u;
             switch (t.gso_spw) {
-            case 1: launch_split<1, 0>(p, g, t.gso_waves, st, lds); break;
-            case 2: launch_split<2, 0>(p, g, t.gso_waves, st, lds); break;
-            case 3: launch_split<3, 0>(p, g, t.gso_waves, st, lds); break;
-            case 4: launch_split<4, 0>(p, g, t.gso_waves, st, lds); break;
-            default: launch_split<0, 0>(p, g, t.gso_waves, st, lds); break;
+            case 1: launch_split<1, 0>(p, g, t.gso_waves, st); break;
+            case 2: launch_split<2, 0>(p, g, t.gso_waves, st); break;
+            case 3: launch_split<3, 0>(p, g, t.gso_waves, st); break;
+            case 4: launch_split<4, 0>(p, g, t.gso_waves, st); break;
+            default: launch_split<0, 0>(p, g, t.gso_waves, st); break;
             }
         }
     }

@@ -35,7 +35,6 @@ struct Tune {
     uint32_t encap_parts; // wg_encap_batch: slices split on a side stream under the previous slice's AEAD (1 = off)
     uint32_t encap_synth; // wg_encap_batch: the AEAD builds eligible segments' headers, the split skips them
     uint32_t gso_ablate;  // GSO A/B variants (1 non-temporal stores, 32 no XCD swizzle; both correct)
-    uint32_t gso_occ;     // full split: at most this many blocks per CU (0 = as registers allow)
 };
 
 // A snapshot of the knobs (copied under the knob mutex: wg_tune_set may run
