@@ -277,50 +277,6 @@ __device__ __forceinline__ void wave_long(uint64_t m, uintptr_t a, uint32_t len,
     }
 }
 
-// wave_long with Q = 1 and the next packet's issue loads sent before the
-// current packet is finished (ping-pong): a wave's long packets overlap by
-// one issue phase instead of running back to back.
-template <bool kL4, bool kNT, int U = 4>
-__device__ __forceinline__ void wave_long_pp(uint64_t m, uintptr_t a, uint32_t len, uint32_t cs, uint32_t fl,
-                                             const uint8_t *base, uint32_t lane, uint32_t &res) {
-    if (!m)
-        return;
-    const uint32_t alo = (uint32_t)a, ahi = (uint32_t)((uint64_t)a >> 32);
-    auto pick = [&](Geom &g, uint32_t &jj) {
-        const uint32_t j = (uint32_t)__builtin_ctzll(m);
-        m &= m - 1;
-        jj = j;
-        g.a = (uintptr_t)(((uint64_t)rdl(ahi, j) << 32) | rdl(alo, j));
-        g.len = rdl(len, j);
-        g.cs = rdl(cs, j);
-        g.fl = rdl(fl, j);
-    };
-    Geom g0, g1;
-    Front f0, f1;
-    uint32_t j0, j1;
-    pick(g0, j0);
-    issue<kL4, kNT>(g0, lane, f0);
-    for (;;) {
-        const bool more = m != 0;
-        if (more) {
-            pick(g1, j1);
-            issue<kL4, kNT>(g1, lane, f1);
-        }
-        uint32_t t = wave_sum_u32(finish<kNT, U>(lane, f0));
-        if (kL4) {
-            const uint32_t proto = (g0.fl & WG_PKT_TCP) ? 6u : 17u;
-            t += (proto << 8) + bswap16((g0.len - g0.cs) & 0xffffu);
-        }
-        if (lane == j0)
-            res = ~fold16_32(t) & 0xffffu;
-        if (!more)
-            break;
-        g0 = g1;
-        f0 = f1;
-        j0 = j1;
-    }
-}
-
 // Uniform PacketBatches of small segments (segment_size <= kSmallMax; knob
 // l4_small_uniform = 2): every segment is small, so a lane per segment, summed
 // by lane_chunks / lane_sum — no descriptors, no wave role.
@@ -388,11 +344,7 @@ __global__ __launch_bounds__(256) void l4csum_split_kernel(L4Params p) {
     const bool own = wib == 0 ? (lane & 15u) < 4u : true;
     const bool mine = live && own && grp_long;
     uint32_t res = 0;
-#ifdef WG_LONG_PP
-    wave_long_pp<kL4, kNT, (U > 4 ? WG_LONG_PP : U)>(__ballot(mine), a, len, cs, fl, p.base, lane, res);
-#else
     wave_long<kL4, kNT, 1, U>(__ballot(mine), a, len, cs, fl, p.base, lane, res);
-#endif
     if (mine)
         p.out[i] = (uint16_t)res;
     // ---- lane role (wave 0): the block's all-small groups

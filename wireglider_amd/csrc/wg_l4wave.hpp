@@ -97,7 +97,7 @@ __device__ __forceinline__ void issue(const Geom &g, uint32_t lane, Front &f) {
 // U: loads in flight per lane while streaming a long packet's rest (4 or 8).
 template <bool kNT, int U = 4>
 __device__ __forceinline__ uint32_t finish(uint32_t lane, const Front &f) {
-    static_assert(U >= 1 && U <= 8, "loads in flight");
+    static_assert(U == 4 || U == 8, "loads in flight");
     Acc acc;
     if (f.nint > 128) {  // long packet (> ~2 KiB): stream the rest, U loads in flight
         const uintptr_t q = f.c0;
