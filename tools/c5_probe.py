@@ -31,10 +31,9 @@ def main():
     seg = bench.SEG
     small = 1 << 20
     outs = torch.empty(n, dtype=torch.uint16, device=dev)
-    l4s = wga.tune_get("l4_small")
 
     def v(name, nb, fn, knob=None):
-        return (name, nb, fn, knob)
+        return (name, nb, fn, knob or {})
 
     variants = []
     for tag, m in (("full", n), ("1M", small)):
@@ -42,14 +41,27 @@ def main():
         d = desc[:m]
         o = outs[:m]
         variants.append(v(f"desc_split_{tag}", m * seg, lambda b=b, d=d, o=o: wga.calc_l4_checksum_desc(b, d, out=o)))
-        variants.append(v(f"desc_wpp_{tag}", m * seg, lambda b=b, d=d, o=o: wga.calc_l4_checksum_desc(b, d, out=o), 0))
+        variants.append(v(f"desc_wpp_{tag}", m * seg, lambda b=b, d=d, o=o: wga.calc_l4_checksum_desc(b, d, out=o),
+                          {"l4_small": 0}))
         variants.append(v(f"uniform_{tag}", m * seg,
                           lambda b=b, o=o: wga.calc_l4_checksum_batch(b, seg, False, False, 20, out=o)))
+    # grid-stride forms: uniform with 4 / 16 iterations per wave (4 / 16
+    # windows through the buffer at once), wave-per-packet descriptors with 16
+    b, d, o = buf, desc, outs
+    for nb_ in (262144, 65536):
+        variants.append(v(f"uniform_full_blocks{nb_}", n * seg,
+                          lambda b=b, o=o: wga.calc_l4_checksum_batch(b, seg, False, False, 20, out=o),
+                          {"l4_blocks": nb_}))
+    variants.append(v("desc_wpp_full_blocks65536", n * seg, lambda b=b, d=d, o=o: wga.calc_l4_checksum_desc(b, d, out=o),
+                      {"l4_small": 0, "l4_blocks": 65536}))
+    keys = sorted({k for *_, kn in variants for k in kn})
+    dflt = {k: wga.tune_get(k) for k in keys}
     res = {name: [] for name, *_ in variants}
     st = torch.cuda.current_stream()
     for r in range(rounds):
         for name, nb, fn, knob in variants:
-            wga.tune_set("l4_small", l4s if knob is None else knob)
+            for k in keys:
+                wga.tune_set(k, knob.get(k, dflt[k]))
             reps = 10 if "full" in name else 100
             for _ in range(3):
                 fn()
@@ -61,7 +73,8 @@ def main():
             e1.synchronize()
             res[name].append(e0.elapsed_time(e1) / reps)
         print(f"round {r} done", flush=True)
-    wga.tune_set("l4_small", l4s)
+    for k in keys:
+        wga.tune_set(k, dflt[k])
     out = {}
     for name, nb, *_ in variants:
         ms = statistics.median(res[name])

@@ -511,8 +511,11 @@ static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
         // descriptor batches under l4_small = 0: 4 iterations per wave with
         // the next iteration's descriptors prefetched)
         uint64_t want = (p.n + 15) / 16;
+#ifndef WG_DESC_ITERS
+#define WG_DESC_ITERS 4
+#endif
         if (kind != kUniformL4)
-            want = (want + 3) / 4;
+            want = (want + WG_DESC_ITERS - 1) / WG_DESC_ITERS;
         uint64_t blocks = want < t.l4_blocks ? want : t.l4_blocks;
         if (blocks >= 8)
             blocks &= ~7ull;  // keep the XCD swizzle bijective
