@@ -107,11 +107,24 @@ __global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
     constexpr bool kL4 = kKind != kDescPlain;
     constexpr int DM = kKind == kUniformL4 ? 0 : kDM;
     const uint32_t lane = lane_id();
+#ifndef WG_L4_LAYOUT
+#define WG_L4_LAYOUT 0
+#endif
+#if WG_L4_LAYOUT == 0
     const uint64_t wave0 = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
     const uint64_t step = (uint64_t)gridDim.x * 4u * P;
+    const uint64_t first = wave0 * P, lim = p.n;
+#else
+    const uint64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
+    const uint64_t per = (uint64_t)gridDim.x * 4u * P;
+    const uint64_t iters = (p.n + per - 1) / per;
+    const uint64_t step = 4u * P;
+    const uint64_t first = blk * iters * step + wave_in_block() * P;
+    const uint64_t lim = (blk + 1) * iters * step < p.n ? (blk + 1) * iters * step : p.n;
+#endif
     v4u nextd = v4u{0, 0, 0, 0};
     bool have_next = false;
-    for (uint64_t i0 = wave0 * P; i0 < p.n; i0 += step) {
+    for (uint64_t i0 = first; i0 < lim; i0 += step) {
         Geom g[P];
         Front f[P];
         if constexpr (DM == 2) {
@@ -130,7 +143,7 @@ __global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
             issue<kL4, kNT>(g[j], lane, f[j]);
         }
         if constexpr (DM == 2) {  // next iteration's descriptors, in flight during the finish
-            have_next = i0 + step < p.n;
+            have_next = i0 + step < lim;
             nextd = load_desc_vec<P>(p, have_next ? i0 + step : i0, lane);
         }
         uint32_t res = 0;
@@ -514,8 +527,12 @@ static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
 #ifndef WG_DESC_ITERS
 #define WG_DESC_ITERS 4
 #endif
+#ifndef WG_DESC_P
+#define WG_DESC_P 4
+#define WG_DESC_DM 2
+#endif
         if (kind != kUniformL4)
-            want = (want + WG_DESC_ITERS - 1) / WG_DESC_ITERS;
+            want = ((p.n + 4 * WG_DESC_P - 1) / (4 * WG_DESC_P) + WG_DESC_ITERS - 1) / WG_DESC_ITERS;
         uint64_t blocks = want < t.l4_blocks ? want : t.l4_blocks;
         if (blocks >= 8)
             blocks &= ~7ull;  // keep the XCD swizzle bijective
@@ -526,7 +543,7 @@ static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
         else if (kind == kUniformL4)
             hipLaunchKernelGGL((l4csum_kernel<kUniformL4, 4, false, 0>), g, b, 0, st, p);
         else if (kind == kDescL4 && nt)
-            hipLaunchKernelGGL((l4csum_kernel<kDescL4, 4, true, 2>), g, b, 0, st, p);
+            hipLaunchKernelGGL((l4csum_kernel<kDescL4, WG_DESC_P, true, WG_DESC_DM>), g, b, 0, st, p);
         else if (kind == kDescL4)
             hipLaunchKernelGGL((l4csum_kernel<kDescL4, 4, false, 2>), g, b, 0, st, p);
         else if (nt)
