@@ -48,19 +48,17 @@ def main():
         variants.append(v(f"uniform_{tag}_4iter", m * seg,
                           lambda b=b, o=o: wga.calc_l4_checksum_batch(b, seg, False, False, 20, out=o),
                           {"l4_blocks": m // 64}))
-    # grid-stride forms: uniform with 4 / 16 iterations per wave (4 / 16
-    # windows through the buffer at once), wave-per-packet descriptors with 16
+    # grid-stride forms (C5_GRID=1): uniform with 16 iterations per wave,
+    # wave-per-packet descriptors with 16
+    import os
     b, d, o = buf, desc, outs
-    # (65536 blocks and more: more blocks than are resident, so several
-    # windows; 2048-8192: persistent waves, ONE window of grid x 64 packets)
-    for nb_ in (65536,):
-        variants.append(v(f"uniform_full_blocks{nb_}", n * seg,
+    if os.environ.get("C5_GRID") == "1":
+        variants.append(v("uniform_full_blocks65536", n * seg,
                           lambda b=b, o=o: wga.calc_l4_checksum_batch(b, seg, False, False, 20, out=o),
-                          {"l4_blocks": nb_}))
-    for nb_ in (65536,):
-        variants.append(v(f"desc_wpp_full_blocks{nb_}", n * seg,
+                          {"l4_blocks": 65536}))
+        variants.append(v("desc_wpp_full_blocks65536", n * seg,
                           lambda b=b, d=d, o=o: wga.calc_l4_checksum_desc(b, d, out=o),
-                          {"l4_small": 0, "l4_blocks": nb_}))
+                          {"l4_small": 0, "l4_blocks": 65536}))
     keys = sorted({k for *_, kn in variants for k in kn})
     dflt = {k: wga.tune_get(k) for k in keys}
     res = {name: [] for name, *_ in variants}

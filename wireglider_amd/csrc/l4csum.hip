@@ -107,26 +107,18 @@ __global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
     constexpr bool kL4 = kKind != kDescPlain;
     constexpr int DM = kKind == kUniformL4 ? 0 : kDM;
     const uint32_t lane = lane_id();
-#ifndef WG_L4_LAYOUT
-#define WG_L4_LAYOUT 0
-#endif
-#if WG_L4_LAYOUT == 0
     const uint64_t wave0 = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
     const uint64_t step = (uint64_t)gridDim.x * 4u * P;
     const uint64_t first = wave0 * P, lim = p.n;
-#else
-    const uint64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
-    const uint64_t per = (uint64_t)gridDim.x * 4u * P;
-    const uint64_t iters = (p.n + per - 1) / per;
-    const uint64_t step = 4u * P;
-    const uint64_t first = blk * iters * step + wave_in_block() * P;
-    const uint64_t lim = (blk + 1) * iters * step < p.n ? (blk + 1) * iters * step : p.n;
-#endif
     v4u nextd = v4u{0, 0, 0, 0};
     bool have_next = false;
     for (uint64_t i0 = first; i0 < lim; i0 += step) {
         Geom g[P];
         Front f[P];
+        if constexpr (DM == 3) {
+            const v4u dv = load_desc_vec<P>(p, i0, lane);
+            geoms_from_vec<kKind, P>(p, i0, dv, g);
+        }
         if constexpr (DM == 2) {
             if (have_next) {
                 geoms_from_vec<kKind, P>(p, i0, nextd, g);
@@ -146,6 +138,13 @@ __global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
             have_next = i0 + step < lim;
             nextd = load_desc_vec<P>(p, have_next ? i0 + step : i0, lane);
         }
+#ifndef WG_PF_DIST
+#define WG_PF_DIST 32768
+#endif
+        if constexpr (DM == 3 && WG_PF_DIST > 0) {  // a later wave's descriptors towards the caches
+            const uint64_t pi = i0 + WG_PF_DIST;
+            nextd = load_desc_vec<P>(p, pi < p.n ? pi : i0, lane);
+        }
         uint32_t res = 0;
 #pragma unroll
         for (int j = 0; j < P; j++) {
@@ -164,6 +163,8 @@ __global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
         if (lane < (uint32_t)P && i0 + lane < p.n)
             p.out[i0 + lane] = (uint16_t)res;
     }
+    if constexpr (DM == 3 && WG_PF_DIST > 0)
+        asm volatile("" ::"v"(nextd.x));
 }
 
 // ---------------------------------------------------------------------------
