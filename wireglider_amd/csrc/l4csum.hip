@@ -109,16 +109,11 @@ __global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
     const uint32_t lane = lane_id();
     const uint64_t wave0 = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
     const uint64_t step = (uint64_t)gridDim.x * 4u * P;
-    const uint64_t first = wave0 * P, lim = p.n;
     v4u nextd = v4u{0, 0, 0, 0};
     bool have_next = false;
-    for (uint64_t i0 = first; i0 < lim; i0 += step) {
+    for (uint64_t i0 = wave0 * P; i0 < p.n; i0 += step) {
         Geom g[P];
         Front f[P];
-        if constexpr (DM == 3) {
-            const v4u dv = load_desc_vec<P>(p, i0, lane);
-            geoms_from_vec<kKind, P>(p, i0, dv, g);
-        }
         if constexpr (DM == 2) {
             if (have_next) {
                 geoms_from_vec<kKind, P>(p, i0, nextd, g);
@@ -135,15 +130,8 @@ __global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
             issue<kL4, kNT>(g[j], lane, f[j]);
         }
         if constexpr (DM == 2) {  // next iteration's descriptors, in flight during the finish
-            have_next = i0 + step < lim;
+            have_next = i0 + step < p.n;
             nextd = load_desc_vec<P>(p, have_next ? i0 + step : i0, lane);
-        }
-#ifndef WG_PF_DIST
-#define WG_PF_DIST 32768
-#endif
-        if constexpr (DM == 3 && WG_PF_DIST > 0) {  // a later wave's descriptors towards the caches
-            const uint64_t pi = i0 + WG_PF_DIST;
-            nextd = load_desc_vec<P>(p, pi < p.n ? pi : i0, lane);
         }
         uint32_t res = 0;
 #pragma unroll
@@ -163,8 +151,6 @@ __global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
         if (lane < (uint32_t)P && i0 + lane < p.n)
             p.out[i0 + lane] = (uint16_t)res;
     }
-    if constexpr (DM == 3 && WG_PF_DIST > 0)
-        asm volatile("" ::"v"(nextd.x));
 }
 
 // ---------------------------------------------------------------------------
@@ -525,15 +511,8 @@ static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
         // descriptor batches under l4_small = 0: 4 iterations per wave with
         // the next iteration's descriptors prefetched)
         uint64_t want = (p.n + 15) / 16;
-#ifndef WG_DESC_ITERS
-#define WG_DESC_ITERS 4
-#endif
-#ifndef WG_DESC_P
-#define WG_DESC_P 4
-#define WG_DESC_DM 2
-#endif
         if (kind != kUniformL4)
-            want = ((p.n + 4 * WG_DESC_P - 1) / (4 * WG_DESC_P) + WG_DESC_ITERS - 1) / WG_DESC_ITERS;
+            want = (want + 3) / 4;
         uint64_t blocks = want < t.l4_blocks ? want : t.l4_blocks;
         if (blocks >= 8)
             blocks &= ~7ull;  // keep the XCD swizzle bijective
@@ -544,7 +523,7 @@ static int launch_l4(int kind, const L4Params &p, hipStream_t st) {
         else if (kind == kUniformL4)
             hipLaunchKernelGGL((l4csum_kernel<kUniformL4, 4, false, 0>), g, b, 0, st, p);
         else if (kind == kDescL4 && nt)
-            hipLaunchKernelGGL((l4csum_kernel<kDescL4, WG_DESC_P, true, WG_DESC_DM>), g, b, 0, st, p);
+            hipLaunchKernelGGL((l4csum_kernel<kDescL4, 4, true, 2>), g, b, 0, st, p);
         else if (kind == kDescL4)
             hipLaunchKernelGGL((l4csum_kernel<kDescL4, 4, false, 2>), g, b, 0, st, p);
         else if (nt)
