@@ -142,8 +142,7 @@ def test_oracle_verify_desc_matches_scalar():
 
 
 VERIFY_VARIANTS = [{"verify_small": 0}, {"verify_small": 6}, {"verify_small": 6, "verify_k2min": 8},
-                   {"verify_small": 7}, {"verify_small": 7, "verify_auto_t": 64}, {"verify_small": 8},
-                   {"verify_small": 8, "verify_walk_k": 2}, {"verify_small": 8, "verify_walk_k": 3}]
+                   {"verify_small": 7}, {"verify_small": 7, "verify_auto_t": 64}, {"verify_small": 8}]
 
 
 @pytest.mark.gpu

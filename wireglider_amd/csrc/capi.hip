@@ -45,7 +45,6 @@ static const Knob kKnobs[] = {
     {"verify_small", nullptr, &Tune::verify_small, 0, 0, kVSmall, WG_N(kVSmall)},
     {"verify_auto_t", nullptr, &Tune::verify_auto_t, 1, 64, nullptr, 0},
     {"verify_k2min", nullptr, &Tune::verify_k2min, 8, 65536, nullptr, 0},
-    {"verify_walk_k", nullptr, &Tune::verify_walk_k, 1, 3, nullptr, 0},
     {"gso_ablate", nullptr, &Tune::gso_ablate, 0, 0, kAbl, WG_N(kAbl)},
     {"host_chunk_mb", nullptr, &Tune::host_chunk_mb, 1, 4096, nullptr, 0},
     {"host_d2h", nullptr, &Tune::host_d2h, 0, 3, nullptr, 0},
@@ -126,7 +125,6 @@ static Tune &tune_storage() {
         x.verify_small = 7;
         x.verify_auto_t = 1;
         x.verify_k2min = 2048;
-        x.verify_walk_k = 1;
         x.gso_ablate = 0;
         // host pipeline chunk: 128-512 MiB reach 97-98 % of the raw H2D rate
         // (8 MiB: 70 %, per-chunk overheads; profiles/r02_host_path.json);

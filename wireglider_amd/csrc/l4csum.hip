@@ -1004,79 +1004,50 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
 // 1 M x 64 B 0.0157 ms against the compacting path's 0.0174; long packets
 // cost it 7-9 % against the one-shot wave kernel (a wave then lives for 16
 // groups), so the cost model sends long-dominated batches there.
-template <int K>
 __global__ __launch_bounds__(256) void verify_walk_kernel(VerifyParams p) {
     const uint32_t lane = lane_id();
     const uint64_t G = (uint64_t)gridDim.x * 4u;
     const uint64_t w = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
-    uint32_t len[K], olo[K], ohi[K], r[K];
-    bool small[K], live[K];
+    const uint64_t i = ((uint64_t)(lane >> 2) * G + w) * 4u + (lane & 3u);
+    const bool live = i < p.n;
+    const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0u));
+    const uint32_t len = live ? dv.z : 0u;
+    const uint32_t olo = live ? dv.x : 0u, ohi = live ? dv.y : 0u;
+    const bool small = live && len <= kSmallMax;
+    uint32_t rv = 0, rc = 0;
+    if (__ballot(small))  // wave-uniform
+        verify_lane(reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)ohi << 32) | olo), small ? len : 0u, small, rv,
+                    rc);
+    uint32_t r = rv | (rc << 8);  // one register across the walk: verdict | L4 result << 8
+    uint64_t m = __ballot(live && !small);
+    while (m) {  // the long packets, 4 at a time in group order
+        // the lane id laundered per iteration: verify_group's lane-derived
+        // constants are recomputed in the body, not held across the loop
+        uint32_t ln = lane_id();
+        asm volatile("" : "+v"(ln));
+        uint64_t doff[4];
+        uint32_t lg[4], tgt[4];
 #pragma unroll
-    for (int k = 0; k < K; k++) {
-        const uint64_t i = ((uint64_t)((lane >> 2) + 16u * k) * G + w) * 4u + (lane & 3u);
-        live[k] = i < p.n;
-        const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live[k] ? i : 0u));
-        len[k] = live[k] ? dv.z : 0u;
-        olo[k] = live[k] ? dv.x : 0u;
-        ohi[k] = live[k] ? dv.y : 0u;
-        small[k] = live[k] && len[k] <= kSmallMax;
-    }
-    if constexpr (K == 1) {
-        uint32_t rv = 0, rc = 0;
-        if (__ballot(small[0]))  // wave-uniform
-            verify_lane(reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)ohi[0] << 32) | olo[0]),
-                        small[0] ? len[0] : 0u, small[0], rv, rc);
-        r[0] = rv | (rc << 8);  // one register across the walk: verdict | L4 result << 8
-    } else {
-        // every small packet's chunks in flight before the first decode
-        v4u W[K][5];
-#pragma unroll
-        for (int k = 0; k < K; k++)
-            verify_lane_load(reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)ohi[k] << 32) | olo[k]),
-                             small[k] ? len[k] : 0u, small[k], W[k]);
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-            uint32_t rv = 0, rc = 0;
-            verify_lane_decode(W[k], reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)ohi[k] << 32) | olo[k]),
-                               small[k] ? len[k] : 0u, rv, rc);
-            r[k] = rv | (rc << 8);
+        for (int k = 0; k < 4; k++) {
+            const bool have = m != 0;
+            const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
+            m = have ? m & (m - 1) : m;
+            tgt[k] = have ? j : 64u;
+            doff[k] = have ? (((uint64_t)rdl(ohi, j) << 32) | rdl(olo, j)) : 0u;
+            lg[k] = have ? rdl(len, j) : 0u;
         }
-    }
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        uint64_t m = __ballot(live[k] && !small[k]);
-        while (m) {  // the long packets, 4 at a time in group order
-            // the lane id laundered per iteration: verify_group's lane-derived
-            // constants are recomputed in the body, not held across the loop
-            uint32_t ln = lane_id();
-            asm volatile("" : "+v"(ln));
-            uint64_t doff[4];
-            uint32_t lg[4], tgt[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const bool have = m != 0;
-                const uint32_t j = have ? (uint32_t)__builtin_ctzll(m) : 0u;
-                m = have ? m & (m - 1) : m;
-                tgt[q] = have ? j : 64u;
-                doff[q] = have ? (((uint64_t)rdl(ohi[k], j) << 32) | rdl(olo[k], j)) : 0u;
-                lg[q] = have ? rdl(len[k], j) : 0u;
-            }
-            uint32_t v2 = 0, c2 = 0;
-            verify_group<4>(p.base, doff, lg, tgt, ln, v2, c2, [] {});
-            r[k] = (ln == tgt[0] || ln == tgt[1] || ln == tgt[2] || ln == tgt[3]) ? (v2 | (c2 << 8)) : r[k];
-        }
+        uint32_t v2 = 0, c2 = 0;
+        verify_group<4>(p.base, doff, lg, tgt, ln, v2, c2, [] {});
+        r = (ln == tgt[0] || ln == tgt[1] || ln == tgt[2] || ln == tgt[3]) ? (v2 | (c2 << 8)) : r;
     }
     // the index recomputed from a laundered lane id (held across the walk it spilled)
     uint32_t l2 = lane_id();
     asm volatile("" : "+v"(l2));
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const uint64_t i2 = ((uint64_t)((l2 >> 2) + 16u * k) * G + w) * 4u + (l2 & 3u);
-        if (i2 < p.n) {
-            p.verdict[i2] = (uint8_t)r[k];
-            if (p.l4)
-                p.l4[i2] = (uint16_t)(r[k] >> 8);
-        }
+    const uint64_t i2 = ((uint64_t)(l2 >> 2) * G + w) * 4u + (l2 & 3u);
+    if (i2 < p.n) {
+        p.verdict[i2] = (uint8_t)r;
+        if (p.l4)
+            p.l4[i2] = (uint16_t)(r >> 8);
     }
     if (p.sample && blockIdx.x == 0 && wave_in_block() == 0)
         verify_sample(p, l2);
@@ -1282,18 +1253,12 @@ static bool verify_pick_compact(uint64_t n, uint32_t smp, uint32_t lb, uint32_t 
 enum VerifyPath { kPathWave, kPathCompact, kPathWalk };
 
 static int verify_launch_walk(const VerifyParams &p, hipStream_t st) {
-    const uint32_t K = tune().verify_walk_k;
-    uint64_t blocks = (p.n + 256 * K - 1) / (256 * K);  // a wave per 64 K descriptors
+    uint64_t blocks = (p.n + 255) / 256;  // a wave per 64 descriptors
     if (blocks >= 8)
         blocks = (blocks + 7) & ~7ull;
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
-    if (K == 3)
-        hipLaunchKernelGGL(verify_walk_kernel<3>, dim3((unsigned)blocks), dim3(256), 0, st, p);
-    else if (K == 2)
-        hipLaunchKernelGGL(verify_walk_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, st, p);
-    else
-        hipLaunchKernelGGL(verify_walk_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, st, p);
+    hipLaunchKernelGGL(verify_walk_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p);
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }
 

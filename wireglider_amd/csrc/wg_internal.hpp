@@ -25,7 +25,6 @@ struct Tune {
     uint32_t verify_small;  // 7 per-call choice (default), 0 wave kernel, 6 compacting path, 8 walking kernel
     uint32_t verify_auto_t;  // verify_small = 7: compacting path when >= this many of 64 sampled packets are small
     uint32_t verify_k2min;   // compacting path: minimum blocks of the long kernel
-    uint32_t verify_walk_k;  // walking verify kernel: descriptors per lane (1-3)
     uint32_t host_chunk_mb;  // host-memory pipeline chunk size, MiB
     uint32_t host_d2h;    // host pipeline downloads into pinned memory by a store kernel (bit 1 encap messages, bit 2 decap plaintext)
     uint32_t l4_unroll;   // split kernel: loads in flight per lane on a long packet's rest (4, 8)
