@@ -30,11 +30,10 @@ def _wga():
                         {"gso_groups": 3, "gso_spw": 2}, {"gso_groups": 2, "gso_spw": 0},
                         {"gso_groups": 12, "gso_waves": 1}, {"gso_groups": 7, "gso_waves": 2},
                         {"gso_groups": 3, "gso_spw": 1}, {"gso_groups": 2, "gso_spw": 3},
-                        {"gso_groups": 1, "gso_spw": 4, "gso_waves": 2}, {"gso_groups": 2, "gso_spw": 6},
-                        {"gso_groups": 1, "gso_spw": 8, "gso_waves": 8}],
+                        {"gso_groups": 1, "gso_spw": 4, "gso_waves": 2}],
                 ids=["swizzled", "launch-order", "groups3", "groups12", "groups5x8", "groups3-pairs",
                      "groups2-serial", "groups12x1", "groups7x2", "groups3-pingpong", "groups2-triples",
-                     "groups1x2-quads", "groups2-sixes", "groups1x8-eights"])
+                     "groups1x2-quads"])
 def variant(request):
     """Every correct block -> (super-buffer, segment slot) mapping of the GSO
     kernel: one looping block per super-buffer (XCD-swizzled or in launch

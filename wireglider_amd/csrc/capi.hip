@@ -40,7 +40,7 @@ static const Knob kKnobs[] = {
     {"gso_waves", nullptr, &Tune::gso_waves, 0, 0, kWaves, WG_N(kWaves)},
     {"gso_split", nullptr, &Tune::gso_split, 1, 64, nullptr, 0},
     {"gso_groups", nullptr, &Tune::gso_groups, 1, 64, nullptr, 0},
-    {"gso_spw", nullptr, &Tune::gso_spw, 0, 8, nullptr, 0},
+    {"gso_spw", nullptr, &Tune::gso_spw, 0, 4, nullptr, 0},
     {"encap_spw", nullptr, &Tune::encap_spw, 0, 4, nullptr, 0},
     {"verify_small", nullptr, &Tune::verify_small, 0, 0, kVSmall, WG_N(kVSmall)},
     {"verify_auto_t", nullptr, &Tune::verify_auto_t, 1, 64, nullptr, 0},

@@ -743,8 +743,6 @@ int gso_split_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n, u
             case 2: launch_split<2, 0>(p, g, t.gso_waves, st); break;
             case 3: launch_split<3, 0>(p, g, t.gso_waves, st); break;
             case 4: launch_split<4, 0>(p, g, t.gso_waves, st); break;
-            case 6: launch_split<6, 0>(p, g, t.gso_waves, st); break;
-            case 8: launch_split<8, 0>(p, g, t.gso_waves, st); break;
             default: launch_split<0, 0>(p, g, t.gso_waves, st); break;
             }
         }
