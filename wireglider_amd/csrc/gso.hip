@@ -491,30 +491,16 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
         } else {
             c.hc0 = hdr_code(c, lane);
             c.hc1 = hdr_code(c, lane + 64);
-#ifndef WG_GSO_PF
-#define WG_GSO_PF 0
-#endif
-            uint32_t pfv = 0;
             for (uint32_t i0 = gw * S; i0 < c.nseg; i0 += gstride) {
                 SegFront f[S];
 #pragma unroll
                 for (int k = 0; k < S; k++)
                     seg_go<Abl>(c, out_base, i0 + k < c.nseg ? i0 + k : c.nseg - 1, lane, f[k]);
-                if (WG_GSO_PF > 0 && gw == 0 && i0 == 0 && !p.list) {
-                    // a later super-buffer's plan (lane 0) and descriptor
-                    // (lane 1) towards the caches
-                    const uint64_t bp = b + WG_GSO_PF < p.n ? b + WG_GSO_PF : b;
-                    const uintptr_t pa = lane == 0 ? reinterpret_cast<uintptr_t>(p.res + bp)
-                                                   : reinterpret_cast<uintptr_t>(p.desc + bp);
-                    pfv = *reinterpret_cast<const __attribute__((address_space(1))) uint32_t *>(pa);
-                }
 #pragma unroll
                 for (int k = 0; k < S; k++)
                     if (i0 + k < c.nseg)
                         seg_done<Abl>(c, out_base, f[k], lane);
             }
-            if (WG_GSO_PF > 0)
-                asm volatile("" ::"v"(pfv));
         }
     }
 }
