@@ -1395,24 +1395,42 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
     parity = gpu_out is not None and bool(np.array_equal(exp, gpu_out))
     scale, unit = (1e-6, "Mflows/s") if kind[0] == "gro" else (2.0**-30, "GiB/s")
     run_all()  # first touch / warm-up, untimed
-    def warm(fn, secs):
+    warm_log = {}
+
+    def warm(name, fn, secs, secs_max=8.0, tol=0.02):
         # untimed runs until the leg's pages have settled where its workers
         # run (round 5: repetitions still rose 30-60 % over the first
         # seconds on a 256-CPU host — page placement, not clocks: every
-        # repetition's CPUs held the same scaling_cur_freq)
+        # repetition's CPUs held the same scaling_cur_freq).  In 0.4-s
+        # chunks: at least `secs`, then until two chunks in a row agree
+        # within `tol`, at most `secs_max`.
         t0 = time.perf_counter()
-        while time.perf_counter() - t0 < secs:
-            fn()
+        rates, prev = [], None
+        while True:
+            k, ts = 0, time.perf_counter()
+            while time.perf_counter() - ts < 0.4:
+                fn()
+                k += 1
+            rate = k / (time.perf_counter() - ts)
+            rates.append(rate)
+            el = time.perf_counter() - t0
+            if el >= secs_max or (el >= secs and prev and abs(rate - prev) <= tol * prev):
+                break
+            prev = rate
+        warm_log[name] = {"seconds": round(el, 2), "chunks": len(rates),
+                          "last_rate_vs_first": round(rates[-1] / rates[0], 3)}
 
-    warm(run_all, min(seconds, 1.5))
+    warm("all", run_all, min(seconds, 1.5))
     thr0 = oracle.cgroup_throttling()
     all_s = _spread(_rep_rates(run_all, nbytes, seconds, reps, after=logger("all", cpus_all)), scale)
     thr1 = oracle.cgroup_throttling()
     cpus_one = pick(1)
-    warm(run_one, min(seconds, 1.5))  # the 1-core leg's first touch on its CPU, untimed
+    warm("one", run_one, min(seconds, 1.5))  # the 1-core leg's first touch on its CPU, untimed
     one_s = _spread(_rep_rates(run_one, nbytes * one_scale, seconds / 2, reps, after=logger("one", cpus_one)), scale)
     all_s["repetitions"] = reps_log["all"]
     one_s["repetitions"] = reps_log["one"]
+    all_s["warm_up"] = warm_log.get("all")
+    one_s["warm_up"] = warm_log.get("one")
     if thr0 and thr1:
         # CPU-quota throttling while the all-core repetitions ran (a share of
         # 16 CPUs leaves no room for a 17th busy thread)
@@ -1450,7 +1468,8 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
                   f"({what}; {nofold} for spans >= 256 B), {threads} pthreads "
                   f"(sched_getaffinity {cores['affinity']}, cgroup quota {cores['cgroup_quota_cpus']}); "
                   f"value = median of {reps - 1} repetitions of >= {seconds:.1f} s after a dropped first one "
-                  f"(and >= {min(seconds, 1.5):.1f} s of untimed runs per leg), "
+                  f"(after untimed runs per leg: >= {min(seconds, 1.5):.1f} s, then until two 0.4-s chunks agree "
+                  f"within 2 %, <= 8 s; spread.warm_up), "
                   f"1 core: the same of >= {seconds / 2:.1f} s; worker t pinned to the t-th least busy CPU of the "
                   f"affinity mask, one per physical core, picked once per leg (host_cores.pinning); "
                   f"bit-exact vs GPU: {parity}",
