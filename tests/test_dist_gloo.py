@@ -87,7 +87,7 @@ def _worker(rank, world, port, n, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
 def test_sharded_equals_single_process(world):
     import oracle
 
