@@ -207,11 +207,12 @@ struct Flight {
         return rc;
     }
     // Before chunk k's uploads.  staging: the slot's pinned staging is about
-    // to be rewritten by the host, so its previous upload must have finished.
+    // to be rewritten by the host, so its previous upload — on the exec
+    // stream, ahead of that chunk's kernels — must have finished.
     int begin(int slot, bool staging) {
         armed = true;
         if (k >= (uint64_t)kSlots) {
-            if (staging && hipEventSynchronize(c.copied[slot]) != hipSuccess)
+            if (staging && hipEventSynchronize(c.computed[slot]) != hipSuccess)
                 return WG_ERR_RUNTIME;
             if (hipStreamWaitEvent(c.s[kH2D], c.computed[slot], 0) != hipSuccess)
                 return WG_ERR_RUNTIME;
@@ -458,15 +459,20 @@ extern "C" int wg_encap_host(const uint8_t *host_in, const wg_gso_desc *host_des
                                       : (1ull << 20);
     if (!max_cnt_call)
         return WG_ERR_INVALID;
+    // The first chunks are 1/8, 1/4 and 1/2 of the budget and the last one is
+    // cut into halves the same way, so the pipeline fills and drains behind
+    // short transfers (its first upload and last download run alone).
     std::vector<uint64_t> bounds{0};
     uint64_t max_cnt = 0, max_span = 0, max_seg = 0;
     for (uint64_t i = 0; i < n;) {
         const uint64_t i0 = i, s0 = host_desc[i0].in_offset;
+        const size_t kb = bounds.size() - 1;
+        const uint64_t cbk = kb < 3 ? cb >> (3 - kb) : cb;
         uint64_t segb = 0;
         do {
             segb += host_desc[i].out_cap;
             i++;
-        } while (i < n && i - i0 < max_cnt_call && host_desc[i].in_offset + host_desc[i].in_len - s0 <= cb &&
+        } while (i < n && i - i0 < max_cnt_call && host_desc[i].in_offset + host_desc[i].in_len - s0 <= cbk &&
                  (i - i0 + 1) * (uint64_t)msg_cap <= ob && segb + host_desc[i].out_cap <= ob);
         const uint64_t span = host_desc[i - 1].in_offset + host_desc[i - 1].in_len - s0;
         bounds.push_back(i);
@@ -474,17 +480,27 @@ extern "C" int wg_encap_host(const uint8_t *host_in, const wg_gso_desc *host_des
         max_span = span > max_span ? span : max_span;
         max_seg = segb > max_seg ? segb : max_seg;
     }
+    if (bounds.size() > 4) {  // the last chunk in pieces of 1/2, 1/4, 1/8, 1/8 (subsets: the slot bounds hold)
+        const uint64_t a = bounds[bounds.size() - 2], b = bounds.back();
+        if (b - a >= 8) {
+            bounds.pop_back();
+            const uint64_t m = b - a;
+            bounds.push_back(a + m / 2);
+            bounds.push_back(a + m / 2 + m / 4);
+            bounds.push_back(a + m / 2 + m / 4 + m / 8);
+            bounds.push_back(b);
+        }
+    }
     const uint64_t nchunks = bounds.size() - 1;
     Pipe &c = g_pipe;
     WG_TRY(pipe_init(c));
-    enum { kIn, kDesc, kSeg, kGres, kMoff, kMsgs, kEres, kWork };
+    enum { kIn, kDesc, kSeg, kGres, kMsgs, kEres, kWork };  // kDesc: rebased descriptors, then message offsets
     const size_t stage_bytes = max_cnt * (sizeof(wg_gso_desc) + sizeof(uint64_t));
     for (int s = 0; s < kSlots; s++) {
         WG_TRY(grow_dev(c.dev[s][kIn], max_span + 64));
-        WG_TRY(grow_dev(c.dev[s][kDesc], max_cnt * sizeof(wg_gso_desc)));
+        WG_TRY(grow_dev(c.dev[s][kDesc], max_cnt * (sizeof(wg_gso_desc) + sizeof(uint64_t))));  // + message offsets
         WG_TRY(grow_dev(c.dev[s][kSeg], max_seg + 64));
         WG_TRY(grow_dev(c.dev[s][kGres], max_cnt * sizeof(wg_gso_result)));
-        WG_TRY(grow_dev(c.dev[s][kMoff], max_cnt * sizeof(uint64_t)));
         WG_TRY(grow_dev(c.dev[s][kMsgs], max_cnt * msg_cap));
         WG_TRY(grow_dev(c.dev[s][kEres], max_cnt * sizeof(wg_encap_result)));
         WG_TRY(grow_dev(c.dev[s][kWork], 4 * (max_cnt + 1024)));
@@ -520,13 +536,21 @@ extern "C" int wg_encap_host(const uint8_t *host_in, const wg_gso_desc *host_des
             oo += sd[j].out_cap;
             so[j] = j * msg_cap;
         }
+        // the H2D stream carries only the payload spans, back to back; the
+        // rebased descriptors and message offsets (contiguous in the staging
+        // buffer and in the slot) go up in ONE copy on the exec stream, ahead
+        // of the kernels (a small copy costs ~30 us of stream latency: three
+        // per chunk on the H2D stream were ~90 us of idle link per chunk)
         WG_TRY(h2d(c, dp(c, slot, kIn), host_in + s0, span));
-        WG_TRY(h2d(c, dp(c, slot, kDesc), sd, cnt * sizeof(wg_gso_desc)));
-        WG_TRY(h2d(c, dp(c, slot, kMoff), so, cnt * sizeof(uint64_t)));
         WG_TRY(f.uploaded(slot));
-        WG_TRY(encap_batch_launch(dp(c, slot, kIn), dp<wg_gso_desc>(c, slot, kDesc), cnt, dp(c, slot, kSeg),
+        uint8_t *const dd = dp(c, slot, kDesc);
+        if (hipMemcpyAsync(dd, sd, cnt * (sizeof(wg_gso_desc) + sizeof(uint64_t)), hipMemcpyHostToDevice,
+                           c.s[kExec]) != hipSuccess)
+            return WG_ERR_RUNTIME;
+        WG_TRY(encap_batch_launch(dp(c, slot, kIn), reinterpret_cast<wg_gso_desc *>(dd), cnt, dp(c, slot, kSeg),
                                   dp<wg_gso_result>(c, slot, kGres), key, receiver_index, counter0,
-                                  dp<uint64_t>(c, slot, kMoff), msg_cap, max_segments, max_segment_size,
+                                  reinterpret_cast<uint64_t *>(dd + cnt * sizeof(wg_gso_desc)), msg_cap, max_segments,
+                                  max_segment_size,
                                   dp(c, slot, kMsgs), dp<wg_encap_result>(c, slot, kEres), dp<uint32_t>(c, slot, kWork),
                                   ctr + k + 1, ctr + k, c.s[kExec]));
         WG_TRY(f.computed(slot));
