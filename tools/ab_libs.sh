@@ -9,7 +9,7 @@ for r in $(seq "$R"); do
   for W in ${WS//,/ }; do
     for L in "$@"; do
       WG_LIB=$L timeout -k 10 300 python3 bench.py --workload "$W" --steps 30 --no-cpu-baseline --no-strong --no-post 2>>"$OUT.err" | \
-        python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'lib': sys.argv[1], 'workload': sys.argv[2], 'kernel_ms': d['roofline']['kernel_ms_avg']}))" "$L" "$W" >> "$OUT" || exit 1
+        python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'lib': sys.argv[1], 'workload': sys.argv[2], 'kernel_ms': d['roofline'].get('kernel_ms_avg', d['ms_per_step'])}))" "$L" "$W" >> "$OUT" || exit 1
     done
   done
 done
