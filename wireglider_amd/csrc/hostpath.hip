@@ -250,6 +250,11 @@ int d2h(Pipe &c, void *dst, const void *src, size_t n) {
     return !n || hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c.s[kD2H]) == hipSuccess ? WG_OK
                                                                                                : WG_ERR_RUNTIME;
 }
+// A small download on the exec stream (behind the chunk's kernels).
+int xd2h(Pipe &c, void *dst, const void *src, size_t n) {
+    return !n || hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c.s[kExec]) == hipSuccess ? WG_OK
+                                                                                                : WG_ERR_RUNTIME;
+}
 
 // Downloads into pinned host memory by a store kernel on the D2H stream
 // (knob host_d2h, bit 1: encap messages, bit 2: decap plaintext): 16-B
@@ -309,6 +314,31 @@ int d2h_big(Pipe &c, uint32_t bit, void *dst, uint8_t *dst_alias, const void *sr
 }
 
 uint64_t chunk_bytes() { return (uint64_t)tune().host_chunk_mb << 20; }
+
+// Chunk boundaries (in units) for n units of at most `per` a chunk: the
+// first chunks are 1/8, 1/4 and 1/2 of `per` and the last full-size chunk is
+// cut into 1/2, 1/4, 1/8, 1/8, so the pipeline fills and drains behind short
+// transfers (its first upload and its last download run alone).
+std::vector<uint64_t> ramped_bounds(uint64_t n, uint64_t per) {
+    std::vector<uint64_t> b{0};
+    while (b.back() < n) {
+        const size_t k = b.size() - 1;
+        uint64_t m = k < 3 ? per >> (3 - k) : per;
+        m = m ? m : 1;
+        b.push_back(n - b.back() < m ? n : b.back() + m);
+    }
+    if (b.size() > 4) {
+        const uint64_t a = b[b.size() - 2], e = b.back(), m = e - a;
+        if (m >= 8) {
+            b.pop_back();
+            b.push_back(a + m / 2);
+            b.push_back(a + m / 2 + m / 4);
+            b.push_back(a + m / 2 + m / 4 + m / 8);
+            b.push_back(e);
+        }
+    }
+    return b;
+}
 
 #define WG_TRY(x)                 \
     do {                          \
@@ -395,11 +425,13 @@ extern "C" int wg_decap_host(const uint8_t *host_msgs, uint64_t total_len, uint3
     auto *gver = static_cast<uint8_t *>(c.gather[kVer].p);
     auto *gl4 = static_cast<uint16_t *>(c.gather[kL4].p);
     uint8_t *const plain_alias = pstride ? pinned_alias(host_plain) : nullptr;
+    const std::vector<uint64_t> bounds = ramped_bounds(n, per);
     Flight f(c);
-    for (uint64_t off = 0; off < total_len; off += chunk) {
+    for (size_t q = 0; q + 1 < bounds.size(); q++) {
         const int slot = (int)(f.k % kSlots);
-        const uint64_t len = total_len - off < chunk ? total_len - off : chunk;
-        const uint64_t first = off / segment_size, m = (len + segment_size - 1) / segment_size;
+        const uint64_t first = bounds[q], m = bounds[q + 1] - first;
+        const uint64_t off = first * segment_size;
+        const uint64_t len = total_len - off < m * segment_size ? total_len - off : m * segment_size;
         WG_TRY(f.begin(slot, false));
         WG_TRY(h2d(c, dp(c, slot, kIn), host_msgs + off, len));
         WG_TRY(f.uploaded(slot));
@@ -410,14 +442,19 @@ extern "C" int wg_decap_host(const uint8_t *host_msgs, uint64_t total_len, uint3
         else
             WG_TRY(wg_aead_decrypt_batch(dp(c, slot, kIn), len, segment_size, key, dp(c, slot, kPlain),
                                          dp<int8_t>(c, slot, kSt), c.s[kExec]));
+        // the small per-message results go down on the exec stream behind
+        // the kernels (each small copy costs ~30 us of stream latency: on the
+        // D2H stream they idled the link between plaintext downloads); the
+        // next chunk's kernels wait for them, which the exec stream's slack
+        // absorbs, and they land in the call's gather buffers, not the slot
+        WG_TRY(xd2h(c, gst + first, dp(c, slot, kSt), m));
+        if (ver) {
+            WG_TRY(xd2h(c, gver + first, dp(c, slot, kVer), m));
+            WG_TRY(xd2h(c, gl4 + first, dp(c, slot, kL4), m * 2));
+        }
         WG_TRY(f.computed(slot));
         WG_TRY(d2h_big(c, 2u, host_plain + first * pstride, plain_alias ? plain_alias + first * pstride : nullptr,
                        dp(c, slot, kPlain), m * pstride));
-        WG_TRY(d2h(c, gst + first, dp(c, slot, kSt), m));
-        if (ver) {
-            WG_TRY(d2h(c, gver + first, dp(c, slot, kVer), m));
-            WG_TRY(d2h(c, gl4 + first, dp(c, slot, kL4), m * 2));
-        }
         WG_TRY(f.end(slot));
     }
     WG_TRY(f.drain());
