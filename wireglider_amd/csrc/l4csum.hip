@@ -102,11 +102,8 @@ __device__ __forceinline__ void geoms_from_vec(const L4Params &p, uint64_t i0, c
 // its packet loads with no descriptor round trip in front of them (the
 // launcher gives each wave 4 iterations; one vector load per iteration
 // without the prefetch measured slower: the readlanes wait on it).
-#ifndef WG_L4_WPE
-#define WG_L4_WPE 1
-#endif
 template <int kKind, int P, bool kNT, int kDM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WG_L4_WPE))) void l4csum_kernel(L4Params p) {
+__global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
     constexpr bool kL4 = kKind != kDescPlain;
     constexpr int DM = kKind == kUniformL4 ? 0 : kDM;
     const uint32_t lane = lane_id();
