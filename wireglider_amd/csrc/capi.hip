@@ -47,7 +47,7 @@ static const Knob kKnobs[] = {
     {"verify_k2min", nullptr, &Tune::verify_k2min, 8, 65536, nullptr, 0},
     {"gso_ablate", nullptr, &Tune::gso_ablate, 0, 0, kAbl, WG_N(kAbl)},
     {"host_chunk_mb", nullptr, &Tune::host_chunk_mb, 1, 4096, nullptr, 0},
-    {"host_d2h", nullptr, &Tune::host_d2h, 0, 7, nullptr, 0},
+    {"host_d2h", nullptr, &Tune::host_d2h, 0, 3, nullptr, 0},
     {"l4_unroll", nullptr, &Tune::l4_unroll, 0, 0, kUnroll, WG_N(kUnroll)},
     {"l4_coop", &Tune::l4_coop, nullptr, 0, 1u << 20, nullptr, 0},
     {"l4_coop_waves", nullptr, &Tune::l4_coop_waves, 0, 0, kCoopW, WG_N(kCoopW)},

@@ -301,25 +301,6 @@ __global__ void __launch_bounds__(256) d2h_store_kernel(const uint4 *__restrict_
     }
 }
 
-// Uploads from pinned host memory by a load kernel on the H2D stream (knob
-// host_d2h bit 4, experiment): 16-B PCIe reads, four in flight per lane,
-// 16-B stores into the slot.
-__global__ void __launch_bounds__(256) h2d_load_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
-                                                       uint64_t n16) {
-    const uint64_t stride = (uint64_t)gridDim.x * 1024u;
-    for (uint64_t i = (uint64_t)blockIdx.x * 1024u + threadIdx.x; i < n16; i += stride) {
-        uint4 v[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            if (i + k * 256u < n16)
-                v[k] = src[i + k * 256u];
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            if (i + k * 256u < n16)
-                dst[i + k * 256u] = v[k];
-    }
-}
-
 // The device-visible address of a caller's host buffer when it is pinned
 // (hipHostMalloc, wg_host_alloc, hipHostRegister), else nullptr: pageable
 // memory is left to the runtime's staged copies.
@@ -349,22 +330,6 @@ int d2h_big(Pipe &c, uint32_t bit, void *dst, uint8_t *dst_alias, const void *sr
     blocks = blocks < 1024 ? blocks : 1024;
     hipLaunchKernelGGL(d2h_store_kernel, dim3((uint32_t)blocks), dim3(256), 0, c.s[kD2H],
                        static_cast<const uint4 *>(src), reinterpret_cast<uint4 *>(dst_alias), n16);
-    return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
-}
-
-// A large upload: the load kernel when knob host_d2h has bit 4 and the
-// source is pinned (src_alias) with 16-B aligned ends, else hipMemcpyAsync.
-int h2d_big(Pipe &c, void *dst, const void *src, const uint8_t *src_alias, size_t n) {
-    if (!n)
-        return WG_OK;
-    if (!src_alias || !(tune().host_d2h & 4u) || ((reinterpret_cast<uintptr_t>(src_alias) | n) & 15) ||
-        (reinterpret_cast<uintptr_t>(dst) & 15))
-        return h2d(c, dst, src, n);
-    const uint64_t n16 = n / 16;
-    uint64_t blocks = (n16 + 1023) / 1024;
-    blocks = blocks < 1024 ? blocks : 1024;
-    hipLaunchKernelGGL(h2d_load_kernel, dim3((uint32_t)blocks), dim3(256), 0, c.s[kH2D],
-                       reinterpret_cast<const uint4 *>(src_alias), static_cast<uint4 *>(dst), n16);
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }
 
@@ -481,7 +446,6 @@ extern "C" int wg_decap_host(const uint8_t *host_msgs, uint64_t total_len, uint3
     auto *gl4 = static_cast<uint16_t *>(c.gather[kL4].p);
     uint8_t *const plain_alias = pstride ? pinned_alias(host_plain) : nullptr;
     uint8_t *const ast = pinned_alias(gst), *const aver = pinned_alias(gver), *const al4 = pinned_alias(gl4);
-    const uint8_t *const msgs_alias_in = pinned_alias(host_msgs);
     const std::vector<uint64_t> bounds = ramped_bounds(n, per);
     Flight f(c);
     for (size_t q = 0; q + 1 < bounds.size(); q++) {
@@ -490,7 +454,7 @@ extern "C" int wg_decap_host(const uint8_t *host_msgs, uint64_t total_len, uint3
         const uint64_t off = first * segment_size;
         const uint64_t len = total_len - off < m * segment_size ? total_len - off : m * segment_size;
         WG_TRY(f.begin(slot, false));
-        WG_TRY(h2d_big(c, dp(c, slot, kIn), host_msgs + off, msgs_alias_in ? msgs_alias_in + off : nullptr, len));
+        WG_TRY(h2d(c, dp(c, slot, kIn), host_msgs + off, len));
         WG_TRY(f.uploaded(slot));
         if (ver)
             WG_TRY(wg_aead_decrypt_verify_batch(dp(c, slot, kIn), len, segment_size, key, dp(c, slot, kPlain),
@@ -606,7 +570,6 @@ extern "C" int wg_encap_host(const uint8_t *host_in, const wg_gso_desc *host_des
     auto *ggres = static_cast<wg_gso_result *>(c.gather[kGres].p);
     auto *ctr = static_cast<uint64_t *>(c.ctr.p);
     uint8_t *const msgs_alias = pinned_alias(host_msgs);
-    const uint8_t *const in_alias = pinned_alias(host_in);
     Flight f(c);
     f.armed = true;
     if (hipMemsetAsync(ctr, 0, sizeof(uint64_t), c.s[kExec]) != hipSuccess)
@@ -634,7 +597,7 @@ extern "C" int wg_encap_host(const uint8_t *host_in, const wg_gso_desc *host_des
         // buffer and in the slot) go up in ONE copy on the exec stream, ahead
         // of the kernels (a small copy costs ~30 us of stream latency: three
         // per chunk on the H2D stream were ~90 us of idle link per chunk)
-        WG_TRY(h2d_big(c, dp(c, slot, kIn), host_in + s0, in_alias ? in_alias + s0 : nullptr, span));
+        WG_TRY(h2d(c, dp(c, slot, kIn), host_in + s0, span));
         WG_TRY(f.uploaded(slot));
         uint8_t *const dd = dp(c, slot, kDesc);
         if (hipMemcpyAsync(dd, sd, cnt * (sizeof(wg_gso_desc) + sizeof(uint64_t)), hipMemcpyHostToDevice,
