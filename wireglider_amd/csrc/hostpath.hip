@@ -335,30 +335,6 @@ int d2h_big(Pipe &c, uint32_t bit, void *dst, uint8_t *dst_alias, const void *sr
 
 uint64_t chunk_bytes() { return (uint64_t)tune().host_chunk_mb << 20; }
 
-// Chunk boundaries (in units) for n units of at most `per` a chunk: the
-// first chunks are 1/8, 1/4 and 1/2 of `per` and the last full-size chunk is
-// cut into 1/2, 1/4, 1/8, 1/8, so the pipeline fills and drains behind short
-// transfers (its first upload and its last download run alone).
-std::vector<uint64_t> ramped_bounds(uint64_t n, uint64_t per) {
-    std::vector<uint64_t> b{0};
-    while (b.back() < n) {
-        const size_t k = b.size() - 1;
-        uint64_t m = k < 3 ? per >> (3 - k) : per;
-        m = m ? m : 1;
-        b.push_back(n - b.back() < m ? n : b.back() + m);
-    }
-    if (b.size() > 4) {
-        const uint64_t a = b[b.size() - 2], e = b.back(), m = e - a;
-        if (m >= 8) {
-            b.pop_back();
-            b.push_back(a + m / 2);
-            b.push_back(a + m / 2 + m / 4);
-            b.push_back(a + m / 2 + m / 4 + m / 8);
-            b.push_back(e);
-        }
-    }
-    return b;
-}
 
 #define WG_TRY(x)                 \
     do {                          \
@@ -446,13 +422,15 @@ extern "C" int wg_decap_host(const uint8_t *host_msgs, uint64_t total_len, uint3
     auto *gl4 = static_cast<uint16_t *>(c.gather[kL4].p);
     uint8_t *const plain_alias = pstride ? pinned_alias(host_plain) : nullptr;
     uint8_t *const ast = pinned_alias(gst), *const aver = pinned_alias(gver), *const al4 = pinned_alias(gl4);
-    const std::vector<uint64_t> bounds = ramped_bounds(n, per);
+    // uniform chunks: a ramped schedule (short first and last chunks, as the
+    // encap step has) made the runtime's plaintext downloads fall to a third
+    // of the link at 32-MiB chunks (87.7 vs 34.0 ms,
+    // profiles/r05_hostpath/ab_decap_ramp_32mib.txt)
     Flight f(c);
-    for (size_t q = 0; q + 1 < bounds.size(); q++) {
+    for (uint64_t off = 0; off < total_len; off += chunk) {
         const int slot = (int)(f.k % kSlots);
-        const uint64_t first = bounds[q], m = bounds[q + 1] - first;
-        const uint64_t off = first * segment_size;
-        const uint64_t len = total_len - off < m * segment_size ? total_len - off : m * segment_size;
+        const uint64_t len = total_len - off < chunk ? total_len - off : chunk;
+        const uint64_t first = off / segment_size, m = (len + segment_size - 1) / segment_size;
         WG_TRY(f.begin(slot, false));
         WG_TRY(h2d(c, dp(c, slot, kIn), host_msgs + off, len));
         WG_TRY(f.uploaded(slot));
