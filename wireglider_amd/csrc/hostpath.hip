@@ -319,10 +319,11 @@ uint8_t *pinned_alias(const void *host) {
 // A large download: the store kernel when knob host_d2h has `bit`, the
 // destination is pinned (dst_alias: its device-visible address) and both
 // ends and the length are 16-B multiples, else hipMemcpyAsync.
-int d2h_big(Pipe &c, uint32_t bit, void *dst, uint8_t *dst_alias, const void *src, size_t n) {
+// force: the store kernel regardless of the knob (same conditions otherwise).
+int d2h_big(Pipe &c, uint32_t bit, void *dst, uint8_t *dst_alias, const void *src, size_t n, bool force = false) {
     if (!n)
         return WG_OK;
-    if (!dst_alias || !(tune().host_d2h & bit) || ((reinterpret_cast<uintptr_t>(dst_alias) | n) & 15) ||
+    if (!dst_alias || !(force || (tune().host_d2h & bit)) || ((reinterpret_cast<uintptr_t>(dst_alias) | n) & 15) ||
         (reinterpret_cast<uintptr_t>(src) & 15))
         return d2h(c, dst, src, n);
     const uint64_t n16 = n / 16;
@@ -450,8 +451,12 @@ extern "C" int wg_decap_host(const uint8_t *host_msgs, uint64_t total_len, uint3
             WG_TRY(xd2h(c, gl4 + first, al4 ? al4 + 2 * first : nullptr, dp(c, slot, kL4), m * 2));
         }
         WG_TRY(f.computed(slot));
+        // plaintext: the runtime's copy (faster from 32 MiB up), the store
+        // kernel below that — the runtime's copies of 16-MiB chunks ran at a
+        // third of the link beside the uploads (109 vs 34 ms a call,
+        // profiles/r05_hostpath/chunk_sweep.jsonl)
         WG_TRY(d2h_big(c, 2u, host_plain + first * pstride, plain_alias ? plain_alias + first * pstride : nullptr,
-                       dp(c, slot, kPlain), m * pstride));
+                       dp(c, slot, kPlain), m * pstride, m * pstride < (32ull << 20)));
         WG_TRY(f.end(slot));
     }
     WG_TRY(f.drain());
