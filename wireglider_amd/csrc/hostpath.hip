@@ -451,12 +451,12 @@ extern "C" int wg_decap_host(const uint8_t *host_msgs, uint64_t total_len, uint3
             WG_TRY(xd2h(c, gl4 + first, al4 ? al4 + 2 * first : nullptr, dp(c, slot, kL4), m * 2));
         }
         WG_TRY(f.computed(slot));
-        // plaintext: the runtime's copy (faster from 32 MiB up), the store
-        // kernel below that — the runtime's copies of 16-MiB chunks ran at a
+        // plaintext: the runtime's copy (faster from ~32 MiB up), the store
+        // kernel under 24 MiB — the runtime's copies of 16-MiB chunks ran at a
         // third of the link beside the uploads (109 vs 34 ms a call,
         // profiles/r05_hostpath/chunk_sweep.jsonl)
         WG_TRY(d2h_big(c, 2u, host_plain + first * pstride, plain_alias ? plain_alias + first * pstride : nullptr,
-                       dp(c, slot, kPlain), m * pstride, m * pstride < (32ull << 20)));
+                       dp(c, slot, kPlain), m * pstride, m * pstride < (24ull << 20)));
         WG_TRY(f.end(slot));
     }
     WG_TRY(f.drain());
