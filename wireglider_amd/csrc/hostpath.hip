@@ -553,7 +553,6 @@ extern "C" int wg_encap_host(const uint8_t *host_in, const wg_gso_desc *host_des
     auto *ggres = static_cast<wg_gso_result *>(c.gather[kGres].p);
     auto *ctr = static_cast<uint64_t *>(c.ctr.p);
     uint8_t *const msgs_alias = pinned_alias(host_msgs);
-    uint8_t *const aeres = pinned_alias(geres), *const agres = pinned_alias(ggres);
     Flight f(c);
     f.armed = true;
     if (hipMemsetAsync(ctr, 0, sizeof(uint64_t), c.s[kExec]) != hipSuccess)
@@ -593,16 +592,12 @@ extern "C" int wg_encap_host(const uint8_t *host_in, const wg_gso_desc *host_des
                                   max_segment_size,
                                   dp(c, slot, kMsgs), dp<wg_encap_result>(c, slot, kEres), dp<uint32_t>(c, slot, kWork),
                                   ctr + k + 1, ctr + k, c.s[kExec]));
-        // per-super-buffer records into the gather buffers by kernels on
-        // the exec stream (xd2h); the D2H stream carries only messages
-        WG_TRY(xd2h(c, geres + i0, aeres ? aeres + i0 * sizeof(wg_encap_result) : nullptr, dp(c, slot, kEres),
-                    cnt * sizeof(wg_encap_result)));
-        if (host_gso_res)
-            WG_TRY(xd2h(c, ggres + i0, agres ? agres + i0 * sizeof(wg_gso_result) : nullptr, dp(c, slot, kGres),
-                        cnt * sizeof(wg_gso_result)));
         WG_TRY(f.computed(slot));
         WG_TRY(d2h_big(c, 1u, host_msgs + i0 * msg_cap, msgs_alias ? msgs_alias + i0 * msg_cap : nullptr,
                        dp(c, slot, kMsgs), cnt * msg_cap));
+        WG_TRY(d2h(c, geres + i0, dp(c, slot, kEres), cnt * sizeof(wg_encap_result)));
+        if (host_gso_res)
+            WG_TRY(d2h(c, ggres + i0, dp(c, slot, kGres), cnt * sizeof(wg_gso_result)));
         WG_TRY(f.end(slot));
     }
     WG_TRY(d2h(c, c.hctr.p, ctr + nchunks, sizeof(uint64_t)));
