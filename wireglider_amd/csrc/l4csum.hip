@@ -709,23 +709,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
                 len[j] = full ? p.seg : (i0 + j + 1 < p.n ? p.seg : (i0 + j + 1 == p.n ? p.last_len : 0u));
             }
         } else if (i0 + P <= p.n) {
-#ifdef WG_VERIFY_VDESC
-            // the group's descriptors by ONE vector load (lane j: descriptor
-            // j), made wave-uniform by v_readlane
-            const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc + i0) + 16u * (lane & (P - 1)));
-#pragma unroll
-            for (int j = 0; j < P; j++) {
-                doff[j] = ((uint64_t)rl(dv.y, j) << 32) | rl(dv.x, j);
-                len[j] = rl(dv.z, j);
-            }
-#else
             const v16u dd = *reinterpret_cast<const c_v16u *>(reinterpret_cast<uintptr_t>(p.desc + i0));
 #pragma unroll
             for (int j = 0; j < P; j++) {
                 doff[j] = ((uint64_t)dd[4 * j + 1] << 32) | dd[4 * j];
                 len[j] = dd[4 * j + 2];
             }
-#endif
         } else {
 #pragma unroll
             for (int j = 0; j < P; j++) {
