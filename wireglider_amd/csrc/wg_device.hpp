@@ -113,19 +113,9 @@ __device__ __forceinline__ uint32_t wave_in_block() {
 // observed round-robin dispatch, so give each XCD a contiguous run of virtual
 // block ids.  Speed only; any placement is correct.  Needs nblocks % 8 == 0
 // for the bijection, otherwise identity.
-#ifndef WG_XCD_CHUNK
-#define WG_XCD_CHUNK 0
-#endif
 __device__ __forceinline__ uint32_t xcd_swizzle(uint32_t b, uint32_t nblocks) {
     if (nblocks & 7u)
         return b;
-    if constexpr (WG_XCD_CHUNK > 0) {  // experiment: runs of K blocks dealt to the XCDs in turn
-        constexpr uint32_t K = WG_XCD_CHUNK;
-        if (nblocks % (8u * K) == 0) {
-            const uint32_t i = b >> 3;
-            return ((i / K) * 8u + (b & 7u)) * K + i % K;
-        }
-    }
     return (b & 7u) * (nblocks >> 3) + (b >> 3);
 }
 
