@@ -1008,7 +1008,11 @@ __global__ __launch_bounds__(256) void verify_walk_kernel(VerifyParams p) {
     const uint32_t lane = lane_id();
     const uint64_t G = (uint64_t)gridDim.x * 4u;
     const uint64_t w = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
+#ifdef WG_WALK_CONSEC
+    const uint64_t i = w * 64u + lane;  // experiment: a wave's 64 descriptors consecutive
+#else
     const uint64_t i = ((uint64_t)(lane >> 2) * G + w) * 4u + (lane & 3u);
+#endif
     const bool live = i < p.n;
     const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0u));
     const uint32_t len = live ? dv.z : 0u;
@@ -1043,7 +1047,11 @@ __global__ __launch_bounds__(256) void verify_walk_kernel(VerifyParams p) {
     // the index recomputed from a laundered lane id (held across the walk it spilled)
     uint32_t l2 = lane_id();
     asm volatile("" : "+v"(l2));
+#ifdef WG_WALK_CONSEC
+    const uint64_t i2 = w * 64u + l2;
+#else
     const uint64_t i2 = ((uint64_t)(l2 >> 2) * G + w) * 4u + (l2 & 3u);
+#endif
     if (i2 < p.n) {
         p.verdict[i2] = (uint8_t)r;
         if (p.l4)
