@@ -467,8 +467,8 @@ def build_workload(wga, torch, name: str, rank: int, world: int, dev) -> Workloa
                            "checksums stored, evaluate_packet checksum gates (wg_verify_desc, default knobs)",
                "packets_per_gpu": n, "segment_size": VSEG, "layout": "descriptor", "parallelism": f"shard{world}"}
         kname = ("wg::verify_kernel<false> (verify_small=7 chose the wave kernel: no small packets sampled)"
-                 if VSEG > 64 else "wg::verify_walk_kernel (verify_small=7 chose the walking kernel: 64 of 64 "
-                 "sampled packets small)")
+                 if VSEG > 64 else "wg::verify_walk_kernel<true> (verify_small=7 chose the walking kernel, "
+                 "consecutive layout: 64 of 64 sampled packets small)")
         return Workload(launch, n, n * VSEG, n * VSEG + 16 * n + n + 2 * n, cfg, "weak", buf,
                         kname, rank * n, sample=sample, counts=[n] * world, probe_run=VSEG,
                         metric="device-resident GiB/s, decap verify gates over packet batch (SURVEY f1)",

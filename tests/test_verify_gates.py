@@ -411,6 +411,41 @@ def test_gpu_verify_auto_switches(gpu):
 
 
 @pytest.mark.gpu
+def test_gpu_verify_walk_consecutive_layout(gpu):
+    """All-small batches back to back on one stream: from the third call the
+    default picks the walking kernel in its consecutive layout (each wave's 64
+    descriptors in a row); a batch whose size is no multiple of 64, packets of
+    0-64 bytes at odd offsets, and the same batch's descriptors reversed (the
+    lanes' packets then run backwards through memory) equal the oracle."""
+    import torch
+
+    import wireglider_amd as wga
+
+    rng = np.random.default_rng(16)
+    pkts = []
+    for _ in range(70001):
+        v6, tcp = bool(rng.integers(0, 2)), bool(rng.integers(0, 2))
+        hl = (40 if v6 else 20) + (20 if tcp else 8)
+        if hl <= 64 and rng.integers(0, 8):
+            al = 16 if v6 else 4
+            pkts.append(pktbuild.build(v6, tcp, rng.integers(0, 256, int(rng.integers(0, 65 - hl)), dtype=np.uint8)
+                                       .tobytes(), rng.integers(0, 256, al, dtype=np.uint8).tobytes(),
+                                       rng.integers(0, 256, al, dtype=np.uint8).tobytes()))
+        else:
+            pkts.append(rng.integers(0, 256, int(rng.integers(0, 65)), dtype=np.uint8).tobytes())
+    buf, d = pack(pkts, rng)
+    rev = (buf, d[::-1].copy())
+    batches = [(buf, d), (buf, d), (buf, d), rev, rev]
+    got = _verify_calls(wga, torch, gpu, batches, {"verify_small": 7})
+    for (b, dd), (v, x) in zip(batches, got):
+        ev, el4 = oracle.verify_desc(b, dd)
+        np.testing.assert_array_equal(v, ev)
+        np.testing.assert_array_equal(x, el4)
+    ev, _ = oracle.verify_desc(buf, d)
+    assert (ev & OK == OK).mean() > 0.5
+
+
+@pytest.mark.gpu
 def test_gpu_verify_compact_grows(gpu):
     """The compacting path's entry lists grow with the batch (a batch larger
     than every earlier one on the stream), and a 1-packet batch after it."""

@@ -1004,15 +1004,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
 // 1 M x 64 B 0.0157 ms against the compacting path's 0.0174; long packets
 // cost it 7-9 % against the one-shot wave kernel (a wave then lives for 16
 // groups), so the cost model sends long-dominated batches there.
+template <bool kConsec>
 __global__ __launch_bounds__(256) void verify_walk_kernel(VerifyParams p) {
     const uint32_t lane = lane_id();
     const uint64_t G = (uint64_t)gridDim.x * 4u;
     const uint64_t w = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
-#ifdef WG_WALK_CONSEC
-    const uint64_t i = w * 64u + lane;  // experiment: a wave's 64 descriptors consecutive
-#else
-    const uint64_t i = ((uint64_t)(lane >> 2) * G + w) * 4u + (lane & 3u);
-#endif
+    const uint64_t i = kConsec ? w * 64u + lane : ((uint64_t)(lane >> 2) * G + w) * 4u + (lane & 3u);
     const bool live = i < p.n;
     const v4u dv = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * (live ? i : 0u));
     const uint32_t len = live ? dv.z : 0u;
@@ -1047,11 +1044,7 @@ __global__ __launch_bounds__(256) void verify_walk_kernel(VerifyParams p) {
     // the index recomputed from a laundered lane id (held across the walk it spilled)
     uint32_t l2 = lane_id();
     asm volatile("" : "+v"(l2));
-#ifdef WG_WALK_CONSEC
-    const uint64_t i2 = w * 64u + l2;
-#else
-    const uint64_t i2 = ((uint64_t)(l2 >> 2) * G + w) * 4u + (l2 & 3u);
-#endif
+    const uint64_t i2 = kConsec ? w * 64u + l2 : ((uint64_t)(l2 >> 2) * G + w) * 4u + (l2 & 3u);
     if (i2 < p.n) {
         p.verdict[i2] = (uint8_t)r;
         if (p.l4)
@@ -1260,13 +1253,21 @@ static bool verify_pick_compact(uint64_t n, uint32_t smp, uint32_t lb, uint32_t 
 
 enum VerifyPath { kPathWave, kPathCompact, kPathWalk };
 
-static int verify_launch_walk(const VerifyParams &p, hipStream_t st) {
+// consec: each wave's 64 descriptors consecutive — for batches sampled all
+// small (1 M x 64 B 0.0145 vs 0.0153 ms: each lane-load instruction of a
+// wave covers one 4-KiB run of packets); otherwise sixteen 4-descriptor
+// groups a sixteenth of the batch apart (long packets walked: 0.2707 vs
+// 0.2772 ms on 1 M x 1500 B), profiles/r05_walk_layout_ab.txt
+static int verify_launch_walk(const VerifyParams &p, hipStream_t st, bool consec = false) {
     uint64_t blocks = (p.n + 255) / 256;  // a wave per 64 descriptors
     if (blocks >= 8)
         blocks = (blocks + 7) & ~7ull;
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
-    hipLaunchKernelGGL(verify_walk_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p);
+    if (consec)
+        hipLaunchKernelGGL(verify_walk_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, p);
+    else
+        hipLaunchKernelGGL(verify_walk_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, p);
     return hipGetLastError() == hipSuccess ? WG_OK : WG_ERR_LAUNCH;
 }
 
@@ -1341,7 +1342,8 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
                 return rc;
             path = kPathWalk;  // no entry lists for this batch: a stateless kernel instead
         }
-        return path == kPathWalk ? verify_launch_walk(p, st) : verify_launch_wave(p, st);
+        // all small by the sample: the consecutive walking layout
+        return path == kPathWalk ? verify_launch_walk(p, st, known && smp == 64u) : verify_launch_wave(p, st);
     }
     return verify_launch_wave(p, st);  // verify_small = 0: the wave kernel
 }
