@@ -37,7 +37,7 @@ STEP_KERNELS = {
     "config4small": ["l4csum_split_kernel"],
     "config5": ["l4csum_split_kernel"],
     "verify": ["verify_kernel<"],
-    "verify64d": ["verify_walk_kernel", "verify_compact"],  # all-small batches: the walking kernel
+    "verify64d": ["verify_walk_kernel<true>"],  # all-small batches: the walking kernel, consecutive layout (the spread one runs only on the first calls)
     "verify64": ["verify_"],
     "verify1500u": ["verify_"],
     "gro": ["gro_finalize"],
