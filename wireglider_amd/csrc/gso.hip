@@ -387,9 +387,9 @@ __device__ __forceinline__ void seg_done(const Ctx &c, uintptr_t out_base, const
 // template bytes, field codes) again: G = 3 x W = 4 measured best.
 // S = segments per wave step: 0 one at a time (occupancy hides latency),
 // 1 ping-pong pipeline (the next segment's loads in flight while this one
-// finishes), 2-4 that many issued then all finished (4, the default: with 3
-// groups of 4 waves a 45-segment super-buffer's wave sends all its ~4
-// segments' loads out at once).
+// finishes), 2-4 that many, a slot stride apart, issued then all finished (4,
+// the default: with 3 groups of 4 waves a 45-segment super-buffer's wave
+// sends all its ~4 segments' loads out at once).
 template <int W, int S, int Abl>
 __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
     constexpr uint32_t kStep = S ? S : 1;
@@ -412,11 +412,7 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
         asm volatile("" ::"s"(pr.w[0]), "s"(pr.w[1]), "s"(pr.w[2]), "s"(pr.w[3]), "s"(pr.w[4]), "s"(pr.w[5]),
                      "s"(dr.w[0]), "s"(dr.w[1]), "s"(dr.w[2]), "s"(dr.w[3]), "s"(dr.w[4]));
         const uint32_t kind = (pr.w[1] >> 16) & 0xffu, nseg = pr.w[2] >> 16;
-#ifdef WG_GSO_SPREAD
-        if (!(kind & kPlanSplit) || (S >= 2 ? gw : gw * kStep) >= nseg)
-#else
-        if (!(kind & kPlanSplit) || gw * kStep >= nseg)
-#endif
+        if (!(kind & kPlanSplit) || gw >= nseg)
             continue;  // passthrough / error (in-place work: gso_finalize_kernel) or no segment for this slot
         if constexpr (Abl & kHdrOnly) {
             if (p.synth && syn_eligible(pr.w[0] & 0xffffu, pr.w[0] >> 16, pr.w[1] & 0xffffu)) {
@@ -495,9 +491,9 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
         } else {
             c.hc0 = hdr_code(c, lane);
             c.hc1 = hdr_code(c, lane + 64);
-#ifdef WG_GSO_SPREAD
-            // experiment: the wave's S segments a slot stride apart (gw, gw +
-            // G W, ...) instead of consecutive
+            // the wave's S segments a slot stride apart (gw, gw + G W, ...):
+            // config 3 -0.85 %, UDP_L4 -0.73 % against S consecutive ones
+            // (profiles/r05_gso/ab_spread_segments.txt)
             const uint32_t sstr = gstride / S;
             for (uint32_t i0 = gw; i0 < c.nseg; i0 += gstride) {
                 SegFront f[S];
@@ -509,18 +505,6 @@ __global__ __launch_bounds__(64 * W) void gso_split_kernel(GsoParams p) {
                     if (i0 + k * sstr < c.nseg)
                         seg_done<Abl>(c, out_base, f[k], lane);
             }
-#else
-            for (uint32_t i0 = gw * S; i0 < c.nseg; i0 += gstride) {
-                SegFront f[S];
-#pragma unroll
-                for (int k = 0; k < S; k++)
-                    seg_go<Abl>(c, out_base, i0 + k < c.nseg ? i0 + k : c.nseg - 1, lane, f[k]);
-#pragma unroll
-                for (int k = 0; k < S; k++)
-                    if (i0 + k < c.nseg)
-                        seg_done<Abl>(c, out_base, f[k], lane);
-            }
-#endif
         }
     }
 }
