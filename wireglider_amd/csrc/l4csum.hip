@@ -123,18 +123,10 @@ __global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
                     g[j] = load_geom<kKind>(p, i0 + j);
             }
         }
-#ifdef WG_L4_SPREAD
-        // experiment (uniform batches): the block's 4 P packets dealt to its
-        // waves round robin — wave k takes packets k, k + 4, ... of the block
-        const uint64_t bb = i0 - (uint64_t)wave_in_block() * P;
-        auto pidx = [&](uint32_t j) -> uint64_t { return bb + wave_in_block() + 4u * j; };
-#else
-        auto pidx = [&](uint32_t j) -> uint64_t { return i0 + j; };
-#endif
 #pragma unroll
         for (int j = 0; j < P; j++) {
             if constexpr (DM == 0)
-                g[j] = load_geom<kKind>(p, pidx(j));
+                g[j] = load_geom<kKind>(p, i0 + j);
             issue<kL4, kNT>(g[j], lane, f[j]);
         }
         if constexpr (DM == 2) {  // next iteration's descriptors, in flight during the finish
@@ -156,13 +148,8 @@ __global__ __launch_bounds__(256) void l4csum_kernel(L4Params p) {
             if (lane == (uint32_t)j)
                 res = r;
         }
-        if constexpr (DM == 0) {
-            if (lane < (uint32_t)P && pidx(lane) < p.n)
-                p.out[pidx(lane)] = (uint16_t)res;
-        } else {
-            if (lane < (uint32_t)P && i0 + lane < p.n)
-                p.out[i0 + lane] = (uint16_t)res;
-        }
+        if (lane < (uint32_t)P && i0 + lane < p.n)
+            p.out[i0 + lane] = (uint16_t)res;
     }
 }
 
