@@ -472,7 +472,9 @@ int wg_device_count(void);
  *                (8 .. 65536; the grid follows the expected long packets)
  *   "host_chunk_mb" host-memory pipeline chunk size in MiB (1 .. 4096)
  *   "host_d2h"   host pipeline downloads into pinned memory by a store
- *                kernel: bit 1 encap messages (default), bit 2 decap plaintext
+ *                kernel (0-7): bit 1 encap messages, bit 2 every decap
+ *                plaintext chunk, bit 4 decap plaintext chunks under 24 MiB
+ *                (default 5 = bits 1 and 4; 0: the runtime's copies always)
  *   "aead_k"     AEAD kernels: consecutive ChaCha20 blocks per lane (2, 3;
  *                0 = 2 or 3, whichever fills a wave better for the batch)
  *   "aead_stage" AEAD encrypt: each wave assembles its messages in LDS and

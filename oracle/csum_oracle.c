@@ -279,6 +279,7 @@ typedef struct {
     const orc_gso_desc *sdesc;
     int8_t *status;
     uint64_t lo, hi;
+    uint64_t acc; /* kind 7 (read probe): the words' sum, kept live */
 } job_t;
 
 static void run_job(job_t *j) {
@@ -300,6 +301,18 @@ static void run_job(job_t *j) {
         } else if (j->kind == 3) {
             const orc_pkt_desc *d = &j->desc[i];
             j->verdict[i] = orc_verify(j->base + d->offset, d->len, j->out ? &j->out[i] : NULL);
+        } else if (j->kind == 7) {
+            /* read probe: 64-bit words of 4-KiB block i (vectorised by the
+             * compiler: the memory path of these CPUs, no checksum work) */
+            const uint64_t *w = (const uint64_t *)(j->base + i * 4096u);
+            uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+            for (int k = 0; k < 512; k += 4) {
+                a0 += w[k];
+                a1 += w[k + 1];
+                a2 += w[k + 2];
+                a3 += w[k + 3];
+            }
+            j->acc += a0 + a1 + a2 + a3;
         } else if (j->kind == 5) {
             const orc_gso_desc *d = &j->sdesc[i];
             orc_vnet_hdr v = d->vnet;
@@ -343,6 +356,16 @@ typedef struct {
     unsigned long seen;  /* pool.gen when the worker was made: it runs the calls after that */
 } worker_arg;
 static worker_arg pool_args[ORC_MAX_THREADS];
+/* Per-worker busy time and calls since the last orc_pool_stats_reset (the
+ * CPU baseline's per-worker rates: a worker's share of the bytes over its own
+ * busy time, so a slow CPU or a straggler shows against the others). */
+static uint64_t pool_busy_ns[ORC_MAX_THREADS], pool_calls[ORC_MAX_THREADS];
+
+static uint64_t mono_ns(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
 
 static void *pool_worker(void *arg) {
     const int idx = ((worker_arg *)arg)->idx;
@@ -356,8 +379,12 @@ static void *pool_worker(void *arg) {
         seen = pool.gen;
         job_t *j = &pool.jobs[idx];
         pthread_mutex_unlock(&pool.mu);
+        const uint64_t t0 = mono_ns();
         run_job(j);
+        const uint64_t t1 = mono_ns();
         pthread_mutex_lock(&pool.mu);
+        pool_busy_ns[idx] += t1 - t0;
+        pool_calls[idx]++;
         if (--pool.pending == 0)
             pthread_cond_signal(&pool.done);
     }
@@ -378,7 +405,7 @@ static void pool_stop(void) {
     pool.stop = 0;
 }
 
-static void run_parallel(job_t proto, uint64_t n, int threads) {
+static void run_parallel_acc(job_t proto, uint64_t n, int threads, uint64_t *acc) {
     if (threads < 1)
         threads = 1;
     if (threads > ORC_MAX_THREADS)
@@ -389,6 +416,8 @@ static void run_parallel(job_t proto, uint64_t n, int threads) {
         proto.lo = 0;
         proto.hi = n;
         run_job(&proto);
+        if (acc)
+            *acc += proto.acc;
         return;
     }
     job_t jobs[ORC_MAX_THREADS];
@@ -420,8 +449,11 @@ static void run_parallel(job_t proto, uint64_t n, int threads) {
         if (made != threads) {  /* no pool: run here */
             pool_stop();
             pthread_mutex_unlock(&pool_mu);
-            for (int t = 0; t < threads; t++)
+            for (int t = 0; t < threads; t++) {
                 run_job(&jobs[t]);
+                if (acc)
+                    *acc += jobs[t].acc;
+            }
             return;
         }
     }
@@ -434,7 +466,12 @@ static void run_parallel(job_t proto, uint64_t n, int threads) {
         pthread_cond_wait(&pool.done, &pool.mu);
     pthread_mutex_unlock(&pool.mu);
     pthread_mutex_unlock(&pool_mu);
+    if (acc)
+        for (int t = 0; t < threads; t++)
+            *acc += jobs[t].acc;
 }
+
+static void run_parallel(job_t proto, uint64_t n, int threads) { run_parallel_acc(proto, n, threads, NULL); }
 
 void orc_l4_uniform(const uint8_t *base, uint64_t total_len, uint32_t segment_size,
                     uint16_t csum_start, uint32_t flags, uint16_t *out, int threads) {
@@ -501,6 +538,34 @@ void orc_gso_split_desc(uint8_t *in_base, const orc_gso_desc *desc, uint64_t n, 
     j.sdesc = desc;
     j.status = status;
     run_parallel(j, n, threads);
+}
+
+void orc_pool_stats_reset(void) {
+    pthread_mutex_lock(&pool.mu);
+    memset(pool_busy_ns, 0, sizeof pool_busy_ns);
+    memset(pool_calls, 0, sizeof pool_calls);
+    pthread_mutex_unlock(&pool.mu);
+}
+
+int orc_pool_stats(uint64_t *busy_ns, uint64_t *calls, int max) {
+    pthread_mutex_lock(&pool.mu);
+    const int n = pool.threads < max ? pool.threads : max;
+    for (int t = 0; t < n; t++) {
+        busy_ns[t] = pool_busy_ns[t];
+        calls[t] = pool_calls[t];
+    }
+    pthread_mutex_unlock(&pool.mu);
+    return n;
+}
+
+uint64_t orc_read_probe(const uint8_t *base, uint64_t nbytes, int threads) {
+    job_t j = {0};
+    j.kind = 7;
+    j.base = base;
+    const uint64_t n = nbytes / 4096u;
+    uint64_t acc = 0;
+    run_parallel_acc(j, n, threads, &acc);
+    return acc;
 }
 
 double orc_time_l4_uniform(const uint8_t *base, uint64_t total_len, uint32_t segment_size,

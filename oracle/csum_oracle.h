@@ -181,6 +181,14 @@ double orc_time_l4_uniform(const uint8_t *base, uint64_t total_len, uint32_t seg
                            uint16_t csum_start, uint32_t flags, uint16_t *out, int threads,
                            int reps);
 
+/* The CPU baseline's placement evidence: per-worker busy nanoseconds and
+ * calls of the persistent pool since the last reset (returns the worker
+ * count), and a read-only probe over [base, base + nbytes) (4-KiB blocks, 64-bit
+ * word sums) on the same pinned workers. */
+void orc_pool_stats_reset(void);
+int orc_pool_stats(uint64_t *busy_ns, uint64_t *calls, int max);
+uint64_t orc_read_probe(const uint8_t *base, uint64_t nbytes, int threads);
+
 #ifdef __cplusplus
 }
 #endif

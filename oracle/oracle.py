@@ -103,6 +103,12 @@ def _load():
     lib.orc_wg_encrypt_batch_mt.argtypes = [vp, u32, u64, vp, u64, u32, vp, i32]
     lib.orc_wg_decrypt_batch_mt.restype = None
     lib.orc_wg_decrypt_batch_mt.argtypes = [vp, vp, u64, u32, vp, vp, i32]
+    lib.orc_pool_stats_reset.restype = None
+    lib.orc_pool_stats_reset.argtypes = []
+    lib.orc_pool_stats.restype = i32
+    lib.orc_pool_stats.argtypes = [vp, vp, i32]
+    lib.orc_read_probe.restype = u64
+    lib.orc_read_probe.argtypes = [vp, u64, i32]
     lib.orc_time_l4_uniform.restype = ctypes.c_double
     lib.orc_time_l4_uniform.argtypes = [vp, u64, u32, u16, u32, vp, i32, i32]
     return lib
@@ -172,28 +178,75 @@ def _core_of(c: int):
         return (0, c)
 
 
+def _l3_of(c: int) -> str:
+    """The L3 domain of CPU c: the first CPU of its L3's shared_cpu_list
+    (EPYC: one CCD), or "?" where sysfs does not say."""
+    try:
+        lst = Path(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list").read_text().strip()
+        return lst.split(",")[0].split("-")[0]
+    except Exception:
+        return "?"
+
+
 def quiet_cpus(n: int) -> dict:
-    """The n least busy CPUs of the affinity mask, one per physical core
-    while there are enough cores (a CPU share of a shared host: the workers
-    go where the neighbours are not).  Returns {"cpus": [...], "busy": mean
-    busy fraction of the chosen CPUs before the run}."""
+    """n CPUs of the affinity mask for n pinned workers, spread over the L3
+    domains (CCDs): one physical core per worker, the domains dealt round
+    robin (quietest domain first), the quietest CPUs first within a domain.
+    A 16-worker leg then spans 16 CCDs instead of the 2-4 CCDs that the lowest
+    CPU numbers of an idle host give (the all-core leg
+    on CPUs 1-30, four CCDs, ran 3.2x one core).  Returns {"cpus": [...],
+    "busy": mean busy fraction of the chosen CPUs before the run, "l3_domains":
+    {domain: [cpus]} of the chosen CPUs}."""
     cpus = sorted(os.sched_getaffinity(0))
     busy = _cpu_busy(cpus)
-    order = sorted(cpus, key=lambda c: (busy.get(c, 1.0), c))
-    chosen, cores = [], set()
-    for c in order:
+    doms: dict = {}
+    seen_cores = set()
+    for c in sorted(cpus, key=lambda c: (busy.get(c, 1.0), c)):
         k = _core_of(c)
-        if k not in cores:
-            chosen.append(c)
-            cores.add(k)
-        if len(chosen) == n:
-            break
-    for c in order:  # fewer cores than n: fill with the quietest remaining CPUs
+        if k in seen_cores:  # one CPU per physical core (SMT siblings left out)
+            continue
+        seen_cores.add(k)
+        doms.setdefault(_l3_of(c), []).append(c)
+    # the domains, quietest first (mean busy of their cores), then by number
+    order = sorted(doms, key=lambda d: (sum(busy.get(c, 1.0) for c in doms[d]) / len(doms[d]),
+                                        int(d) if d.isdigit() else 1 << 30))
+    chosen = []
+    depth = 0
+    while len(chosen) < n and any(depth < len(doms[d]) for d in order):
+        for d in order:
+            if depth < len(doms[d]) and len(chosen) < n:
+                chosen.append(doms[d][depth])
+        depth += 1
+    for c in sorted(cpus, key=lambda c: (busy.get(c, 1.0), c)):  # fewer cores than n: SMT siblings
         if len(chosen) == n:
             break
         if c not in chosen:
             chosen.append(c)
-    return {"cpus": chosen, "busy": round(sum(busy.get(c, 1.0) for c in chosen) / max(1, len(chosen)), 4)}
+    used: dict = {}
+    for c in chosen:
+        used.setdefault(_l3_of(c), []).append(c)
+    return {"cpus": chosen, "busy": round(sum(busy.get(c, 1.0) for c in chosen) / max(1, len(chosen)), 4),
+            "l3_domains": used}
+
+
+def pool_stats_reset() -> None:
+    lib.orc_pool_stats_reset()
+
+
+def pool_stats(max_workers: int = 256) -> list:
+    """[(busy_seconds, calls)] per worker of the persistent pool since the
+    last reset."""
+    busy = np.zeros(max_workers, np.uint64)
+    calls = np.zeros(max_workers, np.uint64)
+    n = int(lib.orc_pool_stats(busy.ctypes.data, calls.ctypes.data, max_workers))
+    return [(float(busy[t]) * 1e-9, int(calls[t])) for t in range(n)]
+
+
+def read_probe(buf, threads: int) -> int:
+    """Read-only pass over buf's whole 4-KiB blocks by `threads` pinned
+    workers (the CPU baseline's memory-path probe); returns the word sum."""
+    a = _u8(buf)
+    return int(lib.orc_read_probe(a.ctypes.data, a.size, threads))
 
 
 def cgroup_throttling() -> dict | None:

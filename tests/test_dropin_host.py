@@ -115,3 +115,17 @@ def test_percall_threads_count_and_scale(tmp_path):
         assert lat[f"threads_{t}"]["results"] == lat["threads_1"]["results"]
     # loose on a shared CI container; the tight bound is the GPU box's figure
     assert lat["threads_8"]["ns_per_call_1500B"] < 4 * lat["threads_1"]["ns_per_call_1500B"] + 200
+
+
+def test_percall_count_after_thread_exit(tmp_path):
+    """Calls made from a thread_local destructor that runs after the
+    library's per-thread slot owner is destroyed are counted
+    once each, into the exited threads' totals, and never touch the
+    destroyed owner."""
+    import json
+
+    exe = _build(tmp_path, "dropin_exit")
+    env = {k: v for k, v in os.environ.items() if k != "WG_PERCALL"}
+    r = subprocess.run([str(exe), "4", "100", "7"], capture_output=True, text=True, timeout=120, env=env, check=True)
+    got = json.loads(r.stdout)
+    assert got == {"threads": 4, "calls": 100, "exit_calls": 7, "gpu": 0, "fallback": 0, "host": 4 * 107}, got

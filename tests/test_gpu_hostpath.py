@@ -247,10 +247,12 @@ def test_decap_host_matches_oracle(gpu, small_chunks, verify):
     check_decap(key, msgs, stride, got)
 
 
-@pytest.mark.parametrize("mode", [1, 3])
+@pytest.mark.parametrize("mode", [0, 1, 3, 5])
 def test_decap_host_pinned_two_threads(gpu, small_chunks, d2h, mode):
-    """Two threads; one decrypts from and into pinned buffers (plaintext by the
-    store kernel when host_d2h = 3)."""
+    """Two threads; one decrypts from and into pinned buffers.  Plaintext by
+    the store kernel when host_d2h has bit 2 (3: every chunk) or bit 4 (5, the
+    default: chunks under 24 MiB, all of them here); by the runtime's copy
+    with neither (0, 1) — ADVICE r05: bit 2 was overridden for small chunks."""
     wga = _wga()
     d2h(mode)
     work = [decap_case(51, 2503, short=1), decap_case(52, 1999, S=1456, short=33)]

@@ -7,6 +7,13 @@
 set -u
 OUT=$1; R=$2; WS=$3; A=$4; B=$5
 : > "$OUT"
+HERE=$(pwd); OUTABS=$(realpath -m "$OUT")
+# each tree's GPU parity subset first, run in that tree against its own
+# library (AB_GSO=1: + GSO)
+for T in "$A" "$B"; do
+  (cd "$T" && "$HERE"/tools/ab_parity.sh "$OUTABS" "$(realpath "$T")/wireglider_amd/lib/libwireglider_amd.so" \
+     ${AB_GSO:+gso}) || exit 1
+done
 for r in $(seq "$R"); do
   for W in ${WS//,/ }; do
     for T in "$A" "$B"; do
@@ -16,9 +23,11 @@ for r in $(seq "$R"); do
   done
 done
 python3 - "$OUT" <<'PY'
-import json, sys, statistics, collections
+import json, os, sys, statistics, collections
 rows = [json.loads(l) for l in open(sys.argv[1])]
+par = {r["lib"].rsplit("/wireglider_amd/lib/", 1)[0]: r["parity"] for r in rows if "parity" in r}
+rows = [r for r in rows if "kernel_ms" in r]
 g = collections.defaultdict(list)
 for r in rows: g[(r["workload"], r["tree"])].append(r["kernel_ms"])
-for (w, t), v in sorted(g.items()): print(w, t, "median ms", round(statistics.median(v), 5), "all", v)
+for (w, t), v in sorted(g.items()): print(w, t, "parity", par.get(os.path.realpath(t), "not run"), "median ms", round(statistics.median(v), 5), "all", v)
 PY

@@ -94,6 +94,31 @@ def build_lib(verbose: bool = False, jobs: int = 8) -> Path:
     return lib
 
 
+HARNESSES = ["mt_batch"]  # tests/cpp/<name>.cpp -> tests/cpp/bin/<name> (test harnesses, not product)
+
+
+def build_harnesses(verbose: bool = False) -> list[Path]:
+    """The GPU test harnesses that drive the C ABI from several host threads
+    (tests/test_mt_batch.py), built here rather than inside a GPU test."""
+    hipcc = _hipcc()
+    lib = LIBDIR / LIBNAME
+    out = []
+    for name in HARNESSES:
+        src = ROOT / "tests" / "cpp" / f"{name}.cpp"
+        exe = ROOT / "tests" / "cpp" / "bin" / name
+        exe.parent.mkdir(parents=True, exist_ok=True)
+        if _needs(exe, [src, lib, ROOT / "include" / "wireglider_amd.h"]):
+            cmd = [hipcc, "-O2", "-std=c++20", f"--offload-arch={ARCH}", "-x", "hip", f"-I{ROOT / 'include'}", str(src),
+                   f"-L{LIBDIR}", "-lwireglider_amd", f"-Wl,-rpath,{LIBDIR}", "-lpthread", "-o", str(exe)]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"harness build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        out.append(exe)
+    return out
+
+
 def build_oracle(verbose: bool = False) -> None:
     """Build the CPU oracle (test infrastructure) and, when the reference is
     mounted, the reference-test golden driver into oracle/_ref/."""
@@ -113,6 +138,7 @@ def main() -> None:
     verbose = "-v" in sys.argv
     build_oracle(verbose)
     print(build_lib(verbose))
+    build_harnesses(verbose)
 
 
 if __name__ == "__main__":

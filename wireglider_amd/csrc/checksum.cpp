@@ -48,12 +48,19 @@ Registry &registry() {
     return *r;
 }
 
-// The calling thread's slot: a trivially initialised thread-local pointer
-// (initial-exec TLS: one load, no guard, no __tls_get_addr call per call),
+// The calling thread's slot: a trivially initialised thread-local pointer,
 // set on the thread's first call by registering a slot whose owner folds it
-// into `gone` when the thread exits.
+// into `gone` when the thread exits.  Default TLS model (the
+// initial-exec model draws on glibc's static-TLS surplus, which a library
+// loaded by dlopen — ctypes after torch — can find used up); the compiler
+// makes these local-dynamic accesses.
 struct SlotOwner;
-__attribute__((tls_model("initial-exec"))) thread_local Slot *t_slot = nullptr;
+thread_local Slot *t_slot = nullptr;
+// Set by ~SlotOwner: a call made later in the thread's exit (from another
+// thread_local's destructor) must not re-register through the destroyed
+// owner; it is counted straight into `gone` instead.  Trivially destructible,
+// so it stays readable through every TLS destructor.
+thread_local bool t_exited = false;
 
 struct SlotOwner {
     Slot slot;
@@ -64,6 +71,7 @@ struct SlotOwner {
     }
     ~SlotOwner() {
         t_slot = nullptr;
+        t_exited = true;
         Registry &r = registry();
         std::lock_guard<std::mutex> g(r.mu);
         r.gone[0] += slot.gpu.load(std::memory_order_relaxed);
@@ -78,21 +86,36 @@ struct SlotOwner {
 };
 
 __attribute__((noinline)) Slot *register_slot() {
+    if (t_exited)
+        return nullptr;  // the thread's owner is gone: the caller counts into `gone`
     thread_local SlotOwner owner;
     t_slot = &owner.slot;
     return t_slot;
 }
 
-inline Slot &my_slot() {
-    Slot *s = t_slot;
-    if (__builtin_expect(s == nullptr, 0))
-        s = register_slot();
-    return *s;
+enum Placement { kGpu = 0, kFallback = 1, kHost = 2 };
+
+__attribute__((noinline)) void count_exited(Placement which) {
+    Registry &r = registry();
+    std::lock_guard<std::mutex> g(r.mu);
+    r.gone[which]++;
 }
 
 // Owner-only increment: a load and a store, no locked read-modify-write.
 inline void bump(std::atomic<uint64_t> &c) {
     c.store(c.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
+}
+
+inline void count(Placement which) {
+    Slot *s = t_slot;
+    if (__builtin_expect(s == nullptr, 0)) {
+        s = register_slot();
+        if (!s) {
+            count_exited(which);
+            return;
+        }
+    }
+    bump(which == kGpu ? s->gpu : which == kFallback ? s->fallback : s->host);
 }
 
 bool percall_gpu() {
@@ -106,18 +129,17 @@ bool percall_gpu() {
 }  // namespace
 
 uint16_t calc_l4_checksum(std::span<const uint8_t> ippkt, bool isv6, bool istcp, uint16_t csum_start) {
-    Slot &s = my_slot();
     if (percall_gpu() && !ippkt.empty()) {
         uint16_t out = 0;
         const int rc = wg_l4csum_uniform_host(ippkt.data(), ippkt.size(), static_cast<uint32_t>(ippkt.size()),
                                               csum_start, (isv6 ? WG_PKT_V6 : 0u) | (istcp ? WG_PKT_TCP : 0u), &out);
         if (rc == WG_OK) {
-            bump(s.gpu);
+            count(kGpu);
             return out;
         }
-        bump(s.fallback);
+        count(kFallback);
     } else {
-        bump(s.host);
+        count(kHost);
     }
     return host::calc_l4_checksum(ippkt, isv6, istcp, csum_start);
 }

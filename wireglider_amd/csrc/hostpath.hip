@@ -454,9 +454,12 @@ extern "C" int wg_decap_host(const uint8_t *host_msgs, uint64_t total_len, uint3
         // plaintext: the runtime's copy (faster from ~32 MiB up), the store
         // kernel under 24 MiB — the runtime's copies of 16-MiB chunks ran at a
         // third of the link beside the uploads (109 vs 34 ms a call,
-        // profiles/r05_hostpath/chunk_sweep.jsonl)
+        // profiles/r05_hostpath/chunk_sweep.jsonl).  Knob host_d2h: bit 2 the
+        // store kernel for every plaintext chunk, bit 4 (default) for chunks
+        // under 24 MiB; neither: the runtime's copy always.
+        const bool small_chunk = m * pstride < (24ull << 20) && (tune().host_d2h & 4u);
         WG_TRY(d2h_big(c, 2u, host_plain + first * pstride, plain_alias ? plain_alias + first * pstride : nullptr,
-                       dp(c, slot, kPlain), m * pstride, m * pstride < (24ull << 20)));
+                       dp(c, slot, kPlain), m * pstride, small_chunk));
         WG_TRY(f.end(slot));
     }
     WG_TRY(f.drain());

@@ -26,7 +26,7 @@ struct Tune {
     uint32_t verify_auto_t;  // verify_small = 7: compacting path when >= this many of 64 sampled packets are small
     uint32_t verify_k2min;   // compacting path: minimum blocks of the long kernel
     uint32_t host_chunk_mb;  // host-memory pipeline chunk size, MiB
-    uint32_t host_d2h;    // host pipeline downloads into pinned memory by a store kernel (bit 1 encap messages, bit 2 decap plaintext)
+    uint32_t host_d2h;    // host pipeline downloads into pinned memory by a store kernel (bit 1 encap messages, bit 2 every decap plaintext chunk, bit 4 decap plaintext chunks < 24 MiB)
     uint32_t l4_unroll;   // split kernel: loads in flight per lane on a long packet's rest (4, 8)
     uint64_t l4_coop;     // descriptor batches of n <= l4_coop: a block of l4_coop_waves waves per packet (0: never)
     uint32_t l4_coop_waves;  // waves per packet in that mode (2, 4, 8, 16)
@@ -37,8 +37,9 @@ struct Tune {
     uint32_t gso_ablate;  // GSO A/B variants (1 non-temporal stores, 32 no XCD swizzle; both correct)
 };
 
-// A snapshot of the knobs (copied under the knob mutex: wg_tune_set may run
-// concurrently on another host thread).
+// A snapshot of the knobs: a copy of the current immutable table, read
+// lock-free (wg_tune_set may run concurrently on another host thread and
+// publishes a new table; capi.hip).
 Tune tune();
 
 // Debugging aid: with WG_DEBUG_SYNC=1 in the environment, synchronise the
