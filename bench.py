@@ -1224,6 +1224,13 @@ def _read_probe_rate(oracle, buf, threads: int, seconds: float = 1.0) -> dict:
     return {"GiB_s": round(best * 2.0**-30, 3), "threads": threads, "bytes": int(buf.size)}
 
 
+def oracle_numa(c):
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle  # test infrastructure: the CPU baseline leg only
+
+    return oracle.numa_of(c)
+
+
 def _placement_evidence(quiet, cpus_all, workers, nbytes, scale, unit, all_s, one_s, read_all, read_one,
                         buf) -> dict:
     """where the all-core leg's CPUs sit (L3
@@ -1237,7 +1244,8 @@ def _placement_evidence(quiet, cpus_all, workers, nbytes, scale, unit, all_s, on
         rates = [round(share * c / b * scale, 3) if b > 0 else None for b, c in workers]
         good = [r for r in rates if r]
         out["per_worker"] = {
-            "cpus": cpus_all, "rate": rates, "unit": unit, "busy_s": [round(b, 3) for b, _ in workers],
+            "cpus": cpus_all, "numa_node": [oracle_numa(c) for c in cpus_all] if cpus_all else None,
+            "rate": rates, "unit": unit, "busy_s": [round(b, 3) for b, _ in workers],
             "calls": [c for _, c in workers],
             "min_over_max": round(min(good) / max(good), 4) if good else None,
             "note": "worker t's equal share of the sample's bytes per call x its calls / its own busy time in "

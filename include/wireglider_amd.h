@@ -10,8 +10,11 @@
  *
  * Ownership follows the reference: every buffer is borrowed
  * from the caller; nothing is allocated per call; entry points are
- * reentrant and may be called from several host threads on different
- * streams.  Launches are asynchronous on `stream`.
+ * reentrant and may be called from several host threads at once, on their
+ * own streams, on hipStreamPerThread, or on the shared NULL stream
+ * (tests/test_mt_batch.py: 1-16 threads, every result against the oracle).
+ * No process-wide lock is taken per launch.  Launches are asynchronous on
+ * `stream`.
  *
  * Error convention: the reference has no error channel (checksum.cpp:8-36
  * returns the checksum only).  Here a negative return is a launch/argument
@@ -457,8 +460,9 @@ int wg_device_count(void);
  *   "encap_parts" wg_encap_batch in slices, each split on a side stream under
  *                the previous slice's AEAD (1 = not pipelined, default; 2-8)
  *   "verify_small" wg_verify_desc kernels: 7 (default) = per call, from the
- *                size mix the previous call on the same (device, stream)
- *                sampled: the walking kernel (8) on the stream's first call
+ *                size mix the previous call on the same stream (per thread
+ *                for hipStreamPerThread) sampled: the walking kernel (8) on
+ *                the stream's first call
  *                and when all 64 sampled packets are <= 64 B, else the
  *                cheaper of the wave kernel (0) and the compacting path (6)
  *                by a cost model; calls under stream capture take a

@@ -229,6 +229,17 @@ def quiet_cpus(n: int) -> dict:
             "l3_domains": used}
 
 
+def numa_of(c: int):
+    """The NUMA node of CPU c (sysfs nodeN link), or None."""
+    try:
+        for e in Path(f"/sys/devices/system/cpu/cpu{c}").iterdir():
+            if e.name.startswith("node") and e.name[4:].isdigit():
+                return int(e.name[4:])
+    except Exception:
+        pass
+    return None
+
+
 def pool_stats_reset() -> None:
     lib.orc_pool_stats_reset()
 

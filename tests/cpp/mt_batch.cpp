@@ -11,10 +11,12 @@
 //   mt_batch <dir> conform <threads> <iters> <own|perthread|legacy|churn>
 //       every call's outputs (refilled with a sentinel on the stream before
 //       the call) compared with the expected files; JSON with mismatch counts
-//   mt_batch <dir> rate <threads> <calls>
+//   mt_batch <dir> rate <threads> <calls> [small]
 //       per entry point, every thread enqueues <calls> calls back to back on
 //       its own stream: host calls/s per thread, plus the HIP runtime's own
-//       floor (an empty kernel launched the same way)
+//       floor (an empty kernel launched the same way); `small`: 64-packet
+//       batches (2 super-buffers for the split), so the device keeps up and
+//       the figure is the host launch path, not the queues' back-pressure
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -148,20 +150,24 @@ const char *op_name[kNumOps] = {"wg_verify_desc", "wg_l4csum_desc", "wg_l4csum_u
 const int kVerifyPattern[] = {2, 2, 2, 0, 1, 2, 2, 0, 0, 1, 1, 2, 2, 2};
 constexpr int kPat = sizeof(kVerifyPattern) / sizeof(kVerifyPattern[0]);
 
-int call(Op op, const Inputs &in, Outs &o, int vk, hipStream_t st) {
+// small: the first 64 packets / segments (2 super-buffers for the split), so
+// a call's device time stays below its host time (rate mode)
+int call(Op op, const Inputs &in, Outs &o, int vk, hipStream_t st, bool small = false) {
+    const auto cut = [small](uint64_t n, uint64_t k) { return small && n > k ? k : n; };
     switch (op) {
     case kVerify:
         return wg_verify_desc(static_cast<const uint8_t *>(in.vbuf[vk].p), static_cast<const wg_pkt_desc *>(in.vdesc[vk].p),
-                              in.vn[vk], static_cast<uint8_t *>(o.verdict.p), static_cast<uint16_t *>(o.l4.p), st);
+                              cut(in.vn[vk], 64), static_cast<uint8_t *>(o.verdict.p), static_cast<uint16_t *>(o.l4.p), st);
     case kL4Desc:
         return wg_l4csum_desc(static_cast<const uint8_t *>(in.l4d_buf.p), static_cast<const wg_pkt_desc *>(in.l4d_desc.p),
-                              in.l4d_n, static_cast<uint16_t *>(o.l4d.p), st);
+                              cut(in.l4d_n, 64), static_cast<uint16_t *>(o.l4d.p), st);
     case kL4Uniform:
-        return wg_l4csum_uniform(static_cast<const uint8_t *>(in.l4u_buf.p), in.l4u_buf.n, in.l4u_seg,
-                                 (uint16_t)in.l4u_cs, in.l4u_flags, static_cast<uint16_t *>(o.l4u.p), st);
+        return wg_l4csum_uniform(static_cast<const uint8_t *>(in.l4u_buf.p), cut(in.l4u_buf.n, 64ull * in.l4u_seg),
+                                 in.l4u_seg, (uint16_t)in.l4u_cs, in.l4u_flags, static_cast<uint16_t *>(o.l4u.p), st);
     case kGso:
-        return wg_gso_split(static_cast<uint8_t *>(o.gso_in.p), static_cast<const wg_gso_desc *>(in.gso_desc.p), in.gso_n,
-                            static_cast<uint8_t *>(o.gso_out.p), static_cast<wg_gso_result *>(o.gso_res.p), st);
+        return wg_gso_split(static_cast<uint8_t *>(o.gso_in.p), static_cast<const wg_gso_desc *>(in.gso_desc.p),
+                            cut(in.gso_n, 2), static_cast<uint8_t *>(o.gso_out.p), static_cast<wg_gso_result *>(o.gso_res.p),
+                            st);
     default:
         return WG_ERR_INVALID;
     }
@@ -300,8 +306,9 @@ __global__ void empty_kernel(uint32_t *p) {
 
 double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 
-int rate(const Inputs &in, int threads, int ncalls) {
-    std::printf("{\"mode\": \"rate\", \"threads\": %d, \"calls_per_thread\": %d, \"ops\": {", threads, ncalls);
+int rate(const Inputs &in, int threads, int ncalls, bool small) {
+    std::printf("{\"mode\": \"rate\", \"batches\": \"%s\", \"threads\": %d, \"calls_per_thread\": %d, \"ops\": {",
+                small ? "small (64 packets / 64 segments / 2 super-buffers)" : "full", threads, ncalls);
     for (int op = 0; op <= kNumOps; op++) {  // kNumOps: the runtime's empty-kernel floor
         std::vector<double> enq(threads), done(threads);
         std::barrier sync_point(threads);
@@ -318,7 +325,7 @@ int rate(const Inputs &in, int threads, int ncalls) {
                 for (int i = 0; i < 8; i++) {
                     if (op == kNumOps)
                         hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, st, nullptr);
-                    else if (call((Op)op, in, o, 2, st) != WG_OK)
+                    else if (call((Op)op, in, o, 2, st, small) != WG_OK)
                         errors++;
                 }
                 CK(hipStreamSynchronize(st));
@@ -327,7 +334,7 @@ int rate(const Inputs &in, int threads, int ncalls) {
                 for (int i = 0; i < ncalls; i++) {
                     if (op == kNumOps)
                         hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, st, nullptr);
-                    else if (call((Op)op, in, o, 2, st) != WG_OK)
+                    else if (call((Op)op, in, o, 2, st, small) != WG_OK)
                         errors++;
                 }
                 const double t1 = now_s();
@@ -371,7 +378,7 @@ int main(int argc, char **argv) {
     if (mode == "conform" && argc >= 6)
         rc = conform(in, threads, std::atoi(argv[4]), argv[5]);
     else if (mode == "rate")
-        rc = rate(in, threads, std::atoi(argv[4]));
+        rc = rate(in, threads, std::atoi(argv[4]), argc >= 6 && std::string(argv[5]) == "small");
     CK(hipDeviceSynchronize());
     return rc;
 }

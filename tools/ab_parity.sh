@@ -11,7 +11,10 @@ TESTS=${AB_PARITY_TESTS:-"tests/test_gpu_l4.py tests/test_gpu_golden_l4.py"}
 [ "$KIND" = gso ] && [ -z "${AB_PARITY_TESTS:-}" ] && TESTS="$TESTS tests/test_gpu_gso.py"
 LOG=$(mktemp)
 # shellcheck disable=SC2086
-WG_LIB=$L timeout -k 10 900 python3 -m pytest $TESTS -q -m gpu --timeout 120 --timeout-method thread >"$LOG" 2>&1
+# WG_LIB for the Python binding; LD_LIBRARY_PATH for the C++ harnesses
+# (tests/cpp/bin/*: their RUNPATH comes after it)
+WG_LIB=$L LD_LIBRARY_PATH="$(dirname "$(realpath "$L")")${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH}" \
+  timeout -k 10 900 python3 -m pytest $TESTS -q -m gpu --timeout 120 --timeout-method thread >"$LOG" 2>&1
 RC=$?
 python3 - "$OUT" "$L" "$RC" "$TESTS" "$LOG" <<'PY'
 import json, sys

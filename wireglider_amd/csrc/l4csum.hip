@@ -15,12 +15,10 @@
 // flight before the first wait, which is what an HBM-bound stream needs.
 // No LDS: every byte is used exactly once; staging it would only add LDS
 // traffic.
-#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <atomic>
-#include <chrono>
 #include <cstdio>
 #include <mutex>
 
@@ -1020,6 +1018,22 @@ __global__ __launch_bounds__(256) void verify_walk_kernel(VerifyParams p) {
     const uint32_t olo = live ? dv.x : 0u, ohi = live ? dv.y : 0u;
     const bool small = live && len <= kSmallMax;
     uint32_t rv = 0, rc = 0;
+#ifdef WG_WALK_PF
+    // experiment: the descriptors of the wave that will run in this one's
+    // slot in the second half of the grid, touched now (same XCD: the
+    // hardware block index differs by a multiple of 8), so that wave finds
+    // them in L2; the value feeds a store that never happens
+    v4u pf{0, 0, 0, 0};
+    if constexpr (kConsec) {
+        const uint32_t half = gridDim.x >> 1;
+        if ((half & 7u) == 0 && blockIdx.x < half) {
+            const uint64_t w2 = (uint64_t)xcd_swizzle(blockIdx.x + half, gridDim.x) * 4u + wave_in_block();
+            const uint64_t i2 = w2 * 64u + lane;
+            if (i2 < p.n)
+                pf = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * i2);
+        }
+    }
+#endif
     if (__ballot(small))  // wave-uniform
         verify_lane(reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)ohi << 32) | olo), small ? len : 0u, small, rv,
                     rc);
@@ -1056,6 +1070,9 @@ __global__ __launch_bounds__(256) void verify_walk_kernel(VerifyParams p) {
     }
     if (p.sample && blockIdx.x == 0 && wave_in_block() == 0)
         verify_sample(p, l2);
+#ifdef WG_WALK_PF
+    asm volatile("" ::"v"(pf.x));  // keeps the touch (its wait lands here, at the wave's end)
+#endif
 }
 
 }  // namespace wg
@@ -1065,46 +1082,46 @@ namespace {
 // Per-stream scratch of the compacting verify path: the entry lists, two
 // counter sets, and the host-mapped sample words read by the next call.
 //
-// Identity.  A state belongs to one STREAM OBJECT, named by (device,
-// hipStreamGetId), never by the handle value alone:
-//  * hipStreamPerThread is one handle value that is a different stream in
-//    every host thread — its id is that thread's own stream, so threads
-//    calling on it get separate states;
-//  * a destroyed stream's handle value can come back for a new stream while
-//    the old one's work is still pending — the new stream has a new id, so it
-//    never inherits the old one's lists and counters;
-//  * the legacy NULL stream is one stream per device: threads calling on it
-//    share its state, serialised by the state's mutex on the host and by
-//    stream order on the device (the protocol below).
-// Measured on MI355X (tools/exp/stream_identity.hip, profiles/r06_stream_identity.txt).
-// Where hipStreamGetId fails, the key is the handle (plus the calling
-// thread for the per-thread handle) and every compacting call waits on the
-// state's last one (hipStreamWaitEvent), which orders any two streams that
-// come to share it.
+// Protocol (per state): the counter set `parity` is this call's and its lane
+// kernel zeroes the other, which the previous call's long kernel has finished
+// reading — stream order.  So a state must only ever be used by ONE stream
+// (or by streams whose earlier work on it has completed).
 //
-// Protocol (per state): the counter set `parity` is this call's and its
-// lane kernel zeroes the other, which the previous call's long kernel has
-// finished reading (stream order; see verify_compact_lane_kernel).  So once a
-// state's last compacting launches have completed, counter set `parity` is
-// zero and the entry lists are free: that is when a state may pass to another
-// stream (`done`, an event recorded behind every compacting call).
+// Key.  A state belongs to the stream object the handle
+// names, on the current device:
+//  * an ordinary handle: the handle value.  The value can come back for a
+//    new stream only after the old stream object is released, and the
+//    runtime releases it only after the stream's work has completed:
+//    hipStreamDestroy blocks until then on both HIP runtimes of this image
+//    (ROCm 7.2 and PyTorch's 7.0: 21 ms for a pending 20 ms kernel), and even
+//    under the documented return-immediately semantics the resources go only
+//    once the device is done (tools/exp/stream_identity.hip,
+//    profiles/r06_stream_identity.txt).  So a state inherited through a
+//    reused value finds its counter set `parity` zero and its lists free;
+//  * hipStreamPerThread: one handle value that is a different stream in every
+//    host thread — keyed by a per-thread serial that is never reused, so no
+//    two threads' streams share a state (round 5 keyed it by the value: four
+//    threads on it ran their compacting kernels over one entry list, and the
+//    stale entries read another batch's offsets — a GPU memory fault,
+//    profiles/r06_mt_before_fix_perthread_vs6.err.txt);
+//  * NULL / hipStreamLegacy: the legacy stream, one per device: threads
+//    calling on it share its state, serialised by the state's mutex on the
+//    host and by stream order on the device.
 //
 // Storage.  Sample words and counter sets of every state on a device come
 // from one pool allocated once per device, right AFTER the device's first
 // verify call has launched its (stateless) kernel; a stream's state is a
 // table entry and a later stream's first call allocates nothing.  Entry
 // lists are per state, allocated when the compacting path first runs there
-// and grown (after draining the stream) when a batch needs more.  When the
-// table is full, a new stream takes over the least recently used state of
-// its device whose compacting work has completed (event query, never a
-// wait); if there is none it runs the stateless walking kernel: the same
-// results by another kernel, never a host fallback.  Lookups go through a
-// small per-thread cache, so a call takes no process-wide lock once its
-// stream has a state.
+// and grown (after draining the stream) when a batch needs more; never freed
+// (a handful per process).  A stream whose state cannot be made (table full:
+// 64 keys, allocation failure, or a call under stream capture) runs the
+// stateless walking kernel: the same results by another kernel, never a host
+// fallback.  Lookups go through a small per-thread cache, so a call takes no
+// process-wide lock once its stream has a state.
 struct VerifyState {
     int dev = -1;
-    unsigned long long id = 0;        // the stream's id (or fallback key)
-    bool id_trusted = true;           // false: key from the handle, compacting calls wait on `done`
+    uint64_t key = 0;
     std::mutex mu;
     uint32_t *host_sample = nullptr;  // host-mapped (pool): [0] small count, [1] long bytes, [2] overflow flag
     uint32_t *dev_sample = nullptr;
@@ -1115,9 +1132,6 @@ struct VerifyState {
     uint32_t parity = 0;
     int last_pick = -1;               // the path the previous call's sample priced (VerifyPath), -1 none
     bool overflow_reported = false;
-    hipEvent_t done = nullptr;        // behind the last compacting call's launches
-    bool done_recorded = false;
-    std::atomic<uint64_t> last_use{0};  // vclock() at the last call (LRU takeover)
 };
 constexpr uint32_t kSampleUnknown = 0xffffffffu;
 constexpr size_t kMaxVerifyStates = 64;  // streams, over all devices
@@ -1130,18 +1144,12 @@ struct VerifyPool {
     size_t used = 0;
 };
 constexpr size_t kMaxVerifyDevices = 64;
-std::mutex g_vstate_mu;  // the table and the pools (state creation / takeover only)
+std::mutex g_vstate_mu;  // the table and the pools (state creation only)
 VerifyState *g_vstate[kMaxVerifyStates];
 size_t g_nvstate = 0;
 VerifyPool g_vpool[kMaxVerifyDevices];
 size_t g_nvpool = 0;
-// LRU clock of the states: the monotonic clock (a shared counter bumped per
-// call would put every worker thread's calls on one contended line)
-uint64_t vclock() {
-    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-               std::chrono::steady_clock::now().time_since_epoch())
-        .count();
-}
+std::atomic<uint64_t> g_thread_serial{0};
 
 // The device's pool (caller holds g_vstate_mu), made on first use; nullptr
 // when an allocation fails (then the walking kernel serves that device).
@@ -1167,138 +1175,71 @@ VerifyPool *verify_pool(int dev) {
     return &p;
 }
 
-// The stream object's key: (current device, hipStreamGetId), or, where the
-// runtime gives no id, the handle (per-thread handle: plus the thread).
+// The stream object's key on the current device (see above): the handle, or
+// for hipStreamPerThread the calling thread's serial (top bit set: never a
+// handle value).
 struct VerifyKey {
     int dev;
-    unsigned long long id;
-    bool trusted;
+    uint64_t key;
 };
-
-// hipStreamGetId where the HIP runtime in the process has it (ROCm >= 7.1;
-// it is looked up, not linked: a process that loaded an older runtime
-// first — PyTorch's bundled one — must still load this library).
-using StreamGetIdFn = hipError_t (*)(hipStream_t, unsigned long long *);
-StreamGetIdFn stream_get_id() {
-    static const StreamGetIdFn f = reinterpret_cast<StreamGetIdFn>(dlsym(RTLD_DEFAULT, "hipStreamGetId"));
-    return f;
-}
 
 bool verify_key(void *stream, VerifyKey &k) {
     if (hipGetDevice(&k.dev) != hipSuccess)
         return false;
-    unsigned long long id = 0;
-    if (const StreamGetIdFn f = stream_get_id()) {
-        if (f(static_cast<hipStream_t>(stream), &id) == hipSuccess) {
-            k.id = id;
-            k.trusted = true;
-            return true;
-        }
-        (void)hipGetLastError();  // the failed query is not a launch error
+    if (stream == static_cast<void *>(hipStreamPerThread)) {
+        static thread_local const uint64_t t_serial = g_thread_serial.fetch_add(1, std::memory_order_relaxed);
+        k.key = t_serial | (1ull << 63);
+    } else {
+        k.key = (uint64_t)reinterpret_cast<uintptr_t>(stream);
     }
-    static thread_local const char t_self = 0;
-    uintptr_t h = reinterpret_cast<uintptr_t>(stream);
-    if (stream == static_cast<void *>(hipStreamPerThread))
-        h ^= reinterpret_cast<uintptr_t>(&t_self) << 1;  // one stream per thread behind that handle
-    k.id = (unsigned long long)h | (1ull << 63);  // never equal to a runtime id of the same value
-    k.trusted = false;
     return true;
 }
 
-void verify_state_bind(VerifyState *s, const VerifyKey &k) {
-    s->dev = k.dev;
-    s->id = k.id;
-    s->id_trusted = k.trusted;
-    s->last_pick = -1;
-    s->overflow_reported = false;
-    __atomic_store_n(s->host_sample, kSampleUnknown, __ATOMIC_RELAXED);
-    __atomic_store_n(s->host_sample + 1, 0u, __ATOMIC_RELAXED);
-    __atomic_store_n(s->host_sample + 2, 0u, __ATOMIC_RELAXED);
-    s->last_use.store(vclock(), std::memory_order_relaxed);
-}
-
-// Per-thread lookup cache: (key -> state), validated against the state's own
-// key under its mutex (a state may have passed to another stream since).
+// Per-thread lookup cache: (key -> state); a state never changes key.
 struct VCacheEnt {
     int dev = -1;
-    unsigned long long id = 0;
+    uint64_t key = 0;
     VerifyState *s = nullptr;
 };
 constexpr int kVCache = 4;
 thread_local VCacheEnt t_vcache[kVCache];
 thread_local int t_vcache_next = 0;
 
-// The stream's state, LOCKED (s->mu held by the caller's unique_lock), or
-// nullptr; with create, made (or taken over) when absent — nullptr when the
-// table is full of busy states or an allocation fails.  No device work is
-// queued or waited for here.
-VerifyState *verify_state(const VerifyKey &k, bool create, std::unique_lock<std::mutex> &lk) {
-    for (VCacheEnt &c : t_vcache) {
-        if (c.s && c.dev == k.dev && c.id == k.id) {
-            std::unique_lock<std::mutex> l(c.s->mu);
-            if (c.s->dev == k.dev && c.s->id == k.id) {
-                lk = std::move(l);
-                return c.s;
-            }
-            c.s = nullptr;  // passed to another stream
-        }
-    }
+// The stream's state, or nullptr; with create, made when absent (nullptr when
+// the table is full or an allocation fails).  No device work is queued or
+// waited for here.
+VerifyState *verify_state(const VerifyKey &k, bool create) {
+    for (const VCacheEnt &c : t_vcache)
+        if (c.s && c.dev == k.dev && c.key == k.key)
+            return c.s;
     VerifyState *s = nullptr;
     {
         std::lock_guard<std::mutex> g(g_vstate_mu);
         for (size_t i = 0; i < g_nvstate && !s; i++)
-            if (g_vstate[i]->dev == k.dev && g_vstate[i]->id == k.id)
+            if (g_vstate[i]->dev == k.dev && g_vstate[i]->key == k.key)
                 s = g_vstate[i];
-        if (!s && create) {
+        if (!s && create && g_nvstate < kMaxVerifyStates) {
             VerifyPool *pool = verify_pool(k.dev);
-            if (pool && pool->used < kMaxVerifyStates && g_nvstate < kMaxVerifyStates) {
+            if (pool && pool->used < kMaxVerifyStates) {
                 const size_t slot = pool->used++;
                 s = new VerifyState;
+                s->dev = k.dev;
+                s->key = k.key;
                 s->host_sample = pool->host + slot * kSampleWords;
                 s->dev_sample = pool->devp + slot * kSampleWords;
                 s->ctr = pool->ctr + slot * kCtrWords;
-                verify_state_bind(s, k);
+                __atomic_store_n(s->host_sample, kSampleUnknown, __ATOMIC_RELAXED);
+                __atomic_store_n(s->host_sample + 1, 0u, __ATOMIC_RELAXED);
+                __atomic_store_n(s->host_sample + 2, 0u, __ATOMIC_RELAXED);
                 g_vstate[g_nvstate++] = s;
-            } else if (pool) {
-                // take over the least recently used idle state of this device
-                // (try-locks only: no wait on a busy state, and the candidate
-                // stays locked from its check to its rebinding)
-                VerifyState *best = nullptr;
-                std::unique_lock<std::mutex> best_lk;
-                uint64_t best_use = UINT64_MAX;
-                for (size_t i = 0; i < g_nvstate; i++) {
-                    VerifyState *c = g_vstate[i];
-                    const uint64_t u = c->last_use.load(std::memory_order_relaxed);
-                    if (c->dev != k.dev || u >= best_use)
-                        continue;
-                    std::unique_lock<std::mutex> l(c->mu, std::try_to_lock);
-                    if (!l.owns_lock())
-                        continue;
-                    if (c->done_recorded && hipEventQuery(c->done) != hipSuccess) {
-                        (void)hipGetLastError();  // hipErrorNotReady is not a launch error
-                        continue;                 // its compacting work is still running
-                    }
-                    best = c;
-                    best_use = u;
-                    best_lk = std::move(l);
-                }
-                if (best) {
-                    verify_state_bind(best, k);
-                    best->done_recorded = false;
-                    s = best;
-                }
             }
         }
     }
-    if (!s)
-        return nullptr;
-    std::unique_lock<std::mutex> l(s->mu);
-    if (s->dev != k.dev || s->id != k.id)
-        return nullptr;  // taken over between the table lookup and the lock: stateless this call
-    VCacheEnt &c = t_vcache[t_vcache_next];
-    t_vcache_next = (t_vcache_next + 1) % kVCache;
-    c = VCacheEnt{k.dev, k.id, s};
-    lk = std::move(l);
+    if (s) {
+        VCacheEnt &c = t_vcache[t_vcache_next];
+        t_vcache_next = (t_vcache_next + 1) % kVCache;
+        c = VCacheEnt{k.dev, k.key, s};
+    }
     return s;
 }
 
@@ -1334,21 +1275,8 @@ static int verify_compact_launch(VerifyParams p, VerifyState *s, uint64_t est_lo
     if (nl >= 8)
         nl = (nl + 7) & ~7ull;
     const uint64_t cap = per_block * ((nl + kVShards - 1) / kVShards);
-    if (nl > 0x7fffffffull || p.n >= (1ull << 32))
+    if (nl > 0x7fffffffull || p.n >= (1ull << 32) || !verify_reserve(s, cap, st))
         return WG_ERR_RUNTIME;  // the caller runs a stateless kernel instead
-    if (!s->done) {
-        if (hipEventCreateWithFlags(&s->done, hipEventDisableTiming) != hipSuccess) {
-            s->done = nullptr;
-            return WG_ERR_RUNTIME;
-        }
-    } else if (s->done_recorded && !s->id_trusted) {
-        // keyed by handle (no stream id from the runtime): whichever stream
-        // called last, this call's launches go after its compacting work
-        if (hipStreamWaitEvent(st, s->done, 0) != hipSuccess)
-            return WG_ERR_RUNTIME;
-    }
-    if (!verify_reserve(s, cap, st))
-        return WG_ERR_RUNTIME;
     if (!s->ctr_zeroed) {  // the stream's first compacting call: both counter sets, in stream order
         if (hipMemsetAsync(s->ctr, 0, 2u * kVShards * kVCtrStride * 4u, st) != hipSuccess)
             return WG_ERR_RUNTIME;
@@ -1369,20 +1297,12 @@ static int verify_compact_launch(VerifyParams p, VerifyState *s, uint64_t est_lo
     nb = nb > nbmax ? nbmax : nb;
     nb = (nb + kVShards - 1) & ~(uint64_t)(kVShards - 1);
     hipLaunchKernelGGL((verify_compact_long_kernel<0, true>), dim3((unsigned)nb), dim3(256), 0, st, p, c);
-    int rc = WG_OK;
     if (hipGetLastError() != hipSuccess) {
         // a launch that did not happen may have left a counter set dirty
         (void)hipMemsetAsync(s->ctr, 0, 2u * kVShards * kVCtrStride * 4u, st);
-        rc = WG_ERR_LAUNCH;
+        return WG_ERR_LAUNCH;
     }
-    // the scratch is free again once this completes (takeover, untrusted keys)
-    s->done_recorded = hipEventRecord(s->done, st) == hipSuccess;
-    if (!s->done_recorded) {
-        // without the marker nothing may take this state over or order
-        // behind it: drain now (a failure path only)
-        (void)hipStreamSynchronize(st);
-    }
-    return rc;
+    return WG_OK;
 }
 
 }  // namespace wg
@@ -1474,8 +1394,7 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
         VerifyKey key;
         if (!verify_key(stream, key))
             return verify_launch_walk(p, st, true);
-        std::unique_lock<std::mutex> g;
-        VerifyState *s = verify_state(key, false, g);
+        VerifyState *s = verify_state(key, false);
         if (!s) {
             // the stream's first call (or capturing before it had state, or
             // no state free): the stateless kernel goes out first — in the
@@ -1483,13 +1402,11 @@ extern "C" int wg_verify_desc(const uint8_t *dev_base, const wg_pkt_desc *dev_de
             // 2.4 % of the spread one on long ones — and the state
             // is made behind it for the next call
             const int rc = verify_launch_walk(p, st, true);
-            if (!capturing) {
-                std::unique_lock<std::mutex> g2;
-                (void)verify_state(key, true, g2);
-            }
+            if (!capturing)
+                (void)verify_state(key, true);
             return rc;
         }
-        s->last_use.store(vclock(), std::memory_order_relaxed);
+        std::lock_guard<std::mutex> g(s->mu);
         const uint32_t smp = __atomic_load_n(s->host_sample, __ATOMIC_RELAXED);
         const uint32_t lb = __atomic_load_n(s->host_sample + 1, __ATOMIC_RELAXED);
         if (__atomic_load_n(s->host_sample + 2, __ATOMIC_RELAXED) && !s->overflow_reported) {
