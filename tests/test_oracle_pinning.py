@@ -51,3 +51,45 @@ def test_pool_follows_the_picked_cpus():
             os.environ.pop("ORC_CPUS", None)
         else:
             os.environ["ORC_CPUS"] = saved
+
+
+def test_quiet_cpus_deals_l3_domains_round_robin():
+    """the all-core leg's CPUs are dealt over the L3
+    domains (CCDs) before a domain gets a second worker, one per physical
+    core; the result names the domains it used."""
+    cpus = sorted(os.sched_getaffinity(0))
+    doms = {}
+    for c in cpus:
+        doms.setdefault(oracle._l3_of(c), set()).add(oracle._core_of(c))
+    n = min(len(cpus), 16)
+    q = oracle.quiet_cpus(n)
+    assert len(q["cpus"]) == n and len(set(q["cpus"])) == n
+    used = q["l3_domains"]
+    assert sum(len(v) for v in used.values()) == n
+    # no domain holds two workers while another holds none (when cores allow)
+    if n <= len(doms):
+        assert len(used) == n
+    counts = [len(v) for v in used.values()]
+    assert max(counts) - min(counts) <= 1 or n > sum(len(v) for v in doms.values())
+
+
+def test_read_probe_and_pool_stats():
+    """The read probe sums the buffer's whole 4-KiB blocks (the same word sum
+    with 1 or 3 workers), and the pool reports one busy time per worker."""
+    buf = np.random.default_rng(9).integers(0, 256, (1 << 20) + 100, dtype=np.uint8)
+    blocks = buf[: buf.size // 4096 * 4096].view(np.uint64)
+    want = int(blocks.sum(dtype=np.uint64))
+    assert oracle.read_probe(buf, 1) == want
+    saved = os.environ.get("ORC_CPUS")
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+        os.environ["ORC_CPUS"] = ",".join(map(str, cpus[:3]))
+        oracle.pool_stats_reset()
+        assert oracle.read_probe(buf, 3) == want
+        st = oracle.pool_stats()
+        assert len(st) == min(3, len(cpus)) and all(calls == 1 and busy > 0 for busy, calls in st)
+    finally:
+        if saved is None:
+            os.environ.pop("ORC_CPUS", None)
+        else:
+            os.environ["ORC_CPUS"] = saved

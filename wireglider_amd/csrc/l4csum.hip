@@ -780,12 +780,25 @@ __device__ __forceinline__ void verify_lane_decode(const v4u W[5], uintptr_t a, 
                              W[4][0], W[4][1], W[4][2], W[4][3]};
     const uint32_t s = (uint32_t)(a & 15u), q4 = s >> 2, sh = s & 3u;
     uint32_t R[16];
+#ifdef WG_LANE_BARREL
+    // the packet's dwords brought to the front in two select stages (by 2,
+    // then by 1 dword): 35 v_cndmask, no branches (the 4-way ternaries below
+    // compile to a branch ladder per word)
+    uint32_t X[18], Y[17];
+#pragma unroll
+    for (uint32_t i = 0; i < 18; i++) X[i] = (q4 & 2u) ? Wd[i + 2] : Wd[i];
+#pragma unroll
+    for (uint32_t i = 0; i < 17; i++) Y[i] = (q4 & 1u) ? X[i + 1] : X[i];
+#pragma unroll
+    for (uint32_t m = 0; m < 16; m++) R[m] = bytes_below(__builtin_amdgcn_alignbyte(Y[m + 1], Y[m], sh), m, len);
+#else
 #pragma unroll
     for (uint32_t m = 0; m < 16; m++) {
         const uint32_t lo = q4 == 0 ? Wd[m] : q4 == 1 ? Wd[m + 1] : q4 == 2 ? Wd[m + 2] : Wd[m + 3];
         const uint32_t hi = q4 == 0 ? Wd[m + 1] : q4 == 1 ? Wd[m + 2] : q4 == 2 ? Wd[m + 3] : Wd[m + 4];
         R[m] = bytes_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, len);
     }
+#endif
     uint32_t v = 0, c = 0;
     if (len >= 1) {
         const uint32_t b0 = R[0] & 0xffu;
@@ -1006,8 +1019,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
 // 1 M x 64 B 0.0157 ms against the compacting path's 0.0174; long packets
 // cost it 7-9 % against the one-shot wave kernel (a wave then lives for 16
 // groups), so the cost model sends long-dominated batches there.
+#ifdef WG_WALK8
+// experiment: the consecutive layout (all-small batches, first calls) at 8
+// waves per SIMD (<= 64 VGPRs) — at 75 VGPRs 6 waves per SIMD hold 6,144 of
+// 1 M x 64 B's 16,384 waves: three rounds of waves instead of two
+#define WG_WALK_WPE __attribute__((amdgpu_waves_per_eu(kConsec ? 8 : 1, 8)))
+#else
+#define WG_WALK_WPE
+#endif
 template <bool kConsec>
-__global__ __launch_bounds__(256) void verify_walk_kernel(VerifyParams p) {
+__global__ __launch_bounds__(256) WG_WALK_WPE void verify_walk_kernel(VerifyParams p) {
     const uint32_t lane = lane_id();
     const uint64_t G = (uint64_t)gridDim.x * 4u;
     const uint64_t w = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
