@@ -1019,16 +1019,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(O ? O : 1, 
 // 1 M x 64 B 0.0157 ms against the compacting path's 0.0174; long packets
 // cost it 7-9 % against the one-shot wave kernel (a wave then lives for 16
 // groups), so the cost model sends long-dominated batches there.
-#ifdef WG_WALK8
-// experiment: the consecutive layout (all-small batches, first calls) at 8
-// waves per SIMD (<= 64 VGPRs) — at 75 VGPRs 6 waves per SIMD hold 6,144 of
-// 1 M x 64 B's 16,384 waves: three rounds of waves instead of two
-#define WG_WALK_WPE __attribute__((amdgpu_waves_per_eu(kConsec ? 8 : 1, 8)))
-#else
-#define WG_WALK_WPE
-#endif
 template <bool kConsec>
-__global__ __launch_bounds__(256) WG_WALK_WPE void verify_walk_kernel(VerifyParams p) {
+__global__ __launch_bounds__(256) void verify_walk_kernel(VerifyParams p) {
     const uint32_t lane = lane_id();
     const uint64_t G = (uint64_t)gridDim.x * 4u;
     const uint64_t w = (uint64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4u + wave_in_block();
@@ -1039,22 +1031,6 @@ __global__ __launch_bounds__(256) WG_WALK_WPE void verify_walk_kernel(VerifyPara
     const uint32_t olo = live ? dv.x : 0u, ohi = live ? dv.y : 0u;
     const bool small = live && len <= kSmallMax;
     uint32_t rv = 0, rc = 0;
-#ifdef WG_WALK_PF
-    // experiment: the descriptors of the wave that will run in this one's
-    // slot in the second half of the grid, touched now (same XCD: the
-    // hardware block index differs by a multiple of 8), so that wave finds
-    // them in L2; the value feeds a store that never happens
-    v4u pf{0, 0, 0, 0};
-    if constexpr (kConsec) {
-        const uint32_t half = gridDim.x >> 1;
-        if ((half & 7u) == 0 && blockIdx.x < half) {
-            const uint64_t w2 = (uint64_t)xcd_swizzle(blockIdx.x + half, gridDim.x) * 4u + wave_in_block();
-            const uint64_t i2 = w2 * 64u + lane;
-            if (i2 < p.n)
-                pf = ld16(reinterpret_cast<uintptr_t>(p.desc) + 16ull * i2);
-        }
-    }
-#endif
     if (__ballot(small))  // wave-uniform
         verify_lane(reinterpret_cast<uintptr_t>(p.base) + (((uint64_t)ohi << 32) | olo), small ? len : 0u, small, rv,
                     rc);
@@ -1091,9 +1067,6 @@ __global__ __launch_bounds__(256) WG_WALK_WPE void verify_walk_kernel(VerifyPara
     }
     if (p.sample && blockIdx.x == 0 && wave_in_block() == 0)
         verify_sample(p, l2);
-#ifdef WG_WALK_PF
-    asm volatile("" ::"v"(pf.x));  // keeps the touch (its wait lands here, at the wave's end)
-#endif
 }
 
 }  // namespace wg
