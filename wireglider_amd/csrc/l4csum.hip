@@ -780,25 +780,12 @@ __device__ __forceinline__ void verify_lane_decode(const v4u W[5], uintptr_t a, 
                              W[4][0], W[4][1], W[4][2], W[4][3]};
     const uint32_t s = (uint32_t)(a & 15u), q4 = s >> 2, sh = s & 3u;
     uint32_t R[16];
-#ifdef WG_LANE_BARREL
-    // the packet's dwords brought to the front in two select stages (by 2,
-    // then by 1 dword): 35 v_cndmask, no branches (the 4-way ternaries below
-    // compile to a branch ladder per word)
-    uint32_t X[18], Y[17];
-#pragma unroll
-    for (uint32_t i = 0; i < 18; i++) X[i] = (q4 & 2u) ? Wd[i + 2] : Wd[i];
-#pragma unroll
-    for (uint32_t i = 0; i < 17; i++) Y[i] = (q4 & 1u) ? X[i + 1] : X[i];
-#pragma unroll
-    for (uint32_t m = 0; m < 16; m++) R[m] = bytes_below(__builtin_amdgcn_alignbyte(Y[m + 1], Y[m], sh), m, len);
-#else
 #pragma unroll
     for (uint32_t m = 0; m < 16; m++) {
         const uint32_t lo = q4 == 0 ? Wd[m] : q4 == 1 ? Wd[m + 1] : q4 == 2 ? Wd[m + 2] : Wd[m + 3];
         const uint32_t hi = q4 == 0 ? Wd[m + 1] : q4 == 1 ? Wd[m + 2] : q4 == 2 ? Wd[m + 3] : Wd[m + 4];
         R[m] = bytes_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, len);
     }
-#endif
     uint32_t v = 0, c = 0;
     if (len >= 1) {
         const uint32_t b0 = R[0] & 0xffu;
