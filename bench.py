@@ -1268,7 +1268,7 @@ def _placement_evidence(quiet, cpus_all, workers, nbytes, scale, unit, all_s, on
     return out
 
 
-def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
+def cpu_baseline(sample_fn, seconds: float, reps: int = 8, npk: int = 1 << 19, warm_max: float = 8.0):
     """The oracle (C restatement of checksum.cpp + a fastcsum-class nofold) on
     the host cores of this box, on a bounded sample of the same workload.
     All cores: `reps` repetitions of >= `seconds` each, the first dropped,
@@ -1280,9 +1280,9 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
     import numpy as np
     import oracle  # test infrastructure: the CPU baseline leg only
 
-    # 2^19 packets (~786 MB for 1500 B) so the sample does not sit in the
-    # host's last-level cache (EPYC 9575F: 256 MB L3) between repetitions.
-    npk = 1 << 19
+    # 2^19 packets (~786 MB for 1500 B) by default, so the sample does not
+    # sit in the host's last-level cache (EPYC 9575F: 256 MB L3) between
+    # repetitions (npk / warm_max: smaller for the CPU test of this leg).
     host, gpu_out, kind = sample_fn(npk)
     cores = oracle.host_cores()
     threads = cores["threads"]
@@ -1467,7 +1467,7 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8):
     run_all()  # first touch / warm-up, untimed
     warm_log = {}
 
-    def warm(name, fn, secs, secs_max=8.0, tol=0.02):
+    def warm(name, fn, secs, secs_max=warm_max, tol=0.02):
         # untimed runs until the leg's pages have settled where its workers
         # run (round 5: repetitions still rose 30-60 % over the first
         # seconds on a 256-CPU host — page placement, not clocks: every
