@@ -1310,6 +1310,19 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8, npk: int = 1 << 19, w
 
     cpus_all = pick(threads)
     quiet = picks[0] if picks else None
+    # the sample's pages moved to the nodes of the workers that read them
+    # (first touch by each pinned worker of its own share), per leg: the
+    # sample was written by this thread, all on its node, and a worker on the
+    # other socket read it remotely (round 6's first L3-spread lines: 17-22
+    # GiB/s per socket-0 worker against 30-34 on socket 1)
+    def retouch(n):
+        if not pin:
+            return None
+        bufs = [host] + ([kind[3]] if kind[0] == "decap" else [])
+        return all(isinstance(b, np.ndarray) and b.flags["C_CONTIGUOUS"] and b.flags["WRITEABLE"]
+                   and oracle.numa_retouch(b, n) for b in bufs)
+
+    numa_all = retouch(threads)
     one_scale = 1.0  # the 1-core leg runs on 1/one_scale of the sample
     extra = {}
     if kind[0] == "uniform":
@@ -1499,6 +1512,7 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8, npk: int = 1 << 19, w
     probe_buf = host if isinstance(host, np.ndarray) and host.dtype == np.uint8 and host.size >= 1 << 20 else None
     read_all = _read_probe_rate(oracle, probe_buf, threads) if probe_buf is not None else None
     cpus_one = pick(1)
+    numa_one = retouch(1)
     warm("one", run_one, min(seconds, 1.5))  # the 1-core leg's first touch on its CPU, untimed
     one_s = _spread(_rep_rates(run_one, nbytes * one_scale, seconds / 2, reps, after=logger("one", cpus_one)), scale)
     read_one = _read_probe_rate(oracle, probe_buf, 1) if probe_buf is not None else None
@@ -1542,6 +1556,9 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8, npk: int = 1 << 19, w
                                    "L3 domains (CCDs) of the mask dealt round robin, quietest domain and quietest "
                                    "CPUs first (0.3-s /proc/stat sample), kept for every repetition of the leg"
                                    if pin else "off"),
+        "numa_first_touch": {"all": numa_all, "one": numa_one,
+                             "what": "before each leg the sample's pages were dropped and copied back by that leg's "
+                                     "pinned workers (oracle.numa_retouch), so each reads memory on its own node"},
         "l3_domains": placement.get("l3_domains"),
         "per_worker": placement.get("per_worker"),
         "read_probe": placement.get("read_probe"),

@@ -12,7 +12,9 @@
 #include "orc_pin.h"
 
 #include <pthread.h>
+#include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -283,6 +285,13 @@ typedef struct {
 } job_t;
 
 static void run_job(job_t *j) {
+    if (j->kind == 8) {
+        /* NUMA re-touch: copy 4-KiB pages [lo, hi) back from the saved copy
+         * (j->base) into the dropped range (j->wbase): the worker's first
+         * write places each page on its own node */
+        memcpy(j->wbase + j->lo * 4096u, j->base + j->lo * 4096u, (size_t)(j->hi - j->lo) * 4096u);
+        return;
+    }
     if (j->kind == 7) {
         /* read probe: 64-bit words of 4-KiB blocks [lo, hi) (vectorised by the
          * compiler: the memory path of these CPUs, no checksum work).  Summed
@@ -572,6 +581,36 @@ uint64_t orc_read_probe(const uint8_t *base, uint64_t nbytes, int threads) {
     uint64_t acc = 0;
     run_parallel_acc(j, n, threads, &acc);
     return acc;
+}
+
+int orc_numa_retouch(uint8_t *buf, uint64_t nbytes, int threads) {
+    /* The buffer's whole pages moved to the nodes of the workers that will
+     * read them (the CPU baseline's pinned pool, ORC_CPUS): saved, dropped
+     * (MADV_DONTNEED: private anonymous pages refault on first touch), and
+     * copied back by the workers, page range t to worker t as run_parallel
+     * splits units.  Contents unchanged.  Returns 0, or -1 when the range
+     * cannot be dropped (the buffer is then left as it was). */
+    const uintptr_t ps = 4096u;
+    const uintptr_t a0 = ((uintptr_t)buf + ps - 1) & ~(ps - 1);
+    const uintptr_t a1 = ((uintptr_t)buf + nbytes) & ~(ps - 1);
+    if (a1 <= a0)
+        return 0;
+    const uint64_t n = (uint64_t)(a1 - a0);
+    uint8_t *save = (uint8_t *)malloc(n);
+    if (!save)
+        return -1;
+    memcpy(save, (void *)a0, n);
+    if (madvise((void *)a0, n, MADV_DONTNEED) != 0) {
+        free(save);
+        return -1;
+    }
+    job_t j = {0};
+    j.kind = 8;
+    j.base = save;
+    j.wbase = (uint8_t *)a0;
+    run_parallel(j, n / ps, threads);
+    free(save);
+    return 0;
 }
 
 double orc_time_l4_uniform(const uint8_t *base, uint64_t total_len, uint32_t segment_size,

@@ -188,6 +188,7 @@ double orc_time_l4_uniform(const uint8_t *base, uint64_t total_len, uint32_t seg
 void orc_pool_stats_reset(void);
 int orc_pool_stats(uint64_t *busy_ns, uint64_t *calls, int max);
 uint64_t orc_read_probe(const uint8_t *base, uint64_t nbytes, int threads);
+int orc_numa_retouch(uint8_t *buf, uint64_t nbytes, int threads);
 
 #ifdef __cplusplus
 }

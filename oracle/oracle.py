@@ -109,6 +109,8 @@ def _load():
     lib.orc_pool_stats.argtypes = [vp, vp, i32]
     lib.orc_read_probe.restype = u64
     lib.orc_read_probe.argtypes = [vp, u64, i32]
+    lib.orc_numa_retouch.restype = i32
+    lib.orc_numa_retouch.argtypes = [vp, u64, i32]
     lib.orc_time_l4_uniform.restype = ctypes.c_double
     lib.orc_time_l4_uniform.argtypes = [vp, u64, u32, u16, u32, vp, i32, i32]
     return lib
@@ -251,6 +253,15 @@ def pool_stats(max_workers: int = 256) -> list:
     calls = np.zeros(max_workers, np.uint64)
     n = int(lib.orc_pool_stats(busy.ctypes.data, calls.ctypes.data, max_workers))
     return [(float(busy[t]) * 1e-9, int(calls[t])) for t in range(n)]
+
+
+def numa_retouch(buf, threads: int) -> bool:
+    """Move buf's whole pages to the NUMA nodes of the pool's pinned workers
+    (ORC_CPUS; page range t copied back by worker t after the range was
+    dropped): contents unchanged.  False when it could not (buf left as is)."""
+    a = np.asarray(buf)
+    assert a.flags["C_CONTIGUOUS"] and a.flags["WRITEABLE"]
+    return int(lib.orc_numa_retouch(a.ctypes.data, a.nbytes, threads)) == 0
 
 
 def read_probe(buf, threads: int) -> int:
