@@ -1294,15 +1294,15 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8, npk: int = 1 << 19, w
     pin = os.environ.get("ORC_PIN", "1") != "0"
     picks = []
 
-    def pick(n):
+    def pick(n, policy="spread"):
         if pin:
-            q = oracle.quiet_cpus(n)
+            q = oracle.quiet_cpus(n, policy)
             os.environ["ORC_CPUS"] = ",".join(map(str, q["cpus"]))
             picks.append(q)
             return q["cpus"]
         return None
 
-    reps_log = {"all": [], "one": []}
+    reps_log = {"spread": [], "socket": [], "one": []}
 
     def logger(leg, cpus):
         # each repetition's CPUs and their clock right after it
@@ -1503,14 +1503,36 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8, npk: int = 1 << 19, w
         warm_log[name] = {"seconds": round(el, 2), "chunks": len(rates),
                           "last_rate_vs_first": round(rates[-1] / rates[0], 3)}
 
-    warm("all", run_all, min(seconds, 1.5))
-    thr0 = oracle.cgroup_throttling()
-    oracle.pool_stats_reset()
-    all_s = _spread(_rep_rates(run_all, nbytes, seconds, reps, after=logger("all", cpus_all)), scale)
-    workers = oracle.pool_stats()
-    thr1 = oracle.cgroup_throttling()
     probe_buf = host if isinstance(host, np.ndarray) and host.dtype == np.uint8 and host.size >= 1 << 20 else None
-    read_all = _read_probe_rate(oracle, probe_buf, threads) if probe_buf is not None else None
+
+    def all_leg(policy, cpus, q, numa):
+        # the all-core leg on one placement: CPUs dealt over the L3 domains of
+        # the whole mask ("spread") or of one package ("socket"), the
+        # sample's pages moved to those workers' nodes
+        run_all()
+        warm(f"all_{policy}", run_all, min(seconds, 1.5))
+        thr0 = oracle.cgroup_throttling()
+        oracle.pool_stats_reset()
+        leg = _spread(_rep_rates(run_all, nbytes, seconds, reps, after=logger(policy, cpus)), scale)
+        workers = oracle.pool_stats()
+        thr1 = oracle.cgroup_throttling()
+        read = _read_probe_rate(oracle, probe_buf, threads) if probe_buf is not None else None
+        leg["repetitions"] = reps_log[policy]
+        leg["warm_up"] = warm_log.get(f"all_{policy}")
+        if thr0 and thr1:
+            # CPU-quota throttling while the all-core repetitions ran (a share
+            # of 16 CPUs leaves no room for a 17th busy thread)
+            leg["cgroup_throttled"] = {k: thr1[k] - thr0[k] for k in thr0}
+        return {"policy": policy, "spread": leg, "cpus": cpus, "quiet": q, "workers": workers, "read": read,
+                "numa": numa}
+
+    legs = [all_leg("spread", cpus_all, quiet, numa_all)]
+    cpus_sock = pick(threads, "socket")
+    if pin and set(cpus_sock or []) != set(cpus_all or []):
+        legs.append(all_leg("socket", cpus_sock, picks[-1], retouch(threads)))
+    best = max(legs, key=lambda L: L["spread"]["median"])
+    all_s, cpus_all, quiet, workers, read_all = best["spread"], best["cpus"], best["quiet"], best["workers"], best["read"]
+    numa_all = best["numa"]
     cpus_one = pick(1)
     numa_one = retouch(1)
     warm("one", run_one, min(seconds, 1.5))  # the 1-core leg's first touch on its CPU, untimed
@@ -1518,14 +1540,13 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8, npk: int = 1 << 19, w
     read_one = _read_probe_rate(oracle, probe_buf, 1) if probe_buf is not None else None
     placement = _placement_evidence(quiet, cpus_all, workers, nbytes, scale, unit, all_s, one_s, read_all, read_one,
                                     probe_buf)
-    all_s["repetitions"] = reps_log["all"]
     one_s["repetitions"] = reps_log["one"]
-    all_s["warm_up"] = warm_log.get("all")
     one_s["warm_up"] = warm_log.get("one")
-    if thr0 and thr1:
-        # CPU-quota throttling while the all-core repetitions ran (a share of
-        # 16 CPUs leaves no room for a 17th busy thread)
-        all_s["cgroup_throttled"] = {k: thr1[k] - thr0[k] for k in thr0}
+    placement["all_core_placements"] = {
+        L["policy"]: {"value": L["spread"]["median"], "spread_pct": L["spread"]["spread_pct"], "cpus": L["cpus"],
+                      "packages": (L["quiet"] or {}).get("packages"), "l3_domains": (L["quiet"] or {}).get("l3_domains"),
+                      "read_probe_GiB_s": (L["read"] or {}).get("GiB_s")} for L in legs}
+    placement["all_core_placement_used"] = best["policy"]
     try:
         cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except Exception:
@@ -1553,12 +1574,15 @@ def cpu_baseline(sample_fn, seconds: float, reps: int = 8, npk: int = 1 << 19, w
                            pinned_cpu_1core=cpus_one[0] if cpus_one else None,
                            pinned_cpus_busy_before=[q["busy"] for q in picks] if picks else None,
                            pinning="per leg, once before its repetitions: one worker per physical core, the "
-                                   "L3 domains (CCDs) of the mask dealt round robin, quietest domain and quietest "
-                                   "CPUs first (0.3-s /proc/stat sample), kept for every repetition of the leg"
-                                   if pin else "off"),
+                                   "L3 domains (CCDs) dealt round robin, quietest domain and quietest CPUs first "
+                                   "(0.3-s /proc/stat sample), kept for every repetition of the leg; the all-core "
+                                   "leg runs twice, over the domains of the whole mask and of one package, and "
+                                   "reports the faster (all_core_placements)" if pin else "off"),
         "numa_first_touch": {"all": numa_all, "one": numa_one,
                              "what": "before each leg the sample's pages were dropped and copied back by that leg's "
                                      "pinned workers (oracle.numa_retouch), so each reads memory on its own node"},
+        "all_core_placements": placement.get("all_core_placements"),
+        "all_core_placement_used": placement.get("all_core_placement_used"),
         "l3_domains": placement.get("l3_domains"),
         "per_worker": placement.get("per_worker"),
         "read_probe": placement.get("read_probe"),

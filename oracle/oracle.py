@@ -190,7 +190,14 @@ def _l3_of(c: int) -> str:
         return "?"
 
 
-def quiet_cpus(n: int) -> dict:
+def _package_of(c: int) -> int:
+    try:
+        return int(Path(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id").read_text())
+    except Exception:
+        return 0
+
+
+def quiet_cpus(n: int, policy: str = "spread") -> dict:
     """n CPUs of the affinity mask for n pinned workers, spread over the L3
     domains (CCDs): one physical core per worker, the domains dealt round
     robin (quietest domain first), the quietest CPUs first within a domain.
@@ -198,7 +205,13 @@ def quiet_cpus(n: int) -> dict:
     CPU numbers of an idle host give (the all-core leg
     on CPUs 1-30, four CCDs, ran 3.2x one core).  Returns {"cpus": [...],
     "busy": mean busy fraction of the chosen CPUs before the run, "l3_domains":
-    {domain: [cpus]} of the chosen CPUs}."""
+    {domain: [cpus]} of the chosen CPUs}.
+
+    policy "socket": the same dealing over the L3 domains of ONE package (the
+    quietest that has n cores), so the workers share a socket's memory and
+    coherence domain — what a library with process-wide atomics (OpenSSL 3's
+    EVP layer) needs; bench.py times the all-core leg both ways and keeps the
+    faster."""
     cpus = sorted(os.sched_getaffinity(0))
     busy = _cpu_busy(cpus)
     doms: dict = {}
@@ -212,6 +225,15 @@ def quiet_cpus(n: int) -> dict:
     # the domains, quietest first (mean busy of their cores), then by number
     order = sorted(doms, key=lambda d: (sum(busy.get(c, 1.0) for c in doms[d]) / len(doms[d]),
                                         int(d) if d.isdigit() else 1 << 30))
+    if policy == "socket":
+        pk: dict = {}
+        for d in order:
+            pk.setdefault(_package_of(doms[d][0]), []).append(d)
+        fits = [k for k, ds in pk.items() if sum(len(doms[d]) for d in ds) >= n]
+        if fits:  # the quietest package that holds n workers
+            best = min(fits, key=lambda k: sum(busy.get(c, 1.0) for d in pk[k] for c in doms[d])
+                       / sum(len(doms[d]) for d in pk[k]))
+            order = [d for d in order if d in pk[best]]
     chosen = []
     depth = 0
     while len(chosen) < n and any(depth < len(doms[d]) for d in order):
@@ -228,7 +250,7 @@ def quiet_cpus(n: int) -> dict:
     for c in chosen:
         used.setdefault(_l3_of(c), []).append(c)
     return {"cpus": chosen, "busy": round(sum(busy.get(c, 1.0) for c in chosen) / max(1, len(chosen)), 4),
-            "l3_domains": used}
+            "l3_domains": used, "policy": policy, "packages": sorted({_package_of(c) for c in chosen})}
 
 
 def numa_of(c: int):
