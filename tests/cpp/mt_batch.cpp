@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <barrier>
 #include <chrono>
@@ -83,6 +84,11 @@ struct Inputs {
     Dev l4u_buf;
     std::vector<uint8_t> l4u_out;
     uint32_t l4u_seg = 0, l4u_cs = 0, l4u_flags = 0;
+    std::vector<uint8_t> plain_out;               // wg_checksum_desc over the l4d batch
+    std::vector<uint8_t> vu_verdict, vu_l4;       // wg_verify_uniform over the l4u batch
+    std::vector<uint8_t> aead_out, aead_key;      // wg_aead_encrypt_batch over the l4u batch
+    uint32_t aead_rx = 0;
+    uint64_t aead_c0 = 0;
     std::vector<uint8_t> gso_in, gso_out, gso_in_after, gso_status;
     Dev gso_desc;
     uint64_t gso_n;
@@ -104,7 +110,12 @@ struct Inputs {
         l4u_buf = upload(load(dir + "/l4u.buf"));
         l4u_out = load(dir + "/l4u.out");
         std::ifstream pf(dir + "/params.txt");
-        pf >> l4u_seg >> l4u_cs >> l4u_flags;
+        pf >> l4u_seg >> l4u_cs >> l4u_flags >> aead_rx >> aead_c0;
+        plain_out = load(dir + "/l4d.plain");
+        vu_verdict = load(dir + "/l4u.verdict");
+        vu_l4 = load(dir + "/l4u.l4");
+        aead_out = load(dir + "/aead.out");
+        aead_key = load(dir + "/aead.key");
         gso_in = load(dir + "/gso.in");
         gso_out = load(dir + "/gso.out");
         gso_in_after = load(dir + "/gso.in_after");
@@ -118,7 +129,7 @@ constexpr uint8_t kSentinel = 0xA5;
 
 // A thread's outputs (device) and its host copies.
 struct Outs {
-    Dev verdict, l4, l4d, l4u, gso_in, gso_out, gso_res;
+    Dev verdict, l4, l4d, l4u, gso_in, gso_out, gso_res, plain, vuv, vul, aout, ast;
     std::vector<uint8_t> h;
     void make(const Inputs &in) {
         uint64_t vmax = std::max({in.vn[0], in.vn[1], in.vn[2]});
@@ -129,6 +140,15 @@ struct Outs {
         gso_in = upload(in.gso_in);
         gso_out = upload(std::vector<uint8_t>(in.gso_out.size(), kSentinel));
         gso_res = upload(std::vector<uint8_t>(in.gso_n * sizeof(wg_gso_result), 0));
+        plain = upload(std::vector<uint8_t>(in.plain_out.size(), 0));
+        vuv = upload(std::vector<uint8_t>(in.vu_verdict.size(), 0));
+        vul = upload(std::vector<uint8_t>(in.vu_l4.size(), 0));
+        aout = upload(std::vector<uint8_t>(in.aead_out.size(), 0));
+        ast = upload(std::vector<uint8_t>(in.vu_verdict.size(), 0));
+    }
+    void release() {
+        for (Dev *d : {&verdict, &l4, &l4d, &l4u, &gso_in, &gso_out, &gso_res, &plain, &vuv, &vul, &aout, &ast})
+            CK(hipFree(d->p));
     }
 };
 
@@ -141,8 +161,9 @@ bool same(const void *dev, const std::vector<uint8_t> &exp, hipStream_t st, std:
     return std::memcmp(h.data(), exp.data(), exp.size()) == 0;
 }
 
-enum Op { kVerify, kL4Desc, kL4Uniform, kGso, kNumOps };
-const char *op_name[kNumOps] = {"wg_verify_desc", "wg_l4csum_desc", "wg_l4csum_uniform", "wg_gso_split"};
+enum Op { kVerify, kL4Desc, kL4Uniform, kGso, kChecksum, kVerifyUniform, kAead, kNumOps };
+const char *op_name[kNumOps] = {"wg_verify_desc", "wg_l4csum_desc",        "wg_l4csum_uniform",    "wg_gso_split",
+                                "wg_checksum_desc", "wg_verify_uniform", "wg_aead_encrypt_batch"};
 
 // Each thread's verify kinds, phase-shifted per thread: runs of mixed batches
 // (the default per-call choice reaches the compacting path after two mixed
@@ -168,6 +189,16 @@ int call(Op op, const Inputs &in, Outs &o, int vk, hipStream_t st, bool small = 
         return wg_gso_split(static_cast<uint8_t *>(o.gso_in.p), static_cast<const wg_gso_desc *>(in.gso_desc.p),
                             cut(in.gso_n, 2), static_cast<uint8_t *>(o.gso_out.p), static_cast<wg_gso_result *>(o.gso_res.p),
                             st);
+    case kChecksum:
+        return wg_checksum_desc(static_cast<const uint8_t *>(in.l4d_buf.p), static_cast<const wg_pkt_desc *>(in.l4d_desc.p),
+                                cut(in.l4d_n, 64), static_cast<uint16_t *>(o.plain.p), st);
+    case kVerifyUniform:
+        return wg_verify_uniform(static_cast<const uint8_t *>(in.l4u_buf.p), cut(in.l4u_buf.n, 64ull * in.l4u_seg),
+                                 in.l4u_seg, static_cast<uint8_t *>(o.vuv.p), static_cast<uint16_t *>(o.vul.p), st);
+    case kAead:
+        return wg_aead_encrypt_batch(static_cast<const uint8_t *>(in.l4u_buf.p), cut(in.l4u_buf.n, 64ull * in.l4u_seg),
+                                     in.l4u_seg, in.aead_key.data(), in.aead_rx, in.aead_c0,
+                                     static_cast<uint8_t *>(o.aout.p), static_cast<int8_t *>(o.ast.p), st);
     default:
         return WG_ERR_INVALID;
     }
@@ -184,6 +215,15 @@ void refill(Op op, const Inputs &in, Outs &o, int vk, hipStream_t st) {
     case kGso:
         CK(hipMemsetAsync(o.gso_out.p, kSentinel, o.gso_out.n, st));
         CK(hipMemsetAsync(o.gso_res.p, 0xff, o.gso_res.n, st));
+        break;
+    case kChecksum: CK(hipMemsetAsync(o.plain.p, kSentinel, o.plain.n, st)); break;
+    case kVerifyUniform:
+        CK(hipMemsetAsync(o.vuv.p, kSentinel, o.vuv.n, st));
+        CK(hipMemsetAsync(o.vul.p, kSentinel, o.vul.n, st));
+        break;
+    case kAead:
+        CK(hipMemsetAsync(o.aout.p, kSentinel, o.aout.n, st));
+        CK(hipMemsetAsync(o.ast.p, kSentinel, o.ast.n, st));
         break;
     default: break;
     }
@@ -206,6 +246,15 @@ bool check(Op op, const Inputs &in, Outs &o, int vk, hipStream_t st) {
             if ((int8_t)r[i * sizeof(wg_gso_result) + offsetof(wg_gso_result, status)] != (int8_t)in.gso_status[i])
                 return false;
         return true;
+    }
+    case kChecksum: return same(o.plain.p, in.plain_out, st, o.h);
+    case kVerifyUniform: return same(o.vuv.p, in.vu_verdict, st, o.h) && same(o.vul.p, in.vu_l4, st, o.h);
+    case kAead: {
+        // messages equal the oracle's; every status 0
+        if (!same(o.aout.p, in.aead_out, st, o.h))
+            return false;
+        const std::vector<uint8_t> zeros(in.vu_verdict.size(), 0);
+        return same(o.ast.p, zeros, st, o.h);
     }
     default: return false;
     }
@@ -278,8 +327,7 @@ int conform(const Inputs &in, int threads, int iters, const std::string &mode) {
             }
             if (own)
                 CK(hipStreamDestroy(own));
-            for (Dev *d : {&o.verdict, &o.l4, &o.l4d, &o.l4u, &o.gso_in, &o.gso_out, &o.gso_res})
-                CK(hipFree(d->p));
+            o.release();
         });
     }
     for (auto &x : th) x.join();
@@ -343,8 +391,7 @@ int rate(const Inputs &in, int threads, int ncalls, bool small) {
                 enq[t] = ncalls / (t1 - t0);
                 done[t] = ncalls / (t2 - t0);
                 CK(hipStreamDestroy(st));
-                for (Dev *d : {&o.verdict, &o.l4, &o.l4d, &o.l4u, &o.gso_in, &o.gso_out, &o.gso_res})
-                    CK(hipFree(d->p));
+                o.release();
             });
         }
         for (auto &x : th) x.join();

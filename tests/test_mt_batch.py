@@ -7,8 +7,9 @@ tests/cpp/mt_batch.cpp (built by build()) drives the C ABI from 1-16
 threads; this file writes its inputs and the oracle's expected outputs and
 reads its JSON.  Conformance: every call's outputs are refilled with a
 sentinel on the calling stream first and compared byte for byte with the
-oracle after it, for wg_verify_desc, wg_l4csum_desc, wg_l4csum_uniform and
-wg_gso_split, with the threads on
+oracle after it, for wg_verify_desc, wg_l4csum_desc, wg_l4csum_uniform,
+wg_gso_split, wg_checksum_desc, wg_verify_uniform and wg_aead_encrypt_batch,
+with the threads on
 
   * their own streams;
   * hipStreamPerThread — one handle value that is a different stream in each
@@ -74,11 +75,34 @@ def write_inputs(d: Path, seed: int = 61, n: int = 3000) -> dict:
     buf.tofile(d / "l4d.buf")
     desc.tofile(d / "l4d.desc")
     oracle.l4_desc(buf, desc).tofile(d / "l4d.out")
-    # uniform PacketBatch: 2,000 x 1,500 B and a short last segment
-    ubuf = rng.integers(0, 256, 2000 * 1500 - 700, dtype=np.uint8)
+    oracle.checksum_desc(buf, desc).tofile(d / "l4d.plain")
+    # uniform PacketBatch: 2,000 valid 1,500-B packets of every family, the
+    # last one cut to 800 B (a short last segment), every 9th corrupted
+    segs = []
+    for i in range(2000):
+        v6, tcp = bool(i & 1), bool(i & 2)
+        hl, al = (40 if v6 else 20) + (20 if tcp else 8), 16 if v6 else 4
+        p = bytearray(tv.pktbuild.build(v6, tcp, rng.integers(0, 256, 1500 - hl, dtype=np.uint8).tobytes(),
+                                        rng.integers(0, 256, al, dtype=np.uint8).tobytes(),
+                                        rng.integers(0, 256, al, dtype=np.uint8).tobytes()))
+        if i % 9 == 0:
+            p[int(rng.integers(0, 1500))] ^= 0x10
+        segs.append(bytes(p))
+    ubuf = np.frombuffer(b"".join(segs), np.uint8)[: 2000 * 1500 - 700].copy()
     ubuf.tofile(d / "l4u.buf")
     oracle.l4_uniform(ubuf, 1500, 20, 2).tofile(d / "l4u.out")
-    (d / "params.txt").write_text("1500 20 2\n")
+    ud = np.zeros(2000, dtype=oracle.PKT_DESC)
+    ud["offset"] = np.arange(2000) * 1500
+    ud["len"] = [min(1500, ubuf.size - 1500 * i) for i in range(2000)]
+    uv, ul4 = oracle.verify_desc(ubuf, ud)
+    uv.astype(np.uint8).tofile(d / "l4u.verdict")
+    ul4.astype(np.uint16).tofile(d / "l4u.l4")
+    key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    rx, c0 = 0x1234567, (1 << 33) + 5
+    (d / "aead.key").write_bytes(key)
+    oracle.wg_encrypt_batch(key, rx, c0, ubuf, 1500).tofile(d / "aead.out")
+    (d / "params.txt").write_text(f"1500 20 2 {rx} {c0}\n")
+    stats["uniform_verified_ok"] = float(np.mean((uv & tv.OK) == tv.OK))
     # GSO: random super-buffers the oracle splits with status 0
     cases = []
     while len(cases) < 48:
@@ -136,6 +160,8 @@ def test_inputs_match_oracle_self_consistency(tmp_path):
     v = np.fromfile(tmp_path / "verify_mixed.desc", dtype=oracle.PKT_DESC)
     assert (v["len"] <= 64).any() and (v["len"] > 64).any()
     assert st["long"]["verified_ok"] > 0.5
+    assert 0.5 < st["uniform_verified_ok"] < 1.0
+    assert (tmp_path / "aead.out").stat().st_size == 1999 * 1536 + 32 + 800
 
 
 @pytest.fixture(scope="module")
@@ -149,8 +175,8 @@ def inputs(tmp_path_factory):
 @pytest.mark.parametrize("verify_small", [7, 6])
 @pytest.mark.parametrize("stream", ["perthread", "own", "legacy"])
 def test_mt_conformance(gpu, inputs, stream, verify_small):
-    """4 threads x 50 iterations x the four entry points, every call's
-    outputs equal the oracle's."""
+    """4 threads x 50 iterations x seven entry points, every call's outputs
+    equal the oracle's."""
     res = run_harness(inputs, "conform", 4, 50, stream, env_extra={"WG_VERIFY_SMALL": str(verify_small)})
     print(json.dumps(res))
     assert res["errors"] == 0 and res["mismatched"] == 0, res
