@@ -30,27 +30,37 @@ typedef struct {
     uint8_t *out;
     uint64_t lo, hi;
     int rc;
+    int slot;
 } job;
 
-/* Each worker thread fetches the cipher in its own library context: the
- * default context's provider objects are shared by every thread, and their
- * reference counts and locks made 16 workers on two sockets scale 3x over
- * one (round 6, profiles/r06_*aead*); a private context keeps them per
- * thread.  Returns the cipher (or NULL) and the context to free. */
-static EVP_CIPHER *own_cipher(OSSL_LIB_CTX **lc) {
-    *lc = OSSL_LIB_CTX_new();
-    return *lc ? EVP_CIPHER_fetch(*lc, "ChaCha20-Poly1305", NULL) : NULL;
-}
+/* Worker t of a call fetches the cipher in library context t: the default
+ * context's provider objects are shared by every thread, and their reference
+ * counts and locks made 16 workers on two sockets scale 3x over one (round
+ * 6, profiles/r06_aead_bench.json).  The contexts are made once and kept
+ * (loading a provider per call per worker cost a visible part of a call);
+ * worker t of one call is the only user of slot t, and calls come one at a
+ * time from bench.py's thread. */
+#define OSS_SLOTS 256
+static struct {
+    OSSL_LIB_CTX *lc;
+    EVP_CIPHER *c;
+} g_slot[OSS_SLOTS];
 
-static void free_cipher(EVP_CIPHER *c, OSSL_LIB_CTX *lc) {
-    EVP_CIPHER_free(c);
-    OSSL_LIB_CTX_free(lc);
+static EVP_CIPHER *slot_cipher(int t) {
+    if (t < 0 || t >= OSS_SLOTS)
+        return NULL;
+    if (!g_slot[t].c) {
+        if (!g_slot[t].lc)
+            g_slot[t].lc = OSSL_LIB_CTX_new();
+        if (g_slot[t].lc)
+            g_slot[t].c = EVP_CIPHER_fetch(g_slot[t].lc, "ChaCha20-Poly1305", NULL);
+    }
+    return g_slot[t].c;
 }
 
 static void *run(void *arg) {
     job *j = (job *)arg;
-    OSSL_LIB_CTX *lc = NULL;
-    EVP_CIPHER *cipher = own_cipher(&lc);
+    EVP_CIPHER *cipher = slot_cipher(j->slot);
     EVP_CIPHER_CTX *ctx = EVP_CIPHER_CTX_new();
     const size_t stride = 16 + (((size_t)j->seg + 15) & ~(size_t)15) + 16;
     j->rc = ctx && cipher && EVP_EncryptInit_ex(ctx, cipher, NULL, j->key, NULL) == 1 ? 0 : -1;
@@ -76,7 +86,6 @@ static void *run(void *arg) {
             j->rc = -1;
     }
     EVP_CIPHER_CTX_free(ctx);
-    free_cipher(cipher, lc);
     return NULL;
 }
 
@@ -92,7 +101,7 @@ int oss_wg_encrypt_batch(const uint8_t key[32], uint32_t rx, uint64_t c0, const 
     job jobs[256];
     for (int t = 0; t < threads; t++) {
         jobs[t] = (job){key, rx, c0, in, total, seg, out, n * (uint64_t)t / (uint64_t)threads,
-                        n * (uint64_t)(t + 1) / (uint64_t)threads, 0};
+                        n * (uint64_t)(t + 1) / (uint64_t)threads, 0, t};
         if (!spawn)
             run(&jobs[t]);
         else {
@@ -117,6 +126,7 @@ typedef struct {
     int8_t *status;
     uint64_t lo, hi;
     int rc;
+    int slot;
 } djob;
 
 /* Peer::decrypt (proto/proto.cpp:496-523) per message of a GRO batch: the
@@ -124,8 +134,7 @@ typedef struct {
  * gets status -1 (plaintext zeroed on a bad tag, as libsodium leaves it). */
 static void *drun(void *arg) {
     djob *j = (djob *)arg;
-    OSSL_LIB_CTX *lc = NULL;
-    EVP_CIPHER *cipher = own_cipher(&lc);
+    EVP_CIPHER *cipher = slot_cipher(j->slot);
     EVP_CIPHER_CTX *ctx = EVP_CIPHER_CTX_new();
     const uint64_t ostride = j->seg > 32 ? j->seg - 32 : 0;
     j->rc = ctx && cipher && EVP_DecryptInit_ex(ctx, cipher, NULL, j->key, NULL) == 1 ? 0 : -1;
@@ -153,7 +162,6 @@ static void *drun(void *arg) {
         j->status[i] = ok ? 0 : -1;
     }
     EVP_CIPHER_CTX_free(ctx);
-    free_cipher(cipher, lc);
     return NULL;
 }
 
@@ -169,7 +177,7 @@ int oss_wg_decrypt_batch(const uint8_t key[32], const uint8_t *in, uint64_t tota
     djob jobs[256];
     for (int t = 0; t < threads; t++) {
         jobs[t] = (djob){key, in, total, seg, out, status, n * (uint64_t)t / (uint64_t)threads,
-                         n * (uint64_t)(t + 1) / (uint64_t)threads, 0};
+                         n * (uint64_t)(t + 1) / (uint64_t)threads, 0, t};
         if (!spawn)
             drun(&jobs[t]);
         else {
