@@ -16,8 +16,8 @@ with the threads on
     thread (wg_verify_desc's per-stream state was keyed
     by the raw handle, so these threads shared entry lists and counters);
   * the legacy NULL stream (one stream shared by every thread);
-  * a fresh stream per call, destroyed while its work is pending (a later
-    stream can get the same handle value).
+  * a fresh stream per call, destroyed right after its launch (the next
+    stream gets the same handle value).
 
 `verify_small` 6 forces the compacting path on every call that has state;
 the default (7) reaches it on runs of mixed batches.
@@ -187,8 +187,9 @@ def test_mt_conformance(gpu, inputs, stream, verify_small):
 @pytest.mark.parametrize("verify_small", [7, 6])
 def test_mt_stream_churn(gpu, inputs, verify_small):
     """4 threads, each verifying 50 mixed / small / long batches on a fresh
-    stream per call, destroyed right after the launch (work still pending):
-    handle values come back while earlier work runs; every call's verdicts
+    stream per call, destroyed right after the launch (hipStreamDestroy waits
+    for the pending work, profiles/r06_stream_identity.txt): the next stream
+    gets the same handle value and inherits its state; every call's verdicts
     and L4 results equal the oracle's."""
     res = run_harness(inputs, "conform", 4, 50, "churn", env_extra={"WG_VERIFY_SMALL": str(verify_small)})
     print(json.dumps(res))
@@ -200,5 +201,14 @@ def test_mt_sixteen_threads(gpu, inputs):
     """16 threads on their own streams (one per tun queue of a 16-queue
     device), 20 iterations each."""
     res = run_harness(inputs, "conform", 16, 20, "own")
+    print(json.dumps(res))
+    assert res["errors"] == 0 and res["mismatched"] == 0, res
+
+
+@pytest.mark.gpu
+def test_mt_one_thread(gpu, inputs):
+    """The same conformance run with one thread (the 1-thread point of the
+    launch-rate figure)."""
+    res = run_harness(inputs, "conform", 1, 50, "own")
     print(json.dumps(res))
     assert res["errors"] == 0 and res["mismatched"] == 0, res
