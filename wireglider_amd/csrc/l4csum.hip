@@ -214,10 +214,25 @@ __device__ __forceinline__ uint32_t lane_sum(const v4u W[5], uintptr_t a, uint32
                              W[3][2], W[3][3], W[4][0], W[4][1], W[4][2], W[4][3]};
     const uint32_t s = (uint32_t)(a & 15u), q4 = s >> 2, sh = s & 3u;
     uint32_t sr = 0, sq = 0;
+#ifdef WG_LANE_BARREL
+    // experiment: the packet's dwords brought to the front by two select
+    // stages (2 dwords, then 1): no per-word branch ladder when the lanes of
+    // a wave sit at different dword offsets (config 4's 64-B packets lie
+    // 8-B aligned between 9000-B ones)
+    // (bit masks rather than ?: selects: the compiler turned the selects
+    // into a dynamically indexed copy of Wd in scratch)
+    const uint32_t m2 = 0u - ((q4 >> 1) & 1u), m1 = 0u - (q4 & 1u);
+    const auto xw = [&](uint32_t i) { return Wd[i] ^ ((Wd[i] ^ Wd[i + 2]) & m2); };  // dword i + 2 * b2, i <= 17
+    const auto pick = [&](uint32_t x0, uint32_t x1) { return x0 ^ ((x0 ^ x1) & m1); };
+#endif
 #pragma unroll
     for (uint32_t m = 0; m < 16; m++) {
+#ifdef WG_LANE_BARREL
+        const uint32_t lo = pick(xw(m), xw(m + 1)), hi = pick(xw(m + 1), xw(m + 2));
+#else
         const uint32_t lo = q4 == 0 ? Wd[m] : q4 == 1 ? Wd[m + 1] : q4 == 2 ? Wd[m + 2] : Wd[m + 3];
         const uint32_t hi = q4 == 0 ? Wd[m + 1] : q4 == 1 ? Wd[m + 2] : q4 == 2 ? Wd[m + 3] : Wd[m + 4];
+#endif
         const uint32_t r = bytes_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, len);
         sr = hacc(sr, bytes_from(r, m, o0));
         if (kL4) {
@@ -780,10 +795,21 @@ __device__ __forceinline__ void verify_lane_decode(const v4u W[5], uintptr_t a, 
                              W[4][0], W[4][1], W[4][2], W[4][3]};
     const uint32_t s = (uint32_t)(a & 15u), q4 = s >> 2, sh = s & 3u;
     uint32_t R[16];
+#ifdef WG_LANE_BARREL
+    // (bit masks rather than ?: selects: the compiler turned the selects
+    // into a dynamically indexed copy of Wd in scratch)
+    const uint32_t m2 = 0u - ((q4 >> 1) & 1u), m1 = 0u - (q4 & 1u);
+    const auto xw = [&](uint32_t i) { return Wd[i] ^ ((Wd[i] ^ Wd[i + 2]) & m2); };  // dword i + 2 * b2, i <= 17
+    const auto pick = [&](uint32_t x0, uint32_t x1) { return x0 ^ ((x0 ^ x1) & m1); };
+#endif
 #pragma unroll
     for (uint32_t m = 0; m < 16; m++) {
+#ifdef WG_LANE_BARREL
+        const uint32_t lo = pick(xw(m), xw(m + 1)), hi = pick(xw(m + 1), xw(m + 2));
+#else
         const uint32_t lo = q4 == 0 ? Wd[m] : q4 == 1 ? Wd[m + 1] : q4 == 2 ? Wd[m + 2] : Wd[m + 3];
         const uint32_t hi = q4 == 0 ? Wd[m + 1] : q4 == 1 ? Wd[m + 2] : q4 == 2 ? Wd[m + 3] : Wd[m + 4];
+#endif
         R[m] = bytes_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, len);
     }
     uint32_t v = 0, c = 0;
