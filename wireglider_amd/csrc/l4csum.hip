@@ -199,6 +199,47 @@ __device__ __forceinline__ void lane_chunks(uintptr_t a, uint32_t len, bool use,
     }
 }
 
+// The lane paths' realignment: the packet's 16 dwords R[m] (bytes 4m..4m+3
+// of the packet at a, bytes at positions >= len zeroed) from the 20 dwords of
+// its five aligned chunks.  The dword offset q4 = (a & 15) >> 2 picks
+// Wd[m + q4]:
+//  * q4 the same in every lane of the wave (aligned batches): one scalar
+//    branch to a straight-line copy for that q4 — no per-lane selects;
+//  * q4 different across the wave (config 4's 64-B packets lie 8-B aligned
+//    between 9000-B ones): two bit-mask select stages (by 2 dwords, then by
+//    1) for every lane.  A 4-way ?: per word compiled to a branch ladder
+//    that ran every case the wave held; plain ?: selects were turned into a
+//    dynamically indexed copy of Wd in scratch.
+// Measured (profiles/r06_barrel_ab.txt): the mask stages alone took config
+// 4's 64-B sub-batch 50.9 -> 47.0 us but a uniform 64-B verify batch 12.3 ->
+// 16.5 us (VALU it did not need); the scalar branch keeps the latter.
+template <uint32_t Q>
+__device__ __forceinline__ void realign_q(const uint32_t Wd[20], uint32_t sh, uint32_t len, uint32_t R[16]) {
+#pragma unroll
+    for (uint32_t m = 0; m < 16; m++)
+        R[m] = bytes_below(__builtin_amdgcn_alignbyte(Wd[m + Q + 1], Wd[m + Q], sh), m, len);
+}
+
+__device__ __forceinline__ void lane_realign(const uint32_t Wd[20], uintptr_t a, uint32_t len, uint32_t R[16]) {
+    const uint32_t s = (uint32_t)(a & 15u), q4 = s >> 2, sh = s & 3u;
+    const uint32_t qf = (uint32_t)__builtin_amdgcn_readfirstlane((int)q4);
+    if (__ballot(q4 != qf) == 0) {  // wave-uniform
+        switch (qf) {
+        case 0: realign_q<0>(Wd, sh, len, R); break;
+        case 1: realign_q<1>(Wd, sh, len, R); break;
+        case 2: realign_q<2>(Wd, sh, len, R); break;
+        default: realign_q<3>(Wd, sh, len, R); break;
+        }
+        return;
+    }
+    const uint32_t m2 = 0u - ((q4 >> 1) & 1u), m1 = 0u - (q4 & 1u);
+    const auto xw = [&](uint32_t i) { return Wd[i] ^ ((Wd[i] ^ Wd[i + 2]) & m2); };  // Wd[i + 2 * (q4 >> 1)]
+    const auto pick = [&](uint32_t x0, uint32_t x1) { return x0 ^ ((x0 ^ x1) & m1); };
+#pragma unroll
+    for (uint32_t m = 0; m < 16; m++)
+        R[m] = bytes_below(__builtin_amdgcn_alignbyte(pick(xw(m + 1), xw(m + 2)), pick(xw(m), xw(m + 1)), sh), m, len);
+}
+
 // ... summed: the chunks funnel-shifted into 16 packet-relative dwords
 // (bytes past the packet zeroed), so the region and address masks are
 // per-dword constants of len / csum_start and the addresses static dwords.
@@ -212,28 +253,12 @@ __device__ __forceinline__ uint32_t lane_sum(const v4u W[5], uintptr_t a, uint32
     const uint32_t Wd[20] = {W[0][0], W[0][1], W[0][2], W[0][3], W[1][0], W[1][1], W[1][2],
                              W[1][3], W[2][0], W[2][1], W[2][2], W[2][3], W[3][0], W[3][1],
                              W[3][2], W[3][3], W[4][0], W[4][1], W[4][2], W[4][3]};
-    const uint32_t s = (uint32_t)(a & 15u), q4 = s >> 2, sh = s & 3u;
+    uint32_t R[16];
+    lane_realign(Wd, a, len, R);
     uint32_t sr = 0, sq = 0;
-#ifdef WG_LANE_BARREL
-    // experiment: the packet's dwords brought to the front by two select
-    // stages (2 dwords, then 1): no per-word branch ladder when the lanes of
-    // a wave sit at different dword offsets (config 4's 64-B packets lie
-    // 8-B aligned between 9000-B ones)
-    // (bit masks rather than ?: selects: the compiler turned the selects
-    // into a dynamically indexed copy of Wd in scratch)
-    const uint32_t m2 = 0u - ((q4 >> 1) & 1u), m1 = 0u - (q4 & 1u);
-    const auto xw = [&](uint32_t i) { return Wd[i] ^ ((Wd[i] ^ Wd[i + 2]) & m2); };  // dword i + 2 * b2, i <= 17
-    const auto pick = [&](uint32_t x0, uint32_t x1) { return x0 ^ ((x0 ^ x1) & m1); };
-#endif
 #pragma unroll
     for (uint32_t m = 0; m < 16; m++) {
-#ifdef WG_LANE_BARREL
-        const uint32_t lo = pick(xw(m), xw(m + 1)), hi = pick(xw(m + 1), xw(m + 2));
-#else
-        const uint32_t lo = q4 == 0 ? Wd[m] : q4 == 1 ? Wd[m + 1] : q4 == 2 ? Wd[m + 2] : Wd[m + 3];
-        const uint32_t hi = q4 == 0 ? Wd[m + 1] : q4 == 1 ? Wd[m + 2] : q4 == 2 ? Wd[m + 3] : Wd[m + 4];
-#endif
-        const uint32_t r = bytes_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, len);
+        const uint32_t r = R[m];
         sr = hacc(sr, bytes_from(r, m, o0));
         if (kL4) {
             if (m == 3u || m == 4u)  // v6 8-39, v4 12-19
@@ -793,25 +818,8 @@ __device__ __forceinline__ void verify_lane_decode(const v4u W[5], uintptr_t a, 
     const uint32_t Wd[20] = {W[0][0], W[0][1], W[0][2], W[0][3], W[1][0], W[1][1], W[1][2], W[1][3],
                              W[2][0], W[2][1], W[2][2], W[2][3], W[3][0], W[3][1], W[3][2], W[3][3],
                              W[4][0], W[4][1], W[4][2], W[4][3]};
-    const uint32_t s = (uint32_t)(a & 15u), q4 = s >> 2, sh = s & 3u;
     uint32_t R[16];
-#ifdef WG_LANE_BARREL
-    // (bit masks rather than ?: selects: the compiler turned the selects
-    // into a dynamically indexed copy of Wd in scratch)
-    const uint32_t m2 = 0u - ((q4 >> 1) & 1u), m1 = 0u - (q4 & 1u);
-    const auto xw = [&](uint32_t i) { return Wd[i] ^ ((Wd[i] ^ Wd[i + 2]) & m2); };  // dword i + 2 * b2, i <= 17
-    const auto pick = [&](uint32_t x0, uint32_t x1) { return x0 ^ ((x0 ^ x1) & m1); };
-#endif
-#pragma unroll
-    for (uint32_t m = 0; m < 16; m++) {
-#ifdef WG_LANE_BARREL
-        const uint32_t lo = pick(xw(m), xw(m + 1)), hi = pick(xw(m + 1), xw(m + 2));
-#else
-        const uint32_t lo = q4 == 0 ? Wd[m] : q4 == 1 ? Wd[m + 1] : q4 == 2 ? Wd[m + 2] : Wd[m + 3];
-        const uint32_t hi = q4 == 0 ? Wd[m + 1] : q4 == 1 ? Wd[m + 2] : q4 == 2 ? Wd[m + 3] : Wd[m + 4];
-#endif
-        R[m] = bytes_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, len);
-    }
+    lane_realign(Wd, a, len, R);
     uint32_t v = 0, c = 0;
     if (len >= 1) {
         const uint32_t b0 = R[0] & 0xffu;
