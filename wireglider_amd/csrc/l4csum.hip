@@ -246,19 +246,33 @@ __device__ __forceinline__ void lane_realign(const uint32_t Wd[20], uintptr_t a,
 // Returns the pre-complement folded sum t (region, byte-swapped when it pairs
 // from an odd packet offset, + pseudo-header when kL4); the caller's result
 // is ~fold16_32(t).
-template <bool kL4>
+template <bool kL4, bool kUni = false>
 __device__ __forceinline__ uint32_t lane_sum(const v4u W[5], uintptr_t a, uint32_t len, uint32_t cs, uint32_t fl) {
     const uint32_t o0 = cs < len ? cs : len;
     const bool v6 = fl & WG_PKT_V6;
     const uint32_t Wd[20] = {W[0][0], W[0][1], W[0][2], W[0][3], W[1][0], W[1][1], W[1][2],
                              W[1][3], W[2][0], W[2][1], W[2][2], W[2][3], W[3][0], W[3][1],
                              W[3][2], W[3][3], W[4][0], W[4][1], W[4][2], W[4][3]};
+    // kUni: a uniform PacketBatch's lane kernel (segments of one size: the
+    // dword offset is the same across a wave when the size is a multiple of
+    // 16) keeps the per-word 4-way select, whose branches then run one case
+    // (the wave-uniform test of lane_realign in front cost a 64-B uniform
+    // verify batch +3.4 %, profiles/r06_hybrid_ab.txt)
     uint32_t R[16];
-    lane_realign(Wd, a, len, R);
+    if constexpr (!kUni)
+        lane_realign(Wd, a, len, R);
+    const uint32_t s = (uint32_t)(a & 15u), q4 = s >> 2, sh = s & 3u;
     uint32_t sr = 0, sq = 0;
 #pragma unroll
     for (uint32_t m = 0; m < 16; m++) {
-        const uint32_t r = R[m];
+        uint32_t r;
+        if constexpr (kUni) {
+            const uint32_t lo = q4 == 0 ? Wd[m] : q4 == 1 ? Wd[m + 1] : q4 == 2 ? Wd[m + 2] : Wd[m + 3];
+            const uint32_t hi = q4 == 0 ? Wd[m + 1] : q4 == 1 ? Wd[m + 2] : q4 == 2 ? Wd[m + 3] : Wd[m + 4];
+            r = bytes_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, len);
+        } else {
+            r = R[m];
+        }
         sr = hacc(sr, bytes_from(r, m, o0));
         if (kL4) {
             if (m == 3u || m == 4u)  // v6 8-39, v4 12-19
@@ -330,7 +344,7 @@ __global__ __launch_bounds__(256) void l4csum_uniform_small_kernel(L4Params p) {
     const uint32_t len = live ? (rem < p.seg ? (uint32_t)rem : p.seg) : 0u;
     v4u W[5];
     lane_chunks(a, len, live && len, W);
-    const uint32_t t = lane_sum<true>(W, a, len, live ? p.cs : 0u, live ? p.flags : 0u);
+    const uint32_t t = lane_sum<true, true>(W, a, len, live ? p.cs : 0u, live ? p.flags : 0u);
     if (live)
         p.out[i] = (uint16_t)(~fold16_32(t) & 0xffffu);
 }
@@ -804,22 +818,35 @@ __device__ __forceinline__ void verify_lane_load(uintptr_t a, uint32_t len, bool
     }
 }
 
+template <bool kUni>
 __device__ __forceinline__ void verify_lane_decode(const v4u W[5], uintptr_t a, uint32_t len, uint32_t &rv,
                                                    uint32_t &rc);
 
+template <bool kUni = false>
 __device__ __forceinline__ void verify_lane(uintptr_t a, uint32_t len, bool use, uint32_t &rv, uint32_t &rc) {
     v4u W[5];
     verify_lane_load(a, len, use, W);
-    verify_lane_decode(W, a, len, rv, rc);
+    verify_lane_decode<kUni>(W, a, len, rv, rc);
 }
 
+template <bool kUni>
 __device__ __forceinline__ void verify_lane_decode(const v4u W[5], uintptr_t a, uint32_t len, uint32_t &rv,
                                                    uint32_t &rc) {
     const uint32_t Wd[20] = {W[0][0], W[0][1], W[0][2], W[0][3], W[1][0], W[1][1], W[1][2], W[1][3],
                              W[2][0], W[2][1], W[2][2], W[2][3], W[3][0], W[3][1], W[3][2], W[3][3],
                              W[4][0], W[4][1], W[4][2], W[4][3]};
     uint32_t R[16];
-    lane_realign(Wd, a, len, R);
+    if constexpr (kUni) {  // as lane_sum's kUni: the per-word 4-way select
+        const uint32_t s = (uint32_t)(a & 15u), q4 = s >> 2, sh = s & 3u;
+#pragma unroll
+        for (uint32_t m = 0; m < 16; m++) {
+            const uint32_t lo = q4 == 0 ? Wd[m] : q4 == 1 ? Wd[m + 1] : q4 == 2 ? Wd[m + 2] : Wd[m + 3];
+            const uint32_t hi = q4 == 0 ? Wd[m + 1] : q4 == 1 ? Wd[m + 2] : q4 == 2 ? Wd[m + 3] : Wd[m + 4];
+            R[m] = bytes_below(__builtin_amdgcn_alignbyte(hi, lo, sh), m, len);
+        }
+    } else {
+        lane_realign(Wd, a, len, R);
+    }
     uint32_t v = 0, c = 0;
     if (len >= 1) {
         const uint32_t b0 = R[0] & 0xffu;
@@ -877,7 +904,7 @@ __global__ __launch_bounds__(256) void verify_uniform_lane_kernel(VerifyParams p
     const uint64_t o = live ? i * (uint64_t)p.seg : 0u;
     const uint32_t len = live ? (p.total_len - o < p.seg ? (uint32_t)(p.total_len - o) : p.seg) : 0u;
     uint32_t rv = 0, rc = 0;
-    verify_lane(reinterpret_cast<uintptr_t>(p.base) + o, len, live, rv, rc);
+    verify_lane<true>(reinterpret_cast<uintptr_t>(p.base) + o, len, live, rv, rc);
     if (live) {
         p.verdict[i] = (uint8_t)rv;
         if (p.l4)
