@@ -286,7 +286,8 @@ int wg_aead_decrypt_verify_batch(const uint8_t *dev_in, uint64_t total_len, uint
  *     reference's outbuf advances over accepted messages only,
  *     worker/encap.cpp:138-140, while encrypt_nonce counts every segment);
  *   dev_work: 4 * (n + 1024) bytes of scratch; dev_total (nullable): messages
- *     in all, i.e. counter0 + *dev_total is the peer's next encrypt_nonce.
+ *     in all, i.e. counter0 + *dev_total is the peer's next encrypt_nonce
+ *     (0 for n = 0, written on the stream like every other output).
  * n <= 2^20 super-buffers per call and max_segments * n < 2^32 (the counter
  * scan indexes messages in 32 bits; larger calls are WG_ERR_INVALID, never a
  * repeated nonce).  A message whose counter reaches RejectAfterMessages is

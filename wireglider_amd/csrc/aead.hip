@@ -1709,6 +1709,16 @@ static int encap_launch(const uint8_t *dev_in, const uint8_t *dev_seg, const wg_
     return launch_aead<false>(p, max_segment_size, st, t);
 }
 
+// An empty batch still reports its message count: *dev_total = 0 (or the
+// chained base), so counter0 + *dev_total stays the peer's next nonce.
+static int encap_empty_total(uint64_t *dev_total, const uint64_t *dev_base, hipStream_t st) {
+    if (!dev_total)
+        return WG_OK;
+    const hipError_t e = dev_base ? hipMemcpyAsync(dev_total, dev_base, sizeof(uint64_t), hipMemcpyDeviceToDevice, st)
+                                  : hipMemsetAsync(dev_total, 0, sizeof(uint64_t), st);
+    return e == hipSuccess ? WG_OK : WG_ERR_RUNTIME;
+}
+
 // the arguments both encap entry points share
 static bool encap_args_ok(const uint8_t *key, uint64_t n, const void *dev_in, const void *dev_seg,
                           const wg_gso_desc *dev_desc, const wg_gso_result *dev_gso_res,
@@ -1738,7 +1748,7 @@ extern "C" int wg_encap_encrypt(const uint8_t *dev_in, const uint8_t *dev_seg, c
                        dev_msgs, dev_res, dev_work))
         return WG_ERR_INVALID;
     if (!n)
-        return WG_OK;
+        return encap_empty_total(dev_total, nullptr, static_cast<hipStream_t>(stream));
     return encap_launch(dev_in, dev_seg, dev_desc, dev_gso_res, n, key, receiver_index, counter0, dev_msg_offset,
                         msg_cap, max_segments, max_segment_size, dev_msgs, dev_res, dev_work, dev_total, 1u,
                         nullptr, static_cast<hipStream_t>(stream), tune(), false);
@@ -1782,7 +1792,7 @@ int encap_batch_launch(uint8_t *dev_in, const wg_gso_desc *dev_desc, uint64_t n,
                        dev_msgs, dev_res, dev_work))
         return WG_ERR_INVALID;
     if (!n)
-        return WG_OK;
+        return encap_empty_total(dev_total, dev_base, st);
     // one knob snapshot for the split and the AEAD: header synthesis
     // (encap_synth) needs the staged kernel, and the split must skip exactly
     // the super-buffers the AEAD synthesizes
