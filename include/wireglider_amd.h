@@ -445,6 +445,9 @@ int wg_device_count(void);
  *                of 4 descriptors whose packets are all <= 64 B are summed a
  *                lane per packet, every other group wave-per-packet; 0 =
  *                wave-per-packet for all
+ *   "lane_coop"  l4_small = 5's lane role: the small packets' bytes loaded
+ *                by the wave together and handed to their lanes through LDS
+ *                (1, default) or each lane loading its own (0)
  *   "l4_small_uniform" uniform batches with segment_size <= 64: a lane per
  *                segment (2, default) or the wave-per-packet kernel (0)
  *   "l4_unroll"  descriptor batches: 16-B loads in flight per lane while

@@ -19,7 +19,7 @@ sys.path.insert(0, str(ROOT))
 
 KEYS = ("l4_blocks", "l4_nt", "l4_small", "l4_small_uniform", "verify_small", "verify_auto_t", "verify_k2min",
         "gso_blocks", "gso_waves", "gso_split", "gso_spw", "encap_spw", "gso_groups", "gso_ablate", "l4_unroll",
-        "host_chunk_mb", "l4_coop", "l4_coop_waves", "aead_k", "aead_stage", "encap_parts", "encap_synth", "host_d2h")
+        "host_chunk_mb", "l4_coop", "l4_coop_waves", "aead_k", "aead_stage", "encap_parts", "encap_synth", "host_d2h", "lane_coop")
 
 
 def main():

@@ -31,7 +31,7 @@ struct Knob {
 
 static const uint64_t kL4Small[] = {0, 5}, kL4SU[] = {0, 2}, kVSmall[] = {0, 6, 7, 8},
                       kWaves[] = {1, 2, 4, 8}, kAbl[] = {0, 1, 32},
-                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {0, 2, 3}, kParts[] = {1, 2, 3, 4, 8};
+                      kUnroll[] = {4, 8}, kCoopW[] = {2, 4, 8, 16}, kAeadK[] = {0, 2, 3}, kParts[] = {1, 2, 3, 4, 8}, kCoop[] = {0, 1};
 #define WG_N(a) (sizeof(a) / sizeof(a[0]))
 static const Knob kKnobs[] = {
     {"l4_blocks", &Tune::l4_blocks, nullptr, 1, 1u << 20, nullptr, 0},
@@ -57,6 +57,7 @@ static const Knob kKnobs[] = {
     {"aead_stage", nullptr, &Tune::aead_stage, 0, 1, nullptr, 0},
     {"encap_parts", nullptr, &Tune::encap_parts, 0, 0, kParts, WG_N(kParts)},
     {"encap_synth", nullptr, &Tune::encap_synth, 0, 1, nullptr, 0},
+    {"lane_coop", nullptr, &Tune::lane_coop, 0, 0, kCoop, WG_N(kCoop)},
 };
 #undef WG_N
 
@@ -124,6 +125,10 @@ static Tune tune_initial() {
     x.verify_auto_t = 1;
     x.verify_k2min = 2048;
     x.gso_ablate = 0;
+    // descriptor batches' small packets: chunks loaded by the wave together
+    // (coop_chunks): config 4's 64-B sub-batch 45.9 -> 44.9 us, config 4 / 5
+    // unchanged (profiles/r06_coop_ab.txt)
+    x.lane_coop = 1;
     // host pipeline chunk: 128-512 MiB reach 97-98 % of the raw H2D rate
     // (8 MiB: 70 %, per-chunk overheads; profiles/r02_host_path.json);
     // with both directions in flight 64 MiB: decap 35.2 ms vs 37.3 at

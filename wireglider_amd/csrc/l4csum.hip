@@ -199,6 +199,45 @@ __device__ __forceinline__ void lane_chunks(uintptr_t a, uint32_t len, bool use,
     }
 }
 
+// The same five chunks per lane, loaded by the whole wave together (the
+// split kernel's lane role, knob lane_coop = 1): the wave's 320 chunk slots
+// (lane j's chunk c = slot 5j + c) are dealt in order, instruction k giving
+// lane l slot 64k + l, so one load instruction covers ~13 packets' windows
+// (each lane learns packet j's window from lane j by two ds_bpermute)
+// instead of one 16-B piece of each of 64 packets; the chunks go through the
+// wave's 5 KiB of LDS rows (slot s at 16 s: each instruction's stores are
+// 1 KiB in a row; lane l's reads at 80 l are conflict-free) back to their
+// packet's lane.  Config 4's 64-B sub-batch 45.9 -> 44.9 us back to back,
+// config 4 / 5 unchanged; the verify kernels' lane paths measured no gain
+// or a loss (profiles/r06_coop_ab.txt).  Every lane of the wave
+// must be active; the rows are used once per wave.
+__device__ __forceinline__ void coop_chunks(uintptr_t a, uint32_t len, bool use, v4u W[5], v4u *rows) {
+    uint64_t mine = (uint64_t)reinterpret_cast<uintptr_t>(&g_zero16);
+    if (use && len) {  // the window lane_chunks loads: first chunk | index of the last (0-4) in its free low bits
+        const uintptr_t a0 = a & ~(uintptr_t)15;
+        mine = (uint64_t)a0 | (uint64_t)((((a + len - 1) & ~(uintptr_t)15) - a0) >> 4);
+    }
+    const uint32_t lo = (uint32_t)mine, hi = (uint32_t)(mine >> 32);
+    const uint32_t lane = lane_id();
+    v4u V[5];
+#pragma unroll
+    for (uint32_t k = 0; k < 5; k++) {
+        const uint32_t sl = 64u * k + lane, j = sl / 5u, c = sl - 5u * j;
+        const uint32_t jl = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)lo);
+        const uint32_t jh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)hi);
+        const uint32_t n = jl & 15u;
+        V[k] = ld16((uintptr_t)((((uint64_t)jh << 32) | (jl & ~15u)) + 16u * (c < n ? c : n)));
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 5; k++)
+        rows[64u * k + lane] = V[k];
+    wave_lds_handoff();
+#pragma unroll
+    for (uint32_t c = 0; c < 5; c++)
+        W[c] = rows[5u * lane + c];
+}
+constexpr uint32_t kCoopRows = 320;  // v4u per wave
+
 // The lane paths' realignment: the packet's 16 dwords R[m] (bytes 4m..4m+3
 // of the packet at a, bytes at positions >= len zeroed) from the 20 dwords of
 // its five aligned chunks.  The dword offset q4 = (a & 15) >> 2 picks
@@ -373,9 +412,10 @@ __global__ __launch_bounds__(256) void l4csum_uniform_small_kernel(L4Params p) {
 // batch keeps a lane per packet (waves 1-3 leave after one descriptor load),
 // an all-long one keeps the short 16-packet waves with every descriptor in
 // one vector load.  One launch, no host knowledge of the mix.
-template <int kKind, bool kNT, int U = 4>  // U: loads in flight per lane on a long packet's rest
+template <int kKind, bool kNT, int U = 4, bool kCoop = true>  // U: loads in flight per lane on a long packet's rest
 __global__ __launch_bounds__(256) void l4csum_split_kernel(L4Params p) {
     constexpr bool kL4 = kKind != kDescPlain;
+    __shared__ v4u s_rows[kCoop ? kCoopRows : 1];  // the lane role's (wave 0)
     const uint32_t lane = lane_id();
     const uint32_t wib = wave_in_block();
     const uint64_t blk = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -405,7 +445,10 @@ __global__ __launch_bounds__(256) void l4csum_split_kernel(L4Params p) {
     const bool small = wib == 0 && live && !grp_long;
     if (__ballot(small)) {  // wave-uniform; never true on waves 1-3
         v4u W[5];
-        lane_chunks(a, len, small && len, W);
+        if constexpr (kCoop)
+            coop_chunks(a, len, small && len, W, s_rows);
+        else
+            lane_chunks(a, len, small && len, W);
         const uint32_t t = lane_sum<kL4>(W, a, small ? len : 0u, cs, fl);
         if (small)
             p.out[i] = (uint16_t)(~fold16_32(t) & 0xffffu);
@@ -530,10 +573,16 @@ static int launch_split(const L4Params &p, hipStream_t st) {
         blocks = (blocks + 7) & ~7ull;  // XCD swizzle bijective; surplus blocks have no live lane
     if (blocks > 0x7fffffffull)
         return WG_ERR_INVALID;
-    if (tune().l4_unroll == 8)
-        hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 8>), dim3((unsigned)blocks), dim3(256), 0, st, q);
+    const Tune t = tune();
+    const dim3 g((unsigned)blocks), b(256);
+    if (t.l4_unroll == 8 && t.lane_coop)
+        hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 8, true>), g, b, 0, st, q);
+    else if (t.l4_unroll == 8)
+        hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 8, false>), g, b, 0, st, q);
+    else if (t.lane_coop)
+        hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 4, true>), g, b, 0, st, q);
     else
-        hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 4>), dim3((unsigned)blocks), dim3(256), 0, st, q);
+        hipLaunchKernelGGL((l4csum_split_kernel<kKind, kNT, 4, false>), g, b, 0, st, q);
     return WG_OK;
 }
 

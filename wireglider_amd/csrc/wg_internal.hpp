@@ -35,6 +35,7 @@ struct Tune {
     uint32_t encap_parts; // wg_encap_batch: slices split on a side stream under the previous slice's AEAD (1 = off)
     uint32_t encap_synth; // wg_encap_batch: the AEAD builds eligible segments' headers, the split skips them
     uint32_t gso_ablate;  // GSO A/B variants (1 non-temporal stores, 32 no XCD swizzle; both correct)
+    uint32_t lane_coop;   // split kernel's lane role: 1 small packets' chunks loaded by the wave together (default), 0 per lane
 };
 
 // A snapshot of the knobs: a copy of the current immutable table, read
