@@ -109,6 +109,7 @@ def test_uniform_geometry_sweep(gpu, seg):
 
 
 DESC_VARIANTS = [{"l4_small": 0}, {"l4_small": 0, "l4_nt": 0}, {"l4_small": 5}, {"l4_small": 5, "l4_nt": 0},
+                 {"l4_small": 5, "lane_coop": 0}, {"l4_small": 5, "lane_coop": 0, "l4_unroll": 4},
                  {"l4_small": 5, "l4_unroll": 4},
                  {"l4_coop": 1 << 20, "l4_coop_waves": 2}, {"l4_coop": 1 << 20, "l4_coop_waves": 4, "l4_unroll": 4},
                  {"l4_coop": 1 << 20, "l4_coop_waves": 8, "l4_nt": 0}, {"l4_coop": 1 << 20, "l4_coop_waves": 16}]
@@ -122,7 +123,8 @@ def test_desc_random(gpu, knobs):
     import torch
 
     wga = _wga()
-    saved = {k: wga.tune_get(k) for k in ("l4_blocks", "l4_small", "l4_nt", "l4_coop", "l4_coop_waves", "l4_unroll")}
+    saved = {k: wga.tune_get(k) for k in ("l4_blocks", "l4_small", "l4_nt", "l4_coop", "l4_coop_waves", "l4_unroll",
+                                          "lane_coop")}
     for k, v in knobs.items():
         wga.tune_set(k, v)
     rng = np.random.default_rng(1234)
@@ -180,9 +182,10 @@ def test_uniform_small_segments(gpu, seg, knob):
         wga.tune_set("l4_small_uniform", saved)
 
 
+@pytest.mark.parametrize("coop", [1, 0])
 @pytest.mark.parametrize("small", [0, 5])
 @pytest.mark.parametrize("seed", [5, 6])
-def test_desc_small_packets(gpu, small, seed):
+def test_desc_small_packets(gpu, small, seed, coop):
     """Batches of mostly small packets (0-130 B, every alignment, csum_start
     inside, at and past the end, truncated pseudo-header addresses) with a few
     long ones mixed in: the thread-per-packet kernel's lane path (<= 64 B),
@@ -191,9 +194,10 @@ def test_desc_small_packets(gpu, small, seed):
     import torch
 
     wga = _wga()
-    saved = {k: wga.tune_get(k) for k in ("l4_small", "l4_coop")}
+    saved = {k: wga.tune_get(k) for k in ("l4_small", "l4_coop", "lane_coop")}
     wga.tune_set("l4_small", small)
     wga.tune_set("l4_coop", 0)
+    wga.tune_set("lane_coop", coop)
     rng = np.random.default_rng(seed)
     n = 30001
     lens = rng.integers(0, 131, n)

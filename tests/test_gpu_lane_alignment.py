@@ -8,6 +8,8 @@ the same in every lane the wave takes one scalar branch (a straight-line copy
 per q4), otherwise bit-mask selects: random offsets (test_gpu_l4.py,
 test_verify_gates.py) reach the select form almost always, so this file puts
 whole batches, and whole 64-descriptor runs, at each of the 16 alignments.
+The split kernel's small packets are checked both loaded by the wave
+together (lane_coop 1, coop_chunks) and by their own lanes (0).
 Config 4's 64-B packets (8-B aligned between 9,000-B ones) are q4 0 and 2.
 
 Checked against the oracle: calc_l4_checksum (checksum.cpp:8-36) and
@@ -85,15 +87,16 @@ def _to_dev(buf, d, dev):
     return tb, td
 
 
-@pytest.mark.parametrize("l4_small", [0, 5])
-def test_l4_desc_uniform_alignment(gpu, l4_small):
+@pytest.mark.parametrize("l4_small,lane_coop", [(0, 1), (5, 1), (5, 0)])
+def test_l4_desc_uniform_alignment(gpu, l4_small, lane_coop):
     import torch
 
     wga = _wga()
-    saved = {k: wga.tune_get(k) for k in ("l4_small", "l4_coop")}
+    saved = {k: wga.tune_get(k) for k in ("l4_small", "l4_coop", "lane_coop")}
     try:
         wga.tune_set("l4_small", l4_small)
         wga.tune_set("l4_coop", 0)
+        wga.tune_set("lane_coop", lane_coop)
         for name, buf, d in _cases(71):
             tb, td = _to_dev(buf, d, gpu)
             out = wga.calc_l4_checksum_desc(tb, td)
