@@ -126,7 +126,7 @@ static Tune tune_initial() {
     x.verify_k2min = 2048;
     x.gso_ablate = 0;
     // descriptor batches' small packets: chunks loaded by the wave together
-    // (coop_chunks): config 4's 64-B sub-batch 45.9 -> 44.9 us, config 4 / 5
+    // (coop_chunks): config 4's 64-B sub-batch 46.0 -> 45.3 us, config 4 / 5
     // unchanged (profiles/r06_coop_ab.txt)
     x.lane_coop = 1;
     // host pipeline chunk: 128-512 MiB reach 97-98 % of the raw H2D rate

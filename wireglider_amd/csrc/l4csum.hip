@@ -207,7 +207,7 @@ __device__ __forceinline__ void lane_chunks(uintptr_t a, uint32_t len, bool use,
 // instead of one 16-B piece of each of 64 packets; the chunks go through the
 // wave's 5 KiB of LDS rows (slot s at 16 s: each instruction's stores are
 // 1 KiB in a row; lane l's reads at 80 l are conflict-free) back to their
-// packet's lane.  Config 4's 64-B sub-batch 45.9 -> 44.9 us back to back,
+// packet's lane.  Config 4's 64-B sub-batch 46.0 -> 45.3 us back to back,
 // config 4 / 5 unchanged; the verify kernels' lane paths measured no gain
 // or a loss (profiles/r06_coop_ab.txt).  Every lane of the wave
 // must be active; the rows are used once per wave.
